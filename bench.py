@@ -1,0 +1,254 @@
+#!/usr/bin/env python3
+"""bench.py -- BASELINE.json's headline metric on MI355X.
+
+Metric: GiB/s device-resident LZ4 compress+decompress of 1M x 16 KiB pages
+(configs[1], "C2"), per GPU, weak scaling over 1/2/4/8 GPUs.  One step = one
+compress pass + one decompress pass over the rank's 1,048,576 resident pages;
+value = uncompressed bytes of all ranks' pages x steps / max-over-ranks wall time.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Prints ONE JSON line on rank 0 with `roofline` (dominant kernel, HIP events on
+the codec's stream) and `cpu_baseline` (the reference's vendored LZ4 1.7.5 from
+oracle/_ref when present, else the oracle port, on the host cores, bounded sample).
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from tyche_amd import _lib, codec, runner  # noqa: E402
+
+GIB = float(1 << 30)
+HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
+METRIC = "GiB/s device-resident LZ4 compress+decompress, 1M×16KiB pages, 1/2/4/8 GPU"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--pages", type=int, default=1 << 20, help="pages per GPU")
+    ap.add_argument("--page-len", type=int, default=16384)
+    ap.add_argument("--dist", type=int, default=0, help="pagegen distribution (0 = pg mix)")
+    ap.add_argument("--seed", type=int, default=20170303)
+    ap.add_argument("--cpu-pages", type=int, default=131072, help="CPU baseline sample (pages)")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--e2e-pages", type=int, default=32768, help="host-buffer (PCIe-inclusive) sample; 0 = skip")
+    return ap.parse_args()
+
+
+def cpu_baseline(pages_dev: torch.Tensor, n: int, threads: int) -> dict:
+    """Vendored LZ4 1.7.5 (or the oracle port) on the host: one codec call per page, pthreads by page range."""
+    import numpy as np
+
+    from oracle import oracle as O
+
+    host = pages_dev[:n].cpu().numpy()
+    plen = host.shape[1]
+    use_ref = O.have_ref()
+    kind = "reference" if use_ref else "port"
+    cap = O.lz4_bound(plen)
+    comp = np.zeros((n, cap), dtype=np.uint8)
+    clen = np.zeros(n, dtype=np.int32)
+    out = np.zeros_like(host)
+    rv = np.zeros(n, dtype=np.int32)
+    chunks = [(i * n // threads, (i + 1) * n // threads) for i in range(threads)]
+
+    if use_ref:
+        import ctypes
+        lib = O._Lib.ref()
+        u8p = ctypes.POINTER(ctypes.c_uint8)
+        base_in, base_c, base_o = host.ctypes.data, comp.ctypes.data, out.ctypes.data
+
+        def comp_range(a, b):
+            for i in range(a, b):
+                clen[i] = lib.LZ4_compress_default(ctypes.cast(base_in + i * plen, u8p),
+                                                   ctypes.cast(base_c + i * cap, u8p), plen, cap)
+
+        def dec_range(a, b):
+            for i in range(a, b):
+                rv[i] = lib.LZ4_decompress_safe(ctypes.cast(base_c + i * cap, u8p),
+                                                ctypes.cast(base_o + i * plen, u8p), int(clen[i]), plen)
+    else:
+        def comp_range(a, b):
+            O.lz4_compress_pages(host, comp, clen, a, b - a)
+
+        def dec_range(a, b):
+            O.lz4_decompress_pages(comp, clen, out, rv, a, b - a)
+
+    best_c = best_d = float("inf")
+    with cf.ThreadPoolExecutor(max_workers=threads) as ex:
+        for _ in range(3):   # best of 3, like the survey's probe
+            t0 = time.perf_counter()
+            list(ex.map(lambda r: comp_range(*r), chunks))
+            t1 = time.perf_counter()
+            list(ex.map(lambda r: dec_range(*r), chunks))
+            t2 = time.perf_counter()
+            best_c, best_d = min(best_c, t1 - t0), min(best_d, t2 - t1)
+    assert (rv == plen).all() and np.array_equal(out, host), "CPU baseline round trip failed"
+    nbytes = n * plen
+    return {
+        "value": round(nbytes / (best_c + best_d) / GIB, 3),
+        "unit": "GiB/s",
+        "cores": threads,
+        "kind": kind,
+        "sample": f"first {n} of the same pages ({nbytes / GIB:.1f} GiB), "
+                  f"{'LZ4_compress_default/LZ4_decompress_safe from oracle/_ref (vendored LZ4 1.7.5)' if use_ref else 'oracle/lz4_oracle.c port'}"
+                  f", one call per page, {threads} threads by page range, best of 3",
+        "compress_gib_s": round(nbytes / best_c / GIB, 3),
+        "decompress_gib_s": round(nbytes / best_d / GIB, 3),
+        "ratio": round(nbytes / float(clen.sum()), 4),
+    }
+
+
+def e2e_host(pages_dev: torch.Tensor, n: int) -> dict:
+    """PCIe-inclusive rate through the host batch API (malloc'd pages -> pinned -> H2D -> kernels -> D2H)."""
+    import ctypes
+
+    import numpy as np
+
+    lib = _lib.load()
+    host = pages_dev[:n].cpu().numpy()
+    plen = host.shape[1]
+    cap = codec.compress_bound(plen)
+    comp = np.zeros((n, cap), dtype=np.uint8)
+    out = np.zeros_like(host)
+    res = np.zeros(n, dtype=np.int32)
+    rv = np.zeros(n, dtype=np.int32)
+    vp = ctypes.c_void_p * n
+    src_p = vp(*[host.ctypes.data + i * plen for i in range(n)])
+    comp_p = vp(*[comp.ctypes.data + i * cap for i in range(n)])
+    out_p = vp(*[out.ctypes.data + i * plen for i in range(n)])
+    u32 = ctypes.c_uint32 * n
+    slen = u32(*([plen] * n))
+    ccap = u32(*([cap] * n))
+    i32p = ctypes.POINTER(ctypes.c_int32)
+    best_c = best_d = float("inf")
+    for _ in range(3):
+        t0 = time.perf_counter()
+        _lib.check(lib.tyche_compress_host(1, 1, n, src_p, slen, comp_p, ccap, res.ctypes.data_as(i32p)),
+                   "tyche_compress_host")
+        t1 = time.perf_counter()
+        clen = u32(*[int(x) for x in res])
+        _lib.check(lib.tyche_decompress_host(1, n, comp_p, clen, out_p, slen, rv.ctypes.data_as(i32p)),
+                   "tyche_decompress_host")
+        t2 = time.perf_counter()
+        best_c, best_d = min(best_c, t1 - t0), min(best_d, t2 - t1)
+    assert (rv == plen).all() and np.array_equal(out, host), "host-path round trip failed"
+    nbytes = n * plen
+    return {"pages": n, "compress_gib_s": round(nbytes / best_c / GIB, 3),
+            "decompress_gib_s": round(nbytes / best_d / GIB, 3),
+            "combined_gib_s": round(nbytes / (best_c + best_d) / GIB, 3)}
+
+
+def main():
+    args = parse()
+    info = runner.init_distributed()
+    dev = torch.device("cuda", info.local_rank)
+    torch.cuda.set_device(dev)
+    lib = _lib.load()
+    if lib.tyche_device_ready() != 1:
+        raise SystemExit(f"device not ready: {_lib.last_error()}")
+
+    n, plen = args.pages, args.page_len
+    first = info.rank * n                       # weak scaling: each rank owns its own 1M pages
+    pages = codec.pagegen(n, plen, seed=args.seed, first=first, dist=args.dist, device=dev)
+    slot = codec.slot_size(plen)
+    comp = torch.empty((n, slot), dtype=torch.uint8, device=dev)
+    clen = torch.empty((n,), dtype=torch.int32, device=dev)
+    out = torch.empty((n, plen), dtype=torch.uint8, device=dev)
+    rv = torch.empty((n,), dtype=torch.int32, device=dev)
+
+    def step(ev=None, max_comp=0):
+        if ev is not None:
+            ev[0].record()
+        codec.compress_pages(pages, out=comp, out_len=clen)
+        if ev is not None:
+            ev[1].record()
+        codec.decompress_pages(comp, clen, plen, out=out, rv=rv, max_comp_len=max_comp)
+        if ev is not None:
+            ev[2].record()
+
+    # warm-up, then a full-size correctness property: every page round-trips bit-exactly
+    step()
+    torch.cuda.synchronize()
+    max_comp = int(clen.max().item())
+    for _ in range(max(args.warmup - 1, 0)):
+        step(max_comp=max_comp)
+    torch.cuda.synchronize()
+    ok = bool((rv == plen).all().item()) and bool((clen > 0).all().item()) and torch.equal(out, pages)
+    if not ok:
+        raise SystemExit("round trip failed on the benchmark pages")
+    comp_bytes = int(clen.to(torch.int64).sum().item())
+
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    runner.barrier(info)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(events[k], max_comp)
+    torch.cuda.synchronize()
+    runner.barrier(info)
+    t1 = time.perf_counter()
+    elapsed = runner.max_over_ranks(info, t1 - t0)
+
+    c_ms = sum(e[0].elapsed_time(e[1]) for e in events) / args.steps
+    d_ms = sum(e[1].elapsed_time(e[2]) for e in events) / args.steps
+    page_bytes = n * plen
+    total_pages = runner.sum_over_ranks(info, float(n))
+    value = total_pages * plen * args.steps / elapsed / GIB
+    algo_bytes = page_bytes + comp_bytes            # per launch, either direction
+    kernels = {"lz4_encode": c_ms, "lz4_decode": d_ms}
+    dom = max(kernels, key=kernels.get)
+    achieved = algo_bytes / (kernels[dom] * 1e-3) / 1e9
+
+    result = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "GiB/s",
+        "n_gpus": info.world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (pagegen.h PostgreSQL-like heap/index pages, LZ4 ratio ~2.65, seed 20170303)",
+        "config": {"workload": "C2: LZ4 block compress+decompress, 1M x 16 KiB pages per GPU, device-resident",
+                   "pages_per_gpu": n, "page_len": plen, "codec": "lz4", "parallelism": f"page-range x{info.world}"},
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "algorithmic_bytes_per_launch": algo_bytes},
+        "compress_gib_s": round(page_bytes / (c_ms * 1e-3) / GIB, 3),
+        "decompress_gib_s": round(page_bytes / (d_ms * 1e-3) / GIB, 3),
+        "kernel_ms": {"lz4_encode": round(c_ms, 4), "lz4_decode": round(d_ms, 4)},
+        "roofline_by_kernel": {k: round(algo_bytes / (v * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) for k, v in kernels.items()},
+        "ratio": round(page_bytes / comp_bytes, 4),
+    }
+    if info.rank == 0 and info.world == 1:
+        if args.e2e_pages > 0:
+            result["e2e_host_path"] = e2e_host(pages, min(args.e2e_pages, n))
+        if not args.no_cpu:
+            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+            result["cpu_baseline"] = cpu_baseline(pages, min(args.cpu_pages, n), threads)
+    if info.rank == 0:
+        print(json.dumps(result), flush=True)
+    runner.shutdown(info)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,179 @@
+"""oracle/gen_golden.py -- TEST INFRASTRUCTURE ONLY.
+
+Generates the committed parity fixtures in tests/golden/ from the REFERENCE's
+own vendored codecs (LZ4 1.7.5 / zlib 1.2.8 / zstd 1.1.2 compiled from
+/root/reference/src by oracle/Makefile into oracle/_ref/libtyche_ref.so).
+Run here, where /root/reference exists:
+
+    make -C oracle ref && python oracle/gen_golden.py
+
+Fixtures (all data, no reference source):
+  kat_lorem.npz       the 4096-byte KAT input of src/tests.c:342-378 and its
+                      LZ4 / zlib-1 / zstd-1 encodings (2578 / 1759 / 1709 B)
+  lz4_generated.npz   reference LZ4 encodings of repo-generated pages
+                      (pagegen.h, every distribution, 8/16/32 KiB) + input digests
+  lz4_sample.npz      reference LZ4 encodings of the 60 sample_data pages, the
+                      SHA-256 of each original, and 6 originals in full
+  lz4_malformed.npz   corrupted / truncated / random streams with the reference
+                      LZ4_decompress_safe return value (and output digest when
+                      the output is defined)
+"""
+from __future__ import annotations
+
+import glob
+import hashlib
+import os
+import re
+import sys
+
+import numpy as np
+
+sys.path[0] = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+from oracle import oracle as O  # noqa: E402
+
+OUT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden")
+REF = "/root/reference"
+SEED = 20170303
+
+
+def sha(b: bytes) -> bytes:
+    return hashlib.sha256(b).digest()
+
+
+def pack(blobs: list[bytes]):
+    lens = np.array([len(b) for b in blobs], dtype=np.int64)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
+    data = np.frombuffer(b"".join(blobs), dtype=np.uint8) if blobs else np.zeros(0, np.uint8)
+    return data, offs, lens
+
+
+def kat_text() -> bytes:
+    s = open(os.path.join(REF, "src", "tests.c")).read()
+    i = s.index("void tests__compression")
+    j = s.index("int src_size", i)
+    return "".join(re.findall(r'"((?:[^"\\]|\\.)*)"', s[i:j])).encode()
+
+
+def gen_kat():
+    t = kat_text()
+    assert len(t) == 4096
+    lz4 = O.ref_lz4_compress(t)
+    zl = O.ref_zlib_compress(t, 1)
+    zs = O.ref_zstd_compress(t, 1)
+    print("KAT", len(lz4), len(zl), len(zs))
+    np.savez_compressed(os.path.join(OUT, "kat_lorem.npz"), text=np.frombuffer(t, np.uint8),
+                        lz4=np.frombuffer(lz4, np.uint8), zlib=np.frombuffer(zl, np.uint8),
+                        zstd=np.frombuffer(zs, np.uint8))
+
+
+def gen_generated():
+    rows = []   # (dist, page_len, index)
+    comps, digests = [], []
+    for dist in range(6):
+        for plen in (8192, 16384, 32768):
+            n = 1 if dist == 4 else 3
+            first = 1000 * dist + plen // 1024
+            pages = O.pagegen(n, plen, seed=SEED, first=first, dist=dist)
+            for k in range(n):
+                p = pages[k].tobytes()
+                c = O.ref_lz4_compress(p)
+                r, out = O.ref_lz4_decompress(c, plen)
+                assert r == plen and out == p
+                rows.append((dist, plen, first + k))
+                comps.append(c)
+                digests.append(sha(p))
+    data, offs, lens = pack(comps)
+    np.savez_compressed(os.path.join(OUT, "lz4_generated.npz"), seed=np.int64(SEED),
+                        meta=np.array(rows, dtype=np.int64), comp=data, comp_off=offs, comp_len=lens,
+                        digest=np.frombuffer(b"".join(digests), np.uint8).reshape(-1, 32))
+    print("generated", len(rows), data.size)
+
+
+def gen_sample():
+    files = sorted(glob.glob(os.path.join(REF, "sample_data", "*", "*", "*", "*")))
+    names, comps, digests, sizes = [], [], [], []
+    raw_keep = []
+    for f in files:
+        p = open(f, "rb").read()
+        c = O.ref_lz4_compress(p)
+        rel = os.path.relpath(f, os.path.join(REF, "sample_data"))
+        names.append(rel)
+        comps.append(c)
+        digests.append(sha(p))
+        sizes.append(len(p))
+    # keep a table page and an index page of each size in full (compress parity inputs)
+    keep = []
+    for sz in ("8k", "16k", "32k"):
+        for kind in ("tables", "indexes"):
+            idx = [i for i, n in enumerate(names) if n.startswith(sz + "/") and f"/{kind}/" in n][0]
+            keep.append(idx)
+            raw_keep.append(open(os.path.join(REF, "sample_data", names[idx]), "rb").read())
+    data, offs, lens = pack(comps)
+    rdata, roffs, rlens = pack(raw_keep)
+    np.savez_compressed(os.path.join(OUT, "lz4_sample.npz"), names=np.array(names), comp=data, comp_off=offs,
+                        comp_len=lens, digest=np.frombuffer(b"".join(digests), np.uint8).reshape(-1, 32),
+                        size=np.array(sizes, np.int64), raw_index=np.array(keep, np.int64), raw=rdata,
+                        raw_off=roffs, raw_len=rlens)
+    print("sample", len(names), data.size, rdata.size)
+
+
+def gen_malformed():
+    rng = np.random.default_rng(SEED)
+    cases = []   # (stream, out_cap)
+    base_pages = O.pagegen(4, 16384, seed=SEED, first=777, dist=0)
+    streams = [O.ref_lz4_compress(p.tobytes()) for p in base_pages]
+    small = O.ref_lz4_compress(kat_text())
+    streams.append(small)
+    for s in streams:
+        n = len(s)
+        for cut in sorted(set([1, 2, 3, 5, 8, 13, n // 3, n // 2, n - 9, n - 6, n - 5, n - 1])):
+            if 0 < cut < n:
+                cases.append((s[:cut], 16384))
+        for _ in range(12):
+            b = bytearray(s)
+            for _ in range(int(rng.integers(1, 4))):
+                b[int(rng.integers(0, n))] = int(rng.integers(0, 256))
+            cases.append((bytes(b), 16384 if len(s) > 3000 else 4096))
+        cases.append((s, 16383))         # output one byte short
+        cases.append((s, 16384 + 100))   # larger capacity: decode stops at the stream end
+        cases.append((s + b"\x00", 16384))   # trailing garbage
+    for _ in range(40):
+        ln = int(rng.integers(1, 300))
+        cases.append((rng.integers(0, 256, ln, dtype=np.uint8).tobytes(), int(rng.choice([64, 1024, 16384]))))
+    # hand-made edge cases
+    cases += [
+        (b"\x00", 0), (b"\x00", 1), (b"\x10A", 0), (b"\x10A", 1), (b"\xf0", 64), (b"\xf0\xff", 64),
+        (b"\x50hello", 5), (b"\x50hello", 4), (b"\x50hello", 64),
+        (b"\x1fa\x01\x00\xff\xff\x00" + b"\x50abcde", 600),      # long RLE match then literals
+        (b"\x1fa\x00\x00\x05" + b"\x50abcde", 64),                 # offset 0
+        (b"\x14a\x02\x00" + b"\x50abcde", 64),                     # offset beyond output
+        (b"\x4fabcd\x04\x00\x10" + b"\x50abcde", 64),              # overlap offset 4
+        (b"\x80abcdefgh" + b"\x00", 8),
+    ]
+    streams_out, caps, rvs, digs, defined = [], [], [], [], []
+    for s, cap in cases:
+        r0, o0 = O.ref_lz4_decompress(s, cap, fill=0)
+        r1, o1 = O.ref_lz4_decompress(s, cap, fill=0xFF)
+        assert r0 == r1
+        streams_out.append(s)
+        caps.append(cap)
+        rvs.append(r0)
+        ok = r0 >= 0 and o0 == o1
+        defined.append(ok)
+        digs.append(sha(o0) if ok else b"\0" * 32)
+    data, offs, lens = pack(streams_out)
+    np.savez_compressed(os.path.join(OUT, "lz4_malformed.npz"), comp=data, comp_off=offs, comp_len=lens,
+                        cap=np.array(caps, np.int64), rv=np.array(rvs, np.int64),
+                        defined=np.array(defined, bool),
+                        digest=np.frombuffer(b"".join(digs), np.uint8).reshape(-1, 32))
+    print("malformed", len(cases), "errors", sum(r < 0 for r in rvs), "undefined", sum(not d for d in defined))
+
+
+if __name__ == "__main__":
+    if not O.have_ref():
+        sys.exit("oracle/_ref/libtyche_ref.so missing: run `make -C oracle ref` where /root/reference exists")
+    os.makedirs(OUT, exist_ok=True)
+    gen_kat()
+    gen_generated()
+    gen_sample()
+    gen_malformed()

@@ -1,0 +1,29 @@
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU; runs the HIP kernels through the C ABI")
+
+
+def load_golden(name: str):
+    return np.load(os.path.join(GOLDEN, name), allow_pickle=False)
+
+
+def unpack(data: np.ndarray, offs: np.ndarray, lens: np.ndarray, i: int) -> bytes:
+    return data[offs[i]:offs[i] + lens[i]].tobytes()
+
+
+@pytest.fixture(scope="session")
+def oracle_mod():
+    from oracle import oracle as O
+    O.build(ref=False) if not os.path.exists(O.ORACLE_SO) else None
+    return O

@@ -1,0 +1,116 @@
+"""The CPU oracle (oracle/lz4_oracle.c) pinned against the reference's outputs.
+
+Fixtures in tests/golden/ were produced by oracle/gen_golden.py from the
+reference's own vendored LZ4 1.7.5 (src/lz4/lz4.c) compiled here.  The KAT is
+src/tests.c:342-378 (4096-byte Lorem text; LZ4 level 1 -> 2578 bytes).
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+from conftest import load_golden, unpack
+
+
+def test_kat_lorem_exact(oracle_mod):
+    O = oracle_mod
+    g = load_golden("kat_lorem.npz")
+    text = g["text"].tobytes()
+    assert len(text) == 4096
+    comp = O.lz4_compress(text)
+    assert len(comp) == 2578
+    assert comp == g["lz4"].tobytes()
+    rv, out = O.lz4_decompress(comp, len(text))
+    assert rv == 4096 and out == text
+    assert len(g["zlib"]) == 1759 and len(g["zstd"]) == 1709
+
+
+def test_generated_pages_exact(oracle_mod):
+    O = oracle_mod
+    g = load_golden("lz4_generated.npz")
+    seed = int(g["seed"])
+    for i, (dist, plen, idx) in enumerate(g["meta"]):
+        page = O.pagegen(1, int(plen), seed=seed, first=int(idx), dist=int(dist))[0].tobytes()
+        assert hashlib.sha256(page).digest() == g["digest"][i].tobytes(), "page generator drifted"
+        ref = unpack(g["comp"], g["comp_off"], g["comp_len"], i)
+        assert O.lz4_compress(page) == ref, (dist, plen, idx)
+        rv, out = O.lz4_decompress(ref, int(plen))
+        assert rv == plen and out == page
+
+
+def test_sample_pages_exact(oracle_mod):
+    O = oracle_mod
+    g = load_golden("lz4_sample.npz")
+    for i in range(len(g["names"])):
+        comp = unpack(g["comp"], g["comp_off"], g["comp_len"], i)
+        rv, out = O.lz4_decompress(comp, int(g["size"][i]))
+        assert rv == g["size"][i]
+        assert hashlib.sha256(out).digest() == g["digest"][i].tobytes()
+    for k, i in enumerate(g["raw_index"]):
+        raw = unpack(g["raw"], g["raw_off"], g["raw_len"], k)
+        assert O.lz4_compress(raw) == unpack(g["comp"], g["comp_off"], g["comp_len"], int(i))
+
+
+def test_malformed_streams(oracle_mod):
+    O = oracle_mod
+    g = load_golden("lz4_malformed.npz")
+    for i in range(len(g["cap"])):
+        s = unpack(g["comp"], g["comp_off"], g["comp_len"], i)
+        rv, out = O.lz4_decompress(s, int(g["cap"][i]))
+        assert rv == g["rv"][i], (i, s[:16], g["cap"][i])
+        if g["defined"][i]:
+            assert hashlib.sha256(out).digest() == g["digest"][i].tobytes()
+
+
+def test_compress_limited_output(oracle_mod):
+    """cap < bound selects limitedOutput (lz4.c:671-675): 0 when it does not fit, else the same bytes."""
+    O = oracle_mod
+    page = O.pagegen(1, 16384, dist=0)[0].tobytes()
+    full = O.lz4_compress(page)
+    assert O.lz4_compress(page, cap=len(full)) == full
+    assert O.lz4_compress(page, cap=len(full) - 1) == b""
+    rnd = O.pagegen(1, 4096, dist=4)[0].tobytes()
+    assert O.lz4_compress(rnd, cap=4096) == b""
+
+
+@pytest.mark.parametrize("n", [0, 1, 5, 12, 13, 14, 100])
+def test_tiny_inputs(oracle_mod, n):
+    O = oracle_mod
+    data = bytes((i * 7) & 0xFF for i in range(n))
+    comp = O.lz4_compress(data)
+    assert len(comp) == 1 + n if n < 13 else len(comp) > 0
+    rv, out = O.lz4_decompress(comp, n)
+    assert rv == n and out == data
+
+
+def test_against_reference_build_random(oracle_mod):
+    """Randomised cross-check with the reference build (only where oracle/_ref exists)."""
+    O = oracle_mod
+    if not O.have_ref():
+        pytest.skip("oracle/_ref/libtyche_ref.so not built (no /root/reference here)")
+    rng = np.random.default_rng(7)
+    pages = O.pagegen(24, 8192, seed=99, dist=0)
+    for t in range(120):
+        kind = t % 4
+        if kind == 0:
+            data = rng.integers(0, 256, int(rng.integers(0, 3000)), dtype=np.uint8).tobytes()
+        elif kind == 1:
+            data = (rng.integers(0, 4, int(rng.integers(1, 5000)), dtype=np.uint8) * 17).tobytes()
+        else:
+            p = bytearray(pages[t % 24].tobytes()[: int(rng.integers(1, 8192))])
+            for _ in range(int(rng.integers(0, 20))):
+                if p:
+                    p[int(rng.integers(0, len(p)))] = int(rng.integers(0, 256))
+            data = bytes(p)
+        ref = O.ref_lz4_compress(data)
+        assert O.lz4_compress(data) == ref
+        # corrupt and compare decoder verdicts
+        s = bytearray(ref)
+        for _ in range(int(rng.integers(0, 3))):
+            if s:
+                s[int(rng.integers(0, len(s)))] = int(rng.integers(0, 256))
+        cap = len(data) + int(rng.integers(-3, 4))
+        cap = max(cap, 0)
+        r1, o1 = O.lz4_decompress(bytes(s), cap)
+        r2, o2 = O.ref_lz4_decompress(bytes(s), cap)
+        assert r1 == r2

@@ -1,0 +1,59 @@
+"""Build recipe for libtyche_codec.so (gfx950 code objects + the C ABI).
+
+hipcc compiles each .hip file to an object (in parallel) and links one shared
+library in-tree, next to this file, so it travels to the GPU box with the repo
+snapshot.  No JIT cache, no site-packages install.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+BUILD = os.path.join(HERE, "..", "build", "tyche_amd")
+LIB = os.path.join(HERE, "libtyche_codec.so")
+SOURCES = ["engine.hip", "lz4_decode.hip", "lz4_encode.hip", "pagegen.hip"]
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+FLAGS = ["--offload-arch=" + ARCH, "-O3", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-variable",
+         "-munsafe-fp-atomics", "-I" + os.path.join(HERE, "..", "include")]
+
+
+def _newer(target: str, deps: list[str]) -> bool:
+    if not os.path.exists(target):
+        return False
+    t = os.path.getmtime(target)
+    return all(os.path.getmtime(d) <= t for d in deps)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    os.makedirs(BUILD, exist_ok=True)
+    headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+    headers.append(os.path.join(HERE, "..", "include", "tyche_codec.h"))
+    objs = []
+    jobs = []
+    for src in SOURCES:
+        s = os.path.join(CSRC, src)
+        o = os.path.join(BUILD, src.replace(".hip", ".o"))
+        objs.append(o)
+        if force or not _newer(o, [s] + headers):
+            jobs.append([HIPCC] + FLAGS + ["-c", s, "-o", o])
+
+    def run(cmd):
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.check_call(cmd)
+
+    if jobs:
+        with cf.ThreadPoolExecutor(max_workers=min(len(jobs), 8)) as ex:
+            list(ex.map(run, jobs))
+    if force or jobs or not _newer(LIB, objs):
+        run([HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB] + objs)
+    return LIB
+
+
+if __name__ == "__main__":
+    import sys
+    print(build(force="--force" in sys.argv, verbose=True))
