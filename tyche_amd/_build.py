@@ -28,18 +28,24 @@ def _newer(target: str, deps: list[str]) -> bool:
     return all(os.path.getmtime(d) <= t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    os.makedirs(BUILD, exist_ok=True)
+def build(force: bool = False, verbose: bool = False, profile: bool = False, ablate: int = 0) -> str:
+    """profile=True builds the diagnostic variant (per-phase cycle stamps, -DTYCHE_PROFILE)
+    as libtyche_codec_prof.so; it is never loaded by the product path."""
+    tag = ("_prof" if profile else "") + (f"_abl{ablate}" if ablate else "")
+    build_dir = BUILD + tag
+    lib_path = LIB.replace(".so", tag + ".so")
+    flags = FLAGS + (["-DTYCHE_PROFILE"] if profile else []) + ([f"-DTYCHE_ABLATE={ablate}"] if ablate else [])
+    os.makedirs(build_dir, exist_ok=True)
     headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
     headers.append(os.path.join(HERE, "..", "include", "tyche_codec.h"))
     objs = []
     jobs = []
     for src in SOURCES:
         s = os.path.join(CSRC, src)
-        o = os.path.join(BUILD, src.replace(".hip", ".o"))
+        o = os.path.join(build_dir, src.replace(".hip", ".o"))
         objs.append(o)
         if force or not _newer(o, [s] + headers):
-            jobs.append([HIPCC] + FLAGS + ["-c", s, "-o", o])
+            jobs.append([HIPCC] + flags + ["-c", s, "-o", o])
 
     def run(cmd):
         if verbose:
@@ -49,11 +55,13 @@ def build(force: bool = False, verbose: bool = False) -> str:
     if jobs:
         with cf.ThreadPoolExecutor(max_workers=min(len(jobs), 8)) as ex:
             list(ex.map(run, jobs))
-    if force or jobs or not _newer(LIB, objs):
-        run([HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB] + objs)
-    return LIB
+    if force or jobs or not _newer(lib_path, objs):
+        run([HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", lib_path] + objs)
+    return lib_path
 
 
 if __name__ == "__main__":
     import sys
-    print(build(force="--force" in sys.argv, verbose=True))
+    abl = [int(a.split("=")[1]) for a in sys.argv if a.startswith("--ablate=")]
+    print(build(force="--force" in sys.argv, verbose=True, profile="--profile" in sys.argv,
+                ablate=abl[0] if abl else 0))

@@ -10,7 +10,7 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libtyche_codec.so")
+LIB_PATH = os.environ.get("TYCHE_CODEC_LIB") or os.path.join(HERE, "libtyche_codec.so")
 HEADER = os.path.join(HERE, "..", "include", "tyche_codec.h")
 
 # compressor IDs, src/globals.h:16-19

@@ -3,30 +3,343 @@
 // Replaces the per-hit LZ4_decompress_safe call of buffer__decompress
 // (reference src/buffer.c:248-253 -> src/lz4/lz4.c:1251, generic decoder
 // lz4.c:1089-1248) with one kernel over a batch of pages.  Results are
-// LZ4_decompress_safe's: decoded size, or -(input bytes consumed)-1 at the
-// same consumption point for a malformed stream; the decoded bytes are
-// bit-identical.
+// LZ4_decompress_safe's: decoded size, or -(input bytes consumed)-1 at the same
+// consumption point for a malformed stream; decoded bytes are bit-identical.
 //
-// Layout: one 64-lane wave per page.  The compressed page is staged into LDS
-// with 16-byte loads; the page is rebuilt in an LDS window and written back to
-// HBM with 16-byte stores, so HBM sees exactly comp_len bytes read and page_len
-// bytes written.  The token chain is parsed with wave-uniform scalar control
-// from a 64-byte window of the stream held one byte per lane (one LDS read per
-// sequence, fields picked out with v_readlane); literal and match bytes are
-// copied 64 per instruction, with modulo addressing for self-overlapping
-// matches (offset < length), which reproduces the forward byte-copy semantics of
-// lz4.c:1209-1236.
+// One 64-lane wave per page; compressed stream and rebuilt page both live in
+// LDS, so HBM sees comp_len bytes read and page_len bytes written (16-byte
+// accesses).  The serial parts of LZ4 decoding are split apart:
+//
+//  1. token chain (parse): the stream is cut into 64 segments; every lane walks
+//     the token chain speculatively from its segment start, marking visited
+//     positions.  A walk from the true entry point (the previous segment's exit)
+//     usually lands on a marked position after a few steps and then agrees with
+//     the speculative walk, so a short fix-up walk per lane, repeated until no
+//     entry changes, yields the exact chain.  The token positions are then
+//     compacted into an ordered list.
+//  2. per 64 sequences, one per lane: literal length, offset and match length
+//     are decoded in parallel, output positions come from a wave prefix sum, and
+//     the reference's acceptance checks are evaluated per sequence; the first
+//     failing sequence in stream order gives the return value.
+//  3. literals are placed in parallel (they depend on nothing).
+//  4. matches are copied in dependency order: the first pending match fixes a
+//     frontier F (every byte before it is final); all pending matches whose
+//     source ends at or before F are independent and are copied together, up to
+//     four per instruction (16 lanes each), with modulo addressing for
+//     self-overlapping matches (offset < length).  This is exactly the forward
+//     byte-copy semantics of lz4.c:1209-1236.
 #include <hip/hip_runtime.h>
 
 #include "engine.h"
 #include "lds_io.h"
+
+#include <algorithm>
 
 namespace tyche {
 
 namespace {
 
 constexpr uint32_t kWave = 64;
-constexpr uint32_t kPad = 64;   // zeroed tail after the staged stream
+constexpr uint32_t kPad = 64;        // zeroed tail after the staged stream
+constexpr uint32_t kEnd = 0xFFFFFFFFu;
+
+// Timing-only ablation builds (-DTYCHE_ABLATE=mask; outputs are wrong):
+//   1 skip literal placement, 2 skip match copies, 4 skip stage-out,
+//   (bit 8 unused)
+#ifndef TYCHE_ABLATE
+#define TYCHE_ABLATE 0
+#endif
+
+// Optional phase profile (diagnostic build only: -DTYCHE_PROFILE).  Shares of
+// shader cycles per phase, summed over pages by lane 0.
+#ifdef TYCHE_PROFILE
+__device__ unsigned long long g_prof[16];
+#define PROF_DECL unsigned long long _pt = clock64();
+#define PROF_MARK(slot)                                                        \
+    do {                                                                       \
+        unsigned long long _n = clock64();                                     \
+        if (lane == 0) atomicAdd(&g_prof[slot], _n - _pt);                     \
+        _pt = _n;                                                              \
+    } while (0)
+#define PROF_ADD(slot, v) do { if (lane == 0) atomicAdd(&g_prof[slot], (unsigned long long)(v)); } while (0)
+#else
+#define PROF_DECL
+#define PROF_MARK(slot) do { } while (0)
+#define PROF_ADD(slot, v) do { } while (0)
+#endif
+
+
+
+// Position of the token after the sequence whose token is at p, or kEnd when
+// that sequence ends the chain on the input side (terminal literal run, or an
+// overrun while reading match-length bytes).  Mirrors the input-side reads of
+// lz4.c:1134-1143, 1147, 1165, 1172-1182.
+__device__ __forceinline__ uint32_t next_token(const uint8_t *in, int32_t L, uint32_t p) {
+    uint32_t t = in[p];
+    int32_t q = (int32_t)p + 1;
+    int32_t lit = (int32_t)(t >> 4);
+    if (lit == kRunMask) {
+        uint32_t s;
+        do {
+            s = in[q];
+            q++;
+            lit += (int32_t)s;
+        } while (q < L - kRunMask && s == 255);
+    }
+    if (q + lit > L - 8) return kEnd;
+    q += lit + 2;
+    if ((t & 15) == 15) {
+        uint32_t s;
+        do {
+            s = in[q];
+            q++;
+            if (q > L - kLastLiterals) return kEnd;
+        } while (s == 255);
+    }
+    return (uint32_t)q;
+}
+
+// inclusive prefix sum over the 64 lanes with DPP row shifts + row broadcasts
+__device__ __forceinline__ int32_t wave_incl_sum(int32_t v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, true);   // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, true);   // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, true);   // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, true);   // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+    return v;
+}
+
+// Parallel token-chain parse.  Writes the ordered token positions to seqpos and
+// returns their number.  owner: L bytes of scratch (the page window, unused
+// until the copy phases).
+//
+//  1. lane k walks the chain from its segment start k*S to the segment end,
+//     stamping owner[p] = k+1 on every position it visits;
+//  2. from its exit it keeps walking ("bridge") until it reaches a position
+//     stamped by a later lane, or the end of the chain;
+//  3. the true chain starts with lane 0's walk; wherever an on-chain lane's
+//     bridge meets lane j's stamp, the chain continues along lane j's walk from
+//     that position.  Following these hand-offs (at most 64, uniform scalar
+//     code) gives every on-chain lane its entry point;
+//  4. each on-chain lane re-walks entry -> hand-off position to count and then
+//     write its positions.
+__device__ uint32_t parse_chain(const uint8_t *in, int32_t L, uint8_t *owner, uint16_t *seqpos, uint32_t lane) {
+    PROF_DECL
+    const uint32_t S = ((uint32_t)L + kWave - 1) / kWave;
+    const uint32_t seg0 = lane * S;
+    const uint32_t seg1 = min(seg0 + S, (uint32_t)L);
+    for (uint32_t w = lane; w < ((uint32_t)L + 3) / 4; w += kWave) ((uint32_t *)owner)[w] = 0;
+    __syncthreads();
+    uint32_t p = seg0;
+    while (p < seg1) {
+        owner[p] = (uint8_t)(lane + 1);
+        p = next_token(in, L, p);
+    }
+    __syncthreads();
+    PROF_MARK(2);
+    uint32_t y = p, o = 0;                        // hand-off position and its stamp (0 = chain ends)
+    if (seg0 < seg1) {
+        while (y < (uint32_t)L) {
+            const uint32_t ow = owner[y];
+            if (ow > lane + 1) { o = ow; break; }
+            y = next_token(in, L, y);
+        }
+    }
+    uint32_t entry = kEnd;
+    {
+        uint32_t cur = 0, e = 0;
+        for (uint32_t it = 0; it < kWave; it++) {
+            if (lane == cur) entry = e;
+            e = rdlane(y, cur);
+            const uint32_t nx = rdlane(o, cur);
+            PROF_ADD(4, 1);
+            if (nx == 0) break;
+            cur = nx - 1;
+        }
+    }
+    PROF_MARK(3);
+    uint32_t cnt = 0;
+    for (uint32_t q = entry; q < (uint32_t)L && q != y; q = next_token(in, L, q)) cnt++;
+    const int32_t incl = wave_incl_sum((int32_t)cnt);
+    uint32_t base = (uint32_t)incl - cnt;
+    for (uint32_t q = entry; q < (uint32_t)L && q != y; q = next_token(in, L, q)) seqpos[base++] = (uint16_t)q;
+    const uint32_t total = rdlane((uint32_t)incl, kWave - 1);
+    __syncthreads();
+    PROF_MARK(5);
+    PROF_ADD(11, total);
+    return total;
+}
+
+__device__ __forceinline__ uint32_t mod_small(uint32_t i, uint32_t m) {
+    // i % m for i < 2^20, m >= 1 without an integer divide
+    uint32_t q = (uint32_t)((float)i * __frcp_rn((float)m));
+    int32_t r = (int32_t)i - (int32_t)(q * m);
+    if (r < 0) r += (int32_t)m;
+    if (r >= (int32_t)m) r -= (int32_t)m;
+    return (uint32_t)r;
+}
+
+// 4 bytes at any LDS byte address from two aligned dword reads
+__device__ __forceinline__ uint32_t lds_ld32(const uint8_t *p) {
+    uintptr_t a = (uintptr_t)p;
+    const uint32_t *w = (const uint32_t *)(a & ~(uintptr_t)3);
+    return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(a & 3));
+}
+
+// Decodes one page held in LDS.  in: stream of L bytes (kPad zero bytes after),
+// out: C-byte LDS window.  slots: 4 x 8 bytes of scratch.  Returns
+// LZ4_decompress_safe's value.
+__device__ int32_t decode_page(const uint8_t *in, int32_t L, uint8_t *out, int32_t C, uint16_t *seqpos,
+                               uint2 *slots, uint32_t lane) {
+    if (C == 0) return (L == 1 && in[0] == 0) ? 0 : -1;
+    if (L <= 0) return -1;
+    const uint32_t nseq = parse_chain(in, L, out, seqpos, lane);
+    PROF_DECL
+    const uint32_t grp = lane >> 4, gl = lane & 15;
+    const uint64_t lt_mask = (1ull << lane) - 1ull;
+    int32_t op_base = 0;
+    for (uint32_t b0 = 0; b0 < nseq; b0 += kWave) {
+        const uint32_t j = b0 + lane;
+        const bool active = j < nseq;
+        PROF_ADD(10, 1);
+        // ---- decode this lane's sequence (input side)
+        int32_t lit = 0, ls = 0, off = 0, ml = 0, q2 = 0;
+        bool in_term = false, ml_err = false;
+        if (active) {
+            int32_t p = seqpos[j];
+            uint32_t t = in[p];
+            int32_t q = p + 1;
+            lit = (int32_t)(t >> 4);
+            if (lit == kRunMask) {
+                uint32_t s;
+                do {
+                    s = in[q];
+                    q++;
+                    lit += (int32_t)s;
+                } while (q < L - kRunMask && s == 255);
+            }
+            ls = q;
+            in_term = q + lit > L - 8;
+            if (!in_term) {
+                off = (int32_t)(lds_ld32(in + q + lit) & 0xFFFFu);
+                q2 = q + lit + 2;
+                ml = (int32_t)(t & 15);
+                if (ml == 15) {
+                    uint32_t s;
+                    do {
+                        s = in[q2];
+                        q2++;
+                        if (q2 > L - kLastLiterals) { ml_err = true; break; }
+                        ml += (int32_t)s;
+                    } while (s == 255);
+                }
+                ml += kMinMatch;
+            }
+        }
+        // ---- output positions
+        const int32_t olen = active ? (in_term ? lit : lit + ml) : 0;
+        const int32_t incl = wave_incl_sum(olen);
+        const int32_t o = op_base + incl - olen;   // output position of this sequence
+        const int32_t d = o + lit;                 // match destination
+        // ---- acceptance checks in the reference's order (lz4.c:1147-1168, 1176, 1225)
+        // status: 0 ok, 1 terminal success, 2 error (rv carried)
+        int32_t status = 0, rv = 0;
+        if (active) {
+            if (o + lit > C - kMfLimit || in_term) {
+                if (ls + lit != L || o + lit > C) { status = 2; rv = -ls - 1; }
+                else { status = 1; rv = o + lit; }
+            } else if (off > d) {
+                status = 2; rv = -(ls + lit + 2) - 1;
+            } else if (ml_err) {
+                status = 2; rv = -q2 - 1;
+            } else if (d + ml > C - kLastLiterals) {
+                status = 2; rv = -q2 - 1;
+            }
+        }
+        const uint64_t stop = __ballot(status != 0);
+        const uint32_t n_ok = stop ? (uint32_t)__builtin_ctzll(stop) : kWave;   // sequences fully applied
+        int32_t final_rv = 0;
+        const bool finished = stop != 0;
+        if (finished) {
+            final_rv = (int32_t)rdlane((uint32_t)rv, n_ok);
+            if (final_rv < 0) return final_rv;                 // output is discarded on error
+        }
+        const bool term_lane = finished && lane == n_ok;       // terminal literal run
+        PROF_MARK(6);
+        // ---- literals: short ones per lane (4 bytes per step), long ones by the whole wave
+        const bool do_lit = (lane < n_ok && active) || term_lane;
+        const bool short_lit = do_lit && lit <= 32 && !(TYCHE_ABLATE & 1);
+        if (short_lit) {
+            for (int32_t i = 0; i < lit; i += 4) {
+                const uint32_t w = lds_ld32(in + ls + i);
+                const int32_t nb = min(lit - i, 4);
+                out[o + i] = (uint8_t)w;
+                if (nb > 1) out[o + i + 1] = (uint8_t)(w >> 8);
+                if (nb > 2) out[o + i + 2] = (uint8_t)(w >> 16);
+                if (nb > 3) out[o + i + 3] = (uint8_t)(w >> 24);
+            }
+        }
+        uint64_t longl = __ballot(do_lit && !short_lit && !(TYCHE_ABLATE & 1));
+        while (longl) {
+            const uint32_t k = (uint32_t)__builtin_ctzll(longl);
+            longl &= longl - 1;
+            const int32_t kl = (int32_t)rdlane((uint32_t)lit, k), ko = (int32_t)rdlane((uint32_t)o, k);
+            const int32_t ks = (int32_t)rdlane((uint32_t)ls, k);
+            for (int32_t i = (int32_t)lane; i < kl; i += kWave) out[ko + i] = in[ks + i];
+        }
+        PROF_MARK(7);
+        // ---- matches: frontier groups.  The first pending match's destination F
+        // bounds every byte that is already final; all pending matches whose source
+        // ends at or before F are independent of each other.
+        const int32_t src = d - off;
+        const int32_t src_end = src + min(ml, off);
+        const bool applied = lane < n_ok && active;
+        uint64_t pending = (TYCHE_ABLATE & 2) ? 0ull : __ballot(applied);
+        const uint64_t shortm = __ballot(applied && ml <= 64);
+        while (pending) {
+            const uint32_t f = (uint32_t)__builtin_ctzll(pending);
+            const int32_t F = (int32_t)rdlane((uint32_t)d, f);
+            PROF_ADD(9, 1);
+            if (!((shortm >> f) & 1ull)) {
+                // a long match (> 64 bytes) is copied by the whole wave, on its own
+                const int32_t mlf = (int32_t)rdlane((uint32_t)ml, f);
+                const int32_t fo = (int32_t)rdlane((uint32_t)off, f);
+                const int32_t fs = F - fo;
+                if (fo >= (int32_t)kWave) {
+                    for (int32_t i = (int32_t)lane; i < mlf; i += kWave) out[F + i] = out[fs + i];
+                } else {
+                    for (int32_t i = (int32_t)lane; i < mlf; i += kWave)
+                        out[F + i] = out[fs + (int32_t)mod_small((uint32_t)i, (uint32_t)fo)];
+                }
+                pending &= ~(1ull << f);
+                continue;
+            }
+            // up to four ready short matches, in stream order, go to the four 16-lane groups
+            const uint64_t ready = pending & shortm & __ballot(src_end <= F);
+            const uint32_t rank = (uint32_t)__popcll(ready & lt_mask);
+            const bool take = ((ready >> lane) & 1ull) && rank < 4;
+            if (take) slots[rank] = make_uint2((uint32_t)d | ((uint32_t)off << 16), (uint32_t)ml);
+            pending &= ~__ballot(take);
+            __builtin_amdgcn_wave_barrier();
+            const uint32_t ntake = (uint32_t)__popcll(ready) < 4 ? (uint32_t)__popcll(ready) : 4u;
+            if (grp < ntake) {
+                const uint2 m = slots[grp];
+                const int32_t md = (int32_t)(m.x & 0xFFFFu), mo = (int32_t)(m.x >> 16), mm = (int32_t)m.y;
+                const int32_t ms = md - mo;
+                for (int32_t i = (int32_t)gl; i < mm; i += 16) {
+                    const int32_t si = (mo >= 16 || mo >= mm) ? i : (int32_t)mod_small((uint32_t)i, (uint32_t)mo);
+                    out[md + i] = out[ms + si];
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+        PROF_MARK(8);
+        if (finished) return final_rv;
+        op_base += (int32_t)rdlane((uint32_t)incl, kWave - 1);
+    }
+    return -1;   // unreachable: the chain always ends in a terminal or failing sequence
+}
 
 struct Window {
     uint32_t base;   // stream position of lane 0
@@ -39,9 +352,11 @@ __device__ __forceinline__ uint32_t window_byte(const Window &w, const uint8_t *
     return rfl(in[pos]);
 }
 
-// Decodes one page held in LDS.  in: stream (len L, kPad zero bytes after),
-// out: LDS window of C bytes.  Returns LZ4_decompress_safe's value.
-__device__ int32_t decode_page(const uint8_t *in, int32_t L, uint8_t *out, int32_t C, uint32_t lane) {
+// Sequential decoder for pages too large for the parallel kernel's LDS layout
+// (no parse scratch): one sequence at a time, wave-uniform parse from a 64-byte
+// window, 64-byte copies.  in: stream (len L, kPad zero bytes after), out: LDS
+// window of C bytes.  Returns LZ4_decompress_safe's value.
+__device__ int32_t decode_page_serial(const uint8_t *in, int32_t L, uint8_t *out, int32_t C, uint32_t lane) {
     if (C == 0) return (L == 1 && rfl(in[0]) == 0) ? 0 : -1;
     if (L <= 0) return -1;
     int32_t ip = 0, op = 0;
@@ -104,7 +419,8 @@ __device__ int32_t decode_page(const uint8_t *in, int32_t L, uint8_t *out, int32
     }
 }
 
-__global__ __launch_bounds__(64) void lz4_decode_wave_kernel(tyche_batch_t b, uint32_t in_cap, uint32_t out_cap) {
+
+__global__ __launch_bounds__(64) void lz4_decode_serial_kernel(tyche_batch_t b, uint32_t in_cap, uint32_t out_cap) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t lane = threadIdx.x;
     const size_t page = blockIdx.x;
@@ -113,32 +429,144 @@ __global__ __launch_bounds__(64) void lz4_decode_wave_kernel(tyche_batch_t b, ui
         if (lane == 0) b.results[page] = kResultTooLarge;
         return;
     }
-    uint8_t *out = smem;                                        // out_cap bytes (rounded to 16)
-    uint8_t *stage = smem + ((out_cap + 15u) & ~15u);           // in_cap + 16 + kPad bytes
+    uint8_t *out = smem;
+    uint8_t *stage = smem + ((out_cap + 15u) & ~15u);
     uint32_t head = stage_in(p.src, p.src_len, stage, lane, kWave);
     uint8_t *in = stage + head;
-    in[p.src_len + lane] = 0;                                   // kPad zero bytes past the end
     __syncthreads();
-    int32_t rv = decode_page(in, (int32_t)p.src_len, out, (int32_t)p.dst_cap, lane);
+    in[p.src_len + lane] = 0;
+    __syncthreads();
+    int32_t rv = decode_page_serial(in, (int32_t)p.src_len, out, (int32_t)p.dst_cap, lane);
     __syncthreads();
     if (rv > 0) stage_out(p.dst, out, (uint32_t)rv, lane, kWave);
     if (lane == 0) b.results[page] = rv;
+}
+
+constexpr uint32_t kPrefetchVec = 8;   // 16-byte vectors per lane prefetched for the next page (8 KiB)
+
+// One wave per page, looping over pages; the next page's stream is prefetched
+// into registers while the current one is decoded.
+__global__ __launch_bounds__(64) void lz4_decode_wave_kernel(tyche_batch_t b, uint32_t in_cap, uint32_t out_cap,
+                                                             uint32_t off_in, uint32_t off_seq, uint32_t off_slots) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint32_t lane = threadIdx.x;
+    uint8_t *out = smem;
+    uint8_t *stage = smem + off_in;
+    uint16_t *seqpos = (uint16_t *)(smem + off_seq);
+    uint2 *slots = (uint2 *)(smem + off_slots);
+    const size_t stride = gridDim.x;
+
+    size_t page = blockIdx.x;
+    if (page >= b.count) return;
+    PageRef p = batch_page(b, page);
+    uint32_t head = stage_in(p.src, p.src_len <= in_cap ? p.src_len : 0, stage, lane, kWave);
+    for (;;) {
+        PROF_DECL
+        const size_t next = page + stride;
+        // ---- prefetch the next page's stream (first 8 KiB) into registers
+        PageRef pn;
+        u32x4 pf[kPrefetchVec];
+        uint32_t nhead = 0, nvec = 0;
+        if (next < b.count) {
+            pn = batch_page(b, next);
+            if (pn.src_len <= in_cap && pn.src_len > 0) {
+                uintptr_t a = (uintptr_t)pn.src;
+                nhead = (uint32_t)(a & 15u);
+                nvec = (nhead + pn.src_len + 15u) >> 4;
+                const u32x4 *g = (const u32x4 *)(a - nhead);
+#pragma unroll
+                for (uint32_t k = 0; k < kPrefetchVec; k++) {
+                    const uint32_t v = lane + k * kWave;
+                    if (v < nvec) pf[k] = __builtin_nontemporal_load(g + v);
+                }
+            }
+        }
+        // ---- current page
+        int32_t rv;
+        if (p.src_len > in_cap || p.dst_cap > out_cap) {
+            rv = kResultTooLarge;
+        } else {
+            uint8_t *in = stage + head;
+            __syncthreads();
+            in[p.src_len + lane] = 0;                           // kPad zero bytes past the end
+            __syncthreads();
+            PROF_MARK(1);
+            PROF_ADD(0, 1);
+            rv = decode_page(in, (int32_t)p.src_len, out, (int32_t)p.dst_cap, seqpos, slots, lane);
+            __syncthreads();
+            PROF_MARK(13);
+            if (rv > 0 && !(TYCHE_ABLATE & 4)) stage_out(p.dst, out, (uint32_t)rv, lane, kWave);
+        }
+        if (lane == 0) b.results[page] = rv;
+        if (next >= b.count) break;
+        // ---- install the prefetched stream (and load any remainder past 8 KiB)
+        __syncthreads();
+        page = next;
+        p = pn;
+        head = nhead;
+        if (p.src_len <= in_cap && p.src_len > 0) {
+            u32x4 *l = (u32x4 *)stage;
+#pragma unroll
+            for (uint32_t k = 0; k < kPrefetchVec; k++) {
+                const uint32_t v = lane + k * kWave;
+                if (v < nvec) l[v] = pf[k];
+            }
+            const u32x4 *g = (const u32x4 *)((uintptr_t)p.src - nhead);
+            for (uint32_t v = lane + kPrefetchVec * kWave; v < nvec; v += kWave) l[v] = __builtin_nontemporal_load(g + v);
+        }
+        PROF_MARK(12);
+    }
 }
 
 }  // namespace
 
 hipError_t launch_lz4_decode(const tyche_batch_t &b, uint32_t in_cap, uint32_t out_cap, hipStream_t s) {
     if (b.count == 0) return hipSuccess;
-    size_t lds = ((out_cap + 15u) & ~15u) + ((in_cap + 16u + kPad + 15u) & ~15u);
-    if (lds > 160 * 1024) return hipErrorInvalidValue;
-    static bool attr_set = false;
-    if (!attr_set) {
-        (void)hipFuncSetAttribute((const void *)lz4_decode_wave_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            160 * 1024);
-        attr_set = true;
+    // page window (also the parse's owner stamps, so at least in_cap bytes), stream, token list, slots
+    const uint32_t off_in = (std::max(out_cap, in_cap + 4u) + 15u) & ~15u;
+    const uint32_t off_seq = off_in + ((in_cap + 16u + kPad + 15u) & ~15u);
+    const uint32_t max_seq = in_cap / 3u + 2u;
+    const uint32_t off_slots = off_seq + ((max_seq * 2u + 15u) & ~15u);
+    const size_t lds = off_slots + 64;
+    if (lds > 160 * 1024) {
+        // large pages: sequential decoder, LDS = page window + stream only
+        const size_t lds2 = ((out_cap + 15u) & ~15u) + ((in_cap + 16u + kPad + 15u) & ~15u);
+        if (lds2 > 160 * 1024) return hipErrorInvalidValue;
+        static bool attr2 = false;
+        if (!attr2) {
+            (void)hipFuncSetAttribute((const void *)lz4_decode_serial_kernel,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            attr2 = true;
+        }
+        hipLaunchKernelGGL(lz4_decode_serial_kernel, dim3((unsigned)b.count), dim3(kWave), lds2, s, b, in_cap,
+                           out_cap);
+        return hipGetLastError();
     }
-    hipLaunchKernelGGL(lz4_decode_wave_kernel, dim3((unsigned)b.count), dim3(kWave), lds, s, b, in_cap, out_cap);
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    static int cus[64] = {0};
+    if (dev < 64 && cus[dev] == 0) {
+        (void)hipFuncSetAttribute((const void *)lz4_decode_wave_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
+        int n = 0;
+        (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+        cus[dev] = n > 0 ? n : 256;
+    }
+    const size_t per_cu = std::max<size_t>(1, std::min<size_t>(32, (160 * 1024) / lds));
+    const size_t grid = std::min<size_t>(b.count, (size_t)(dev < 64 ? cus[dev] : 256) * per_cu);
+    hipLaunchKernelGGL(lz4_decode_wave_kernel, dim3((unsigned)grid), dim3(kWave), lds, s, b, in_cap, out_cap, off_in,
+                       off_seq, off_slots);
     return hipGetLastError();
 }
+
+#ifdef TYCHE_PROFILE
+extern "C" int tyche_debug_decode_profile(unsigned long long *host16, int reset) {
+    if (reset) {
+        unsigned long long z[16] = {0};
+        return hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof(z)) == hipSuccess ? 0 : 1;
+    }
+    return hipMemcpyFromSymbol(host16, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * 16) == hipSuccess ? 0 : 1;
+}
+#endif
 
 }  // namespace tyche
