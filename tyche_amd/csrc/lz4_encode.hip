@@ -4,20 +4,30 @@
 // (reference src/buffer.c:178-188 -> src/lz4/lz4.c:697 -> LZ4_compress_generic
 // lz4.c:459-656) with one kernel over a batch of pages.  The output is a
 // standard LZ4 block that LZ4_decompress_safe (lz4.c:1251) -- the reference's
-// own decoder -- restores bit-exactly; it is not required to be the same bytes
-// 1.7.5 emits.  The parsing rules the decoder enforces are
-// kept: every match starts at or before iend-MFLIMIT (12) and ends at or before
-// iend-LASTLITERALS (5), lz4.c:266-267, 1147-1156, 1225.
+// own decoder -- restores bit-exactly; it is not required to be the bytes 1.7.5
+// emits.  The decoder's parsing rules are kept: every match
+// starts at or before iend-MFLIMIT (12) and ends at or before iend-LASTLITERALS
+// (5) (lz4.c:266-267, 1147-1156, 1225); output never exceeds the caller's
+// capacity (limitedOutput semantics: 0 when it would not fit).
 //
-// Layout: one 64-lane wave per page.  The page is staged into LDS; a position
-// table of 2^kHashLog 16-bit offsets (the byU16 scheme of lz4.c:402-408) lives
-// next to it.  Match finding is lane-parallel: for a 64-position block every
-// lane hashes its 4 bytes, reads the candidate left by earlier blocks, checks
-// it and measures the match length.  The greedy parse then walks the block
-// with ballots (first position >= cursor that has a match), and each chosen
-// sequence is emitted as one coalesced byte store per lane (token, length
-// bytes, literals, offset).
+// One 64-lane wave per page, looping over pages with the next page prefetched
+// into registers.  The page is staged in LDS next to a table of 2^12 16-bit
+// positions (the byU16 scheme of lz4.c:402-408, hash 2654435761 of 4 bytes).
+// The page is scanned in blocks of 64 positions:
+//   * every lane hashes its position, takes the candidate left by earlier
+//     blocks, verifies 4 bytes, probes the match length up to 20 bytes and the
+//     backward extension up to 4 bytes (lz4.c:549's catch-up);
+//   * the greedy parse over the block runs on scalar registers only: first
+//     match at or after the cursor (ballot mask), cursor = its end; a match
+//     that reached the probe limit is extended by the whole wave (256 bytes per
+//     step);
+//   * the block's sequences are encoded together: each selected lane computes
+//     its literal run (from the previous selected match's end), catch-up, token
+//     and length bytes; a wave prefix sum places them, and output bytes are
+//     written 64 per store instruction, contiguous.
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 
 #include "engine.h"
 #include "lds_io.h"
@@ -30,160 +40,246 @@ constexpr uint32_t kWave = 64;
 constexpr uint32_t kHashLog = 12;
 constexpr uint32_t kHashSize = 1u << kHashLog;
 constexpr uint32_t kPad = 64;
-constexpr uint32_t kLaneExtendCap = 128;   // per-lane length probe; the chosen match extends further
+constexpr uint32_t kProbe = 16;          // bytes probed per lane beyond MINMATCH
+constexpr uint32_t kPrefetchVec = 16;    // 16-byte vectors per lane prefetched for the next page (16 KiB)
 
-// 4 bytes at an arbitrary LDS byte offset (little endian), from two aligned dwords
-__device__ __forceinline__ uint32_t ld32(const uint8_t *base, uint32_t off) {
-    const uint32_t *w = (const uint32_t *)base;
-    uint32_t lo = w[off >> 2], hi = w[(off >> 2) + 1];
-    return __builtin_amdgcn_alignbyte(hi, lo, off & 3u);
+__device__ __forceinline__ uint32_t lds_ld32(const uint8_t *p) {
+    uintptr_t a = (uintptr_t)p;
+    const uint32_t *w = (const uint32_t *)(a & ~(uintptr_t)3);
+    return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(a & 3));
 }
 
 __device__ __forceinline__ uint32_t hash4(uint32_t v) { return (v * 2654435761u) >> (32 - kHashLog); }
 
-// number of equal bytes at a and b, a advancing up to (exclusive) limit;
-// positions are offsets from the 16-byte-aligned staging base
-__device__ __forceinline__ uint32_t match_extend(const uint8_t *in, uint32_t a, uint32_t b, uint32_t limit) {
-    uint32_t n = 0;
-    while (a + n + 4 <= limit) {
-        uint32_t x = ld32(in, a + n) ^ ld32(in, b + n);
-        if (x) return n + (__builtin_ctz(x) >> 3);
-        n += 4;
-    }
-    while (a + n < limit && in[a + n] == in[b + n]) n++;
-    return n;
+__device__ __forceinline__ int32_t wave_incl_sum(int32_t v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, true);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, true);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, true);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, true);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);
+    return v;
 }
 
-// wave-cooperative extension from a (match) / b (candidate), 256 bytes per step
+// equal bytes at a and b going forward, a stopping before `limit` (whole wave, 256 bytes per step)
 __device__ uint32_t wave_extend(const uint8_t *in, uint32_t a, uint32_t b, uint32_t limit, uint32_t lane) {
     uint32_t n = 0;
     for (;;) {
-        uint32_t pa = a + n + 4 * lane;
-        bool full = pa + 4 <= limit;
-        uint32_t x = full ? (ld32(in, pa) ^ ld32(in, b + n + 4 * lane)) : 1u;
-        uint64_t bad = __ballot(x != 0);
-        if (bad == 0) { n += 4 * kWave; continue; }
-        uint32_t first = (uint32_t)__builtin_ctzll(bad);
-        uint32_t xf = rdlane(x, first);
-        uint32_t pf = a + n + 4 * first;
-        if (pf + 4 <= limit) return n + 4 * first + (__builtin_ctz(xf) >> 3);
-        // tail shorter than 4 bytes
-        uint32_t m = n + 4 * first;
-        while (a + m < limit && rfl(in[a + m]) == rfl(in[b + m])) m++;
-        return m;
+        const uint32_t pa = a + n + 4 * lane;
+        const bool full = pa + 4 <= limit;
+        const uint32_t x = full ? (lds_ld32(in + pa) ^ lds_ld32(in + b + n + 4 * lane)) : 1u;
+        const uint64_t bad = __ballot(x != 0);
+        if (bad == 0) {
+            n += 4 * kWave;
+            continue;
+        }
+        const uint32_t first = (uint32_t)__builtin_ctzll(bad);
+        const uint32_t pf = a + n + 4 * first;
+        if (pf + 4 <= limit) return n + 4 * first + (__builtin_ctz(rdlane(x, first)) >> 3);
+        uint32_t m = n + 4 * first;   // fewer than 4 bytes left before the limit
+        while (a + m < limit && in[a + m] == in[b + m]) m++;
+        return rfl(m);
     }
 }
 
-struct Emitter {
-    uint8_t *dst;
-    uint32_t cap;
-    uint32_t op;
-    bool overflow;
+// byte `rel` of a sequence's encoding: token, literal-length bytes, literals, offset, match-length bytes
+struct SeqFields {
+    uint32_t lit, lext, anchor, off, mc, token, total;
 };
 
-// Emits one sequence (literals in[anchor, anchor+lit), then, if has_match, a
-// match of length ml at distance off) with one byte store per lane per 64 bytes.
-__device__ void emit_sequence(Emitter &e, const uint8_t *in, uint32_t anchor, uint32_t lit, bool has_match,
-                              uint32_t off, uint32_t ml, uint32_t lane) {
-    uint32_t lit_ext = lit >= 15 ? (lit - 15) / 255 + 1 : 0;
-    uint32_t mc = has_match ? ml - kMinMatch : 0;
-    uint32_t ml_ext = (has_match && mc >= 15) ? (mc - 15) / 255 + 1 : 0;
-    uint32_t total = 1 + lit_ext + lit + (has_match ? 2 : 0) + ml_ext;
-    if (e.overflow || e.op + total > e.cap) {
-        e.overflow = true;
-        return;
-    }
-    uint32_t token = ((lit >= 15 ? 15u : lit) << 4) | (has_match ? (mc >= 15 ? 15u : mc) : 0u);
-    const uint32_t lit_begin = 1 + lit_ext, off_begin = lit_begin + lit, ml_begin = off_begin + 2;
-    for (uint32_t j = lane; j < total; j += kWave) {
-        uint32_t v;
-        if (j == 0) v = token;
-        else if (j < lit_begin) v = (j == lit_begin - 1) ? (lit - 15) % 255 : 255;
-        else if (j < off_begin) v = in[anchor + (j - lit_begin)];
-        else if (j == off_begin) v = off & 0xFF;
-        else if (j == off_begin + 1) v = off >> 8;
-        else v = (j == total - 1) ? (mc - 15) % 255 : 255;
-        e.dst[e.op + j] = (uint8_t)v;
-    }
-    e.op += total;
+__device__ __forceinline__ uint32_t seq_byte(const SeqFields &f, const uint8_t *in, uint32_t rel) {
+    if (rel == 0) return f.token;
+    if (rel <= f.lext) return rel == f.lext ? (f.lit - 15u) % 255u : 255u;
+    const uint32_t lb = 1 + f.lext;
+    if (rel < lb + f.lit) return in[f.anchor + rel - lb];
+    const uint32_t ob = lb + f.lit;
+    if (rel == ob) return f.off & 0xFFu;
+    if (rel == ob + 1) return f.off >> 8;
+    return rel == f.total - 1 ? (f.mc - 15u) % 255u : 255u;
 }
 
-__global__ __launch_bounds__(64) void lz4_encode_wave_kernel(tyche_batch_t b, uint32_t in_cap) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const uint32_t lane = threadIdx.x;
-    const size_t page = blockIdx.x;
-    PageRef p = batch_page(b, page);
-    if (p.src_len > in_cap) {
-        if (lane == 0) b.results[page] = kResultTooLarge;
-        return;
-    }
-    uint16_t *table = (uint16_t *)smem;                              // kHashSize entries
-    uint8_t *stage = smem + kHashSize * sizeof(uint16_t);
-    // stage the page so that it starts 16-byte aligned: copy at head then the
-    // matcher addresses it through `in`
-    uint32_t head = stage_in(p.src, p.src_len, stage, lane, kWave);
-    uint8_t *in = stage + head;
-    const uint32_t L = p.src_len;
-    for (uint32_t h = lane; h < kHashSize / 2; h += kWave) ((uint32_t *)table)[h] = 0;
-    __syncthreads();
-    in[L + lane] = 0;
-    __syncthreads();
-
-    Emitter e{p.dst, p.dst_cap, 0, false};
-    uint32_t anchor = 0;
+// Encodes one page held in LDS into dst (global, capacity cap).  Returns the
+// compressed size, or 0 if it does not fit in cap.
+__device__ int32_t encode_page(const uint8_t *in, uint32_t L, uint16_t *table, uint8_t *dst, uint32_t cap,
+                               uint32_t lane) {
+    uint32_t op = 0, anchor = 0;
     if (L >= (uint32_t)(kMfLimit + 1)) {
         const uint32_t mflimit = L - kMfLimit;          // last position a match may start
-        const uint32_t matchlimit = L - kLastLiterals;  // matches end before this
-        uint32_t cursor = 0;
-        while (cursor <= mflimit && !e.overflow) {
-            const uint32_t blk = cursor & ~(kWave - 1);
+        const uint32_t matchlimit = L - kLastLiterals;  // matches end at or before this
+        uint32_t cursor = 0;     // matches may start here (end of the last match)
+        uint32_t blk = 0;        // current 64-position block
+        bool done = false;
+        for (; !done && blk <= mflimit; blk = max(blk + kWave, cursor & ~(kWave - 1))) {
             const uint32_t pos = blk + lane;
-            // ---- lane-parallel match finding for positions blk .. blk+63
-            uint32_t cand = 0, len = 0;
-            bool live = pos <= mflimit;
-            uint32_t v = 0, h = 0;
-            if (live) {
-                v = ld32(stage, head + pos);
-                h = hash4(v);
-                cand = table[h];
-            }
+            const bool live = pos <= mflimit;
+            // ---- candidates from earlier blocks, then insert this block's positions
+            const uint32_t v = lds_ld32(in + pos);
+            const uint32_t h = hash4(v);
+            const uint32_t cand = live ? table[h] : 0u;
             __builtin_amdgcn_wave_barrier();
             if (live) table[h] = (uint16_t)pos;
-            if (live && cand < pos && ld32(stage, head + cand) == v) {
-                uint32_t lim = min(matchlimit, pos + kLaneExtendCap);
-                len = kMinMatch + match_extend(stage, head + pos + kMinMatch, head + cand + kMinMatch, head + lim);
+            const bool ok = live && cand < pos && lds_ld32(in + cand) == v;
+            // ---- forward probe (MINMATCH + up to kProbe bytes) and backward probe (up to 4 bytes)
+            uint32_t len = 0, back = 0;
+            bool capped = false;
+            if (ok) {
+                const uint32_t e = min(matchlimit, pos + kMinMatch + kProbe);
+                uint32_t n = kMinMatch;
+                for (;;) {
+                    if (pos + n + 4 > e) {
+                        while (pos + n < e && in[pos + n] == in[cand + n]) n++;
+                        break;
+                    }
+                    const uint32_t x = lds_ld32(in + pos + n) ^ lds_ld32(in + cand + n);
+                    if (x) { n += __builtin_ctz(x) >> 3; break; }
+                    n += 4;
+                }
+                len = n;
+                capped = pos + n == e && e < matchlimit;
+                if (pos >= 4 && cand >= 4) {
+                    const uint32_t x = lds_ld32(in + pos - 4) ^ lds_ld32(in + cand - 4);
+                    back = x ? (__builtin_clz(x) >> 3) : 4u;
+                }
             }
-            // ---- greedy parse over this block
-            for (;;) {
-                uint64_t m = __ballot(len != 0 && pos >= cursor);
-                if (m == 0) {
-                    cursor = blk + kWave;
-                    break;
+            // ---- greedy parse of this block on scalar registers
+            uint64_t m = __ballot(ok && pos >= cursor);
+            uint64_t sel = 0;
+            if (m == 0) continue;
+            while (m) {
+                const uint32_t li = (uint32_t)__builtin_ctzll(m);
+                uint32_t ln = rdlane(len, li);
+                if (rdlane((uint32_t)capped, li)) {
+                    const uint32_t mp = blk + li, mc = rdlane(cand, li);
+                    ln += wave_extend(in, mp + ln, mc + ln, matchlimit, lane);
+                    if (lane == li) len = ln;
                 }
-                uint32_t ln = (uint32_t)__builtin_ctzll(m);
-                uint32_t mpos = blk + ln;
-                uint32_t mcand = rdlane(cand, ln);
-                uint32_t mlen = rdlane(len, ln);
-                if (mlen >= kLaneExtendCap && mpos + mlen < matchlimit) {
-                    mlen = kMinMatch + wave_extend(stage, head + mpos + kMinMatch, head + mcand + kMinMatch,
-                                                   head + matchlimit, lane);
-                }
-                // catch up backwards over pending literals (lz4.c:549)
-                while (mpos > anchor && mcand > 0 && rfl(in[mpos - 1]) == rfl(in[mcand - 1])) {
-                    mpos--;
-                    mcand--;
-                    mlen++;
-                }
-                emit_sequence(e, in, anchor, mpos - anchor, true, mpos - mcand, mlen, lane);
-                anchor = mpos + mlen;
-                cursor = anchor;
-                if (cursor >= blk + kWave || cursor > mflimit || e.overflow) break;
+                sel |= 1ull << li;
+                cursor = blk + li + ln;
+                if (cursor > mflimit) { done = true; break; }
+                if (cursor >= blk + kWave) break;
+                m &= ~((1ull << (cursor - blk)) - 1ull);
             }
+            // ---- encode the selected sequences together
+            const bool is_sel = (sel >> lane) & 1ull;
+            const uint32_t mend = pos + len;
+            const uint64_t below = sel & ((1ull << lane) - 1ull);
+            const uint32_t prev_lane = below ? 63u - (uint32_t)__builtin_clzll(below) : 0u;
+            const uint32_t prev_end_x = __shfl(mend, prev_lane);
+            const uint32_t prev_end = below ? prev_end_x : anchor;
+            SeqFields f{};
+            uint32_t enc = 0;
+            if (is_sel) {
+                const uint32_t k = min(min(back, pos - prev_end), cand);   // catch-up
+                f.anchor = prev_end;
+                f.lit = pos - k - prev_end;
+                f.lext = f.lit >= 15 ? (f.lit - 15) / 255 + 1 : 0;
+                f.off = pos - cand;
+                f.mc = len + k - kMinMatch;
+                const uint32_t mext = f.mc >= 15 ? (f.mc - 15) / 255 + 1 : 0;
+                f.token = (min(f.lit, 15u) << 4) | min(f.mc, 15u);
+                f.total = 1 + f.lext + f.lit + 2 + mext;
+                enc = f.total;
+            }
+            const int32_t incl = wave_incl_sum((int32_t)enc);
+            const uint32_t eo = (uint32_t)incl - enc;
+            const uint32_t et = rdlane((uint32_t)incl, 63);
+            if (op + et > cap) return 0;
+            for (uint32_t j0 = 0; j0 < et; j0 += kWave) {
+                const uint32_t j = j0 + lane;
+                // owner: the last selected lane whose encoding starts at or before j
+                uint32_t owner = 0;
+                for (uint64_t r = sel; r; r &= r - 1) {
+                    const uint32_t s = (uint32_t)__builtin_ctzll(r);
+                    if (rdlane(eo, s) <= j) owner = s;
+                }
+                SeqFields g;
+                g.lit = __shfl(f.lit, owner);
+                g.lext = __shfl(f.lext, owner);
+                g.anchor = __shfl(f.anchor, owner);
+                g.off = __shfl(f.off, owner);
+                g.mc = __shfl(f.mc, owner);
+                g.token = __shfl(f.token, owner);
+                g.total = __shfl(f.total, owner);
+                const uint32_t ge = __shfl(eo, owner);
+                if (j < et) dst[op + j] = (uint8_t)seq_byte(g, in, j - ge);
+            }
+            op += et;
+            anchor = cursor;
         }
     }
-    // last literals
-    emit_sequence(e, in, anchor, L - anchor, false, 0, 0, lane);
-    if (lane == 0) b.results[page] = e.overflow ? 0 : (int32_t)e.op;
+    // ---- last literals: in[anchor, L)
+    const uint32_t lit = L - anchor;
+    const uint32_t lext = lit >= 15 ? (lit - 15) / 255 + 1 : 0;
+    const uint32_t total = 1 + lext + lit;
+    if (op + total > cap) return 0;
+    for (uint32_t j = lane; j < total; j += kWave) {
+        uint32_t v;
+        if (j == 0) v = min(lit, 15u) << 4;
+        else if (j <= lext) v = j == lext ? (lit - 15) % 255 : 255;
+        else v = in[anchor + j - 1 - lext];
+        dst[op + j] = (uint8_t)v;
+    }
+    return (int32_t)(op + total);
+}
+
+__global__ __launch_bounds__(64) void lz4_encode_kernel(tyche_batch_t b, uint32_t in_cap) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint32_t lane = threadIdx.x;
+    uint16_t *table = (uint16_t *)smem;
+    uint8_t *stage = smem + kHashSize * sizeof(uint16_t);
+    const size_t stride = gridDim.x;
+
+    size_t page = blockIdx.x;
+    if (page >= b.count) return;
+    PageRef p = batch_page(b, page);
+    uint32_t head = stage_in(p.src, p.src_len <= in_cap ? p.src_len : 0, stage, lane, kWave);
+    for (;;) {
+        const size_t next = page + stride;
+        PageRef pn;
+        u32x4 pf[kPrefetchVec];
+        uint32_t nhead = 0, nvec = 0;
+        if (next < b.count) {
+            pn = batch_page(b, next);
+            if (pn.src_len <= in_cap && pn.src_len > 0) {
+                uintptr_t a = (uintptr_t)pn.src;
+                nhead = (uint32_t)(a & 15u);
+                nvec = (nhead + pn.src_len + 15u) >> 4;
+                const u32x4 *g = (const u32x4 *)(a - nhead);
+#pragma unroll
+                for (uint32_t k = 0; k < kPrefetchVec; k++) {
+                    const uint32_t v = lane + k * kWave;
+                    if (v < nvec) pf[k] = __builtin_nontemporal_load(g + v);
+                }
+            }
+        }
+        int32_t rv;
+        if (p.src_len > in_cap) {
+            rv = kResultTooLarge;
+        } else {
+            uint8_t *in = stage + head;
+            for (uint32_t w = lane; w < kHashSize / 8; w += kWave) ((u32x4 *)table)[w] = u32x4{0, 0, 0, 0};
+            __syncthreads();
+            in[p.src_len + lane] = 0;
+            __syncthreads();
+            rv = encode_page(in, p.src_len, table, p.dst, p.dst_cap, lane);
+        }
+        if (lane == 0) b.results[page] = rv;
+        if (next >= b.count) break;
+        __syncthreads();
+        page = next;
+        p = pn;
+        head = nhead;
+        if (p.src_len <= in_cap && p.src_len > 0) {
+            u32x4 *l = (u32x4 *)stage;
+#pragma unroll
+            for (uint32_t k = 0; k < kPrefetchVec; k++) {
+                const uint32_t v = lane + k * kWave;
+                if (v < nvec) l[v] = pf[k];
+            }
+            const u32x4 *g = (const u32x4 *)((uintptr_t)p.src - nhead);
+            for (uint32_t v = lane + kPrefetchVec * kWave; v < nvec; v += kWave) l[v] = __builtin_nontemporal_load(g + v);
+        }
+    }
 }
 
 }  // namespace
@@ -191,14 +287,20 @@ __global__ __launch_bounds__(64) void lz4_encode_wave_kernel(tyche_batch_t b, ui
 hipError_t launch_lz4_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream_t s) {
     if (b.count == 0) return hipSuccess;
     if (in_cap > 65535u) return hipErrorInvalidValue;    // 16-bit positions (byU16 regime)
-    size_t lds = kHashSize * sizeof(uint16_t) + ((in_cap + 16u + kPad + 15u) & ~15u);
-    static bool attr_set = false;
-    if (!attr_set) {
-        (void)hipFuncSetAttribute((const void *)lz4_encode_wave_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            160 * 1024);
-        attr_set = true;
+    const size_t lds = kHashSize * sizeof(uint16_t) + ((in_cap + 16u + kPad + 15u) & ~15u);
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    static int cus[64] = {0};
+    if (dev < 64 && cus[dev] == 0) {
+        (void)hipFuncSetAttribute((const void *)lz4_encode_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
+        int n = 0;
+        (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+        cus[dev] = n > 0 ? n : 256;
     }
-    hipLaunchKernelGGL(lz4_encode_wave_kernel, dim3((unsigned)b.count), dim3(kWave), lds, s, b, in_cap);
+    const size_t per_cu = std::max<size_t>(1, std::min<size_t>(32, (160 * 1024) / lds));
+    const size_t grid = std::min<size_t>(b.count, (size_t)(dev < 64 ? cus[dev] : 256) * per_cu);
+    hipLaunchKernelGGL(lz4_encode_kernel, dim3((unsigned)grid), dim3(kWave), lds, s, b, in_cap);
     return hipGetLastError();
 }
 
