@@ -385,7 +385,7 @@ int tyche_buffers_compress(Buffer **bufs, void **compressed, int *status, size_t
         size_t i = idx[k];
         if (rc != TYCHE_E_OK || res[k] < 1) {
             free(dst[k]);   // the reference leaks here (buffer.c:185-186)
-            status[i] = rc != TYCHE_E_OK ? TYCHE_E_BUFFER_COMPRESSION_PROBLEM : TYCHE_E_BUFFER_COMPRESSION_PROBLEM;
+            status[i] = rc != TYCHE_E_OK ? TYCHE_E_DEVICE : TYCHE_E_BUFFER_COMPRESSION_PROBLEM;
             continue;
         }
         compressed[i] = dst[k];
@@ -447,7 +447,7 @@ int tyche_buffers_decompress(Buffer **bufs, int *status, size_t n, int compresso
         size_t i = idx[k];
         if (rc != TYCHE_E_OK || res[k] < 0) {       // LZ4 accepts any rv >= 0 (buffer.c:251-253)
             free(dst[k]);                           // the reference leaks here
-            status[i] = TYCHE_E_BUFFER_COMPRESSION_PROBLEM;
+            status[i] = rc != TYCHE_E_OK ? TYCHE_E_DEVICE : TYCHE_E_BUFFER_COMPRESSION_PROBLEM;
             continue;
         }
         free(b->data);

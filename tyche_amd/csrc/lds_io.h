@@ -7,8 +7,39 @@ namespace tyche {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+// LDS accesses at any byte address: gfx950 runs in unaligned DS mode, so a
+// 32-bit access through an align(1) type is a single ds_read_b32 / ds_write_b32
+// (checked by tools/probes/lds_unaligned.hip).
+typedef uint32_t u32_ua __attribute__((aligned(1)));
+typedef uint16_t u16_ua __attribute__((aligned(1)));
+__device__ __forceinline__ uint32_t lds_ld32(const uint8_t *p) { return *(const u32_ua *)p; }
+__device__ __forceinline__ uint32_t lds_ld16(const uint8_t *p) { return *(const u16_ua *)p; }
+__device__ __forceinline__ void lds_st32(uint8_t *p, uint32_t v) { *(u32_ua *)p = v; }
+
 __device__ __forceinline__ uint32_t rfl(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 __device__ __forceinline__ uint32_t rdlane(uint32_t v, uint32_t lane) { return __builtin_amdgcn_readlane(v, lane); }
+
+// inclusive prefix sum over the 64 lanes with DPP row shifts + row broadcasts
+__device__ __forceinline__ int32_t wave_incl_sum(int32_t v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, true);   // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, true);   // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, true);   // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, true);   // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+    return v;
+}
+
+// inclusive max-scan over the 64 lanes (values >= -1; lanes shifted in from outside a row read -1)
+__device__ __forceinline__ int32_t wave_incl_max(int32_t v) {
+    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x111, 0xF, 0xF, false));
+    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x112, 0xF, 0xF, false));
+    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x114, 0xF, 0xF, false));
+    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x118, 0xF, 0xF, false));
+    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x142, 0xA, 0xF, false));
+    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x143, 0xC, 0xF, false));
+    return v;
+}
 
 // Copies n bytes of global memory (any alignment) into 16-byte-aligned LDS with
 // 16-byte loads (1 KiB per wave instruction).  Byte j of src lands at

@@ -99,17 +99,6 @@ __device__ __forceinline__ uint32_t next_token(const uint8_t *in, int32_t L, uin
     return (uint32_t)q;
 }
 
-// inclusive prefix sum over the 64 lanes with DPP row shifts + row broadcasts
-__device__ __forceinline__ int32_t wave_incl_sum(int32_t v) {
-    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, true);   // row_shr:1
-    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, true);   // row_shr:2
-    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, true);   // row_shr:4
-    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, true);   // row_shr:8
-    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
-    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
-    return v;
-}
-
 // Parallel token-chain parse.  Writes the ordered token positions to seqpos and
 // returns their number.  owner: L bytes of scratch (the page window, unused
 // until the copy phases).
@@ -180,13 +169,6 @@ __device__ __forceinline__ uint32_t mod_small(uint32_t i, uint32_t m) {
     return (uint32_t)r;
 }
 
-// 4 bytes at any LDS byte address from two aligned dword reads
-__device__ __forceinline__ uint32_t lds_ld32(const uint8_t *p) {
-    uintptr_t a = (uintptr_t)p;
-    const uint32_t *w = (const uint32_t *)(a & ~(uintptr_t)3);
-    return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(a & 3));
-}
-
 // Decodes one page held in LDS.  in: stream of L bytes (kPad zero bytes after),
 // out: C-byte LDS window.  slots: 4 x 8 bytes of scratch.  Returns
 // LZ4_decompress_safe's value.
@@ -222,7 +204,7 @@ __device__ int32_t decode_page(const uint8_t *in, int32_t L, uint8_t *out, int32
             ls = q;
             in_term = q + lit > L - 8;
             if (!in_term) {
-                off = (int32_t)(lds_ld32(in + q + lit) & 0xFFFFu);
+                off = (int32_t)lds_ld16(in + q + lit);
                 q2 = q + lit + 2;
                 ml = (int32_t)(t & 15);
                 if (ml == 15) {
@@ -271,14 +253,10 @@ __device__ int32_t decode_page(const uint8_t *in, int32_t L, uint8_t *out, int32
         const bool do_lit = (lane < n_ok && active) || term_lane;
         const bool short_lit = do_lit && lit <= 32 && !(TYCHE_ABLATE & 1);
         if (short_lit) {
-            for (int32_t i = 0; i < lit; i += 4) {
-                const uint32_t w = lds_ld32(in + ls + i);
-                const int32_t nb = min(lit - i, 4);
-                out[o + i] = (uint8_t)w;
-                if (nb > 1) out[o + i + 1] = (uint8_t)(w >> 8);
-                if (nb > 2) out[o + i + 2] = (uint8_t)(w >> 16);
-                if (nb > 3) out[o + i + 3] = (uint8_t)(w >> 24);
-            }
+            // whole unaligned dwords; the up-to-3-byte overrun lands in this
+            // sequence's own match area (rewritten by the match phase) or past the
+            // page end (slack in the window)
+            for (int32_t i = 0; i < lit; i += 4) lds_st32(out + o + i, lds_ld32(in + ls + i));
         }
         uint64_t longl = __ballot(do_lit && !short_lit && !(TYCHE_ABLATE & 1));
         while (longl) {
@@ -297,6 +275,7 @@ __device__ int32_t decode_page(const uint8_t *in, int32_t L, uint8_t *out, int32
         const bool applied = lane < n_ok && active;
         uint64_t pending = (TYCHE_ABLATE & 2) ? 0ull : __ballot(applied);
         const uint64_t shortm = __ballot(applied && ml <= 64);
+        const uint32_t dpk = (uint32_t)d | ((uint32_t)off << 16);
         while (pending) {
             const uint32_t f = (uint32_t)__builtin_ctzll(pending);
             const int32_t F = (int32_t)rdlane((uint32_t)d, f);
@@ -315,24 +294,28 @@ __device__ int32_t decode_page(const uint8_t *in, int32_t L, uint8_t *out, int32
                 pending &= ~(1ull << f);
                 continue;
             }
-            // up to four ready short matches, in stream order, go to the four 16-lane groups
-            const uint64_t ready = pending & shortm & __ballot(src_end <= F);
-            const uint32_t rank = (uint32_t)__popcll(ready & lt_mask);
-            const bool take = ((ready >> lane) & 1ull) && rank < 4;
-            if (take) slots[rank] = make_uint2((uint32_t)d | ((uint32_t)off << 16), (uint32_t)ml);
-            pending &= ~__ballot(take);
-            __builtin_amdgcn_wave_barrier();
-            const uint32_t ntake = (uint32_t)__popcll(ready) < 4 ? (uint32_t)__popcll(ready) : 4u;
-            if (grp < ntake) {
-                const uint2 m = slots[grp];
-                const int32_t md = (int32_t)(m.x & 0xFFFFu), mo = (int32_t)(m.x >> 16), mm = (int32_t)m.y;
+            // up to four ready short matches, in stream order, go to the four 16-lane
+            // groups; their fields are fetched with v_readlane (scalar picks, no LDS trip)
+            uint64_t ready = pending & shortm & __ballot(src_end <= F);
+            uint32_t gpk = 0, gml = 0;          // this group's packed (d | off << 16) and length
+#pragma unroll
+            for (uint32_t k = 0; k < 4; k++) {
+                if (ready) {
+                    const uint32_t r = (uint32_t)__builtin_ctzll(ready);
+                    ready &= ready - 1;
+                    pending &= ~(1ull << r);
+                    const uint32_t pk = rdlane(dpk, r), mlr = rdlane((uint32_t)ml, r);
+                    if (grp == k) { gpk = pk; gml = mlr; }
+                }
+            }
+            {
+                const int32_t md = (int32_t)(gpk & 0xFFFFu), mo = (int32_t)(gpk >> 16), mm = (int32_t)gml;
                 const int32_t ms = md - mo;
                 for (int32_t i = (int32_t)gl; i < mm; i += 16) {
                     const int32_t si = (mo >= 16 || mo >= mm) ? i : (int32_t)mod_small((uint32_t)i, (uint32_t)mo);
                     out[md + i] = out[ms + si];
                 }
             }
-            __builtin_amdgcn_wave_barrier();
         }
         PROF_MARK(8);
         if (finished) return final_rv;
@@ -523,7 +506,7 @@ __global__ __launch_bounds__(64) void lz4_decode_wave_kernel(tyche_batch_t b, ui
 hipError_t launch_lz4_decode(const tyche_batch_t &b, uint32_t in_cap, uint32_t out_cap, hipStream_t s) {
     if (b.count == 0) return hipSuccess;
     // page window (also the parse's owner stamps, so at least in_cap bytes), stream, token list, slots
-    const uint32_t off_in = (std::max(out_cap, in_cap + 4u) + 15u) & ~15u;
+    const uint32_t off_in = (std::max(out_cap, in_cap + 4u) + 16u + 15u) & ~15u;
     const uint32_t off_seq = off_in + ((in_cap + 16u + kPad + 15u) & ~15u);
     const uint32_t max_seq = in_cap / 3u + 2u;
     const uint32_t off_slots = off_seq + ((max_seq * 2u + 15u) & ~15u);

@@ -43,23 +43,7 @@ constexpr uint32_t kPad = 64;
 constexpr uint32_t kProbe = 16;          // bytes probed per lane beyond MINMATCH
 constexpr uint32_t kPrefetchVec = 16;    // 16-byte vectors per lane prefetched for the next page (16 KiB)
 
-__device__ __forceinline__ uint32_t lds_ld32(const uint8_t *p) {
-    uintptr_t a = (uintptr_t)p;
-    const uint32_t *w = (const uint32_t *)(a & ~(uintptr_t)3);
-    return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(a & 3));
-}
-
 __device__ __forceinline__ uint32_t hash4(uint32_t v) { return (v * 2654435761u) >> (32 - kHashLog); }
-
-__device__ __forceinline__ int32_t wave_incl_sum(int32_t v) {
-    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, true);
-    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, true);
-    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, true);
-    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, true);
-    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);
-    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);
-    return v;
-}
 
 // equal bytes at a and b going forward, a stopping before `limit` (whole wave, 256 bytes per step)
 __device__ uint32_t wave_extend(const uint8_t *in, uint32_t a, uint32_t b, uint32_t limit, uint32_t lane) {
@@ -100,8 +84,8 @@ __device__ __forceinline__ uint32_t seq_byte(const SeqFields &f, const uint8_t *
 
 // Encodes one page held in LDS into dst (global, capacity cap).  Returns the
 // compressed size, or 0 if it does not fit in cap.
-__device__ int32_t encode_page(const uint8_t *in, uint32_t L, uint16_t *table, uint8_t *dst, uint32_t cap,
-                               uint32_t lane) {
+__device__ int32_t encode_page(const uint8_t *in, uint32_t L, uint16_t *table, uint8_t *map, uint8_t *dst,
+                               uint32_t cap, uint32_t lane) {
     uint32_t op = 0, anchor = 0;
     if (L >= (uint32_t)(kMfLimit + 1)) {
         const uint32_t mflimit = L - kMfLimit;          // last position a match may start
@@ -123,17 +107,17 @@ __device__ int32_t encode_page(const uint8_t *in, uint32_t L, uint16_t *table, u
             uint32_t len = 0, back = 0;
             bool capped = false;
             if (ok) {
+                // four unaligned dword compares, no branches; clamp to the match limit
                 const uint32_t e = min(matchlimit, pos + kMinMatch + kProbe);
-                uint32_t n = kMinMatch;
-                for (;;) {
-                    if (pos + n + 4 > e) {
-                        while (pos + n < e && in[pos + n] == in[cand + n]) n++;
-                        break;
-                    }
-                    const uint32_t x = lds_ld32(in + pos + n) ^ lds_ld32(in + cand + n);
-                    if (x) { n += __builtin_ctz(x) >> 3; break; }
-                    n += 4;
-                }
+                const uint32_t x0 = lds_ld32(in + pos + 4) ^ lds_ld32(in + cand + 4);
+                const uint32_t x1 = lds_ld32(in + pos + 8) ^ lds_ld32(in + cand + 8);
+                const uint32_t x2 = lds_ld32(in + pos + 12) ^ lds_ld32(in + cand + 12);
+                const uint32_t x3 = lds_ld32(in + pos + 16) ^ lds_ld32(in + cand + 16);
+                uint32_t n = x0 ? 4 + (__builtin_ctz(x0) >> 3)
+                           : x1 ? 8 + (__builtin_ctz(x1) >> 3)
+                           : x2 ? 12 + (__builtin_ctz(x2) >> 3)
+                           : x3 ? 16 + (__builtin_ctz(x3) >> 3) : 20u;
+                n = min(n, e - pos);
                 len = n;
                 capped = pos + n == e && e < matchlimit;
                 if (pos >= 4 && cand >= 4) {
@@ -184,24 +168,33 @@ __device__ int32_t encode_page(const uint8_t *in, uint32_t L, uint16_t *table, u
             const uint32_t eo = (uint32_t)incl - enc;
             const uint32_t et = rdlane((uint32_t)incl, 63);
             if (op + et > cap) return 0;
+            // fields travel packed: 4 bpermutes per output chunk
+            const uint32_t pk0 = f.lit | (f.lext << 16), pk1 = f.anchor | (f.off << 16);
+            const uint32_t pk2 = f.mc | (f.total << 16), pk3 = eo | (f.token << 16);
             for (uint32_t j0 = 0; j0 < et; j0 += kWave) {
                 const uint32_t j = j0 + lane;
-                // owner: the last selected lane whose encoding starts at or before j
-                uint32_t owner = 0;
-                for (uint64_t r = sel; r; r &= r - 1) {
-                    const uint32_t s = (uint32_t)__builtin_ctzll(r);
-                    if (rdlane(eo, s) <= j) owner = s;
-                }
+                // owner of byte j: the last selected lane whose encoding starts at or before j.
+                // Starts inside this chunk are stamped into a 64-byte map and max-scanned.
+                const uint64_t before = __ballot(is_sel && eo <= j0);
+                const int32_t owner0 = before ? 63 - (int32_t)__builtin_clzll(before) : 0;
+                map[lane] = 0xFF;
+                __builtin_amdgcn_wave_barrier();
+                if (is_sel && eo > j0 && eo < j0 + kWave) map[eo - j0] = (uint8_t)lane;
+                __builtin_amdgcn_wave_barrier();
+                const uint32_t mv = map[lane];
+                const uint32_t owner = (uint32_t)max(wave_incl_max(mv == 0xFF ? -1 : (int32_t)mv), owner0);
+                const uint32_t g0 = __shfl(pk0, owner), g1 = __shfl(pk1, owner);
+                const uint32_t g2 = __shfl(pk2, owner), g3 = __shfl(pk3, owner);
                 SeqFields g;
-                g.lit = __shfl(f.lit, owner);
-                g.lext = __shfl(f.lext, owner);
-                g.anchor = __shfl(f.anchor, owner);
-                g.off = __shfl(f.off, owner);
-                g.mc = __shfl(f.mc, owner);
-                g.token = __shfl(f.token, owner);
-                g.total = __shfl(f.total, owner);
-                const uint32_t ge = __shfl(eo, owner);
-                if (j < et) dst[op + j] = (uint8_t)seq_byte(g, in, j - ge);
+                g.lit = g0 & 0xFFFFu;
+                g.lext = g0 >> 16;
+                g.anchor = g1 & 0xFFFFu;
+                g.off = g1 >> 16;
+                g.mc = g2 & 0xFFFFu;
+                g.total = g2 >> 16;
+                g.token = g3 >> 16;
+                if (j < et) dst[op + j] = (uint8_t)seq_byte(g, in, j - (g3 & 0xFFFFu));
+                __builtin_amdgcn_wave_barrier();
             }
             op += et;
             anchor = cursor;
@@ -226,7 +219,8 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel(tyche_batch_t b, uint32_
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t lane = threadIdx.x;
     uint16_t *table = (uint16_t *)smem;
-    uint8_t *stage = smem + kHashSize * sizeof(uint16_t);
+    uint8_t *map = smem + kHashSize * sizeof(uint16_t);                 // 64-byte owner map
+    uint8_t *stage = map + kWave;
     const size_t stride = gridDim.x;
 
     size_t page = blockIdx.x;
@@ -261,7 +255,7 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel(tyche_batch_t b, uint32_
             __syncthreads();
             in[p.src_len + lane] = 0;
             __syncthreads();
-            rv = encode_page(in, p.src_len, table, p.dst, p.dst_cap, lane);
+            rv = encode_page(in, p.src_len, table, map, p.dst, p.dst_cap, lane);
         }
         if (lane == 0) b.results[page] = rv;
         if (next >= b.count) break;
@@ -287,7 +281,7 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel(tyche_batch_t b, uint32_
 hipError_t launch_lz4_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream_t s) {
     if (b.count == 0) return hipSuccess;
     if (in_cap > 65535u) return hipErrorInvalidValue;    // 16-bit positions (byU16 regime)
-    const size_t lds = kHashSize * sizeof(uint16_t) + ((in_cap + 16u + kPad + 15u) & ~15u);
+    const size_t lds = kHashSize * sizeof(uint16_t) + kWave + ((in_cap + 16u + kPad + 15u) & ~15u);
     int dev = 0;
     (void)hipGetDevice(&dev);
     static int cus[64] = {0};
