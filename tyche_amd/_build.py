@@ -28,13 +28,15 @@ def _newer(target: str, deps: list[str]) -> bool:
     return all(os.path.getmtime(d) <= t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = False, profile: bool = False, ablate: int = 0) -> str:
+def build(force: bool = False, verbose: bool = False, profile: bool = False, ablate: int = 0,
+          eablate: int = 0) -> str:
     """profile=True builds the diagnostic variant (per-phase cycle stamps, -DTYCHE_PROFILE)
     as libtyche_codec_prof.so; it is never loaded by the product path."""
-    tag = ("_prof" if profile else "") + (f"_abl{ablate}" if ablate else "")
+    tag = ("_prof" if profile else "") + (f"_abl{ablate}" if ablate else "") + (f"_eabl{eablate}" if eablate else "")
     build_dir = BUILD + tag
     lib_path = LIB.replace(".so", tag + ".so")
-    flags = FLAGS + (["-DTYCHE_PROFILE"] if profile else []) + ([f"-DTYCHE_ABLATE={ablate}"] if ablate else [])
+    flags = FLAGS + (["-DTYCHE_PROFILE"] if profile else []) + ([f"-DTYCHE_ABLATE={ablate}"] if ablate else []) + \
+        ([f"-DTYCHE_EABLATE={eablate}"] if eablate else [])
     os.makedirs(build_dir, exist_ok=True)
     headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
     headers.append(os.path.join(HERE, "..", "include", "tyche_codec.h"))
@@ -63,5 +65,6 @@ def build(force: bool = False, verbose: bool = False, profile: bool = False, abl
 if __name__ == "__main__":
     import sys
     abl = [int(a.split("=")[1]) for a in sys.argv if a.startswith("--ablate=")]
+    eabl = [int(a.split("=")[1]) for a in sys.argv if a.startswith("--eablate=")]
     print(build(force="--force" in sys.argv, verbose=True, profile="--profile" in sys.argv,
-                ablate=abl[0] if abl else 0))
+                ablate=abl[0] if abl else 0, eablate=eabl[0] if eabl else 0))

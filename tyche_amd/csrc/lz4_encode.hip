@@ -43,6 +43,14 @@ constexpr uint32_t kPad = 64;
 constexpr uint32_t kProbe = 16;          // bytes probed per lane beyond MINMATCH
 constexpr uint32_t kPrefetchVec = 16;    // 16-byte vectors per lane prefetched for the next page (16 KiB)
 
+// Timing-only ablation builds (-DTYCHE_EABLATE=mask; outputs are wrong):
+//   1 skip the byte emission loop (sizes still computed), 2 no probes (every match 4 bytes),
+//   4 no greedy parse (no sequences: the page becomes one literal run)
+//   8 no whole-wave extension of probe-capped matches (valid output, shorter matches)
+#ifndef TYCHE_EABLATE
+#define TYCHE_EABLATE 0
+#endif
+
 __device__ __forceinline__ uint32_t hash4(uint32_t v) { return (v * 2654435761u) >> (32 - kHashLog); }
 
 // equal bytes at a and b going forward, a stopping before `limit` (whole wave, 256 bytes per step)
@@ -82,15 +90,79 @@ __device__ __forceinline__ uint32_t seq_byte(const SeqFields &f, const uint8_t *
     return rel == f.total - 1 ? (f.mc - 15u) % 255u : 255u;
 }
 
+// Encodes n accumulated sequences (records in LDS, stream order) after the
+// literal run that starts at `anchor`, writing their bytes to dst + op.  One
+// record per lane: the previous record's end gives each sequence's literal run;
+// a DPP prefix sum places the encodings; output bytes go out 64 per store, each
+// lane finding its sequence through an LDS owner map and a max-scan.  Returns
+// false if the output would exceed cap.
+__device__ bool emit_records(const uint2 *rec, uint32_t n, uint32_t anchor, const uint8_t *in, uint8_t *dst,
+                             uint32_t &op, uint32_t cap, uint8_t *map, uint32_t lane) {
+    const bool is_sel = lane < n;
+    const uint2 r = rec[is_sel ? lane : 0];
+    const uint2 rp = rec[lane > 0 && is_sel ? lane - 1 : 0];
+    const uint32_t pos = r.x & 0xFFFFu, cand = r.x >> 16, len = r.y & 0xFFFFu, back = r.y >> 16;
+    const uint32_t prev_end = lane == 0 ? anchor : (rp.x & 0xFFFFu) + (rp.y & 0xFFFFu);
+    SeqFields f{};
+    uint32_t enc = 0;
+    if (is_sel) {
+        const uint32_t k = min(min(back, pos - prev_end), cand);   // catch-up (lz4.c:549)
+        f.anchor = prev_end;
+        f.lit = pos - k - prev_end;
+        f.lext = f.lit >= 15 ? (f.lit - 15) / 255 + 1 : 0;
+        f.off = pos - cand;
+        f.mc = len + k - kMinMatch;
+        const uint32_t mext = f.mc >= 15 ? (f.mc - 15) / 255 + 1 : 0;
+        f.token = (min(f.lit, 15u) << 4) | min(f.mc, 15u);
+        f.total = 1 + f.lext + f.lit + 2 + mext;
+        enc = f.total;
+    }
+    const int32_t incl = wave_incl_sum((int32_t)enc);
+    const uint32_t eo = (uint32_t)incl - enc;
+    const uint32_t et = rdlane((uint32_t)incl, 63);
+    if (op + et > cap) return false;
+    // fields travel packed: 4 bpermutes per output chunk
+    const uint32_t pk0 = f.lit | (f.lext << 16), pk1 = f.anchor | (f.off << 16);
+    const uint32_t pk2 = f.mc | (f.total << 16), pk3 = eo | (f.token << 16);
+    for (uint32_t j0 = 0; j0 < ((TYCHE_EABLATE & 1) ? 0u : et); j0 += kWave) {
+        const uint32_t j = j0 + lane;
+        // owner of byte j: the last sequence whose encoding starts at or before j.
+        // Starts inside this chunk are stamped into a 64-byte map and max-scanned.
+        const uint64_t before = __ballot(is_sel && eo <= j0);
+        const int32_t owner0 = before ? 63 - (int32_t)__builtin_clzll(before) : 0;
+        map[lane] = 0xFF;
+        __builtin_amdgcn_wave_barrier();
+        if (is_sel && eo > j0 && eo < j0 + kWave) map[eo - j0] = (uint8_t)lane;
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t mv = map[lane];
+        const uint32_t owner = (uint32_t)max(wave_incl_max(mv == 0xFF ? -1 : (int32_t)mv), owner0);
+        const uint32_t g0 = __shfl(pk0, owner), g1 = __shfl(pk1, owner);
+        const uint32_t g2 = __shfl(pk2, owner), g3 = __shfl(pk3, owner);
+        SeqFields g;
+        g.lit = g0 & 0xFFFFu;
+        g.lext = g0 >> 16;
+        g.anchor = g1 & 0xFFFFu;
+        g.off = g1 >> 16;
+        g.mc = g2 & 0xFFFFu;
+        g.total = g2 >> 16;
+        g.token = g3 >> 16;
+        if (j < et) dst[op + j] = (uint8_t)seq_byte(g, in, j - (g3 & 0xFFFFu));
+        __builtin_amdgcn_wave_barrier();
+    }
+    op += et;
+    return true;
+}
+
 // Encodes one page held in LDS into dst (global, capacity cap).  Returns the
 // compressed size, or 0 if it does not fit in cap.
-__device__ int32_t encode_page(const uint8_t *in, uint32_t L, uint16_t *table, uint8_t *map, uint8_t *dst,
-                               uint32_t cap, uint32_t lane) {
+__device__ int32_t encode_page(const uint8_t *in, uint32_t L, uint16_t *table, uint8_t *map, uint2 *rec,
+                               uint8_t *dst, uint32_t cap, uint32_t lane) {
     uint32_t op = 0, anchor = 0;
     if (L >= (uint32_t)(kMfLimit + 1)) {
         const uint32_t mflimit = L - kMfLimit;          // last position a match may start
         const uint32_t matchlimit = L - kLastLiterals;  // matches end at or before this
         uint32_t cursor = 0;     // matches may start here (end of the last match)
+        uint32_t nacc = 0;       // sequences accumulated in rec[] since the last emission
         uint32_t blk = 0;        // current 64-position block
         bool done = false;
         for (; !done && blk <= mflimit; blk = max(blk + kWave, cursor & ~(kWave - 1))) {
@@ -104,9 +176,9 @@ __device__ int32_t encode_page(const uint8_t *in, uint32_t L, uint16_t *table, u
             if (live) table[h] = (uint16_t)pos;
             const bool ok = live && cand < pos && lds_ld32(in + cand) == v;
             // ---- forward probe (MINMATCH + up to kProbe bytes) and backward probe (up to 4 bytes)
-            uint32_t len = 0, back = 0;
+            uint32_t len = (TYCHE_EABLATE & 2) ? 4u : 0u, back = 0;
             bool capped = false;
-            if (ok) {
+            if (ok && !(TYCHE_EABLATE & 2)) {
                 // four unaligned dword compares, no branches; clamp to the match limit
                 const uint32_t e = min(matchlimit, pos + kMinMatch + kProbe);
                 const uint32_t x0 = lds_ld32(in + pos + 4) ^ lds_ld32(in + cand + 4);
@@ -125,78 +197,54 @@ __device__ int32_t encode_page(const uint8_t *in, uint32_t L, uint16_t *table, u
                     back = x ? (__builtin_clz(x) >> 3) : 4u;
                 }
             }
-            // ---- greedy parse of this block on scalar registers
-            uint64_t m = __ballot(ok && pos >= cursor);
+            // ---- greedy parse of this block.  Every lane precomputes where the parse
+            // goes if it stands at its position: the first match at or after it
+            // (ballot mask) and that match's end.  The parse itself then only hops
+            // through these values with v_readlane (scalar code, no memory).
+            const uint64_t mall = (TYCHE_EABLATE & 4) ? 0ull : __ballot(ok);
+            uint32_t at = cursor > blk ? cursor - blk : 0u;        // parse position within the block
+            if ((mall >> at) == 0) continue;                       // no match starts at or after it
+            const uint64_t ahead = mall & ~((1ull << lane) - 1ull);
+            const uint32_t nml = ahead ? (uint32_t)__builtin_ctzll(ahead) : 64u;
+            const uint32_t nlen = __shfl(len | ((uint32_t)capped << 16), nml & 63u);
+            // hop word: bits 0..6 lane of the next match (64 = none), bit 7 capped, bits 8.. its end
+            const uint32_t hop = nml | ((nlen >> 16) << 7) | ((blk + nml + (nlen & 0xFFFFu)) << 8);
             uint64_t sel = 0;
-            if (m == 0) continue;
-            while (m) {
-                const uint32_t li = (uint32_t)__builtin_ctzll(m);
-                uint32_t ln = rdlane(len, li);
-                if (rdlane((uint32_t)capped, li)) {
-                    const uint32_t mp = blk + li, mc = rdlane(cand, li);
-                    ln += wave_extend(in, mp + ln, mc + ln, matchlimit, lane);
+            for (;;) {
+                const uint32_t h = rdlane(hop, at);
+                const uint32_t li = h & 127u;
+                if (li >= 64) break;                                 // no further match in this block
+                uint32_t end = h >> 8;
+                if ((h & 128u) && !(TYCHE_EABLATE & 8)) {
+                    // reached the probe limit: extend with the whole wave
+                    const uint32_t mp = blk + li, mc = rdlane(cand, li), ln0 = end - mp;
+                    const uint32_t ln = ln0 + wave_extend(in, mp + ln0, mc + ln0, matchlimit, lane);
                     if (lane == li) len = ln;
+                    end = mp + ln;
                 }
                 sel |= 1ull << li;
-                cursor = blk + li + ln;
+                cursor = end;
                 if (cursor > mflimit) { done = true; break; }
                 if (cursor >= blk + kWave) break;
-                m &= ~((1ull << (cursor - blk)) - 1ull);
+                at = cursor - blk;
             }
-            // ---- encode the selected sequences together
+            if (sel == 0) continue;
+            // ---- append this block's sequences to the LDS records (stream order)
             const bool is_sel = (sel >> lane) & 1ull;
-            const uint32_t mend = pos + len;
-            const uint64_t below = sel & ((1ull << lane) - 1ull);
-            const uint32_t prev_lane = below ? 63u - (uint32_t)__builtin_clzll(below) : 0u;
-            const uint32_t prev_end_x = __shfl(mend, prev_lane);
-            const uint32_t prev_end = below ? prev_end_x : anchor;
-            SeqFields f{};
-            uint32_t enc = 0;
-            if (is_sel) {
-                const uint32_t k = min(min(back, pos - prev_end), cand);   // catch-up
-                f.anchor = prev_end;
-                f.lit = pos - k - prev_end;
-                f.lext = f.lit >= 15 ? (f.lit - 15) / 255 + 1 : 0;
-                f.off = pos - cand;
-                f.mc = len + k - kMinMatch;
-                const uint32_t mext = f.mc >= 15 ? (f.mc - 15) / 255 + 1 : 0;
-                f.token = (min(f.lit, 15u) << 4) | min(f.mc, 15u);
-                f.total = 1 + f.lext + f.lit + 2 + mext;
-                enc = f.total;
+            const uint32_t rank = nacc + (uint32_t)__popcll(sel & ((1ull << lane) - 1ull));
+            if (is_sel) rec[rank] = make_uint2(pos | (cand << 16), len | (back << 16));
+            nacc += (uint32_t)__popcll(sel);
+            // a block adds at most 16 sequences (each covers >= 4 positions)
+            if (nacc > kWave - 16 || done) {
+                __builtin_amdgcn_wave_barrier();
+                if (!emit_records(rec, nacc, anchor, in, dst, op, cap, map, lane)) return 0;
+                anchor = cursor;
+                nacc = 0;
             }
-            const int32_t incl = wave_incl_sum((int32_t)enc);
-            const uint32_t eo = (uint32_t)incl - enc;
-            const uint32_t et = rdlane((uint32_t)incl, 63);
-            if (op + et > cap) return 0;
-            // fields travel packed: 4 bpermutes per output chunk
-            const uint32_t pk0 = f.lit | (f.lext << 16), pk1 = f.anchor | (f.off << 16);
-            const uint32_t pk2 = f.mc | (f.total << 16), pk3 = eo | (f.token << 16);
-            for (uint32_t j0 = 0; j0 < et; j0 += kWave) {
-                const uint32_t j = j0 + lane;
-                // owner of byte j: the last selected lane whose encoding starts at or before j.
-                // Starts inside this chunk are stamped into a 64-byte map and max-scanned.
-                const uint64_t before = __ballot(is_sel && eo <= j0);
-                const int32_t owner0 = before ? 63 - (int32_t)__builtin_clzll(before) : 0;
-                map[lane] = 0xFF;
-                __builtin_amdgcn_wave_barrier();
-                if (is_sel && eo > j0 && eo < j0 + kWave) map[eo - j0] = (uint8_t)lane;
-                __builtin_amdgcn_wave_barrier();
-                const uint32_t mv = map[lane];
-                const uint32_t owner = (uint32_t)max(wave_incl_max(mv == 0xFF ? -1 : (int32_t)mv), owner0);
-                const uint32_t g0 = __shfl(pk0, owner), g1 = __shfl(pk1, owner);
-                const uint32_t g2 = __shfl(pk2, owner), g3 = __shfl(pk3, owner);
-                SeqFields g;
-                g.lit = g0 & 0xFFFFu;
-                g.lext = g0 >> 16;
-                g.anchor = g1 & 0xFFFFu;
-                g.off = g1 >> 16;
-                g.mc = g2 & 0xFFFFu;
-                g.total = g2 >> 16;
-                g.token = g3 >> 16;
-                if (j < et) dst[op + j] = (uint8_t)seq_byte(g, in, j - (g3 & 0xFFFFu));
-                __builtin_amdgcn_wave_barrier();
-            }
-            op += et;
+        }
+        if (nacc) {
+            __builtin_amdgcn_wave_barrier();
+            if (!emit_records(rec, nacc, anchor, in, dst, op, cap, map, lane)) return 0;
             anchor = cursor;
         }
     }
@@ -220,7 +268,8 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel(tyche_batch_t b, uint32_
     const uint32_t lane = threadIdx.x;
     uint16_t *table = (uint16_t *)smem;
     uint8_t *map = smem + kHashSize * sizeof(uint16_t);                 // 64-byte owner map
-    uint8_t *stage = map + kWave;
+    uint2 *rec = (uint2 *)(map + kWave);                               // 64 sequence records
+    uint8_t *stage = (uint8_t *)(rec + kWave);
     const size_t stride = gridDim.x;
 
     size_t page = blockIdx.x;
@@ -255,7 +304,7 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel(tyche_batch_t b, uint32_
             __syncthreads();
             in[p.src_len + lane] = 0;
             __syncthreads();
-            rv = encode_page(in, p.src_len, table, map, p.dst, p.dst_cap, lane);
+            rv = encode_page(in, p.src_len, table, map, rec, p.dst, p.dst_cap, lane);
         }
         if (lane == 0) b.results[page] = rv;
         if (next >= b.count) break;
@@ -281,7 +330,7 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel(tyche_batch_t b, uint32_
 hipError_t launch_lz4_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream_t s) {
     if (b.count == 0) return hipSuccess;
     if (in_cap > 65535u) return hipErrorInvalidValue;    // 16-bit positions (byU16 regime)
-    const size_t lds = kHashSize * sizeof(uint16_t) + kWave + ((in_cap + 16u + kPad + 15u) & ~15u);
+    const size_t lds = kHashSize * sizeof(uint16_t) + kWave + kWave * 8 + ((in_cap + 16u + kPad + 15u) & ~15u);
     int dev = 0;
     (void)hipGetDevice(&dev);
     static int cus[64] = {0};
