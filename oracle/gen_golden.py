@@ -17,6 +17,11 @@ Fixtures (all data, no reference source):
   lz4_malformed.npz   corrupted / truncated / random streams with the reference
                       LZ4_decompress_safe return value (and output digest when
                       the output is defined)
+  zlib_streams.npz    reference compress2 encodings (levels 0/1/6/9: stored,
+                      fixed and dynamic blocks) of generated pages, sample pages
+                      and short inputs, with the input digests
+  zlib_malformed.npz  corrupted / truncated / short-capacity zlib streams with the
+                      reference uncompress() result (Z_OK length or error code)
 """
 from __future__ import annotations
 
@@ -215,6 +220,94 @@ def gen_malformed():
     print("malformed", len(cases), "errors", sum(r < 0 for r in rvs), "undefined", sum(not d for d in defined))
 
 
+def zlib_inputs():
+    """(label, bytes) inputs for the zlib fixtures."""
+    out = []
+    for dist in range(6):
+        for plen in (8192, 16384, 32768):
+            first = 5000 + 1000 * dist + plen // 1024
+            out.append((f"gen/{dist}/{plen}/{first}", O.pagegen(1, plen, seed=SEED, first=first, dist=dist)[0].tobytes()))
+    files = sorted(glob.glob(os.path.join(REF, "sample_data", "*", "*", "*", "*")))
+    for f in files[::3]:
+        out.append(("sample/" + os.path.relpath(f, os.path.join(REF, "sample_data")), open(f, "rb").read()))
+    out.append(("kat", kat_text()))
+    for n in (0, 1, 2, 3, 7, 64, 300):
+        out.append((f"short/{n}", bytes((i * 37 + 11) & 0xFF for i in range(n))))
+    out.append(("short/hello", b"hello hello hello hello"))
+    return out
+
+
+def gen_zlib_streams():
+    labels, levels, comps, digests, sizes = [], [], [], [], []
+    for label, data in zlib_inputs():
+        for level in (0, 1, 6, 9):
+            if level != 1 and not (label.startswith("gen/0/16384") or label.startswith("short") or label == "kat"):
+                continue
+            c = O.ref_zlib_compress(data, level)
+            r, out = O.ref_zlib_uncompress(c, len(data))
+            assert r == len(data) and out == data
+            labels.append(label)
+            levels.append(level)
+            comps.append(c)
+            digests.append(sha(data))
+            sizes.append(len(data))
+    data, offs, lens = pack(comps)
+    np.savez_compressed(os.path.join(OUT, "zlib_streams.npz"), seed=np.int64(SEED), labels=np.array(labels),
+                        level=np.array(levels, np.int64), comp=data, comp_off=offs, comp_len=lens,
+                        size=np.array(sizes, np.int64),
+                        digest=np.frombuffer(b"".join(digests), np.uint8).reshape(-1, 32))
+    print("zlib streams", len(labels), data.size)
+
+
+def gen_zlib_malformed():
+    rng = np.random.default_rng(SEED + 2)
+    cases = []   # (stream, out_cap)
+    srcs = [O.pagegen(1, 16384, seed=SEED, first=9000 + k, dist=k % 4)[0].tobytes() for k in range(3)]
+    srcs.append(kat_text())
+    srcs.append(b"hello hello hello hello")
+    streams = [O.ref_zlib_compress(d, 1) for d in srcs] + [O.ref_zlib_compress(srcs[0][:3000], 0)]
+    sizes = [len(d) for d in srcs] + [3000]
+    for s, n_out in zip(streams, sizes):
+        n = len(s)
+        for cut in sorted(set([1, 2, 3, 5, 9, n // 3, n // 2, n - 5, n - 4, n - 1])):
+            if 0 < cut < n:
+                cases.append((s[:cut], n_out))
+        for _ in range(14):
+            b = bytearray(s)
+            for _ in range(int(rng.integers(1, 3))):
+                b[int(rng.integers(0, n))] ^= 1 << int(rng.integers(0, 8))
+            cases.append((bytes(b), n_out))
+        cases.append((s, n_out - 1))           # output one byte short
+        cases.append((s, n_out + 100))         # larger capacity (Z_OK with the true length)
+        cases.append((s + b"\x00\x00", n_out))   # trailing bytes after the adler32
+    for _ in range(30):
+        ln = int(rng.integers(1, 200))
+        cases.append((rng.integers(0, 256, ln, dtype=np.uint8).tobytes(), 4096))
+    for _ in range(10):   # valid header, random body
+        ln = int(rng.integers(1, 200))
+        cases.append((b"\x78\x01" + rng.integers(0, 256, ln, dtype=np.uint8).tobytes(), 4096))
+    cases += [
+        (b"", 16), (b"\x78", 16), (b"\x78\x01", 16), (b"\x78\x02", 16), (b"\x79\x01", 16),
+        (b"\x78\xbb\x00\x00\x00\x00", 16),                      # FDICT
+        (b"\x78\x01\x01\x00\x00\xff\xff\x00\x00\x00\x01", 16),  # empty stored block, adler 1
+        (b"\x78\x01\x01\x01\x00\xfe\xff\x41\x00\x42\x00\x42", 16),  # stored 'A'
+        (b"\x78\x01\x01\x01\x00\xfe\xfe\x41\x00\x42\x00\x42", 16),  # bad NLEN
+        (b"\x78\x01\x07", 16),                                  # reserved block type
+    ]
+    streams_out, caps, rvs, digs = [], [], [], []
+    for s, cap in cases:
+        r, out = O.ref_zlib_uncompress(s, cap)
+        streams_out.append(s)
+        caps.append(cap)
+        rvs.append(r)
+        digs.append(sha(out) if r >= 0 else b"\0" * 32)
+    data, offs, lens = pack(streams_out)
+    np.savez_compressed(os.path.join(OUT, "zlib_malformed.npz"), comp=data, comp_off=offs, comp_len=lens,
+                        cap=np.array(caps, np.int64), rv=np.array(rvs, np.int64),
+                        digest=np.frombuffer(b"".join(digs), np.uint8).reshape(-1, 32))
+    print("zlib malformed", len(cases), "errors", sum(r < 0 for r in rvs))
+
+
 if __name__ == "__main__":
     if not O.have_ref():
         sys.exit("oracle/_ref/libtyche_ref.so missing: run `make -C oracle ref` where /root/reference exists")
@@ -223,3 +316,5 @@ if __name__ == "__main__":
     gen_generated()
     gen_sample()
     gen_malformed()
+    gen_zlib_streams()
+    gen_zlib_malformed()

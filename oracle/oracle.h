@@ -13,6 +13,9 @@ long oracle_lz4_compress_pages(const uint8_t *src, uint64_t src_stride, uint32_t
                                uint64_t dst_stride, int32_t *out_len, long first, long count);
 long oracle_lz4_decompress_pages(const uint8_t *src, uint64_t src_stride, const int32_t *in_len, uint8_t *dst,
                                  uint64_t dst_stride, uint32_t page_len, int32_t *rv, long first, long count);
+/* zlib (RFC 1950/1951) restatement: decoded length or negative zlib code */
+int oracle_zlib_uncompress(const uint8_t *src, int srclen, uint8_t *dst, int dstcap);
+uint32_t oracle_adler32(const uint8_t *p, int n);
 /* host copy of the synthetic page generator (tyche_amd/csrc/pagegen.h) */
 void oracle_pagegen(uint8_t *dst, uint64_t dst_stride, uint32_t page_len, uint64_t seed, uint64_t first,
                     long count, uint32_t dist);

@@ -66,6 +66,10 @@ class _Lib:
             lib.oracle_pagegen.argtypes = [_u8p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64,
                                            ctypes.c_long, ctypes.c_uint32]
             lib.oracle_pagegen.restype = None
+            lib.oracle_zlib_uncompress.argtypes = [_u8p, ctypes.c_int, _u8p, ctypes.c_int]
+            lib.oracle_zlib_uncompress.restype = ctypes.c_int
+            lib.oracle_adler32.argtypes = [_u8p, ctypes.c_int]
+            lib.oracle_adler32.restype = ctypes.c_uint32
             cls._oracle = lib
         return cls._oracle
 
@@ -137,6 +141,21 @@ def lz4_decompress(comp, out_cap: int) -> tuple[int, bytes]:
     return r, (dst[:r].tobytes() if r > 0 else b"")
 
 
+def zlib_uncompress(comp, out_cap: int) -> tuple[int, bytes]:
+    """uncompress() restated (src/zlib/uncompr.c:22): (decoded length or negative zlib code, bytes)."""
+    src = _as_u8(comp)
+    srcbuf = np.zeros(src.size + 16, dtype=np.uint8)
+    srcbuf[:src.size] = src
+    dst = np.zeros(max(out_cap, 1), dtype=np.uint8)
+    r = _Lib.oracle().oracle_zlib_uncompress(_ptr(srcbuf), src.size, _ptr(dst), out_cap)
+    return r, (dst[:r].tobytes() if r > 0 else b"")
+
+
+def adler32(data) -> int:
+    src = _as_u8(data)
+    return int(_Lib.oracle().oracle_adler32(_ptr(src), src.size))
+
+
 def pagegen(n: int, page_len: int, seed: int = 20170303, first: int = 0, dist: int = 0) -> np.ndarray:
     """Host copy of tyche_amd/csrc/pagegen.h: (n, page_len) uint8 pages."""
     out = np.zeros((n, page_len), dtype=np.uint8)
@@ -185,6 +204,20 @@ def ref_zlib_compress(data, level: int = 1) -> bytes:
     r = lib.compress2(_ptr(dst), ctypes.byref(cap), _ptr(src), src.size, level)
     assert r == 0, r
     return dst[:cap.value].tobytes()
+
+
+def ref_zlib_uncompress(comp, out_cap: int) -> tuple[int, bytes]:
+    """The reference's uncompress(): (decoded length or negative zlib code, bytes)."""
+    lib = _Lib.ref()
+    src = _as_u8(comp)
+    srcbuf = np.zeros(src.size + 16, dtype=np.uint8)
+    srcbuf[:src.size] = src
+    dst = np.zeros(max(out_cap, 1) + 16, dtype=np.uint8)
+    n = ctypes.c_ulong(out_cap)
+    r = lib.uncompress(_ptr(dst), ctypes.byref(n), _ptr(srcbuf), src.size)
+    if r != 0:
+        return r, b""
+    return n.value, dst[:n.value].tobytes()
 
 
 def ref_zstd_compress(data, level: int = 1) -> bytes:

@@ -114,3 +114,44 @@ def test_against_reference_build_random(oracle_mod):
         r1, o1 = O.lz4_decompress(bytes(s), cap)
         r2, o2 = O.ref_lz4_decompress(bytes(s), cap)
         assert r1 == r2
+
+
+# ----------------------------------------------------------------- zlib (A11)
+def test_zlib_kat(oracle_mod):
+    """src/tests.c:384-413: zlib level 1 of the Lorem KAT is 1759 bytes and inflates back."""
+    O = oracle_mod
+    g = load_golden("kat_lorem.npz")
+    rv, out = O.zlib_uncompress(g["zlib"].tobytes(), 4096)
+    assert rv == 4096 and out == g["text"].tobytes()
+    assert O.adler32(out) == int.from_bytes(g["zlib"].tobytes()[-4:], "big")
+
+
+def test_zlib_streams_exact(oracle_mod):
+    """Stored (level 0), fixed and dynamic-Huffman blocks produced by the reference's compress2."""
+    O = oracle_mod
+    g = load_golden("zlib_streams.npz")
+    for i in range(len(g["labels"])):
+        s = unpack(g["comp"], g["comp_off"], g["comp_len"], i)
+        n = int(g["size"][i])
+        rv, out = O.zlib_uncompress(s, n)
+        assert rv == n, (g["labels"][i], g["level"][i], rv)
+        assert hashlib.sha256(out).digest() == g["digest"][i].tobytes()
+
+
+def test_zlib_malformed(oracle_mod):
+    """Reference uncompress() verdicts.  Success, length and bytes must match exactly.  On failure
+    the code must match except Z_BUF_ERROR(-5) vs Z_DATA_ERROR(-3), whose split in the reference
+    depends on how far inflate's bit buffer had read ahead when the output filled (uncompr.c:47-53);
+    buffer__decompress maps both to E_BUFFER_DECOMPRESSION_PROBLEM (src/buffer.c:257-260)."""
+    O = oracle_mod
+    g = load_golden("zlib_malformed.npz")
+    for i in range(len(g["cap"])):
+        s = unpack(g["comp"], g["comp_off"], g["comp_len"], i)
+        rv, out = O.zlib_uncompress(s, int(g["cap"][i]))
+        want = int(g["rv"][i])
+        if want >= 0:
+            assert rv == want, (i, rv, want)
+            assert hashlib.sha256(out).digest() == g["digest"][i].tobytes()
+        else:
+            assert rv < 0, (i, rv, want)
+            assert rv == want or {rv, want} == {-3, -5}, (i, rv, want)
