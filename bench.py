@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import argparse
 import concurrent.futures as cf
+import glob
 import json
 import os
 import sys
@@ -154,6 +155,19 @@ def e2e_host(pages_dev: torch.Tensor, n: int) -> dict:
             "combined_gib_s": round(nbytes / (best_c + best_d) / GIB, 3)}
 
 
+def pmc_traffic(kernel: str, pages: int, page_len: int):
+    """HBM bytes per launch for `kernel` from the newest committed PMC summary
+    (profiles/rNN_traffic.json, made by tools/pmc_traffic.py from separate
+    FETCH_SIZE / WRITE_SIZE rocprofv3 passes of the same kernels), scaled from
+    bytes per page to this launch's page count; None when no summary matches."""
+    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r*_traffic.json")))
+    for f in reversed(files):
+        t = json.load(open(f))
+        if t.get("page_len") == page_len and kernel in t.get("bytes_per_page", {}):
+            return {"bytes": int(t["bytes_per_page"][kernel] * pages), "source": os.path.basename(f)}
+    return None
+
+
 def main():
     args = parse()
     info = runner.init_distributed()
@@ -214,6 +228,7 @@ def main():
     kernels = {"lz4_encode": c_ms, "lz4_decode": d_ms}
     dom = max(kernels, key=kernels.get)
     achieved = algo_bytes / (kernels[dom] * 1e-3) / 1e9
+    traffic = pmc_traffic(dom, n, plen)
 
     result = {
         "metric": METRIC,
@@ -231,7 +246,9 @@ def main():
         "config": {"workload": "C2: LZ4 block compress+decompress, 1M x 16 KiB pages per GPU, device-resident",
                    "pages_per_gpu": n, "page_len": plen, "codec": "lz4", "parallelism": f"page-range x{info.world}"},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": traffic["bytes"] if traffic else None,
+                     "traffic_source": traffic["source"] if traffic else None,
                      "algorithmic_bytes_per_launch": algo_bytes},
         "compress_gib_s": round(page_bytes / (c_ms * 1e-3) / GIB, 3),
         "decompress_gib_s": round(page_bytes / (d_ms * 1e-3) / GIB, 3),

@@ -1,0 +1,62 @@
+"""Turns the two rocprofv3 PMC passes of tools/run_codec.py into HBM bytes per page.
+
+    python tools/pmc_traffic.py profiles/r01_pmc_fetch_size.csv profiles/r01_pmc_write_size.csv \
+        --pages 262144 --page-len 16384 -o profiles/r01_traffic.json
+
+Correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE and WRITE_SIZE are in
+KiB; on gfx950 FETCH_SIZE reports half the bytes of a 16-B/lane streaming read,
+so HBM bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.  Each kernel's figure is
+the mean over its dispatches, divided by the pages one dispatch processes.
+bench.py scales the per-page figure to its own launch for `roofline.traffic`.
+"""
+import argparse
+import csv
+import json
+from collections import defaultdict
+
+KERNELS = {"lz4_encode": "lz4_encode_kernel", "lz4_decode": "lz4_decode_wave_kernel"}
+
+
+def per_dispatch(path, counter):
+    acc = defaultdict(float)
+    names = {}
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] != counter:
+            continue
+        acc[r["Dispatch_Id"]] += float(r["Counter_Value"])
+        names[r["Dispatch_Id"]] = r["Kernel_Name"]
+    out = defaultdict(list)
+    for d, v in acc.items():
+        for k, sym in KERNELS.items():
+            if sym in names[d]:
+                out[k].append(v)
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("fetch")
+    ap.add_argument("write")
+    ap.add_argument("--pages", type=int, required=True)
+    ap.add_argument("--page-len", type=int, default=16384)
+    ap.add_argument("-o", "--out", required=True)
+    a = ap.parse_args()
+    f = per_dispatch(a.fetch, "FETCH_SIZE")
+    w = per_dispatch(a.write, "WRITE_SIZE")
+    res = {"pages_per_dispatch": a.pages, "page_len": a.page_len,
+           "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024 / pages (gfx950 FETCH_SIZE half-count corrected)",
+           "bytes_per_page": {}, "read_bytes_per_page": {}, "write_bytes_per_page": {}}
+    for k in KERNELS:
+        if not f.get(k) or not w.get(k):
+            continue
+        rd = 2 * 1024 * sum(f[k]) / len(f[k]) / a.pages
+        wr = 1024 * sum(w[k]) / len(w[k]) / a.pages
+        res["read_bytes_per_page"][k] = round(rd, 1)
+        res["write_bytes_per_page"][k] = round(wr, 1)
+        res["bytes_per_page"][k] = round(rd + wr, 1)
+    json.dump(res, open(a.out, "w"), indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
