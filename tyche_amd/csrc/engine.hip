@@ -62,13 +62,18 @@ int ensure_device() {
     return TYCHE_E_OK;
 }
 
+// codecs with a gfx950 kernel, per direction
 bool valid_codec(int id) { return id == TYCHE_LZ4_COMPRESSOR_ID; }
+bool valid_decode_codec(int id) { return id == TYCHE_LZ4_COMPRESSOR_ID || id == TYCHE_ZLIB_COMPRESSOR_ID; }
 
 std::string codec_msg(int id) {
     if (id == TYCHE_ZLIB_COMPRESSOR_ID || id == TYCHE_ZSTD_COMPRESSOR_ID)
-        return "compressor id " + std::to_string(id) + " has no gfx950 kernel in this build (LZ4 only)";
+        return "compressor id " + std::to_string(id) + " has no gfx950 kernel for this direction in this build";
     return "unknown compressor id " + std::to_string(id);
 }
+
+// zlib 1.2.8 compressBound (compress.c:74-78)
+inline uint32_t zlib_bound(uint32_t n) { return n + (n >> 12) + (n >> 14) + (n >> 25) + 13u; }
 
 // ---------------------------------------------------------------- host batches
 // One context per calling thread (tyche calls the codec from its compressor
@@ -203,6 +208,7 @@ int tyche_device_ready(void) { return ensure_device() == TYCHE_E_OK ? 1 : 0; }
 
 uint32_t tyche_compress_bound(int compressor_id, uint32_t n) {
     if (compressor_id == TYCHE_LZ4_COMPRESSOR_ID) return lz4_bound(n);
+    if (compressor_id == TYCHE_ZLIB_COMPRESSOR_ID) return zlib_bound(n);
     return 0;
 }
 
@@ -223,10 +229,15 @@ int tyche_compress_batch(int compressor_id, int compressor_level, const tyche_ba
 
 int tyche_decompress_batch(int compressor_id, const tyche_batch_t *batch, void *stream) {
     if (!batch) return TYCHE_E_BAD_ARGS;
-    if (!valid_codec(compressor_id)) { t_error = codec_msg(compressor_id); return TYCHE_E_BAD_ARGS; }
+    if (!valid_decode_codec(compressor_id)) { t_error = codec_msg(compressor_id); return TYCHE_E_BAD_ARGS; }
     if (batch->count == 0) return TYCHE_E_OK;
     if (!batch->src || !batch->dst || !batch->results) return TYCHE_E_BAD_ARGS;
     uint32_t out_cap = batch->dst_capacity;
+    if (compressor_id == TYCHE_ZLIB_COMPRESSOR_ID) {
+        hipError_t e = launch_zlib_inflate(*batch, out_cap, (hipStream_t)stream);
+        if (e != hipSuccess) return fail("zlib inflate launch", e);
+        return TYCHE_E_OK;
+    }
     uint32_t in_cap = batch->src_lengths ? batch->max_src_length : batch->src_length;
     if (batch->src_lengths && in_cap == 0) in_cap = lz4_bound(out_cap);
     hipError_t e = launch_lz4_decode(*batch, in_cap, out_cap, (hipStream_t)stream);
@@ -251,8 +262,13 @@ int tyche_compress_host(int compressor_id, int compressor_level, size_t n, const
 
 int tyche_decompress_host(int compressor_id, size_t n, const void *const *src, const uint32_t *src_lengths,
                           void *const *dst, const uint32_t *dst_capacities, int32_t *results) {
-    if (!valid_codec(compressor_id)) { t_error = codec_msg(compressor_id); return TYCHE_E_BAD_ARGS; }
+    if (!valid_decode_codec(compressor_id)) { t_error = codec_msg(compressor_id); return TYCHE_E_BAD_ARGS; }
     if (n == 0) return TYCHE_E_OK;
+    if (compressor_id == TYCHE_ZLIB_COMPRESSOR_ID)
+        return run_host_batch(n, src, src_lengths, dst, dst_capacities, results, true,
+                              [](const tyche_batch_t &b, hipStream_t s) {
+                                  return launch_zlib_inflate(b, b.dst_capacity, s);
+                              });
     return run_host_batch(n, src, src_lengths, dst, dst_capacities, results, true,
                           [](const tyche_batch_t &b, hipStream_t s) {
                               return launch_lz4_decode(b, b.max_src_length, b.dst_capacity, s);
@@ -402,10 +418,10 @@ int tyche_buffers_decompress(Buffer **bufs, int *status, size_t n, int compresso
     for (size_t i = 0; i < n; i++) {
         status[i] = decompress_precheck(bufs[i], compressor_id);
         if (status[i] == -1) {
-            if (!valid_codec(compressor_id) && compressor_id >= 1 && compressor_id <= 3) {
+            if (!valid_decode_codec(compressor_id) && compressor_id >= 1 && compressor_id <= 3) {
                 t_error = codec_msg(compressor_id);
                 status[i] = TYCHE_E_BUFFER_COMPRESSION_PROBLEM;
-            } else if (!valid_codec(compressor_id)) {
+            } else if (!valid_decode_codec(compressor_id)) {
                 // unknown id: the reference swaps in an unfilled malloc(data_length) block and
                 // reports success (buffer.c:244-279); mirrored, with the block zeroed.
                 Buffer *b = bufs[i];
@@ -445,7 +461,9 @@ int tyche_buffers_decompress(Buffer **bufs, int *status, size_t n, int compresso
     for (size_t k = 0; k < m; k++) {
         Buffer *b = bufs[idx[k]];
         size_t i = idx[k];
-        if (rc != TYCHE_E_OK || res[k] < 0) {       // LZ4 accepts any rv >= 0 (buffer.c:251-253)
+        // LZ4 accepts any rv >= 0 (buffer.c:251-253); zlib needs Z_OK and the exact length (:257-260)
+        const bool bad = res[k] < 0 || (compressor_id == TYCHE_ZLIB_COMPRESSOR_ID && (uint32_t)res[k] != b->data_length);
+        if (rc != TYCHE_E_OK || bad) {
             free(dst[k]);                           // the reference leaks here
             status[i] = rc != TYCHE_E_OK ? TYCHE_E_DEVICE : TYCHE_E_BUFFER_COMPRESSION_PROBLEM;
             continue;

@@ -1,0 +1,591 @@
+// zlib_inflate.hip -- gfx950 decoder for zlib-wrapped deflate streams, the
+// codec behind buffer__decompress for ZLIB_COMPRESSOR_ID (src/buffer.c:256-260
+// -> uncompress, src/zlib/uncompr.c:22-59 -> inflate, inflate.c:605,
+// inffast.c:67, inftrees.c:32; adler32.c:65).
+//
+// One wave per page, waves loop over pages.  The serial part of inflate -- the
+// Huffman bit stream -- runs on scalar registers:
+//   * the compressed stream is read from HBM into a two-register window
+//     (2 x 256 B per wave, the next 256 B loaded while the current ones are
+//     decoded); 32-bit refills come out of it with v_readlane, so the bit
+//     reader never touches LDS;
+//   * each Huffman table is a 1024-entry root table held in 16 VGPRs (entry
+//     r*64+lane in register r of that lane) and read with v_readlane; codes
+//     longer than 10 bits go through a canonical-code slow path;
+//   * decoded literals (position, byte) and matches (position, distance,
+//     length) are collected in VGPRs with v_writelane and applied 64 at a time:
+//     literals with one byte store per lane, matches with the frontier-grouped
+//     copy (every pending match whose source ends before the first pending
+//     destination is independent; four 16-lane groups copy four of them per
+//     instruction).
+// Table construction (canonical codes, completeness rules of inflate_table) is
+// lane-parallel: ballots count code lengths, rank symbols and fill the root
+// table.  The adler32 trailer is checked with a lane-parallel sum over the
+// rebuilt page in LDS.
+//
+// Results follow the repo's restatement oracle/zlib_oracle.c exactly: the
+// decoded length, or -3 (Z_DATA_ERROR) / -5 (Z_BUF_ERROR) at the same point of
+// the stream.
+#include <algorithm>
+
+#include "engine.h"
+#include "lds_io.h"
+
+namespace tyche {
+namespace {
+
+constexpr uint32_t kWave = 64;
+constexpr int32_t kZData = -3;   // Z_DATA_ERROR
+constexpr int32_t kZBuf = -5;    // Z_BUF_ERROR (output full, input left: uncompr.c:47-53)
+
+// ---------------------------------------------------------------- table entries
+// bits 0-3 code length, 4-6 kind, 8-11 extra bits, 16-31 value
+enum : uint32_t { kLit = 0, kLen = 1, kEob = 2, kLong = 3, kBad = 4 };
+
+__device__ __forceinline__ uint32_t mk(uint32_t kind, uint32_t extra, uint32_t val) {
+    return (kind << 4) | (extra << 8) | (val << 16);
+}
+__device__ __forceinline__ uint32_t e_len(uint32_t e) { return e & 15u; }
+__device__ __forceinline__ uint32_t e_kind(uint32_t e) { return (e >> 4) & 7u; }
+__device__ __forceinline__ uint32_t e_extra(uint32_t e) { return (e >> 8) & 15u; }
+__device__ __forceinline__ uint32_t e_val(uint32_t e) { return e >> 16; }
+
+// literal/length alphabet (RFC 1951 3.2.5): 0-255 literal, 256 end of block,
+// 257-285 lengths 3..258; 286/287 (fixed code only) are invalid (inflate.c LEN)
+__device__ __forceinline__ uint32_t litlen_entry(uint32_t sym) {
+    if (sym < 256u) return mk(kLit, 0, sym);
+    if (sym == 256u) return mk(kEob, 0, 0);
+    const uint32_t i = sym - 257u;
+    if (i >= 29u) return mk(kBad, 0, 0);
+    if (i == 28u) return mk(kLen, 0, 258);
+    if (i < 8u) return mk(kLen, 0, 3u + i);
+    const uint32_t x = (i - 4u) >> 2;
+    return mk(kLen, x, 3u + ((4u + (i & 3u)) << x));
+}
+// distance alphabet: 0-29 distances 1..32768; 30/31 invalid
+__device__ __forceinline__ uint32_t dist_entry(uint32_t sym) {
+    if (sym >= 30u) return mk(kBad, 0, 0);
+    if (sym < 4u) return mk(kLen, 0, 1u + sym);
+    const uint32_t x = (sym - 2u) >> 1;
+    return mk(kLen, x, 1u + ((2u + (sym & 1u)) << x));
+}
+__device__ __forceinline__ uint32_t sym_entry(uint32_t table_kind, uint32_t sym) {
+    if (table_kind == 1) return litlen_entry(sym);
+    if (table_kind == 2) return dist_entry(sym);
+    return mk(kLit, 0, sym);   // code-length alphabet
+}
+
+// A decoder: 1024-entry root table in registers plus the canonical-code
+// limits used by the slow path (lane k holds the value for code length k).
+typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));   // one register tuple, indexed with v_movrels
+
+struct Table {
+    u32x16 root;
+    uint32_t lim;   // (first[k] + count[k]) << (15 - k): left-justified end of the length-k codes
+    uint32_t dlt;   // offs[k] - first[k]: sorted-symbol index of code c of length k is dlt + c
+};
+
+__device__ __forceinline__ uint32_t lookup(const Table &t, uint32_t idx) {
+    return rdlane(t.root[idx >> 6], idx & 63u);
+}
+
+// Canonical decode of a code longer than the root (the bits are LSB-first in bb).
+__device__ __forceinline__ uint32_t slow_entry(const Table &t, const uint16_t *sorted, uint32_t table_kind,
+                                               uint64_t bb, uint32_t lane) {
+    const uint32_t v15 = __builtin_bitreverse32((uint32_t)bb) >> 17;
+    const uint64_t m = __ballot(lane >= 1u && lane <= 15u && t.lim <= v15);
+    const uint32_t l = (uint32_t)__builtin_popcountll(m) + 1u;
+    if (l > 15u) return mk(kBad, 0, 0);
+    const uint32_t idx = rdlane(t.dlt, l) + (v15 >> (15u - l));
+    const uint32_t sym = rfl(sorted[idx]);
+    return sym_entry(table_kind, sym) | l;
+}
+
+// Builds the decoder for code lengths lens[0..n) (LDS).  table_kind 0 = code
+// lengths (must be complete), 1 = literal/length, 2 = distance (an incomplete
+// code is accepted only when it is a single 1-bit code; an empty one decodes
+// nothing).  Same acceptance as oracle build() / inflate_table (inftrees.c:32).
+__device__ __forceinline__ bool build_table(const uint8_t *lens, uint32_t n, uint32_t table_kind, Table &t, uint16_t *sorted,
+                            uint32_t lane) {
+    uint32_t cnt[16];
+#pragma unroll
+    for (int l = 0; l < 16; l++) cnt[l] = 0;
+    for (uint32_t c = 0; c < n; c += kWave) {
+        const uint32_t s = c + lane;
+        const uint32_t len = s < n ? lens[s] : 0u;
+#pragma unroll
+        for (uint32_t l = 1; l <= 15; l++) cnt[l] += (uint32_t)__builtin_popcountll(__ballot(len == l));
+    }
+    uint32_t maxl = 0;
+#pragma unroll
+    for (uint32_t l = 1; l <= 15; l++) if (cnt[l]) maxl = l;
+    if (maxl == 0 && table_kind == 0) return false;
+    int32_t left = 1;
+#pragma unroll
+    for (uint32_t l = 1; l <= 15; l++) {
+        left = left * 2 - (int32_t)cnt[l];
+        if (left < 0) return false;                              // over-subscribed
+    }
+    if (left > 0 && (table_kind == 0 || maxl != 1)) return false;   // incomplete
+    // canonical first codes, sorted-symbol offsets, left-justified limits
+    uint32_t run[16], lim_s[16], dlt_s[16];
+    {
+        uint32_t first = 0, offs = 0;
+#pragma unroll
+        for (uint32_t l = 1; l <= 15; l++) {
+            run[l] = offs;
+            dlt_s[l] = offs - first;
+            lim_s[l] = (first + cnt[l]) << (15 - l);
+            offs += cnt[l];
+            first = (first + cnt[l]) << 1;
+        }
+    }
+    t.lim = 0xFFFFFFFFu;
+    t.dlt = 0;
+#pragma unroll
+    for (uint32_t l = 1; l <= 15; l++)
+        if (lane == l) { t.lim = lim_s[l]; t.dlt = dlt_s[l]; }
+    // symbols sorted by (length, value)
+    for (uint32_t c = 0; c < n; c += kWave) {
+        const uint32_t s = c + lane;
+        const uint32_t len = s < n ? lens[s] : 0u;
+        uint32_t pos = 0;
+#pragma unroll
+        for (uint32_t l = 1; l <= 15; l++) {
+            const uint64_t m = __ballot(len == l);
+            if (len == l) pos = run[l] + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+            run[l] += (uint32_t)__builtin_popcountll(m);
+        }
+        if (len) sorted[pos] = (uint16_t)s;
+    }
+    // root table: entry idx holds the code whose first 10 bits (LSB-first) are idx
+    uint32_t sidx[16], l_of[16];
+#pragma unroll
+    for (uint32_t r = 0; r < 16; r++) {
+        const uint32_t v = __builtin_bitreverse32(r * kWave + lane) >> 22;
+        const uint32_t vlj = v << 5;
+        uint32_t l = 1, d = dlt_s[1];
+#pragma unroll
+        for (uint32_t k = 1; k <= 15; k++) {
+            if (lim_s[k] <= vlj) {
+                l = k + 1;
+                d = k < 15 ? dlt_s[k < 15 ? k + 1 : 15] : 0u;
+            }
+        }
+        l_of[r] = l;
+        sidx[r] = l <= 10 ? d + (v >> (10 - l)) : 0u;
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < 16; r++) {
+        const uint32_t l = l_of[r];
+        uint32_t e;
+        if (l <= 10) e = sym_entry(table_kind, sorted[sidx[r]]) | l;
+        else if (l <= 15) e = mk(kLong, 0, 0);
+        else e = mk(kBad, 0, 0);
+        t.root[r] = e;
+    }
+    return true;
+}
+
+// The fixed codes of RFC 1951 3.2.6, computed per entry.
+__device__ __forceinline__ void fixed_tables(Table &L, Table &D, uint32_t lane) {
+#pragma unroll
+    for (uint32_t r = 0; r < 16; r++) {
+        const uint32_t v = __builtin_bitreverse32(r * kWave + lane) >> 22;
+        uint32_t sym, len;
+        if ((v >> 3) < 24u) { sym = 256u + (v >> 3); len = 7; }
+        else if ((v >> 2) < 192u) { sym = (v >> 2) - 48u; len = 8; }
+        else if ((v >> 2) < 200u) { sym = 280u + (v >> 2) - 192u; len = 8; }
+        else { sym = 144u + (v >> 1) - 400u; len = 9; }
+        L.root[r] = litlen_entry(sym) | len;
+        D.root[r] = dist_entry(v >> 5) | 5u;
+    }
+    L.lim = D.lim = 0xFFFFFFFFu;
+    L.dlt = D.dlt = 0;
+}
+
+// ---------------------------------------------------------------- bit reader
+struct BitReader {
+    uint64_t bb;         // bit buffer, next bit at bit 0
+    uint32_t bc;         // valid bits in bb (may run past the end of the stream: avail guards)
+    uint32_t inpos;      // stream byte that enters bb next
+    int32_t avail;       // stream bits not yet consumed
+    const uint32_t *s4;  // stream start rounded down to 4 bytes
+    uint32_t h;          // stream start & 3
+    uint32_t nd;         // dwords of s4 that hold stream bytes
+    uint32_t wbase;      // byte offset (from s4) of window A
+    uint32_t wa, wb;     // window A = s4 bytes [wbase, wbase+256), B = the next 256
+};
+
+__device__ __forceinline__ uint32_t load_win(const BitReader &r, uint32_t base, uint32_t lane) {
+    const uint32_t q = (base >> 2) + lane;
+    return q < r.nd ? __builtin_nontemporal_load(r.s4 + q) : 0u;
+}
+
+__device__ __forceinline__ void refill(BitReader &r, uint32_t lane) {
+    if (r.bc >= 32) return;
+    uint32_t rel = r.inpos + r.h - r.wbase;
+    if (rel >= 256u) {
+        r.wa = r.wb;
+        r.wbase += 256u;
+        r.wb = load_win(r, r.wbase + 256u, lane);
+        rel -= 256u;
+    }
+    const uint32_t q = rel >> 2, sh = (rel & 3u) * 8u;
+    const uint32_t d0 = rdlane(r.wa, q);
+    const uint32_t d1 = q + 1 < 64u ? rdlane(r.wa, q + 1) : rdlane(r.wb, 0);
+    const uint32_t w = (uint32_t)((((uint64_t)d1 << 32) | d0) >> sh);
+    r.bb |= (uint64_t)w << r.bc;
+    r.bc += 32;
+    r.inpos += 4;
+}
+
+__device__ __forceinline__ uint32_t take(BitReader &r, uint32_t n) {
+    const uint32_t v = (uint32_t)(r.bb & ((1ull << n) - 1ull));
+    r.bb >>= n;
+    r.bc -= n;
+    r.avail -= (int32_t)n;
+    return v;
+}
+
+// restart the reader at stream byte pos (after a stored block)
+__device__ __forceinline__ void seek(BitReader &r, uint32_t pos, uint32_t lane) {
+    r.bb = 0;
+    r.bc = 0;
+    r.inpos = pos;
+    r.wbase = (pos + r.h) & ~255u;
+    r.wa = load_win(r, r.wbase, lane);
+    r.wb = load_win(r, r.wbase + 256u, lane);
+}
+
+// v_writelane: lane j of v takes the (uniform) value x
+__device__ __forceinline__ uint32_t put_lane(uint32_t v, uint32_t j, uint32_t x, uint32_t lane) {
+    return lane == j ? x : v;
+}
+
+__device__ __forceinline__ uint32_t mod_small(uint32_t i, uint32_t m) {
+    // i % m for i < 2^20, m >= 1 without an integer divide
+    uint32_t q = (uint32_t)((float)i * __frcp_rn((float)m));
+    int32_t r = (int32_t)i - (int32_t)(q * m);
+    if (r < 0) r += (int32_t)m;
+    if (r >= (int32_t)m) r -= (int32_t)m;
+    return (uint32_t)r;
+}
+
+// ------------------------------------------------------------- batched output
+struct Pending {
+    uint32_t lit;    // lane j: (position << 8) | byte of the j-th pending literal
+    uint32_t md;     // lane j: destination of the j-th pending match
+    uint32_t mx;     // lane j: distance | length << 16
+    uint32_t nlit, nmat;
+};
+
+__device__ __forceinline__ void flush_literals(Pending &q, uint8_t *out, uint32_t lane) {
+    if (lane < q.nlit) out[q.lit >> 8] = (uint8_t)q.lit;
+    q.nlit = 0;
+}
+
+// Applies the pending matches in stream order semantics (RFC 1951 3.2.3: a copy
+// may overlap its own output).  Literals must have been flushed.
+__device__ __forceinline__ void flush_matches(Pending &q, uint8_t *out, uint32_t lane) {
+    const bool act = lane < q.nmat;
+    const int32_t d = (int32_t)q.md;
+    const int32_t off = (int32_t)(q.mx & 0xFFFFu);
+    const int32_t ml = (int32_t)(q.mx >> 16);
+    const int32_t src_end = d - off + min(ml, off);
+    uint64_t pending = __ballot(act);
+    const uint64_t shortm = __ballot(act && ml <= 64);
+    const uint32_t dpk = (uint32_t)d | ((uint32_t)off << 16);
+    const uint32_t grp = lane >> 4, gl = lane & 15u;
+    q.nmat = 0;
+    while (pending) {
+        const uint32_t f = (uint32_t)__builtin_ctzll(pending);
+        const int32_t F = (int32_t)rdlane((uint32_t)d, f);
+        if (!((shortm >> f) & 1ull)) {
+            const int32_t mlf = (int32_t)rdlane((uint32_t)ml, f);
+            const int32_t fo = (int32_t)rdlane((uint32_t)off, f);
+            const int32_t fs = F - fo;
+            if (fo >= (int32_t)kWave) {
+                for (int32_t i = (int32_t)lane; i < mlf; i += kWave) out[F + i] = out[fs + i];
+            } else {
+                for (int32_t i = (int32_t)lane; i < mlf; i += kWave)
+                    out[F + i] = out[fs + (int32_t)mod_small((uint32_t)i, (uint32_t)fo)];
+            }
+            pending &= ~(1ull << f);
+            continue;
+        }
+        uint64_t ready = pending & shortm & __ballot(src_end <= F);
+        uint32_t gpk = 0, gml = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++) {
+            if (ready) {
+                const uint32_t r = (uint32_t)__builtin_ctzll(ready);
+                ready &= ready - 1;
+                pending &= ~(1ull << r);
+                const uint32_t pk = rdlane(dpk, r), mlr = rdlane((uint32_t)ml, r);
+                if (grp == k) { gpk = pk; gml = mlr; }
+            }
+        }
+        const int32_t md = (int32_t)(gpk & 0xFFFFu), mo = (int32_t)(gpk >> 16), mm = (int32_t)gml;
+        const int32_t ms = md - mo;
+        for (int32_t i = (int32_t)gl; i < mm; i += 16) {
+            const int32_t si = (mo >= 16 || mo >= mm) ? i : (int32_t)mod_small((uint32_t)i, (uint32_t)mo);
+            out[md + i] = out[ms + si];
+        }
+    }
+}
+
+// adler32 (adler32.c:65) of out[0..n) in LDS: A = 1 + sum b_i, B = n + sum (n - i) b_i, mod 65521
+__device__ __forceinline__ uint32_t adler_lds(const uint8_t *out, uint32_t n, uint32_t lane) {
+    uint32_t A = 0;
+    uint64_t B = 0;
+    for (uint32_t i = lane * 4u; i < n; i += 4u * kWave) {
+        uint32_t w = *(const uint32_t *)(out + i);
+        const uint32_t rem = n - i;
+        if (rem < 4u) w &= (1u << (8u * rem)) - 1u;
+        const uint32_t b0 = w & 255u, b1 = (w >> 8) & 255u, b2 = (w >> 16) & 255u, b3 = w >> 24;
+        const uint32_t s = b0 + b1 + b2 + b3;
+        A += s;
+        B += (uint64_t)rem * s - (b1 + 2u * b2 + 3u * b3);
+    }
+    const int32_t a = wave_incl_sum((int32_t)(A % 65521u));
+    const int32_t b = wave_incl_sum((int32_t)(uint32_t)(B % 65521u));
+    const uint32_t at = (1u + rdlane((uint32_t)a, kWave - 1)) % 65521u;
+    const uint32_t bt = (n % 65521u + rdlane((uint32_t)b, kWave - 1)) % 65521u;
+    return (bt << 16) | at;
+}
+
+// code-length code order (RFC 1951 3.2.7), 5 bits per entry
+__device__ __forceinline__ uint32_t cl_order(uint32_t i) {
+    // 16 17 18 0 8 7 9 6 10 5 11 4 | 12 3 13 2 14 1 15
+    const uint64_t lo = 16ull | 17ull << 5 | 18ull << 10 | 0ull << 15 | 8ull << 20 | 7ull << 25 | 9ull << 30 |
+                        6ull << 35 | 10ull << 40 | 5ull << 45 | 11ull << 50 | 4ull << 55;
+    const uint64_t hi = 12ull | 3ull << 5 | 13ull << 10 | 2ull << 15 | 14ull << 20 | 1ull << 25 | 15ull << 30;
+    return (uint32_t)((i < 12 ? lo >> (5 * i) : hi >> (5 * (i - 12))) & 31u);
+}
+
+// Decodes one zlib stream into out (LDS, cap bytes).  Returns the decoded
+// length or kZData / kZBuf, as oracle_zlib_uncompress.
+__device__ __forceinline__ int32_t inflate_page(BitReader &r, const uint8_t *src, uint8_t *out, int32_t cap, uint8_t *lens,
+                                uint16_t *sortL, uint16_t *sortD, uint32_t lane) {
+    refill(r, lane);
+    if (r.avail < 16) return kZData;
+    const uint32_t cmf = take(r, 8), flg = take(r, 8);
+    if (((cmf << 8) | flg) % 31u) return kZData;
+    if ((cmf & 15u) != 8u) return kZData;
+    if ((cmf >> 4) + 8u > 15u) return kZData;
+    if (flg & 0x20u) return kZData;
+    Table L, D;
+    Pending q;
+    q.lit = q.md = q.mx = 0;
+    q.nlit = q.nmat = 0;
+    int32_t op = 0;
+    uint32_t last;
+    do {
+        refill(r, lane);
+        if (r.avail < 3) return kZData;
+        last = take(r, 1);
+        const uint32_t type = take(r, 2);
+        if (type == 0) {
+            // stored block (inflate.c STORED/COPY)
+            take(r, r.bc & 7u);
+            refill(r, lane);
+            if (r.avail < 32) return kZData;
+            const uint32_t len = take(r, 16), nlen = take(r, 16);
+            if (len != (~nlen & 0xFFFFu)) return kZData;
+            const uint32_t A = (uint32_t)r.avail >> 3;
+            const uint32_t P = r.inpos - (r.bc >> 3);
+            const uint32_t R = (uint32_t)(cap - op);
+            if (len > min(A, R)) return A <= R ? kZData : kZBuf;
+            for (uint32_t j = lane; j < len; j += kWave) out[op + (int32_t)j] = src[P + j];
+            op += (int32_t)len;
+            r.avail -= (int32_t)(len * 8u);
+            seek(r, P + len, lane);
+            continue;
+        }
+        if (type == 3) return kZData;
+        if (type == 1) {
+            fixed_tables(L, D, lane);
+        } else {
+            refill(r, lane);
+            if (r.avail < 14) return kZData;
+            const uint32_t nlen = take(r, 5) + 257u, ndist = take(r, 5) + 1u, ncode = take(r, 4) + 4u;
+            if (nlen > 286u || ndist > 30u) return kZData;
+            if (r.avail < (int32_t)(3u * ncode)) return kZData;
+            uint32_t clv = 0;
+            for (uint32_t i = 0; i < ncode; i++) {
+                refill(r, lane);
+                clv = put_lane(clv, cl_order(i), take(r, 3), lane);
+            }
+            if (lane < 19u) lens[lane] = (uint8_t)clv;
+            if (!build_table(lens, 19, 0, L, sortL, lane)) return kZData;
+            const uint32_t total = nlen + ndist;
+            uint32_t n = 0, prev = 0;
+            while (n < total) {
+                refill(r, lane);
+                const uint32_t e = lookup(L, (uint32_t)r.bb & 1023u);
+                const uint32_t l = e_len(e);
+                if (e_kind(e) != kLit || (int32_t)l > r.avail) return kZData;
+                take(r, l);
+                const uint32_t sym = e_val(e);
+                if (sym < 16u) {
+                    if (lane == 0) lens[n] = (uint8_t)sym;
+                    prev = sym;
+                    n++;
+                    continue;
+                }
+                uint32_t rep, val = 0;
+                if (sym == 16u) {
+                    if (n == 0) return kZData;
+                    if (r.avail < 2) return kZData;
+                    val = prev;
+                    rep = 3u + take(r, 2);
+                } else if (sym == 17u) {
+                    if (r.avail < 3) return kZData;
+                    rep = 3u + take(r, 3);
+                } else {
+                    if (r.avail < 7) return kZData;
+                    rep = 11u + take(r, 7);
+                }
+                if (n + rep > total) return kZData;
+                for (uint32_t j = lane; j < rep; j += kWave) lens[n + j] = (uint8_t)val;
+                prev = val;
+                n += rep;
+            }
+            if (rfl(lens[256]) == 0) return kZData;
+            if (!build_table(lens, nlen, 1, L, sortL, lane)) return kZData;
+            if (!build_table(lens + nlen, ndist, 2, D, sortD, lane)) return kZData;
+        }
+        // ---- compressed data (inflate.c LEN/DIST; inffast.c)
+        for (;;) {
+            refill(r, lane);
+            uint32_t e = lookup(L, (uint32_t)r.bb & 1023u);
+            if (e_kind(e) == kLong) e = slow_entry(L, sortL, 1, r.bb, lane);
+            uint32_t l = e_len(e), kind = e_kind(e);
+            if (kind == kBad || (int32_t)l > r.avail) return kZData;
+            take(r, l);
+            if (kind == kLit) {
+                if (op >= cap) return kZBuf;
+                q.lit = put_lane(q.lit, q.nlit, ((uint32_t)op << 8) | e_val(e), lane);
+                op++;
+                if (++q.nlit == kWave) flush_literals(q, out, lane);
+                continue;
+            }
+            if (kind == kEob) break;
+            uint32_t x = e_extra(e);
+            if ((int32_t)x > r.avail) return kZData;
+            const uint32_t len = e_val(e) + take(r, x);
+            refill(r, lane);
+            e = lookup(D, (uint32_t)r.bb & 1023u);
+            if (e_kind(e) == kLong) e = slow_entry(D, sortD, 2, r.bb, lane);
+            l = e_len(e);
+            if (e_kind(e) == kBad || (int32_t)l > r.avail) return kZData;
+            take(r, l);
+            x = e_extra(e);
+            if ((int32_t)x > r.avail) return kZData;
+            const uint32_t dist = e_val(e) + take(r, x);
+            if ((int32_t)dist > op) return kZData;
+            if (op + (int32_t)len > cap) return kZBuf;
+            q.md = put_lane(q.md, q.nmat, (uint32_t)op, lane);
+            q.mx = put_lane(q.mx, q.nmat, dist | (len << 16), lane);
+            op += (int32_t)len;
+            if (++q.nmat == kWave) {
+                flush_literals(q, out, lane);
+                flush_matches(q, out, lane);
+            }
+        }
+    } while (!last);
+    // adler32 trailer, big-endian, byte aligned (inflate.c CHECK)
+    take(r, r.bc & 7u);
+    refill(r, lane);
+    if (r.avail < 32) return kZData;
+    const uint32_t want = __builtin_bswap32(take(r, 32));
+    flush_literals(q, out, lane);
+    flush_matches(q, out, lane);
+    if (adler_lds(out, (uint32_t)op, lane) != want) return kZData;
+    return op;
+}
+
+__device__ __forceinline__ void reader_init(BitReader &r, const PageRef &p, uint32_t lane) {
+    const uintptr_t a = (uintptr_t)p.src;
+    r.h = (uint32_t)(a & 3u);
+    r.s4 = (const uint32_t *)(a - r.h);
+    r.nd = (r.h + p.src_len + 3u) >> 2;
+    r.avail = (int32_t)(p.src_len * 8u);
+    r.bb = 0;
+    r.bc = 0;
+    r.inpos = 0;
+    r.wbase = 0;
+    (void)lane;
+}
+
+__global__ __launch_bounds__(64) void zlib_inflate_kernel(tyche_batch_t b, uint32_t out_cap, uint32_t off_lens) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint32_t lane = threadIdx.x;
+    uint8_t *out = smem;
+    uint8_t *lens = smem + off_lens;
+    uint16_t *sortL = (uint16_t *)(lens + 320);
+    uint16_t *sortD = sortL + 320;
+    const size_t stride = gridDim.x;
+    size_t page = blockIdx.x;
+    if (page >= b.count) return;
+    PageRef p = batch_page(b, page);
+    BitReader r;
+    reader_init(r, p, lane);
+    r.wa = load_win(r, 0, lane);
+    r.wb = load_win(r, 256, lane);
+    for (;;) {
+        const size_t next = page + stride;
+        // the next page's first 512 stream bytes are loaded behind this page's decode
+        PageRef pn;
+        BitReader rn;
+        if (next < b.count) {
+            pn = batch_page(b, next);
+            reader_init(rn, pn, lane);
+            rn.wa = load_win(rn, 0, lane);
+            rn.wb = load_win(rn, 256, lane);
+        }
+        int32_t rv;
+        if (p.dst_cap > out_cap || p.src_len > 0x0FFFFFFFu) {
+            rv = kResultTooLarge;
+        } else {
+            rv = inflate_page(r, p.src, out, (int32_t)p.dst_cap, lens, sortL, sortD, lane);
+            __syncthreads();
+            if (rv > 0) stage_out(p.dst, out, (uint32_t)rv, lane, kWave);
+        }
+        if (lane == 0) b.results[page] = rv;
+        if (next >= b.count) break;
+        __syncthreads();
+        page = next;
+        p = pn;
+        r = rn;
+    }
+}
+
+}  // namespace
+
+hipError_t launch_zlib_inflate(const tyche_batch_t &b, uint32_t out_cap, hipStream_t s) {
+    if (b.count == 0) return hipSuccess;
+    const uint32_t off_lens = (out_cap + 64u + 15u) & ~15u;
+    const size_t lds = off_lens + 320 + 2 * 320 + 2 * 32;
+    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    static int cus[64] = {0};
+    if (dev < 64 && cus[dev] == 0) {
+        (void)hipFuncSetAttribute((const void *)zlib_inflate_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
+        int n = 0;
+        (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+        cus[dev] = n > 0 ? n : 256;
+    }
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)zlib_inflate_kernel, kWave, lds) !=
+            hipSuccess || per_cu <= 0)
+        per_cu = std::max<int>(1, (int)std::min<size_t>(32, (160 * 1024) / lds));
+    const size_t grid = std::min<size_t>(b.count, (size_t)(dev < 64 ? cus[dev] : 256) * (size_t)per_cu);
+    hipLaunchKernelGGL(zlib_inflate_kernel, dim3((unsigned)grid), dim3(kWave), lds, s, b, out_cap, off_lens);
+    return hipGetLastError();
+}
+
+}  // namespace tyche
