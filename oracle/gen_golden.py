@@ -22,6 +22,14 @@ Fixtures (all data, no reference source):
                       and short inputs, with the input digests
   zlib_malformed.npz  corrupted / truncated / short-capacity zlib streams with the
                       reference uncompress() result (Z_OK length or error code)
+  zstd_streams.npz    reference ZSTD_compress frames (levels 1/3/9/19: raw, RLE and
+                      Huffman 1X/4X literals, predefined / RLE / FSE-compressed
+                      sequence tables), multi-block frames from ZSTD_compressContinue
+                      (no content size, set_repeat tables, carried repeat offsets)
+                      and frames with an XXH64 content checksum, with input digests
+  zstd_malformed.npz  corrupted / truncated / short-capacity frames with the
+                      reference ZSTD_decompress result (size, or -1 for ZSTD_isError)
+                      and the output digest when it succeeds
 """
 from __future__ import annotations
 
@@ -308,6 +316,106 @@ def gen_zlib_malformed():
     print("zlib malformed", len(cases), "errors", sum(r < 0 for r in rvs))
 
 
+def with_checksum(frame: bytes, content: bytes) -> bytes:
+    """Sets the Content_Checksum_flag of a frame and appends XXH64(content) low 32 bits
+    (the layout ZSTD_compressEnd writes, zstd_compress.c:2638-2674); the hash comes
+    from the reference build's ZSTD_XXH64."""
+    b = bytearray(frame)
+    b[4] |= 0x04
+    return bytes(b) + (O.ref_xxh64(content) & 0xFFFFFFFF).to_bytes(4, "little")
+
+
+def zstd_cases():
+    """(label, level, frame, content) for zstd_streams.npz."""
+    out = []
+    for label, data in zlib_inputs():
+        levels = (1,) if not (label.startswith("gen/") or label == "kat" or label.startswith("short")) else (1, 3, 9, 19)
+        for level in levels:
+            out.append((label, level, O.ref_zstd_compress(data, level), data))
+        if label.startswith("gen/0/") or label.startswith("gen/3/") or label == "kat":
+            for chunk in (4096, 1500):
+                if len(data) > chunk:
+                    out.append((label + f"/blocks{chunk}", 1, O.ref_zstd_compress_blocks(data, chunk, 1), data))
+        if label.startswith("gen/1/") or label == "kat":
+            out.append((label + "/xxh64", 1, with_checksum(O.ref_zstd_compress(data, 1), data), data))
+    return out
+
+
+def gen_zstd_streams():
+    labels, levels, comps, digests, sizes = [], [], [], [], []
+    for label, level, c, data in zstd_cases():
+        r, out = O.ref_zstd_decompress(c, len(data))
+        assert r == len(data) and out == data, label
+        labels.append(label)
+        levels.append(level)
+        comps.append(c)
+        digests.append(sha(data))
+        sizes.append(len(data))
+    data, offs, lens = pack(comps)
+    np.savez_compressed(os.path.join(OUT, "zstd_streams.npz"), seed=np.int64(SEED), labels=np.array(labels),
+                        level=np.array(levels, np.int64), comp=data, comp_off=offs, comp_len=lens,
+                        size=np.array(sizes, np.int64),
+                        digest=np.frombuffer(b"".join(digests), np.uint8).reshape(-1, 32))
+    print("zstd streams", len(labels), data.size)
+
+
+def gen_zstd_malformed():
+    rng = np.random.default_rng(SEED + 3)
+    cases = []   # (frame, out_cap)
+    srcs = [O.pagegen(1, 16384, seed=SEED, first=9100 + k, dist=k % 4)[0].tobytes() for k in range(3)]
+    srcs.append(kat_text())
+    frames = [O.ref_zstd_compress(d, 1) for d in srcs] + [O.ref_zstd_compress(srcs[0], 19),
+                                                          O.ref_zstd_compress_blocks(srcs[1], 1500, 1),
+                                                          with_checksum(O.ref_zstd_compress(srcs[3], 1), srcs[3])]
+    sizes = [len(d) for d in srcs] + [len(srcs[0]), len(srcs[1]), len(srcs[3])]
+    for s, n_out in zip(frames, sizes):
+        n = len(s)
+        for cut in sorted(set([1, 4, 5, 8, 9, 12, n // 3, n // 2, n - 5, n - 4, n - 1])):
+            if 0 < cut < n:
+                cases.append((s[:cut], n_out))
+        for _ in range(24):
+            b = bytearray(s)
+            for _ in range(int(rng.integers(1, 3))):
+                b[int(rng.integers(0, n))] ^= 1 << int(rng.integers(0, 8))
+            cases.append((bytes(b), n_out))
+        for _ in range(8):
+            b = bytearray(s)
+            i = int(rng.integers(0, n))
+            b[i:i + 4] = rng.integers(0, 256, 4, dtype=np.uint8).tobytes()
+            cases.append((bytes(b[:n]), n_out))
+        cases.append((s, n_out - 1))            # output one byte short
+        cases.append((s, n_out + 100))          # larger capacity
+        cases.append((s + b"\x00", n_out))       # trailing byte
+    for _ in range(20):
+        ln = int(rng.integers(1, 200))
+        cases.append((rng.integers(0, 256, ln, dtype=np.uint8).tobytes(), 4096))
+    for _ in range(20):   # valid magic + single-segment header, random body
+        ln = int(rng.integers(1, 200))
+        cases.append((b"\x28\xb5\x2f\xfd\x20\x40" + rng.integers(0, 256, ln, dtype=np.uint8).tobytes(), 4096))
+    cases += [
+        (b"", 16), (b"\x28\xb5\x2f\xfd", 16), (b"\x28\xb5\x2f\xfd\x20\x00\x01\x00\x00", 16),  # empty raw block
+        (b"\x28\xb5\x2f\xfd\x20\x05\x29\x00\x00hello", 16),     # raw block "hello"
+        (b"\x28\xb5\x2f\xfd\x20\x07\x3b\x00\x00x", 16),         # RLE block of 7 'x'
+        (b"\x28\xb5\x2f\xfd\x20\x07\x3b\x00\x00x", 6),          # RLE block too long for capacity
+        (b"\x28\xb5\x2f\xfd\x28\x05\x29\x00\x00hello", 16),     # reserved FHD bit
+        (b"\x28\xb5\x2f\xfd\x20\x05\x2f\x00\x00hello", 16),     # reserved block type
+        (b"\x50\x2a\x4d\x18\x00\x00\x00\x00\x01\x00\x00", 16),  # skippable magic
+        (b"\x28\xb5\x2f\xfd\x21\x05\x01\x29\x00\x00hello", 16),  # dictionary id
+    ]
+    streams_out, caps, rvs, digs = [], [], [], []
+    for s, cap in cases:
+        r, out = O.ref_zstd_decompress(s, cap)
+        streams_out.append(s)
+        caps.append(cap)
+        rvs.append(r)
+        digs.append(sha(out) if r >= 0 else b"\0" * 32)
+    data, offs, lens = pack(streams_out)
+    np.savez_compressed(os.path.join(OUT, "zstd_malformed.npz"), comp=data, comp_off=offs, comp_len=lens,
+                        cap=np.array(caps, np.int64), rv=np.array(rvs, np.int64),
+                        digest=np.frombuffer(b"".join(digs), np.uint8).reshape(-1, 32))
+    print("zstd malformed", len(cases), "errors", sum(r < 0 for r in rvs))
+
+
 if __name__ == "__main__":
     if not O.have_ref():
         sys.exit("oracle/_ref/libtyche_ref.so missing: run `make -C oracle ref` where /root/reference exists")
@@ -318,3 +426,5 @@ if __name__ == "__main__":
     gen_malformed()
     gen_zlib_streams()
     gen_zlib_malformed()
+    gen_zstd_streams()
+    gen_zstd_malformed()

@@ -1,5 +1,6 @@
 /* oracle/oracle.h -- TEST INFRASTRUCTURE ONLY (see lz4_oracle.c header). */
 #pragma once
+#include <stddef.h>
 #include <stdint.h>
 #ifdef __cplusplus
 extern "C" {
@@ -16,6 +17,10 @@ long oracle_lz4_decompress_pages(const uint8_t *src, uint64_t src_stride, const 
 /* zlib (RFC 1950/1951) restatement: decoded length or negative zlib code */
 int oracle_zlib_uncompress(const uint8_t *src, int srclen, uint8_t *dst, int dstcap);
 uint32_t oracle_adler32(const uint8_t *p, int n);
+/* zstd v1.1.2 frame decoder restatement: decoded size or negative error */
+int oracle_zstd_decompress(const uint8_t *src, int srclen, uint8_t *dst, int dstcap);
+int oracle_zstd_compress_bound(int n);
+uint64_t oracle_xxh64(const uint8_t *p, size_t len, uint64_t seed);
 /* host copy of the synthetic page generator (tyche_amd/csrc/pagegen.h) */
 void oracle_pagegen(uint8_t *dst, uint64_t dst_stride, uint32_t page_len, uint64_t seed, uint64_t first,
                     long count, uint32_t dist);

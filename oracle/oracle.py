@@ -70,6 +70,12 @@ class _Lib:
             lib.oracle_zlib_uncompress.restype = ctypes.c_int
             lib.oracle_adler32.argtypes = [_u8p, ctypes.c_int]
             lib.oracle_adler32.restype = ctypes.c_uint32
+            lib.oracle_zstd_decompress.argtypes = [_u8p, ctypes.c_int, _u8p, ctypes.c_int]
+            lib.oracle_zstd_decompress.restype = ctypes.c_int
+            lib.oracle_zstd_compress_bound.argtypes = [ctypes.c_int]
+            lib.oracle_zstd_compress_bound.restype = ctypes.c_int
+            lib.oracle_xxh64.argtypes = [_u8p, ctypes.c_size_t, ctypes.c_uint64]
+            lib.oracle_xxh64.restype = ctypes.c_uint64
             cls._oracle = lib
         return cls._oracle
 
@@ -99,6 +105,18 @@ class _Lib:
             lib.ZSTD_compressBound.restype = ctypes.c_size_t
             lib.ZSTD_isError.argtypes = [ctypes.c_size_t]
             lib.ZSTD_isError.restype = ctypes.c_uint
+            lib.ZSTD_createCCtx.argtypes = []
+            lib.ZSTD_createCCtx.restype = ctypes.c_void_p
+            lib.ZSTD_freeCCtx.argtypes = [ctypes.c_void_p]
+            lib.ZSTD_freeCCtx.restype = ctypes.c_size_t
+            lib.ZSTD_compressBegin.argtypes = [ctypes.c_void_p, ctypes.c_int]
+            lib.ZSTD_compressBegin.restype = ctypes.c_size_t
+            for name in ("ZSTD_compressContinue", "ZSTD_compressEnd"):
+                f = getattr(lib, name)
+                f.argtypes = [ctypes.c_void_p, _u8p, ctypes.c_size_t, _u8p, ctypes.c_size_t]
+                f.restype = ctypes.c_size_t
+            lib.ZSTD_XXH64.argtypes = [_u8p, ctypes.c_size_t, ctypes.c_ulonglong]
+            lib.ZSTD_XXH64.restype = ctypes.c_ulonglong
             cls._ref = lib
         return cls._ref
 
@@ -149,6 +167,25 @@ def zlib_uncompress(comp, out_cap: int) -> tuple[int, bytes]:
     dst = np.zeros(max(out_cap, 1), dtype=np.uint8)
     r = _Lib.oracle().oracle_zlib_uncompress(_ptr(srcbuf), src.size, _ptr(dst), out_cap)
     return r, (dst[:r].tobytes() if r > 0 else b"")
+
+
+def zstd_decompress(comp, out_cap: int) -> tuple[int, bytes]:
+    """ZSTD_decompress restated (zstd_decompress.c:1459): (decoded size or negative error, bytes)."""
+    src = _as_u8(comp)
+    srcbuf = np.zeros(src.size + 16, dtype=np.uint8)
+    srcbuf[:src.size] = src
+    dst = np.zeros(max(out_cap, 1) + 16, dtype=np.uint8)
+    r = _Lib.oracle().oracle_zstd_decompress(_ptr(srcbuf), src.size, _ptr(dst), out_cap)
+    return r, (dst[:r].tobytes() if r > 0 else b"")
+
+
+def zstd_bound(n: int) -> int:
+    return _Lib.oracle().oracle_zstd_compress_bound(n)
+
+
+def xxh64(data, seed: int = 0) -> int:
+    src = _as_u8(data)
+    return int(_Lib.oracle().oracle_xxh64(_ptr(src), src.size, seed))
 
 
 def adler32(data) -> int:
@@ -228,3 +265,49 @@ def ref_zstd_compress(data, level: int = 1) -> bytes:
     r = lib.ZSTD_compress(_ptr(dst), cap, _ptr(src), src.size, level)
     assert not lib.ZSTD_isError(r)
     return dst[:r].tobytes()
+
+
+def ref_zstd_decompress(comp, out_cap: int) -> tuple[int, bytes]:
+    """The reference's ZSTD_decompress: (decoded size, or -1 when ZSTD_isError, bytes)."""
+    lib = _Lib.ref()
+    src = _as_u8(comp)
+    srcbuf = np.zeros(src.size + 16, dtype=np.uint8)
+    srcbuf[:src.size] = src
+    dst = np.zeros(max(out_cap, 1) + 16, dtype=np.uint8)
+    r = lib.ZSTD_decompress(_ptr(dst), out_cap, _ptr(srcbuf), src.size)
+    if lib.ZSTD_isError(r):
+        return -1, b""
+    return int(r), dst[:r].tobytes()
+
+
+def ref_zstd_compress_blocks(data, chunk: int, level: int = 1) -> bytes:
+    """A multi-block frame: ZSTD_compressBegin + ZSTD_compressContinue per `chunk`
+    bytes + ZSTD_compressEnd (zstd_compress.c), i.e. no content size in the header,
+    one block per chunk, entropy tables and repeat offsets carried across blocks."""
+    lib = _Lib.ref()
+    src = _as_u8(data)
+    cap = lib.ZSTD_compressBound(src.size) + 64 * (src.size // max(chunk, 1) + 2)
+    dst = np.zeros(cap, dtype=np.uint8)
+    cctx = lib.ZSTD_createCCtx()
+    try:
+        assert not lib.ZSTD_isError(lib.ZSTD_compressBegin(cctx, level))
+        pos = out = 0
+        base = src.ctypes.data
+        while True:
+            n = min(chunk, src.size - pos)
+            last = pos + n >= src.size
+            f = lib.ZSTD_compressEnd if last else lib.ZSTD_compressContinue
+            r = f(cctx, ctypes.cast(dst.ctypes.data + out, _u8p), cap - out, ctypes.cast(base + pos, _u8p), n)
+            assert not lib.ZSTD_isError(r), r
+            out += r
+            pos += n
+            if last:
+                break
+    finally:
+        lib.ZSTD_freeCCtx(cctx)
+    return dst[:out].tobytes()
+
+
+def ref_xxh64(data, seed: int = 0) -> int:
+    src = _as_u8(data)
+    return int(_Lib.ref().ZSTD_XXH64(_ptr(src), src.size, seed))

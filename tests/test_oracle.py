@@ -155,3 +155,50 @@ def test_zlib_malformed(oracle_mod):
         else:
             assert rv < 0, (i, rv, want)
             assert rv == want or {rv, want} == {-3, -5}, (i, rv, want)
+
+
+# ----------------------------------------------------------------- zstd (A9)
+def test_zstd_kat(oracle_mod):
+    """src/tests.c:415-436: zstd level 1 of the Lorem KAT is 1709 bytes and decodes back."""
+    O = oracle_mod
+    g = load_golden("kat_lorem.npz")
+    rv, out = O.zstd_decompress(g["zstd"].tobytes(), 4096)
+    assert rv == 4096 and out == g["text"].tobytes()
+
+
+def test_zstd_streams_exact(oracle_mod):
+    """Reference ZSTD_compress frames at levels 1/3/9/19, multi-block ZSTD_compressContinue
+    frames and XXH64-checksummed frames decode to the original bytes."""
+    O = oracle_mod
+    g = load_golden("zstd_streams.npz")
+    kinds = set()
+    for i in range(len(g["labels"])):
+        s = unpack(g["comp"], g["comp_off"], g["comp_len"], i)
+        n = int(g["size"][i])
+        rv, out = O.zstd_decompress(s, n)
+        assert rv == n, (g["labels"][i], g["level"][i], rv)
+        assert hashlib.sha256(out).digest() == g["digest"][i].tobytes()
+        kinds.add(s[4])   # frame header descriptors seen
+    assert len(kinds) >= 3
+
+
+def test_zstd_malformed(oracle_mod):
+    """Reference ZSTD_decompress verdicts on corrupted / truncated / short-capacity frames:
+    error where the reference errs (buffer.c:264-266 only tests ZSTD_isError), otherwise the
+    same size and bytes -- including frames whose corruption the reference does not detect."""
+    O = oracle_mod
+    g = load_golden("zstd_malformed.npz")
+    for i in range(len(g["cap"])):
+        s = unpack(g["comp"], g["comp_off"], g["comp_len"], i)
+        rv, out = O.zstd_decompress(s, int(g["cap"][i]))
+        want = int(g["rv"][i])
+        if want >= 0:
+            assert rv == want, (i, rv, want)
+            assert hashlib.sha256(out).digest() == g["digest"][i].tobytes()
+        else:
+            assert rv < 0, (i, rv, want)
+
+
+def test_zstd_xxh64_known_answer(oracle_mod):
+    """XXH64 of the empty input with seed 0 (published xxHash test vector)."""
+    assert oracle_mod.xxh64(b"") == 0xEF46DB3751D8E999
