@@ -1,0 +1,210 @@
+"""GPU parity for the gfx950 zstd decoder, called through the
+C ABI, against the reference's frames and the restatement oracle.
+
+* frames made by the reference's own ZSTD_compress at levels 1/3/9/19, the
+  multi-block frames of ZSTD_compressContinue and XXH64-checksummed frames
+  (tests/golden/zstd_streams.npz) decode bit-exactly, at several byte
+  alignments of the staged frame;
+* every corrupted / truncated / short-capacity frame of
+  tests/golden/zstd_malformed.npz gets the reference's verdict: the same size
+  and bytes where ZSTD_decompress succeeds, an error where it fails
+  (buffer.c:264-266 only tests ZSTD_isError);
+* seeded corruptions of the reference frames agree with the oracle
+  (oracle/zstd_oracle.c, pinned to the reference by tests/test_oracle.py);
+* the Buffer API (accepts any non-error result) and a 16K-page batch.
+"""
+import ctypes
+import hashlib
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_golden, unpack
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda:0")
+ZSTD = 3
+
+
+@pytest.fixture(scope="module")
+def tc():
+    from tyche_amd import _lib, codec
+    lib = _lib.load()
+    assert lib.tyche_device_ready() == 1, _lib.last_error()
+    return codec
+
+
+def ragged_decode(tc, streams, caps, shift=0, codec_id=ZSTD):
+    """Decode byte strings (each placed at a 16-byte boundary + shift) into per-page capacities."""
+    n = len(streams)
+    lens = [len(s) for s in streams]
+    offs = np.zeros(n, np.int64)
+    pos = 0
+    for i, s in enumerate(streams):
+        offs[i] = pos + shift
+        pos += (len(s) + shift + 15) // 16 * 16 + 16
+    buf = np.zeros(pos + 64, np.uint8)
+    for i, s in enumerate(streams):
+        buf[offs[i]:offs[i] + len(s)] = np.frombuffer(s, np.uint8)
+    ooffs = np.zeros(n, np.int64)
+    opos = 0
+    for i, c in enumerate(caps):
+        ooffs[i] = opos
+        opos += (c + 15) // 16 * 16 + 16
+    d_stream = torch.from_numpy(buf).to(DEV)
+    d_out = torch.full((opos + 64,), 0xAB, dtype=torch.uint8, device=DEV)
+    d_offs = torch.from_numpy(offs).to(DEV)
+    d_lens = torch.tensor(lens, dtype=torch.int32, device=DEV)
+    d_caps = torch.tensor(caps, dtype=torch.int32, device=DEV)
+    d_ooffs = torch.from_numpy(ooffs).to(DEV)
+    d_rv = torch.empty(n, dtype=torch.int32, device=DEV)
+    tc.decompress_ragged(d_stream, d_offs, d_lens, d_caps, d_out, d_ooffs, d_rv,
+                         max_src_length=max(lens + [1]), max_capacity=max(caps + [0]), compressor_id=codec_id)
+    torch.cuda.synchronize()
+    rv = d_rv.cpu().numpy()
+    out = d_out.cpu().numpy()
+    return rv, [out[ooffs[i]:ooffs[i] + max(int(rv[i]), 0)].tobytes() for i in range(n)]
+
+
+def test_zstd_kat(tc):
+    """src/tests.c:415-436: the 1709-byte zstd-1 encoding of the Lorem KAT."""
+    g = load_golden("kat_lorem.npz")
+    rv, outs = ragged_decode(tc, [g["zstd"].tobytes()], [4096])
+    assert rv[0] == 4096 and outs[0] == g["text"].tobytes()
+
+
+@pytest.mark.parametrize("shift", [0, 1, 3, 7])
+def test_zstd_reference_frames(tc, shift):
+    g = load_golden("zstd_streams.npz")
+    streams = [unpack(g["comp"], g["comp_off"], g["comp_len"], i) for i in range(len(g["labels"]))]
+    caps = [int(x) for x in g["size"]]
+    rv, outs = ragged_decode(tc, streams, caps, shift)
+    for i in range(len(streams)):
+        assert rv[i] == caps[i], (g["labels"][i], int(g["level"][i]), rv[i])
+        assert hashlib.sha256(outs[i]).digest() == g["digest"][i].tobytes(), (g["labels"][i], int(g["level"][i]))
+
+
+def test_zstd_reference_frames_larger_capacity(tc):
+    """dstCapacity above the content size: same bytes, the literal buffer sits at the window tail."""
+    g = load_golden("zstd_streams.npz")
+    streams = [unpack(g["comp"], g["comp_off"], g["comp_len"], i) for i in range(len(g["labels"]))]
+    caps = [int(x) + 777 for x in g["size"]]
+    rv, outs = ragged_decode(tc, streams, caps)
+    for i in range(len(streams)):
+        assert rv[i] == int(g["size"][i]), (g["labels"][i], rv[i])
+        assert hashlib.sha256(outs[i]).digest() == g["digest"][i].tobytes(), g["labels"][i]
+
+
+def test_zstd_malformed(tc, oracle_mod):
+    g = load_golden("zstd_malformed.npz")
+    streams = [unpack(g["comp"], g["comp_off"], g["comp_len"], i) for i in range(len(g["cap"]))]
+    caps = [int(c) for c in g["cap"]]
+    rv, outs = ragged_decode(tc, streams, caps)
+    for i, s in enumerate(streams):
+        want = int(g["rv"][i])
+        if want >= 0:
+            assert rv[i] == want, (i, rv[i], want)
+            assert hashlib.sha256(outs[i]).digest() == g["digest"][i].tobytes(), i
+        else:
+            assert rv[i] < 0, (i, rv[i], want)
+        orv, oout = oracle_mod.zstd_decompress(s, caps[i])
+        assert (orv < 0) == (rv[i] < 0), (i, orv, rv[i])
+
+
+def test_zstd_fuzz_vs_oracle(tc, oracle_mod):
+    """Seeded bit flips, byte stores and truncations of the reference frames: the device verdict
+    and bytes equal the oracle's (success: size and bytes; failure: an error)."""
+    g = load_golden("zstd_streams.npz")
+    base = [unpack(g["comp"], g["comp_off"], g["comp_len"], i) for i in range(len(g["labels"]))]
+    sizes = [int(x) for x in g["size"]]
+    rng = np.random.default_rng(4242)
+    streams, caps = [], []
+    for _ in range(3000):
+        k = int(rng.integers(len(base)))
+        b = bytearray(base[k])
+        mode = int(rng.integers(4))
+        if mode == 0:
+            for _ in range(int(rng.integers(1, 4))):
+                b[int(rng.integers(len(b)))] ^= 1 << int(rng.integers(8))
+        elif mode == 1:
+            b = b[:int(rng.integers(1, len(b)))]
+        elif mode == 2:
+            b[int(rng.integers(len(b)))] = int(rng.integers(256))
+        else:
+            i = int(rng.integers(len(b)))
+            b[i:i + 3] = rng.integers(0, 256, 3, dtype=np.uint8).tobytes()
+        streams.append(bytes(b))
+        caps.append(sizes[k] if rng.random() < 0.85 else int(sizes[k] * rng.random()))
+    rv, outs = ragged_decode(tc, streams, caps)
+    n_ok = 0
+    for i, s in enumerate(streams):
+        orv, oout = oracle_mod.zstd_decompress(s, caps[i])
+        if orv >= 0:
+            n_ok += 1
+            assert rv[i] == orv and outs[i] == oout, (i, rv[i], orv)
+        else:
+            assert rv[i] < 0, (i, rv[i], orv)
+    assert n_ok > 50
+
+
+def test_zstd_buffer_api(tc):
+    """buffer__decompress(ZSTD): any non-error result is accepted (src/buffer.c:263-266)."""
+    from tyche_amd import buffer as B
+    from tyche_amd._lib import E_OK
+    g = load_golden("kat_lorem.npz")
+    text, comp = g["text"].tobytes(), g["zstd"].tobytes()
+
+    def compressed_buffer(data_length, payload):
+        buf = B.new_buffer(b"\0" * data_length, id=9)
+        mem = B._libc.malloc(len(payload))
+        ctypes.memmove(mem, payload, len(payload))
+        B.swap_data(buf, mem)
+        buf.contents.comp_length = len(payload)
+        return buf
+
+    buf = compressed_buffer(4096, comp)
+    assert B.buffer__decompress(buf, ZSTD) == E_OK
+    assert buf.contents.comp_length == 0 and buf.contents.comp_hits == 1
+    assert B.buffer_bytes(buf) == text
+    B.destroy(buf)
+    buf = compressed_buffer(4095, comp)          # dstSize_tooSmall
+    assert B.buffer__decompress(buf, ZSTD) == 126
+    assert buf.contents.comp_length == len(comp)
+    B.destroy(buf)
+    bad = bytearray(comp)
+    bad[0] ^= 1                                   # bad magic
+    buf = compressed_buffer(4096, bytes(bad))
+    assert B.buffer__decompress(buf, ZSTD) == 126
+    B.destroy(buf)
+
+
+def test_zstd_large_batch(tc):
+    """16K fixed-stride slots of reference frames (16 KiB and 32 KiB pages), decoded twice: exact and repeatable."""
+    g = load_golden("zstd_streams.npz")
+    idx = [i for i in range(len(g["labels"])) if g["labels"][i].startswith("gen/") and int(g["size"][i]) == 16384
+           and "/" not in g["labels"][i][len("gen/x/16384/"):]]
+    assert idx
+    frames = [unpack(g["comp"], g["comp_off"], g["comp_len"], i) for i in idx]
+    n, plen = 16384, 16384
+    slot = (max(len(c) for c in frames) + 127) // 128 * 128
+    slots = np.zeros((n, slot), np.uint8)
+    clen = np.zeros(n, np.int32)
+    for i in range(n):
+        c = frames[i % len(frames)]
+        slots[i, :len(c)] = np.frombuffer(c, np.uint8)
+        clen[i] = len(c)
+    d_slots = torch.from_numpy(slots).to(DEV)
+    d_clen = torch.from_numpy(clen).to(DEV)
+    out, rv = tc.decompress_pages(d_slots, d_clen, plen, compressor_id=ZSTD)
+    out2, rv2 = tc.decompress_pages(d_slots, d_clen, plen, compressor_id=ZSTD)
+    torch.cuda.synchronize()
+    assert bool((rv == plen).all()), rv[:8]
+    digs = [g["digest"][i].tobytes() for i in idx]
+    host = out.cpu().numpy()
+    for i in range(len(frames)):
+        assert hashlib.sha256(host[i].tobytes()).digest() == digs[i]
+    assert torch.equal(out2, out) and torch.equal(rv2, rv)
+    for i in range(len(frames), n, 997):
+        assert np.array_equal(host[i], host[i % len(frames)])

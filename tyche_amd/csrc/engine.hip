@@ -64,7 +64,9 @@ int ensure_device() {
 
 // codecs with a gfx950 kernel, per direction
 bool valid_codec(int id) { return id == TYCHE_LZ4_COMPRESSOR_ID; }
-bool valid_decode_codec(int id) { return id == TYCHE_LZ4_COMPRESSOR_ID || id == TYCHE_ZLIB_COMPRESSOR_ID; }
+bool valid_decode_codec(int id) {
+    return id == TYCHE_LZ4_COMPRESSOR_ID || id == TYCHE_ZLIB_COMPRESSOR_ID || id == TYCHE_ZSTD_COMPRESSOR_ID;
+}
 
 std::string codec_msg(int id) {
     if (id == TYCHE_ZLIB_COMPRESSOR_ID || id == TYCHE_ZSTD_COMPRESSOR_ID)
@@ -74,6 +76,15 @@ std::string codec_msg(int id) {
 
 // zlib 1.2.8 compressBound (compress.c:74-78)
 inline uint32_t zlib_bound(uint32_t n) { return n + (n >> 12) + (n >> 14) + (n >> 25) + 13u; }
+// zstd 1.1.2 ZSTD_compressBound (zstd_compress.c:37): FSE_compressBound(n) + 12
+inline uint32_t zstd_bound(uint32_t n) { return n + (n >> 7) + 512u + 12u; }
+
+// in_cap for a decode batch: the largest stream length (or a bound for unknown lengths)
+inline uint32_t decode_in_cap(const tyche_batch_t &b, uint32_t fallback) {
+    uint32_t in_cap = b.src_lengths ? b.max_src_length : b.src_length;
+    if (b.src_lengths && in_cap == 0) in_cap = fallback;
+    return in_cap;
+}
 
 // ---------------------------------------------------------------- host batches
 // One context per calling thread (tyche calls the codec from its compressor
@@ -209,6 +220,7 @@ int tyche_device_ready(void) { return ensure_device() == TYCHE_E_OK ? 1 : 0; }
 uint32_t tyche_compress_bound(int compressor_id, uint32_t n) {
     if (compressor_id == TYCHE_LZ4_COMPRESSOR_ID) return lz4_bound(n);
     if (compressor_id == TYCHE_ZLIB_COMPRESSOR_ID) return zlib_bound(n);
+    if (compressor_id == TYCHE_ZSTD_COMPRESSOR_ID) return zstd_bound(n);
     return 0;
 }
 
@@ -238,9 +250,13 @@ int tyche_decompress_batch(int compressor_id, const tyche_batch_t *batch, void *
         if (e != hipSuccess) return fail("zlib inflate launch", e);
         return TYCHE_E_OK;
     }
-    uint32_t in_cap = batch->src_lengths ? batch->max_src_length : batch->src_length;
-    if (batch->src_lengths && in_cap == 0) in_cap = lz4_bound(out_cap);
-    hipError_t e = launch_lz4_decode(*batch, in_cap, out_cap, (hipStream_t)stream);
+    if (compressor_id == TYCHE_ZSTD_COMPRESSOR_ID) {
+        hipError_t e = launch_zstd_decode(*batch, decode_in_cap(*batch, zstd_bound(out_cap)), out_cap,
+                                          (hipStream_t)stream);
+        if (e != hipSuccess) return fail("zstd decode launch", e);
+        return TYCHE_E_OK;
+    }
+    hipError_t e = launch_lz4_decode(*batch, decode_in_cap(*batch, lz4_bound(out_cap)), out_cap, (hipStream_t)stream);
     if (e != hipSuccess) return fail("lz4 decode launch", e);
     return TYCHE_E_OK;
 }
@@ -268,6 +284,11 @@ int tyche_decompress_host(int compressor_id, size_t n, const void *const *src, c
         return run_host_batch(n, src, src_lengths, dst, dst_capacities, results, true,
                               [](const tyche_batch_t &b, hipStream_t s) {
                                   return launch_zlib_inflate(b, b.dst_capacity, s);
+                              });
+    if (compressor_id == TYCHE_ZSTD_COMPRESSOR_ID)
+        return run_host_batch(n, src, src_lengths, dst, dst_capacities, results, true,
+                              [](const tyche_batch_t &b, hipStream_t s) {
+                                  return launch_zstd_decode(b, b.max_src_length, b.dst_capacity, s);
                               });
     return run_host_batch(n, src, src_lengths, dst, dst_capacities, results, true,
                           [](const tyche_batch_t &b, hipStream_t s) {
@@ -461,7 +482,8 @@ int tyche_buffers_decompress(Buffer **bufs, int *status, size_t n, int compresso
     for (size_t k = 0; k < m; k++) {
         Buffer *b = bufs[idx[k]];
         size_t i = idx[k];
-        // LZ4 accepts any rv >= 0 (buffer.c:251-253); zlib needs Z_OK and the exact length (:257-260)
+        // LZ4 accepts any rv >= 0 (buffer.c:251-253); zlib needs Z_OK and the exact length (:257-260);
+        // zstd only !ZSTD_isError (:264-266)
         const bool bad = res[k] < 0 || (compressor_id == TYCHE_ZLIB_COMPRESSOR_ID && (uint32_t)res[k] != b->data_length);
         if (rc != TYCHE_E_OK || bad) {
             free(dst[k]);                           // the reference leaks here

@@ -1,0 +1,1065 @@
+// zstd_decode.hip -- gfx950 decoder for zstd frames, the codec behind
+// buffer__decompress for ZSTD_COMPRESSOR_ID (src/buffer.c:263-266 ->
+// ZSTD_decompress, src/zstd/zstd_decompress.c:1459; vendored zstd v1.1.2).
+//
+// One wave per page, waves loop over pages.  Per wave, LDS holds the rebuilt
+// page (the match window), the staged frame, the Huffman table (4096 x 16 bit)
+// and the three sequence FSE tables.  The decode follows the restatement in
+// oracle/zstd_oracle.c step by step:
+//
+//   * frame / block headers, FSE_readNCount, FSE table spreading and the
+//     sequence FSE chain are inherently serial: they run as wave-uniform code
+//     (every lane computes the same value; loads are LDS broadcasts);
+//   * Huffman tables are built lane-parallel (a ballot-ranked fill of the
+//     X2 single-symbol table, huf_decompress.c:86-131);
+//   * the four Huffman literal streams of a 4X section decode in four lanes at
+//     once; the literals land at the tail of the page window [cap-litSize, cap):
+//     every literal's output position is at or below its buffer position, so
+//     sequences executed in order never overwrite a literal before it is read
+//     (the "literals in dst" layout), and no separate literal buffer is needed;
+//   * sequences are decoded 64 at a time (v_writelane into one register per
+//     field) and executed like the LZ4 decoder's batches: output positions from
+//     a DPP prefix sum, the reference's per-sequence checks in parallel
+//     (zstd_decompress.c:940-954), literal runs placed in parallel, matches
+//     copied in dependency (frontier) order.  The prefix of a batch whose output
+//     stays below the first unread literal runs in parallel; the rest (the last
+//     sequences of a block, when the window has no slack left) runs in order.
+//
+// The backward bit reader uses the reference's container (64 bits, the same
+// BIT_lookBits / BIT_lookBitsFast / BIT_reloadDStream arithmetic) wherever the
+// number of symbols depends on it (FSE-compressed Huffman weights, the
+// sequence loop); Huffman literal streams reload whenever fewer than 12 bits
+// remain, which yields the same symbols and the same exact-end verdict.
+//
+// Result per page: decoded size, or a negative value (any ZSTD_isError).
+#include <algorithm>
+
+#include "engine.h"
+#include "lds_io.h"
+
+namespace tyche {
+namespace {
+
+constexpr uint32_t kWave = 64;
+constexpr int32_t kErr = -20;          // corruption_detected (any error: buffer.c only tests ZSTD_isError)
+constexpr int32_t kErrDst = -70;       // dstSize_tooSmall
+constexpr uint32_t kBlockMax = 128u * 1024u;
+constexpr uint32_t kStreamPad = 32;    // zero bytes after the staged frame (8-byte container reads)
+constexpr uint32_t kWinPad = 32;       // slack after the window (4X streams may run 3 bytes past)
+
+// ------------------------------------------------------------ constant tables
+__device__ __constant__ uint8_t c_ll_bits[36] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
+                                                 1, 1, 1, 1, 2, 2, 3, 3, 4, 6, 7, 8, 9, 10, 11, 12,
+                                                 13, 14, 15, 16};
+__device__ __constant__ uint8_t c_ml_bits[53] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
+                                                 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
+                                                 1, 1, 1, 1, 2, 2, 3, 3, 4, 4, 5, 7, 8, 9, 10, 11,
+                                                 12, 13, 14, 15, 16};
+__device__ __constant__ uint32_t c_ll_base[36] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15,
+                                                  16, 18, 20, 22, 24, 28, 32, 40, 48, 64, 0x80, 0x100, 0x200, 0x400,
+                                                  0x800, 0x1000, 0x2000, 0x4000, 0x8000, 0x10000};
+__device__ __constant__ uint32_t c_ml_base[53] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18,
+                                                  19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 34,
+                                                  35, 37, 39, 41, 43, 47, 51, 59, 67, 83, 99, 0x83, 0x103, 0x203,
+                                                  0x403, 0x803, 0x1003, 0x2003, 0x4003, 0x8003, 0x10003};
+__device__ __constant__ uint32_t c_of_base[29] = {0, 1, 1, 5, 0xD, 0x1D, 0x3D, 0x7D, 0xFD, 0x1FD, 0x3FD, 0x7FD,
+                                                  0xFFD, 0x1FFD, 0x3FFD, 0x7FFD, 0xFFFD, 0x1FFFD, 0x3FFFD, 0x7FFFD,
+                                                  0xFFFFD, 0x1FFFFD, 0x3FFFFD, 0x7FFFFD, 0xFFFFFD, 0x1FFFFFD,
+                                                  0x3FFFFFD, 0x7FFFFFD, 0xFFFFFFD};
+// default distributions (zstd_internal.h:118-136)
+__device__ __constant__ int8_t c_ll_norm[36] = {4, 3, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 1, 1, 1,
+                                                2, 2, 2, 2, 2, 2, 2, 2, 2, 3, 2, 1, 1, 1, 1, 1,
+                                                -1, -1, -1, -1};
+__device__ __constant__ int8_t c_ml_norm[53] = {1, 4, 3, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1,
+                                                1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1,
+                                                1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1,
+                                                -1, -1, -1, -1, -1};
+__device__ __constant__ int8_t c_of_norm[29] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1,
+                                                1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1};
+
+// ------------------------------------------------------------ LDS workspace
+struct Work {
+    uint8_t *win;        // page window (cap + kWinPad)
+    const uint8_t *in;   // staged frame (len + kStreamPad zero bytes)
+    uint16_t *huf;       // 4096 entries: symbol | nbBits << 8
+    uint32_t *ll, *of, *ml;   // FSE cells: newState | symbol << 16 | nbBits << 24
+    uint32_t *wt;        // 64 cells for the Huffman-weight FSE table
+    int16_t *norm;       // 256 normalized counts
+    uint16_t *next;      // 256 symbolNext counters
+    uint8_t *w;          // 256 Huffman weights
+};
+
+__device__ __forceinline__ uint64_t ld64(const uint8_t *p) {
+    return (uint64_t)lds_ld32(p) | ((uint64_t)lds_ld32(p + 4) << 32);
+}
+__device__ __forceinline__ uint32_t highbit(uint32_t v) { return 31u - (uint32_t)__builtin_clz(v); }
+
+// ------------------------------------------------------------ bit reader (bitstream.h:260-408)
+enum : uint32_t { kUnfinished = 0, kEndOfBuffer = 1, kCompleted = 2, kOverflow = 3 };
+
+struct BitD {
+    uint64_t c;
+    uint32_t used;
+    int32_t ptr, start;   // byte offsets into the staged frame
+};
+
+// Returns false when BIT_initDStream fails (empty stream or no end mark).
+__device__ __forceinline__ bool bitd_init(BitD &b, const uint8_t *in, int32_t start, int32_t n) {
+    b.start = start;
+    b.c = 0;
+    b.used = 0;
+    b.ptr = start;
+    if (n < 1) return false;
+    const uint32_t last = in[start + n - 1];
+    if (last == 0) return false;
+    const uint32_t mark = 8u - highbit(last);
+    if (n >= 8) {
+        b.ptr = start + n - 8;
+        b.c = ld64(in + b.ptr);
+        b.used = mark;
+    } else {
+        uint64_t c = in[start];
+        for (int32_t k = 1; k < n; k++) {
+            const uint32_t sh = k <= 3 ? 8u * (uint32_t)k : 64u - 8u * (8u - (uint32_t)k);
+            c += (uint64_t)in[start + k] << sh;
+        }
+        b.c = c;
+        b.used = mark + (uint32_t)(8 - n) * 8u;
+    }
+    return true;
+}
+__device__ __forceinline__ uint64_t bitd_look(const BitD &b, uint32_t nb) {
+    return ((b.c << (b.used & 63u)) >> 1) >> ((63u - nb) & 63u);
+}
+__device__ __forceinline__ uint64_t bitd_look_fast(const BitD &b, uint32_t nb) {
+    return (b.c << (b.used & 63u)) >> ((64u - nb) & 63u);
+}
+__device__ __forceinline__ uint32_t bitd_read(BitD &b, uint32_t nb) {
+    const uint32_t v = (uint32_t)bitd_look(b, nb);
+    b.used += nb;
+    return v;
+}
+__device__ __forceinline__ uint32_t bitd_read_fast(BitD &b, uint32_t nb) {
+    const uint32_t v = (uint32_t)bitd_look_fast(b, nb);
+    b.used += nb;
+    return v;
+}
+__device__ __forceinline__ uint32_t bitd_reload(BitD &b, const uint8_t *in) {
+    if (b.used > 64u) return kOverflow;
+    if (b.ptr >= b.start + 8) {
+        b.ptr -= (int32_t)(b.used >> 3);
+        b.used &= 7u;
+        b.c = ld64(in + b.ptr);
+        return kUnfinished;
+    }
+    if (b.ptr == b.start) return b.used < 64u ? kEndOfBuffer : kCompleted;
+    int32_t nbytes = (int32_t)(b.used >> 3);
+    uint32_t r = kUnfinished;
+    if (b.ptr - nbytes < b.start) {
+        nbytes = b.ptr - b.start;
+        r = kEndOfBuffer;
+    }
+    b.ptr -= nbytes;
+    b.used -= (uint32_t)nbytes * 8u;
+    b.c = ld64(in + b.ptr);
+    return r;
+}
+
+// ------------------------------------------------------------ FSE (uniform code)
+// FSE_readNCount (entropy_common.c:65-157) over in[ip0, ip0+n).  Returns header
+// bytes or < 0; max_sv in/out, table_log out.
+__device__ int32_t read_ncount(const uint8_t *in, int32_t ip0, int32_t n, int16_t *norm, uint32_t &max_sv,
+                               uint32_t &table_log) {
+    if (n < 4) return kErr;
+    const int32_t iend = ip0 + n;
+    int32_t ip = ip0;
+    uint32_t bits = lds_ld32(in + ip);
+    int32_t nb = (int32_t)(bits & 0xFu) + 5;
+    if (nb > 15) return kErr;
+    bits >>= 4;
+    int32_t bitcount = 4;
+    table_log = (uint32_t)nb;
+    int32_t remaining = (1 << nb) + 1, threshold = 1 << nb;
+    nb++;
+    uint32_t charnum = 0;
+    bool prev0 = false;
+    while ((remaining > 1) & (charnum <= max_sv)) {
+        if (prev0) {
+            uint32_t n0 = charnum;
+            while ((bits & 0xFFFFu) == 0xFFFFu) {
+                n0 += 24;
+                if (ip < iend - 5) {
+                    ip += 2;
+                    bits = lds_ld32(in + ip) >> (bitcount & 31);
+                } else {
+                    bits >>= 16;
+                    bitcount += 16;
+                }
+            }
+            while ((bits & 3u) == 3u) {
+                n0 += 3;
+                bits >>= 2;
+                bitcount += 2;
+            }
+            n0 += bits & 3u;
+            bitcount += 2;
+            if (n0 > max_sv) return kErr;
+            while (charnum < n0) norm[charnum++] = 0;
+            if ((ip <= iend - 7) || (ip + (bitcount >> 3) <= iend - 4)) {
+                ip += bitcount >> 3;
+                bitcount &= 7;
+                bits = lds_ld32(in + ip) >> bitcount;
+            } else {
+                bits >>= 2;
+            }
+        }
+        const int32_t mx = (2 * threshold - 1) - remaining;
+        int32_t count;
+        if ((bits & (uint32_t)(threshold - 1)) < (uint32_t)mx) {
+            count = (int32_t)(bits & (uint32_t)(threshold - 1));
+            bitcount += nb - 1;
+        } else {
+            count = (int32_t)(bits & (uint32_t)(2 * threshold - 1));
+            if (count >= threshold) count -= mx;
+            bitcount += nb;
+        }
+        count--;
+        remaining -= count < 0 ? -count : count;
+        norm[charnum++] = (int16_t)count;
+        prev0 = count == 0;
+        while (remaining < threshold) {
+            nb--;
+            threshold >>= 1;
+        }
+        if ((ip <= iend - 7) || (ip + (bitcount >> 3) <= iend - 4)) {
+            ip += bitcount >> 3;
+            bitcount &= 7;
+        } else {
+            bitcount -= 8 * (iend - 4 - ip);
+            ip = iend - 4;
+        }
+        bits = lds_ld32(in + ip) >> (bitcount & 31);
+    }
+    if (remaining != 1) return kErr;
+    if (bitcount > 32) return kErr;
+    max_sv = charnum - 1;
+    ip += (bitcount + 7) >> 3;
+    return ip - ip0;
+}
+
+__device__ __forceinline__ uint32_t cell(uint32_t new_state, uint32_t sym, uint32_t nb) {
+    return new_state | (sym << 16) | (nb << 24);
+}
+__device__ __forceinline__ uint32_t cell_state(uint32_t c) { return c & 0xFFFFu; }
+__device__ __forceinline__ uint32_t cell_sym(uint32_t c) { return (c >> 16) & 0xFFu; }
+__device__ __forceinline__ uint32_t cell_nb(uint32_t c) { return c >> 24; }
+
+// FSE_buildDTable (fse_decompress.c:113-168) from norm[0..max_sv]; cells[] gets
+// 1 << table_log entries.  The symbol spread is a serial walk (wave-uniform);
+// lanes then finish the cells of each 64-entry chunk with per-symbol ranks.
+// Returns false on the reference's GENERIC error (spread did not close).
+__device__ bool build_dtable(uint32_t *cells, const int16_t *norm, uint32_t max_sv, uint32_t table_log,
+                             uint16_t *next, uint32_t lane) {
+    const uint32_t size = 1u << table_log, mask = size - 1u;
+    const uint32_t step = (size >> 1) + (size >> 3) + 3u;
+    uint32_t high = size - 1u;
+    // symbols are written into bits 16..23 first (cell = sym << 16)
+    for (uint32_t s = 0; s <= max_sv; s++) {
+        const int32_t c = norm[s];
+        if (c == -1) {
+            if (lane == 0) cells[high] = s << 16;
+            high--;
+        }
+        if (lane == 0) next[s] = (uint16_t)(c == -1 ? 1 : c);
+    }
+    uint32_t pos = 0;
+    for (uint32_t s = 0; s <= max_sv; s++) {
+        const int32_t c = norm[s];
+        // occurrences of s go 64 at a time: lane i takes the i-th next valid position
+        for (int32_t i0 = 0; i0 < c; i0 += (int32_t)kWave) {
+            const uint32_t take = (uint32_t)min((int32_t)kWave, c - i0);
+            // walk serially (positions above `high` are skipped)
+            uint32_t mine = 0;
+            for (uint32_t k = 0; k < take; k++) {
+                if (lane == k) mine = pos;
+                pos = (pos + step) & mask;
+                while (pos > high) pos = (pos + step) & mask;
+            }
+            if (lane < take) cells[mine] = s << 16;
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (pos != 0) return false;
+    // nextState = symbolNext[s]++ in cell order: per 64-cell chunk, rank lanes by symbol
+    for (uint32_t u0 = 0; u0 < size; u0 += kWave) {
+        const uint32_t u = u0 + lane;
+        const bool act = u < size;
+        const uint32_t s = act ? cell_sym(cells[u]) : 0xFFFFu;
+        uint64_t todo = __ballot(act);
+        uint32_t ns = 0;
+        while (todo) {
+            const uint32_t l = (uint32_t)__builtin_ctzll(todo);
+            const uint32_t sl = rdlane(s, l);
+            const uint64_t m = __ballot(act && s == sl);
+            const uint32_t base = next[sl];
+            if (s == sl && act) ns = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+            __builtin_amdgcn_wave_barrier();
+            if (lane == l) next[sl] = (uint16_t)(base + (uint32_t)__builtin_popcountll(m));
+            __builtin_amdgcn_wave_barrier();
+            todo &= ~m;
+        }
+        if (act) {
+            const uint32_t nb = table_log - highbit(ns);
+            cells[u] = cell((ns << nb) - size, s, nb);
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    return true;
+}
+
+// default tables (ZSTD_buildSeqTable set_basic), from the constant norms
+__device__ void build_default(uint32_t *cells, const int8_t *cnorm, uint32_t max_sv, uint32_t log, int16_t *norm,
+                              uint16_t *next, uint32_t lane) {
+    if (lane <= max_sv) norm[lane] = cnorm[lane];
+    __builtin_amdgcn_wave_barrier();
+    build_dtable(cells, norm, max_sv, log, next, lane);
+}
+
+// ------------------------------------------------------------ Huffman (HUF_readStats + HUF_readDTableX2)
+// Reads the table description at in[ip, ip+n).  Returns header bytes or < 0;
+// fills W.huf and sets tlog.
+__device__ int32_t huf_read_table(const Work &W, int32_t ip, int32_t n, uint32_t &tlog, uint32_t lane) {
+    const uint8_t *in = W.in;
+    if (n < 1) return kErr;
+    int32_t isize = in[ip];
+    uint32_t osize;
+    if (isize >= 128) {
+        osize = (uint32_t)isize - 127u;
+        isize = (int32_t)((osize + 1) / 2);
+        if (isize + 1 > n) return kErr;
+        if (osize >= 256) return kErr;
+        for (uint32_t k = lane; k < (osize + 1) / 2 * 2; k += kWave) {
+            const uint32_t b = in[ip + 1 + (int32_t)(k / 2)];
+            W.w[k] = (uint8_t)((k & 1) ? (b & 15u) : (b >> 4));
+        }
+    } else {
+        if (isize + 1 > n) return kErr;
+        // FSE_decompress_wksp(w, 255, ip+1, isize, ws, 6)
+        uint32_t max_sv = 255, flog;
+        const int32_t hs = read_ncount(in, ip + 1, isize, W.norm, max_sv, flog);
+        if (hs < 0) return hs;
+        if (hs > isize) return kErr;
+        if (flog > 6) return kErr;
+        if (!build_dtable(W.wt, W.norm, max_sv, flog, W.next, lane)) return kErr;
+        bool fast = true;
+        const int32_t large = 1 << (flog - 1);
+        for (uint32_t s = 0; s <= max_sv; s++)
+            if (W.norm[s] >= large) fast = false;
+        // FSE_decompress_usingDTable_generic (fse_decompress.c:218-275)
+        BitD b;
+        if (!bitd_init(b, in, ip + 1 + hs, isize - hs)) return kErr;
+        uint32_t s1 = bitd_read(b, flog);
+        bitd_reload(b, in);
+        uint32_t s2 = bitd_read(b, flog);
+        bitd_reload(b, in);
+        uint32_t op = 0;
+        const uint32_t omax = 255, olimit = omax - 3;
+        auto sym = [&](uint32_t &st) -> uint32_t {
+            const uint32_t c = W.wt[st];
+            const uint32_t nbb = cell_nb(c);
+            const uint32_t low = fast ? bitd_read_fast(b, nbb) : bitd_read(b, nbb);
+            st = cell_state(c) + low;
+            return cell_sym(c);
+        };
+        for (;;) {
+            const uint32_t st = bitd_reload(b, in);
+            if (!((st == kUnfinished) & (op < olimit))) break;
+            const uint32_t a0 = sym(s1), a1 = sym(s2), a2 = sym(s1), a3 = sym(s2);
+            if (lane == 0) {
+                W.w[op] = (uint8_t)a0;
+                W.w[op + 1] = (uint8_t)a1;
+                W.w[op + 2] = (uint8_t)a2;
+                W.w[op + 3] = (uint8_t)a3;
+            }
+            op += 4;
+        }
+        for (;;) {
+            if (op > omax - 2) return kErr;
+            uint32_t a = sym(s1);
+            if (lane == 0) W.w[op] = (uint8_t)a;
+            op++;
+            if (bitd_reload(b, in) == kOverflow) {
+                a = sym(s2);
+                if (lane == 0) W.w[op] = (uint8_t)a;
+                op++;
+                break;
+            }
+            if (op > omax - 2) return kErr;
+            a = sym(s2);
+            if (lane == 0) W.w[op] = (uint8_t)a;
+            op++;
+            if (bitd_reload(b, in) == kOverflow) {
+                a = sym(s1);
+                if (lane == 0) W.w[op] = (uint8_t)a;
+                op++;
+                break;
+            }
+        }
+        osize = op;
+    }
+    __builtin_amdgcn_wave_barrier();
+    // weight statistics (ballots over 64-symbol chunks)
+    uint32_t rank[13];
+#pragma unroll
+    for (int k = 0; k < 13; k++) rank[k] = 0;
+    uint32_t total = 0;
+    bool bad = false;
+    for (uint32_t s0 = 0; s0 < osize; s0 += kWave) {
+        const uint32_t s = s0 + lane;
+        const uint32_t wv = s < osize ? W.w[s] : 0u;
+        if (__ballot(s < osize && wv >= 12u)) bad = true;
+        const uint32_t part = s < osize && wv < 12u ? (1u << wv) >> 1 : 0u;
+        total += rdlane((uint32_t)wave_incl_sum((int32_t)part), kWave - 1);
+#pragma unroll
+        for (uint32_t k = 1; k < 12; k++) rank[k] += (uint32_t)__builtin_popcountll(__ballot(s < osize && wv == k));
+    }
+    if (bad) return kErr;
+    if (total == 0) return kErr;
+    tlog = highbit(total) + 1u;
+    if (tlog > 12u) return kErr;
+    {
+        const uint32_t rest = (1u << tlog) - total;
+        const uint32_t lastw = highbit(rest) + 1u;
+        if ((1u << highbit(rest)) != rest) return kErr;
+        if (lane == 0) W.w[osize] = (uint8_t)lastw;
+#pragma unroll
+        for (uint32_t k = 1; k < 13; k++)
+            if (k == lastw) rank[k]++;
+    }
+    if (rank[1] < 2 || (rank[1] & 1u)) return kErr;
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t nsym = osize + 1u;
+    // rank starts (HUF_readDTableX2 "Prepare ranks")
+    uint32_t start[13];
+    {
+        uint32_t nx = 0;
+#pragma unroll
+        for (uint32_t k = 1; k < 13; k++) {
+            start[k] = nx;
+            if (k < tlog + 1u) nx += rank[k] << (k - 1);
+        }
+    }
+    // fill: symbol s of weight w takes (1 << w) >> 1 entries after the earlier symbols of that weight
+    for (uint32_t s0 = 0; s0 < nsym; s0 += kWave) {
+        const uint32_t s = s0 + lane;
+        const uint32_t wv = s < nsym ? W.w[s] : 0u;
+        uint32_t at = 0;
+#pragma unroll
+        for (uint32_t k = 1; k < 13; k++) {
+            const uint64_t m = __ballot(s < nsym && wv == k);
+            if (wv == k) at = start[k] + (__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0)) << (k - 1));
+            start[k] += (uint32_t)__builtin_popcountll(m) << (k - 1);
+        }
+        const uint32_t len = s < nsym && wv ? (1u << wv) >> 1 : 0u;
+        const uint16_t e = (uint16_t)(s | ((tlog + 1u - wv) << 8));
+        if (len <= 16) {
+            for (uint32_t i = 0; i < len; i++) W.huf[at + i] = e;
+        }
+        uint64_t big = __ballot(len > 16);
+        while (big) {
+            const uint32_t l = (uint32_t)__builtin_ctzll(big);
+            big &= big - 1;
+            const uint32_t bat = rdlane(at, l), blen = rdlane(len, l), be = rdlane((uint32_t)e, l);
+            for (uint32_t i = lane; i < blen; i += kWave) W.huf[bat + i] = (uint16_t)be;
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    return isize + 1;
+}
+
+// Decodes the Huffman stream(s) of a literals section: 1 or 4 streams, lanes 0-3
+// each take one.  Literal k is written to out[k].  Returns false on error.
+__device__ bool huf_decode(const Work &W, int32_t cs, int32_t n, bool single, uint32_t lsize, uint32_t tlog,
+                           uint8_t *out, uint32_t lane) {
+    const uint8_t *in = W.in;
+    int32_t s_start = 0, s_len = 0;
+    uint32_t o0 = 0, cnt = 0;
+    bool ok = true;
+    if (single) {
+        s_start = cs;
+        s_len = n;
+        cnt = lane == 0 ? lsize : 0u;
+    } else {
+        if (n < 10) return false;
+        const int32_t l1 = (int32_t)lds_ld16(in + cs), l2 = (int32_t)lds_ld16(in + cs + 2),
+                      l3 = (int32_t)lds_ld16(in + cs + 4);
+        const int32_t l4 = n - (l1 + l2 + l3 + 6);
+        if (l4 < 0 || l4 > n) return false;
+        const uint32_t seg = (lsize + 3u) / 4u;
+        const uint32_t n4 = lsize > 3u * seg ? lsize - 3u * seg : 0u;
+        const int32_t st[4] = {cs + 6, cs + 6 + l1, cs + 6 + l1 + l2, cs + 6 + l1 + l2 + l3};
+        const int32_t ln[4] = {l1, l2, l3, l4};
+        if (lane < 4) {
+            s_start = st[lane];
+            s_len = ln[lane];
+            o0 = seg * lane;
+            cnt = lane < 3 ? seg : n4;
+        }
+    }
+    BitD b;
+    if (lane < (single ? 1u : 4u)) ok = bitd_init(b, in, s_start, s_len);
+    if (__ballot(lane < (single ? 1u : 4u) && !ok)) return false;
+    const uint32_t act_n = single ? 1u : 4u;
+    const uint32_t mc = rdlane(cnt, 0);   // stream 1 holds the most symbols
+    for (uint32_t i = 0; i < mc; i++) {
+        if (lane < act_n && i < cnt) {
+            if (b.used > 52u) bitd_reload(b, in);
+            const uint32_t v = (uint32_t)bitd_look_fast(b, tlog);
+            const uint32_t e = W.huf[v];
+            out[o0 + i] = (uint8_t)e;
+            b.used += e >> 8;
+        }
+    }
+    // exact end of every stream (BIT_endOfDStream); a reload settles ptr/used
+    bool end_ok = true;
+    if (lane < act_n) {
+        if (b.used <= 64u) bitd_reload(b, in);
+        end_ok = b.ptr == b.start && b.used == 64u;
+    }
+    return __ballot(lane < act_n && !end_ok) == 0;
+}
+
+// ------------------------------------------------------------ sequence execution
+__device__ __forceinline__ uint32_t mod_small(uint32_t i, uint32_t m) {
+    uint32_t q = (uint32_t)((float)i * __frcp_rn((float)m));
+    int32_t r = (int32_t)i - (int32_t)(q * m);
+    if (r < 0) r += (int32_t)m;
+    if (r >= (int32_t)m) r -= (int32_t)m;
+    return (uint32_t)r;
+}
+
+// whole-wave forward copy out[d, d+ml) <- out[d-off, ...) (overlap semantics)
+__device__ __forceinline__ void wave_match(uint8_t *out, int32_t d, int32_t off, int32_t ml, uint32_t lane) {
+    const int32_t s = d - off;
+    if (off >= (int32_t)kWave || off >= ml) {
+        for (int32_t i = (int32_t)lane; i < ml; i += (int32_t)kWave) out[d + i] = out[s + i];
+    } else {
+        for (int32_t i = (int32_t)lane; i < ml; i += (int32_t)kWave) out[d + i] = out[s + (int32_t)mod_small((uint32_t)i, (uint32_t)off)];
+    }
+}
+
+// Applies n <= 64 decoded sequences (lane j: ll, ml, off) in order.  op: output
+// position (frame offset); lp: literal cursor (literal k lives at lit[k]).
+// Returns false on a reference exec error.
+__device__ bool exec_batch(uint8_t *out, const uint8_t *lit, bool lit_in_window, int32_t lit_win_base, uint32_t n,
+                           uint32_t ll, uint32_t ml, uint32_t off, int32_t &op, int32_t &lp, int32_t lsize,
+                           int32_t cap, uint32_t lane) {
+    const bool act = lane < n;
+    const int32_t olen = act ? (int32_t)(ll + ml) : 0;
+    const int32_t llen = act ? (int32_t)ll : 0;
+    const int32_t oi = wave_incl_sum(olen), li = wave_incl_sum(llen);
+    const int32_t o = op + oi - olen;     // this sequence's output position
+    const int32_t l0 = lp + li - llen;    // its first literal
+    const int32_t d = o + (int32_t)ll;    // match destination
+    // ZSTD_execSequence checks (zstd_decompress.c:940-954)
+    const bool bad = act && (o + olen > cap || l0 + llen > lsize || (int32_t)off > d);
+    if (__ballot(bad)) return false;
+    const int32_t out_end = op + (int32_t)rdlane((uint32_t)oi, kWave - 1);
+    const int32_t lit_end = lp + (int32_t)rdlane((uint32_t)li, kWave - 1);
+    // parallel prefix: sequences whose output ends at or below the first unread literal
+    uint32_t npar = n;
+    if (lit_in_window) {
+        const int32_t first_buf = lit_win_base + lp;
+        const uint64_t unsafe = __ballot(act && o + olen > first_buf);
+        npar = unsafe ? (uint32_t)__builtin_ctzll(unsafe) : n;
+    }
+    // ---- literals of the parallel prefix
+    const bool pl = lane < npar;
+    const bool short_lit = pl && ll <= 32u;
+    if (short_lit)
+        for (int32_t i = 0; i < (int32_t)ll; i += 4) lds_st32(out + o + i, lds_ld32(lit + l0 + i));
+    uint64_t longl = __ballot(pl && !short_lit);
+    while (longl) {
+        const uint32_t k = (uint32_t)__builtin_ctzll(longl);
+        longl &= longl - 1;
+        const int32_t kl = (int32_t)rdlane(ll, k), ko = (int32_t)rdlane((uint32_t)o, k), ks = (int32_t)rdlane((uint32_t)l0, k);
+        for (int32_t i = (int32_t)lane; i < kl; i += (int32_t)kWave) out[ko + i] = lit[ks + i];
+    }
+    // ---- matches of the parallel prefix, frontier order
+    const int32_t src_end = d - (int32_t)off + min((int32_t)ml, (int32_t)off);
+    uint64_t pending = __ballot(pl && ml > 0);
+    const uint64_t shortm = __ballot(pl && ml <= 64u);
+    const uint32_t grp = lane >> 4, gl = lane & 15u;
+    while (pending) {
+        const uint32_t f = (uint32_t)__builtin_ctzll(pending);
+        const int32_t F = (int32_t)rdlane((uint32_t)d, f);
+        if (!((shortm >> f) & 1ull)) {
+            wave_match(out, F, (int32_t)rdlane(off, f), (int32_t)rdlane(ml, f), lane);
+            pending &= ~(1ull << f);
+            continue;
+        }
+        uint64_t ready = pending & shortm & __ballot(src_end <= F);
+        int32_t gd = 0, go = 1, gm = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++) {
+            if (ready) {
+                const uint32_t r = (uint32_t)__builtin_ctzll(ready);
+                ready &= ready - 1;
+                pending &= ~(1ull << r);
+                const int32_t rd = (int32_t)rdlane((uint32_t)d, r), ro = (int32_t)rdlane(off, r), rm = (int32_t)rdlane(ml, r);
+                if (grp == k) { gd = rd; go = ro; gm = rm; }
+            }
+        }
+        const int32_t gs = gd - go;
+        for (int32_t i = (int32_t)gl; i < gm; i += 16) {
+            const int32_t si = (go >= 16 || go >= gm) ? i : (int32_t)mod_small((uint32_t)i, (uint32_t)go);
+            out[gd + i] = out[gs + si];
+        }
+    }
+    // ---- the rest in stream order, one sequence at a time
+    for (uint32_t j = npar; j < n; j++) {
+        const int32_t jo = (int32_t)rdlane((uint32_t)o, j), jl = (int32_t)rdlane(ll, j), js = (int32_t)rdlane((uint32_t)l0, j);
+        // chunked so that a chunk's reads precede its writes (output position <= buffer position)
+        for (int32_t c = 0; c < jl; c += (int32_t)kWave) {
+            const int32_t i = c + (int32_t)lane;
+            const uint8_t v = i < jl ? lit[js + i] : 0;
+            __builtin_amdgcn_wave_barrier();
+            if (i < jl) out[jo + i] = v;
+            __builtin_amdgcn_wave_barrier();
+        }
+        wave_match(out, jo + jl, (int32_t)rdlane(off, j), (int32_t)rdlane(ml, j), lane);
+        __builtin_amdgcn_wave_barrier();
+    }
+    op = out_end;
+    lp = lit_end;
+    return true;
+}
+
+// ------------------------------------------------------------ XXH64 of out[0, n) (checksum frames)
+__device__ __forceinline__ uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+constexpr uint64_t kP1 = 11400714785074694791ull, kP2 = 14029467366897019727ull, kP3 = 1609587929392839161ull,
+                   kP4 = 9650029242287828579ull, kP5 = 2870177450012600261ull;
+__device__ __forceinline__ uint64_t xround(uint64_t acc, uint64_t v) { return rotl64(acc + v * kP2, 31) * kP1; }
+
+__device__ uint32_t xxh64_lds(const uint8_t *p, uint32_t len, uint32_t lane) {
+    uint64_t h;
+    uint32_t i = 0;
+    if (len >= 32) {
+        // lanes 0-3 run the four accumulators over all stripes
+        uint64_t v = lane == 0 ? kP1 + kP2 : lane == 1 ? kP2 : lane == 2 ? 0ull : (uint64_t)0 - kP1;
+        const uint32_t nst = len / 32;
+        if (lane < 4)
+            for (uint32_t s = 0; s < nst; s++) v = xround(v, ld64(p + s * 32 + lane * 8));
+        const uint64_t v1 = ((uint64_t)rdlane((uint32_t)(v >> 32), 0) << 32) | rdlane((uint32_t)v, 0);
+        const uint64_t v2 = ((uint64_t)rdlane((uint32_t)(v >> 32), 1) << 32) | rdlane((uint32_t)v, 1);
+        const uint64_t v3 = ((uint64_t)rdlane((uint32_t)(v >> 32), 2) << 32) | rdlane((uint32_t)v, 2);
+        const uint64_t v4 = ((uint64_t)rdlane((uint32_t)(v >> 32), 3) << 32) | rdlane((uint32_t)v, 3);
+        h = rotl64(v1, 1) + rotl64(v2, 7) + rotl64(v3, 12) + rotl64(v4, 18);
+        h = (h ^ xround(0, v1)) * kP1 + kP4;
+        h = (h ^ xround(0, v2)) * kP1 + kP4;
+        h = (h ^ xround(0, v3)) * kP1 + kP4;
+        h = (h ^ xround(0, v4)) * kP1 + kP4;
+        i = nst * 32;
+    } else {
+        h = kP5;
+    }
+    h += (uint64_t)len;
+    for (; i + 8 <= len; i += 8) h = rotl64(h ^ xround(0, ld64(p + i)), 27) * kP1 + kP4;
+    if (i + 4 <= len) {
+        h ^= (uint64_t)lds_ld32(p + i) * kP1;
+        h = rotl64(h, 23) * kP2 + kP3;
+        i += 4;
+    }
+    for (; i < len; i++) h = rotl64(h ^ (uint64_t)p[i] * kP5, 11) * kP1;
+    h ^= h >> 33;
+    h *= kP2;
+    h ^= h >> 29;
+    h *= kP3;
+    h ^= h >> 32;
+    return (uint32_t)h;
+}
+
+// ------------------------------------------------------------ block / frame
+struct SeqTables {
+    uint32_t ll_log, of_log, ml_log;
+    bool fse_entropy, lit_entropy;
+    uint32_t huf_log;
+    uint32_t rep0, rep1, rep2;
+};
+
+// ZSTD_buildSeqTable (zstd_decompress.c:693-724).  Returns bytes read or < 0.
+__device__ int32_t seq_table(const Work &W, uint32_t *cells, uint32_t &log, uint32_t type, uint32_t max,
+                             uint32_t max_log, int32_t ip, int32_t n, const int8_t *cnorm, uint32_t def_log,
+                             bool flag_repeat, uint32_t lane) {
+    if (type == 1) {   // set_rle
+        if (n < 1) return kErr;
+        const uint32_t sym = W.in[ip];
+        if (sym > max) return kErr;
+        if (lane == 0) cells[0] = cell(0, sym, 0);
+        log = 0;
+        return 1;
+    }
+    if (type == 0) {   // set_basic
+        build_default(cells, cnorm, max, def_log, W.norm, W.next, lane);
+        log = def_log;
+        return 0;
+    }
+    if (type == 3) return flag_repeat ? 0 : kErr;
+    uint32_t tl, mx = max;
+    const int32_t hs = read_ncount(W.in, ip, n, W.norm, mx, tl);
+    if (hs < 0) return kErr;
+    if (tl > max_log) return kErr;
+    build_dtable(cells, W.norm, mx, tl, W.next, lane);   // its result is ignored by the reference (:720)
+    log = tl;
+    return hs;
+}
+
+// One compressed block at in[ip, ip+n); output from op (frame offset) up to cap.
+// Returns bytes written or < 0.
+__device__ int32_t decode_block(const Work &W, SeqTables &T, int32_t ip, int32_t n, int32_t op, int32_t cap,
+                                uint32_t lane) {
+    const uint8_t *in = W.in;
+    if (n >= (int32_t)kBlockMax) return kErr;
+    // ---- literals section (ZSTD_decodeLiteralsBlock)
+    if (n < 3) return kErr;
+    const uint32_t b0 = in[ip];
+    const uint32_t ltype = b0 & 3u, lhl = (b0 >> 2) & 3u;
+    const uint8_t *lit;
+    bool lit_in_window;
+    int32_t lsize, lcons, lit_win_base = 0;
+    if (ltype >= 2u) {
+        if (ltype == 3u && !T.lit_entropy) return kErr;
+        if (n < 5) return kErr;
+        const uint32_t lhc = lds_ld32(in + ip);
+        int32_t lh, csize;
+        bool single = false;
+        if (lhl <= 1u) { single = lhl == 0; lh = 3; lsize = (int32_t)((lhc >> 4) & 0x3FFu); csize = (int32_t)((lhc >> 14) & 0x3FFu); }
+        else if (lhl == 2u) { lh = 4; lsize = (int32_t)((lhc >> 4) & 0x3FFFu); csize = (int32_t)(lhc >> 18); }
+        else { lh = 5; lsize = (int32_t)((lhc >> 4) & 0x3FFFFu); csize = (int32_t)((lhc >> 22) + ((uint32_t)in[ip + 4] << 10)); }
+        if (lsize > (int32_t)kBlockMax) return kErr;
+        if (csize + lh > n) return kErr;
+        // the block's output is lsize + sum(ml) bytes: a section that cannot fit the
+        // remaining capacity makes the reference fail later in any case
+        if (op + lsize > cap) return kErrDst;
+        uint8_t *dst = W.win + (cap - lsize);
+        const int32_t cs = ip + lh;
+        bool ok;
+        if (ltype == 3u) {
+            ok = huf_decode(W, cs, csize, single, (uint32_t)lsize, T.huf_log, dst, lane);
+        } else if (single) {
+            uint32_t tl;
+            const int32_t hs = huf_read_table(W, cs, csize, tl, lane);
+            ok = hs >= 0 && hs < csize;
+            if (ok) {
+                T.huf_log = tl;
+                ok = huf_decode(W, cs + hs, csize - hs, true, (uint32_t)lsize, tl, dst, lane);
+            }
+        } else {
+            ok = lsize != 0 && csize < lsize && csize > 1;
+            if (ok) {
+                uint32_t tl;
+                const int32_t hs = huf_read_table(W, cs, csize, tl, lane);
+                ok = hs >= 0 && hs < csize;
+                if (ok) {
+                    T.huf_log = tl;
+                    ok = huf_decode(W, cs + hs, csize - hs, false, (uint32_t)lsize, tl, dst, lane);
+                }
+            }
+        }
+        if (!ok) return kErr;
+        T.lit_entropy = true;
+        lit = dst;
+        lit_in_window = true;
+        lit_win_base = cap - lsize;
+        lcons = lh + csize;
+    } else {
+        int32_t lh;
+        if (lhl == 1u) { lh = 2; lsize = (int32_t)(lds_ld16(in + ip) >> 4); }
+        else if (lhl == 3u) { lh = 3; lsize = (int32_t)((lds_ld32(in + ip) & 0xFFFFFFu) >> 4); }
+        else { lh = 1; lsize = (int32_t)(b0 >> 3); }
+        if (ltype == 0u) {   // raw
+            if (lh + lsize > n) return kErr;
+            lit = in + ip + lh;
+            lit_in_window = false;
+            lcons = lh + lsize;
+        } else {             // RLE
+            if (lhl == 3u && n < 4) return kErr;
+            if (lsize > (int32_t)kBlockMax) return kErr;
+            if (op + lsize > cap) return kErrDst;
+            uint8_t *dst = W.win + (cap - lsize);
+            const uint8_t v = in[ip + lh];
+            for (int32_t i = (int32_t)lane; i < lsize; i += (int32_t)kWave) dst[i] = v;
+            lit = dst;
+            lit_in_window = true;
+            lit_win_base = cap - lsize;
+            lcons = lh + 1;
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    // ---- sequences section (ZSTD_decodeSeqHeaders)
+    int32_t sp = ip + lcons;
+    const int32_t send = ip + n;
+    if (send - sp < 1) return kErr;
+    int32_t nbseq = in[sp++];
+    int32_t op0 = op, lp = 0;
+    if (nbseq) {
+        if (nbseq > 0x7F) {
+            if (nbseq == 0xFF) {
+                if (sp + 2 > send) return kErr;
+                nbseq = (int32_t)lds_ld16(in + sp) + 0x7F00;
+                sp += 2;
+            } else {
+                if (sp >= send) return kErr;
+                nbseq = ((nbseq - 0x80) << 8) + in[sp++];
+            }
+        }
+        if (sp + 4 > send) return kErr;
+        const uint32_t modes = in[sp++];
+        int32_t r = seq_table(W, W.ll, T.ll_log, modes >> 6, 35, 9, sp, send - sp, c_ll_norm, 6, T.fse_entropy, lane);
+        if (r < 0) return kErr;
+        sp += r;
+        r = seq_table(W, W.of, T.of_log, (modes >> 4) & 3u, 28, 8, sp, send - sp, c_of_norm, 5, T.fse_entropy, lane);
+        if (r < 0) return kErr;
+        sp += r;
+        r = seq_table(W, W.ml, T.ml_log, (modes >> 2) & 3u, 52, 9, sp, send - sp, c_ml_norm, 6, T.fse_entropy, lane);
+        if (r < 0) return kErr;
+        sp += r;
+        __builtin_amdgcn_wave_barrier();
+        // ---- sequence loop (ZSTD_decompressSequences)
+        T.fse_entropy = true;
+        BitD b;
+        if (!bitd_init(b, in, sp, send - sp)) return kErr;
+        uint32_t sll = bitd_read(b, T.ll_log);
+        bitd_reload(b, in);
+        uint32_t sof = bitd_read(b, T.of_log);
+        bitd_reload(b, in);
+        uint32_t sml = bitd_read(b, T.ml_log);
+        bitd_reload(b, in);
+        uint32_t rep0 = T.rep0, rep1 = T.rep1, rep2 = T.rep2;
+        bool more = true;
+        while (more) {
+            // decode up to 64 sequences into lanes
+            uint32_t vll = 0, vml = 0, voff = 0, k = 0;
+            for (; k < kWave; k++) {
+                if (!((bitd_reload(b, in) <= kCompleted) && nbseq)) { more = false; break; }
+                nbseq--;
+                const uint32_t cl = W.ll[sll], cm = W.ml[sml], co = W.of[sof];
+                const uint32_t llc = cell_sym(cl), mlc = cell_sym(cm), ofc = cell_sym(co);
+                uint32_t offv;
+                if (!ofc) offv = 0;
+                else offv = c_of_base[ofc] + bitd_read_fast(b, ofc);
+                if (ofc <= 1u) {
+                    offv += llc == 0;
+                    if (offv) {
+                        uint32_t t = offv == 3u ? rep0 - 1u : (offv == 1u ? rep1 : rep2);
+                        t += t == 0;
+                        if (offv != 1u) rep2 = rep1;
+                        rep1 = rep0;
+                        rep0 = offv = t;
+                    } else {
+                        offv = rep0;
+                    }
+                } else {
+                    rep2 = rep1;
+                    rep1 = rep0;
+                    rep0 = offv;
+                }
+                const uint32_t mlb = c_ml_bits[mlc], llb = c_ll_bits[llc];
+                const uint32_t mlv = c_ml_base[mlc] + (mlc > 31u ? bitd_read_fast(b, mlb) : 0u);
+                const uint32_t llv = c_ll_base[llc] + (llc > 15u ? bitd_read_fast(b, llb) : 0u);
+                if (llb + mlb + ofc > 31u) bitd_reload(b, in);
+                sll = cell_state(cl) + bitd_read(b, cell_nb(cl));
+                sml = cell_state(cm) + bitd_read(b, cell_nb(cm));
+                sof = cell_state(co) + bitd_read(b, cell_nb(co));
+                if (lane == k) {
+                    vll = llv;
+                    vml = mlv;
+                    voff = offv;
+                }
+            }
+            if (k == 0) break;
+            if (!exec_batch(W.win, lit, lit_in_window, lit_win_base, k, vll, vml, voff, op, lp, lsize, cap, lane))
+                return kErr;
+        }
+        if (nbseq) return kErr;
+        T.rep0 = rep0;
+        T.rep1 = rep1;
+        T.rep2 = rep2;
+    }
+    // ---- last literals
+    const int32_t last = lsize - lp;
+    if (last > cap - op) return kErrDst;
+    for (int32_t c = 0; c < last; c += (int32_t)kWave) {
+        const int32_t i = c + (int32_t)lane;
+        const uint8_t v = i < last ? lit[lp + i] : 0;
+        __builtin_amdgcn_wave_barrier();
+        if (i < last) W.win[op + i] = v;
+        __builtin_amdgcn_wave_barrier();
+    }
+    op += last;
+    return op - op0;
+}
+
+// ZSTD_decompressFrame (zstd_decompress.c:1369-1436) for the frame staged at
+// W.in[0, L).  Returns the decoded size or < 0.
+__device__ int32_t decode_frame(const Work &W, int32_t L, int32_t cap, uint32_t lane) {
+    const uint8_t *in = W.in;
+    if (L < 9) return kErr;
+    const uint32_t magic = lds_ld32(in);
+    const uint32_t fhd = in[4];
+    const uint32_t did = fhd & 3u, single = (fhd >> 5) & 1u, fcs_id = fhd >> 6;
+    bool checksum = (fhd >> 2) & 1u;
+    const int32_t fh = 5 + (int32_t)!single + (int32_t)(did == 3 ? 4 : did) + (int32_t)(fcs_id == 0 ? 0 : 1u << fcs_id) +
+                       (int32_t)(single && !fcs_id);
+    if (L < fh + 3) return kErr;
+    if ((magic & 0xFFFFFFF0u) == 0x184D2A50u) {
+        if (fh < 8) return kErr;
+        checksum = false;
+    } else if (magic != 0xFD2FB528u) {
+        return kErr;
+    } else {
+        if (fhd & 0x08u) return kErr;
+        int32_t pos = 5;
+        uint64_t window = 0, fcs = 0;
+        uint32_t dict_id = 0;
+        if (!single) {
+            const uint32_t wl = in[pos++];
+            const uint32_t wlog = (wl >> 3) + 10u;
+            if (wlog > 27u) return kErr;
+            window = 1ull << wlog;
+            window += (window >> 3) * (wl & 7u);
+        }
+        if (did == 1) { dict_id = in[pos]; pos += 1; }
+        else if (did == 2) { dict_id = lds_ld16(in + pos); pos += 2; }
+        else if (did == 3) { dict_id = lds_ld32(in + pos); pos += 4; }
+        if (fcs_id == 0) { if (single) fcs = in[pos]; }
+        else if (fcs_id == 1) fcs = (uint64_t)lds_ld16(in + pos) + 256u;
+        else if (fcs_id == 2) fcs = lds_ld32(in + pos);
+        else fcs = ld64(in + pos);
+        if (!window) window = (uint32_t)fcs;
+        if (window > (1ull << 27)) return kErr;
+        if (dict_id) return kErr;
+    }
+    SeqTables T;
+    T.ll_log = T.of_log = T.ml_log = 0;
+    T.fse_entropy = T.lit_entropy = false;
+    T.huf_log = 0;
+    T.rep0 = 1;
+    T.rep1 = 4;
+    T.rep2 = 8;
+    int32_t ip = fh, remaining = L - fh, op = 0;
+    for (;;) {
+        if (remaining < 3) return kErr;
+        const uint32_t bh = (uint32_t)in[ip] | ((uint32_t)in[ip + 1] << 8) | ((uint32_t)in[ip + 2] << 16);
+        const uint32_t last = bh & 1u, btype = (bh >> 1) & 3u, csize0 = bh >> 3;
+        if (btype == 3u) return kErr;
+        const int32_t csize = btype == 1u ? 1 : (int32_t)csize0;
+        ip += 3;
+        remaining -= 3;
+        if (csize > remaining) return kErr;
+        int32_t dec;
+        if (btype == 2u) {
+            dec = decode_block(W, T, ip, csize, op, cap, lane);
+        } else if (btype == 0u) {
+            if (csize > cap - op) return kErrDst;
+            for (int32_t i = (int32_t)lane; i < csize; i += (int32_t)kWave) W.win[op + i] = in[ip + i];
+            dec = csize;
+        } else {
+            if ((int64_t)csize0 > (int64_t)(cap - op)) return kErrDst;
+            const uint8_t v = in[ip];
+            for (int32_t i = (int32_t)lane; i < (int32_t)csize0; i += (int32_t)kWave) W.win[op + i] = v;
+            dec = (int32_t)csize0;
+        }
+        if (dec < 0) return dec;
+        op += dec;
+        ip += csize;
+        remaining -= csize;
+        __builtin_amdgcn_wave_barrier();
+        if (last) break;
+    }
+    if (checksum) {
+        if (remaining < 4) return kErr;
+        if (lds_ld32(in + ip) != xxh64_lds(W.win, (uint32_t)op, lane)) return kErr;
+        remaining -= 4;
+    }
+    if (remaining) return kErr;
+    return op;
+}
+
+struct Layout {
+    uint32_t off_in, off_huf, off_ll, off_of, off_ml, off_wt, off_norm, off_next, off_w, total;
+};
+
+__host__ __device__ inline Layout make_layout(uint32_t in_cap, uint32_t out_cap) {
+    Layout l;
+    l.off_in = (out_cap + kWinPad + 15u) & ~15u;
+    l.off_huf = l.off_in + ((in_cap + 16u + kStreamPad + 15u) & ~15u);
+    l.off_ll = l.off_huf + 4096u * 2u;
+    l.off_of = l.off_ll + 512u * 4u;
+    l.off_ml = l.off_of + 256u * 4u;
+    l.off_wt = l.off_ml + 512u * 4u;
+    l.off_norm = l.off_wt + 64u * 4u;
+    l.off_next = l.off_norm + 256u * 2u;
+    l.off_w = l.off_next + 256u * 2u;
+    l.total = l.off_w + 256u + 16u;
+    return l;
+}
+
+__global__ __launch_bounds__(64) void zstd_decode_kernel(tyche_batch_t b, uint32_t in_cap, uint32_t out_cap, Layout lay) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint32_t lane = threadIdx.x;
+    Work W;
+    W.win = smem;
+    W.huf = (uint16_t *)(smem + lay.off_huf);
+    W.ll = (uint32_t *)(smem + lay.off_ll);
+    W.of = (uint32_t *)(smem + lay.off_of);
+    W.ml = (uint32_t *)(smem + lay.off_ml);
+    W.wt = (uint32_t *)(smem + lay.off_wt);
+    W.norm = (int16_t *)(smem + lay.off_norm);
+    W.next = (uint16_t *)(smem + lay.off_next);
+    W.w = smem + lay.off_w;
+    uint8_t *stage = smem + lay.off_in;
+    for (size_t page = blockIdx.x; page < b.count; page += gridDim.x) {
+        const PageRef p = batch_page(b, page);
+        int32_t rv;
+        if (p.src_len > in_cap || p.dst_cap > out_cap) {
+            rv = kResultTooLarge;
+        } else {
+            __syncthreads();
+            const uint32_t head = stage_in(p.src, p.src_len, stage, lane, kWave);
+            uint8_t *in = stage + head;
+            __syncthreads();
+            if (lane < kStreamPad / 4) lds_st32(in + p.src_len + lane * 4, 0u);
+            __syncthreads();
+            W.in = in;
+            rv = decode_frame(W, (int32_t)p.src_len, (int32_t)p.dst_cap, lane);
+            __syncthreads();
+            if (rv > 0) stage_out(p.dst, W.win, (uint32_t)rv, lane, kWave);
+        }
+        if (lane == 0) b.results[page] = rv;
+    }
+}
+
+}  // namespace
+
+hipError_t launch_zstd_decode(const tyche_batch_t &b, uint32_t in_cap, uint32_t out_cap, hipStream_t s) {
+    if (b.count == 0) return hipSuccess;
+    const Layout lay = make_layout(in_cap, out_cap);
+    if (lay.total > 160u * 1024u) return hipErrorInvalidValue;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    static int cus[64] = {0};
+    if (dev < 64 && cus[dev] == 0) {
+        (void)hipFuncSetAttribute((const void *)zstd_decode_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
+        int n = 0;
+        (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+        cus[dev] = n > 0 ? n : 256;
+    }
+    const size_t per_cu = std::max<size_t>(1, std::min<size_t>(32, (160 * 1024) / lay.total));
+    const size_t grid = std::min<size_t>(b.count, (size_t)(dev < 64 ? cus[dev] : 256) * per_cu);
+    hipLaunchKernelGGL(zstd_decode_kernel, dim3((unsigned)grid), dim3(kWave), lay.total, s, b, in_cap, out_cap, lay);
+    return hipGetLastError();
+}
+
+}  // namespace tyche
