@@ -12,6 +12,11 @@ C ABI, against the reference's frames and the restatement oracle.
 * seeded corruptions of the reference frames agree with the oracle
   (oracle/zstd_oracle.c, pinned to the reference by tests/test_oracle.py);
 * the Buffer API (accepts any non-error result) and a 16K-page batch.
+
+Encoder: every device-encoded frame decodes with the
+reference's own ZSTD_decompress (oracle/_ref build) and the oracle back to the
+page, for every page distribution and size, edge sizes, multi-block and
+incompressible pages; the encoder is deterministic.
 """
 import ctypes
 import hashlib
@@ -208,3 +213,123 @@ def test_zstd_large_batch(tc):
     assert torch.equal(out2, out) and torch.equal(rv2, rv)
     for i in range(len(frames), n, 997):
         assert np.array_equal(host[i], host[i % len(frames)])
+
+
+# ----------------------------------------------------------------- encoder (A8)
+def _check_frames(O, comp, clen, host, plen):
+    ch, lh = comp.cpu().numpy(), clen.cpu().numpy()
+    for i in range(host.shape[0]):
+        assert 0 < lh[i] <= O.zstd_bound(plen), (i, lh[i])
+        frame = ch[i, :lh[i]].tobytes()
+        r, dec = O.zstd_decompress(frame, plen)
+        assert r == plen and dec == host[i].tobytes(), (i, r)
+        if O.have_ref():
+            r2, dec2 = O.ref_zstd_decompress(frame, plen)
+            assert r2 == plen and dec2 == host[i].tobytes(), (i, r2)
+    return int(lh.sum())
+
+
+@pytest.mark.parametrize("dist", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("plen", [8192, 16384, 32768])
+def test_encode_roundtrip_reference_decoder(tc, oracle_mod, dist, plen):
+    """Every device-encoded frame decodes with the reference's ZSTD_decompress (oracle/_ref) and
+    the restatement, back to the page; the device decoder round-trips it too."""
+    O = oracle_mod
+    n = 32
+    pages = tc.pagegen(n, plen, seed=777, first=plen + dist * 100, dist=dist, device=DEV)
+    comp, clen = tc.compress_pages(pages, compressor_id=ZSTD)
+    out, rv = tc.decompress_pages(comp, clen, plen, compressor_id=ZSTD)
+    torch.cuda.synchronize()
+    assert torch.equal(out, pages) and bool((rv == plen).all())
+    total = _check_frames(O, comp, clen, pages.cpu().numpy(), plen)
+    if dist in (0, 1):   # compressible database pages: the frame is well below the page
+        assert total < 0.6 * n * plen
+
+
+@pytest.mark.parametrize("n", [0, 1, 5, 12, 13, 64, 255, 256, 300, 4095, 65535])
+def test_encode_sizes(tc, oracle_mod, n):
+    """Edge sizes: empty page (one empty raw block), below the parse minimum, the 1/2-byte
+    content-size boundary (255/256), and the largest 16-bit page."""
+    from tyche_amd import _lib
+    import ctypes
+    O = oracle_mod
+    rng = np.random.default_rng(n)
+    data = (rng.integers(0, 3, n, dtype=np.uint8) * 40).tobytes()
+    src = torch.from_numpy(np.frombuffer(data, np.uint8).copy().reshape(1, n) if n else np.zeros((1, 1), np.uint8))
+    src = src.to(DEV)
+    slot = tc.slot_size(max(n, 1), ZSTD)
+    comp = torch.zeros((1, slot), dtype=torch.uint8, device=DEV)
+    clen = torch.zeros(1, dtype=torch.int32, device=DEV)
+    b = _lib.Batch(count=1, src=src.data_ptr(), src_stride=max(n, 1), src_length=n, max_src_length=n,
+                   dst=comp.data_ptr(), dst_stride=slot, dst_capacity=slot, results=clen.data_ptr())
+    _lib.check(_lib.load().tyche_compress_batch(ZSTD, 1, ctypes.byref(b), torch.cuda.current_stream().cuda_stream),
+               "compress")
+    torch.cuda.synchronize()
+    L = int(clen[0])
+    assert L > 0
+    frame = comp[0, :L].cpu().numpy().tobytes()
+    r, dec = O.zstd_decompress(frame, n)
+    assert r == n and dec == data
+    if O.have_ref():
+        r2, dec2 = O.ref_zstd_decompress(frame, n)
+        assert r2 == n and dec2 == data
+
+
+def test_encode_multiblock_and_incompressible(tc, oracle_mod):
+    """Pages with > 1024 sequences span several blocks (kSeqCap); random pages go out as raw blocks."""
+    O = oracle_mod
+    rng = np.random.default_rng(9)
+    pages = []
+    for k in range(8):   # short repeats: thousands of 4..6-byte matches
+        words = rng.integers(0, 256, (64, 5), dtype=np.uint8)
+        pages.append(words[rng.integers(0, 64, 32768 // 5 + 1)].reshape(-1)[:32768])
+    for k in range(4):
+        pages.append(rng.integers(0, 256, 32768, dtype=np.uint8))
+    host = np.stack(pages)
+    d = torch.from_numpy(host).to(DEV)
+    comp, clen = tc.compress_pages(d, compressor_id=ZSTD)
+    torch.cuda.synchronize()
+    _check_frames(O, comp, clen, host, 32768)
+    lh = clen.cpu().numpy()
+    assert (lh[8:] <= 32768 + 16).all()
+
+
+def test_encode_large_batch_deterministic(tc):
+    n, plen = 32768, 32768
+    pages = tc.pagegen(n, plen, seed=5, dist=0, device=DEV)
+    comp, clen = tc.compress_pages(pages, compressor_id=ZSTD)
+    out, rv = tc.decompress_pages(comp, clen, plen, compressor_id=ZSTD)
+    comp2, clen2 = tc.compress_pages(pages, compressor_id=ZSTD)
+    torch.cuda.synchronize()
+    assert bool((rv == plen).all()) and torch.equal(out, pages)
+    assert torch.equal(clen, clen2)
+    mask = torch.arange(comp.shape[1], device=DEV)[None, :] < clen[:, None].long()
+    assert torch.equal(comp * mask, comp2 * mask)
+
+
+def test_encode_buffer_api(tc, oracle_mod):
+    """buffer__compress(ZSTD) -> free()-able frame within ZSTD_compressBound (buffer.c:203-212),
+    then buffer__decompress(ZSTD) restores the page; the batch form too."""
+    from tyche_amd import buffer as B
+    from tyche_amd._lib import E_OK
+    g = load_golden("kat_lorem.npz")
+    text = g["text"].tobytes()
+    buf = B.new_buffer(text, id=7)
+    rv, comp = B.buffer__compress(buf, ZSTD, 1)
+    assert rv == E_OK and comp
+    assert 0 < buf.contents.comp_length <= oracle_mod.zstd_bound(4096)
+    B.swap_data(buf, comp)
+    assert B.buffer__decompress(buf, ZSTD) == E_OK
+    assert B.buffer_bytes(buf) == text
+    B.destroy(buf)
+    pages = oracle_mod.pagegen(40, 16384, seed=3, dist=1)
+    bufs = [B.new_buffer(pages[i].tobytes(), id=i) for i in range(40)]
+    rc, st, ptrs = B.buffers_compress(bufs, ZSTD, 1)
+    assert rc == 0 and st == [0] * 40
+    for b, p in zip(bufs, ptrs):
+        B.swap_data(b, p)
+    rc, st = B.buffers_decompress(bufs, ZSTD)
+    assert rc == 0 and st == [0] * 40
+    for i, b in enumerate(bufs):
+        assert B.buffer_bytes(b) == pages[i].tobytes()
+        B.destroy(b)

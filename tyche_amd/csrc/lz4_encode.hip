@@ -31,48 +31,16 @@
 
 #include "engine.h"
 #include "lds_io.h"
+#include "lz_parse.h"
 
 namespace tyche {
 
 namespace {
 
-constexpr uint32_t kWave = 64;
-constexpr uint32_t kHashLog = 12;
-constexpr uint32_t kHashSize = 1u << kHashLog;
+using lzp::kWave;
+using lzp::kHashSize;
 constexpr uint32_t kPad = 64;
-constexpr uint32_t kProbe = 16;          // bytes probed per lane beyond MINMATCH
 constexpr uint32_t kPrefetchVec = 16;    // 16-byte vectors per lane prefetched for the next page (16 KiB)
-
-// Timing-only ablation builds (-DTYCHE_EABLATE=mask; outputs are wrong):
-//   1 skip the byte emission loop (sizes still computed), 2 no probes (every match 4 bytes),
-//   4 no greedy parse (no sequences: the page becomes one literal run)
-//   8 no whole-wave extension of probe-capped matches (valid output, shorter matches)
-#ifndef TYCHE_EABLATE
-#define TYCHE_EABLATE 0
-#endif
-
-__device__ __forceinline__ uint32_t hash4(uint32_t v) { return (v * 2654435761u) >> (32 - kHashLog); }
-
-// equal bytes at a and b going forward, a stopping before `limit` (whole wave, 256 bytes per step)
-__device__ uint32_t wave_extend(const uint8_t *in, uint32_t a, uint32_t b, uint32_t limit, uint32_t lane) {
-    uint32_t n = 0;
-    for (;;) {
-        const uint32_t pa = a + n + 4 * lane;
-        const bool full = pa + 4 <= limit;
-        const uint32_t x = full ? (lds_ld32(in + pa) ^ lds_ld32(in + b + n + 4 * lane)) : 1u;
-        const uint64_t bad = __ballot(x != 0);
-        if (bad == 0) {
-            n += 4 * kWave;
-            continue;
-        }
-        const uint32_t first = (uint32_t)__builtin_ctzll(bad);
-        const uint32_t pf = a + n + 4 * first;
-        if (pf + 4 <= limit) return n + 4 * first + (__builtin_ctz(rdlane(x, first)) >> 3);
-        uint32_t m = n + 4 * first;   // fewer than 4 bytes left before the limit
-        while (a + m < limit && in[a + m] == in[b + m]) m++;
-        return rfl(m);
-    }
-}
 
 // byte `rel` of a sequence's encoding: token, literal-length bytes, literals, offset, match-length bytes
 struct SeqFields {
@@ -157,97 +125,12 @@ __device__ bool emit_records(const uint2 *rec, uint32_t n, uint32_t anchor, cons
 // compressed size, or 0 if it does not fit in cap.
 __device__ int32_t encode_page(const uint8_t *in, uint32_t L, uint16_t *table, uint8_t *map, uint2 *rec,
                                uint8_t *dst, uint32_t cap, uint32_t lane) {
-    uint32_t op = 0, anchor = 0;
-    if (L >= (uint32_t)(kMfLimit + 1)) {
-        const uint32_t mflimit = L - kMfLimit;          // last position a match may start
-        const uint32_t matchlimit = L - kLastLiterals;  // matches end at or before this
-        uint32_t cursor = 0;     // matches may start here (end of the last match)
-        uint32_t nacc = 0;       // sequences accumulated in rec[] since the last emission
-        uint32_t blk = 0;        // current 64-position block
-        bool done = false;
-        for (; !done && blk <= mflimit; blk = max(blk + kWave, cursor & ~(kWave - 1))) {
-            const uint32_t pos = blk + lane;
-            const bool live = pos <= mflimit;
-            // ---- candidates from earlier blocks, then insert this block's positions
-            const uint32_t v = lds_ld32(in + pos);
-            const uint32_t h = hash4(v);
-            const uint32_t cand = live ? table[h] : 0u;
-            __builtin_amdgcn_wave_barrier();
-            if (live) table[h] = (uint16_t)pos;
-            const bool ok = live && cand < pos && lds_ld32(in + cand) == v;
-            // ---- forward probe (MINMATCH + up to kProbe bytes) and backward probe (up to 4 bytes)
-            uint32_t len = (TYCHE_EABLATE & 2) ? 4u : 0u, back = 0;
-            bool capped = false;
-            if (ok && !(TYCHE_EABLATE & 2)) {
-                // four unaligned dword compares, no branches; clamp to the match limit
-                const uint32_t e = min(matchlimit, pos + kMinMatch + kProbe);
-                const uint32_t x0 = lds_ld32(in + pos + 4) ^ lds_ld32(in + cand + 4);
-                const uint32_t x1 = lds_ld32(in + pos + 8) ^ lds_ld32(in + cand + 8);
-                const uint32_t x2 = lds_ld32(in + pos + 12) ^ lds_ld32(in + cand + 12);
-                const uint32_t x3 = lds_ld32(in + pos + 16) ^ lds_ld32(in + cand + 16);
-                uint32_t n = x0 ? 4 + (__builtin_ctz(x0) >> 3)
-                           : x1 ? 8 + (__builtin_ctz(x1) >> 3)
-                           : x2 ? 12 + (__builtin_ctz(x2) >> 3)
-                           : x3 ? 16 + (__builtin_ctz(x3) >> 3) : 20u;
-                n = min(n, e - pos);
-                len = n;
-                capped = pos + n == e && e < matchlimit;
-                if (pos >= 4 && cand >= 4) {
-                    const uint32_t x = lds_ld32(in + pos - 4) ^ lds_ld32(in + cand - 4);
-                    back = x ? (__builtin_clz(x) >> 3) : 4u;
-                }
-            }
-            // ---- greedy parse of this block.  Every lane precomputes where the parse
-            // goes if it stands at its position: the first match at or after it
-            // (ballot mask) and that match's end.  The parse itself then only hops
-            // through these values with v_readlane (scalar code, no memory).
-            const uint64_t mall = (TYCHE_EABLATE & 4) ? 0ull : __ballot(ok);
-            uint32_t at = cursor > blk ? cursor - blk : 0u;        // parse position within the block
-            if ((mall >> at) == 0) continue;                       // no match starts at or after it
-            const uint64_t ahead = mall & ~((1ull << lane) - 1ull);
-            const uint32_t nml = ahead ? (uint32_t)__builtin_ctzll(ahead) : 64u;
-            const uint32_t nlen = __shfl(len | ((uint32_t)capped << 16), nml & 63u);
-            // hop word: bits 0..6 lane of the next match (64 = none), bit 7 capped, bits 8.. its end
-            const uint32_t hop = nml | ((nlen >> 16) << 7) | ((blk + nml + (nlen & 0xFFFFu)) << 8);
-            uint64_t sel = 0;
-            for (;;) {
-                const uint32_t h = rdlane(hop, at);
-                const uint32_t li = h & 127u;
-                if (li >= 64) break;                                 // no further match in this block
-                uint32_t end = h >> 8;
-                if ((h & 128u) && !(TYCHE_EABLATE & 8)) {
-                    // reached the probe limit: extend with the whole wave
-                    const uint32_t mp = blk + li, mc = rdlane(cand, li), ln0 = end - mp;
-                    const uint32_t ln = ln0 + wave_extend(in, mp + ln0, mc + ln0, matchlimit, lane);
-                    if (lane == li) len = ln;
-                    end = mp + ln;
-                }
-                sel |= 1ull << li;
-                cursor = end;
-                if (cursor > mflimit) { done = true; break; }
-                if (cursor >= blk + kWave) break;
-                at = cursor - blk;
-            }
-            if (sel == 0) continue;
-            // ---- append this block's sequences to the LDS records (stream order)
-            const bool is_sel = (sel >> lane) & 1ull;
-            const uint32_t rank = nacc + (uint32_t)__popcll(sel & ((1ull << lane) - 1ull));
-            if (is_sel) rec[rank] = make_uint2(pos | (cand << 16), len | (back << 16));
-            nacc += (uint32_t)__popcll(sel);
-            // a block adds at most 16 sequences (each covers >= 4 positions)
-            if (nacc > kWave - 16 || done) {
-                __builtin_amdgcn_wave_barrier();
-                if (!emit_records(rec, nacc, anchor, in, dst, op, cap, map, lane)) return 0;
-                anchor = cursor;
-                nacc = 0;
-            }
-        }
-        if (nacc) {
-            __builtin_amdgcn_wave_barrier();
-            if (!emit_records(rec, nacc, anchor, in, dst, op, cap, map, lane)) return 0;
-            anchor = cursor;
-        }
-    }
+    uint32_t op = 0;
+    auto sink = [&](const uint2 *r, uint32_t n, uint32_t anchor) -> bool {
+        return emit_records(r, n, anchor, in, dst, op, cap, map, lane);
+    };
+    const uint32_t anchor = lzp::parse_page(in, L, table, rec, lane, sink);
+    if (anchor == 0xFFFFFFFFu) return 0;
     // ---- last literals: in[anchor, L)
     const uint32_t lit = L - anchor;
     const uint32_t lext = lit >= 15 ? (lit - 15) / 255 + 1 : 0;

@@ -1,0 +1,185 @@
+// lz_parse.h -- the wave-parallel greedy LZ77 parse shared by the gfx950
+// encoders (LZ4 blocks, zstd frames).
+//
+// One 64-lane wave parses one page held in LDS next to a table of 2^12 16-bit
+// positions (the byU16 scheme of lz4.c:402-408, hash 2654435761 of 4 bytes).
+// The page is scanned in blocks of 64 positions:
+//   * every lane hashes its position, takes the candidate left by earlier
+//     blocks, verifies 4 bytes, probes the match length up to 20 bytes and the
+//     backward extension up to 4 bytes (lz4.c:549's catch-up);
+//   * the greedy parse over the block runs on scalar registers only: first
+//     match at or after the cursor (ballot mask), cursor = its end; a match
+//     that reached the probe limit is extended by the whole wave (256 bytes per
+//     step);
+//   * selected matches are appended to LDS records in stream order and handed
+//     to the codec's sink in batches of at most 64.
+// Every match starts at or before L-MFLIMIT (12) and ends at or before
+// L-LASTLITERALS (5) (lz4.c:266-267): required by the LZ4 block format,
+// harmless for zstd.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "engine.h"
+#include "lds_io.h"
+
+namespace tyche {
+namespace lzp {
+
+constexpr uint32_t kWave = 64;
+constexpr uint32_t kHashLog = 12;
+constexpr uint32_t kHashSize = 1u << kHashLog;
+constexpr uint32_t kProbe = 16;          // bytes probed per lane beyond MINMATCH
+
+// Timing-only ablation builds (-DTYCHE_EABLATE=mask; outputs are wrong):
+//   1 skip the byte emission loop (sizes still computed), 2 no probes (every match 4 bytes),
+//   4 no greedy parse (no sequences: the page becomes one literal run)
+//   8 no whole-wave extension of probe-capped matches (valid output, shorter matches)
+#ifndef TYCHE_EABLATE
+#define TYCHE_EABLATE 0
+#endif
+
+__device__ __forceinline__ uint32_t hash4(uint32_t v) { return (v * 2654435761u) >> (32 - kHashLog); }
+
+// equal bytes at a and b going forward, a stopping before `limit` (whole wave, 256 bytes per step)
+__device__ inline uint32_t wave_extend(const uint8_t *in, uint32_t a, uint32_t b, uint32_t limit, uint32_t lane) {
+    uint32_t n = 0;
+    for (;;) {
+        const uint32_t pa = a + n + 4 * lane;
+        const bool full = pa + 4 <= limit;
+        const uint32_t x = full ? (lds_ld32(in + pa) ^ lds_ld32(in + b + n + 4 * lane)) : 1u;
+        const uint64_t bad = __ballot(x != 0);
+        if (bad == 0) {
+            n += 4 * kWave;
+            continue;
+        }
+        const uint32_t first = (uint32_t)__builtin_ctzll(bad);
+        const uint32_t pf = a + n + 4 * first;
+        if (pf + 4 <= limit) return n + 4 * first + (__builtin_ctz(rdlane(x, first)) >> 3);
+        uint32_t m = n + 4 * first;   // fewer than 4 bytes left before the limit
+        while (a + m < limit && in[a + m] == in[b + m]) m++;
+        return rfl(m);
+    }
+}
+
+// A record: x = pos | cand << 16, y = len | back << 16 (match at pos from cand,
+// len bytes forward, up to `back` bytes of backward extension available).
+// The literal run before a record starts at the previous record's end (or the
+// anchor); the catch-up actually taken is min(back, pos - prev_end, cand).
+__device__ __forceinline__ void decode_record(const uint2 *rec, uint32_t n, uint32_t anchor, uint32_t lane,
+                                              uint32_t &lit_start, uint32_t &lit_len, uint32_t &match_len,
+                                              uint32_t &offset) {
+    const bool is_sel = lane < n;
+    const uint2 r = rec[is_sel ? lane : 0];
+    const uint2 rp = rec[lane > 0 && is_sel ? lane - 1 : 0];
+    const uint32_t pos = r.x & 0xFFFFu, cand = r.x >> 16, len = r.y & 0xFFFFu, back = r.y >> 16;
+    const uint32_t prev_end = lane == 0 ? anchor : (rp.x & 0xFFFFu) + (rp.y & 0xFFFFu);
+    const uint32_t k = min(min(back, pos - prev_end), cand);
+    lit_start = prev_end;
+    lit_len = is_sel ? pos - k - prev_end : 0u;
+    match_len = is_sel ? len + k : 0u;
+    offset = pos - cand;
+}
+
+// Greedy parse of in[0, L) (LDS, 64 zero bytes after).  table: kHashSize 16-bit
+// slots, zeroed by the caller.  rec: 64 uint2 records.  sink(rec, n, anchor)
+// consumes n >= 1 records whose literal runs start at `anchor`, and returns
+// false to abort.  Returns the anchor where the last literal run starts, or
+// 0xFFFFFFFF if the sink aborted.
+template <typename Sink>
+__device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *table, uint2 *rec, uint32_t lane,
+                                      Sink &sink) {
+    uint32_t anchor = 0;
+    if (L < (uint32_t)(kMfLimit + 1)) return 0;
+    const uint32_t mflimit = L - kMfLimit;          // last position a match may start
+    const uint32_t matchlimit = L - kLastLiterals;  // matches end at or before this
+    uint32_t cursor = 0;     // matches may start here (end of the last match)
+    uint32_t nacc = 0;       // records accumulated since the last hand-off
+    uint32_t blk = 0;        // current 64-position block
+    bool done = false;
+    for (; !done && blk <= mflimit; blk = max(blk + kWave, cursor & ~(kWave - 1))) {
+        const uint32_t pos = blk + lane;
+        const bool live = pos <= mflimit;
+        // ---- candidates from earlier blocks, then insert this block's positions
+        const uint32_t v = lds_ld32(in + pos);
+        const uint32_t h = hash4(v);
+        const uint32_t cand = live ? table[h] : 0u;
+        __builtin_amdgcn_wave_barrier();
+        if (live) table[h] = (uint16_t)pos;
+        const bool ok = live && cand < pos && lds_ld32(in + cand) == v;
+        // ---- forward probe (MINMATCH + up to kProbe bytes) and backward probe (up to 4 bytes)
+        uint32_t len = (TYCHE_EABLATE & 2) ? 4u : 0u, back = 0;
+        bool capped = false;
+        if (ok && !(TYCHE_EABLATE & 2)) {
+            // four unaligned dword compares, no branches; clamp to the match limit
+            const uint32_t e = min(matchlimit, pos + kMinMatch + kProbe);
+            const uint32_t x0 = lds_ld32(in + pos + 4) ^ lds_ld32(in + cand + 4);
+            const uint32_t x1 = lds_ld32(in + pos + 8) ^ lds_ld32(in + cand + 8);
+            const uint32_t x2 = lds_ld32(in + pos + 12) ^ lds_ld32(in + cand + 12);
+            const uint32_t x3 = lds_ld32(in + pos + 16) ^ lds_ld32(in + cand + 16);
+            uint32_t n = x0 ? 4 + (__builtin_ctz(x0) >> 3)
+                       : x1 ? 8 + (__builtin_ctz(x1) >> 3)
+                       : x2 ? 12 + (__builtin_ctz(x2) >> 3)
+                       : x3 ? 16 + (__builtin_ctz(x3) >> 3) : 20u;
+            n = min(n, e - pos);
+            len = n;
+            capped = pos + n == e && e < matchlimit;
+            if (pos >= 4 && cand >= 4) {
+                const uint32_t x = lds_ld32(in + pos - 4) ^ lds_ld32(in + cand - 4);
+                back = x ? (__builtin_clz(x) >> 3) : 4u;
+            }
+        }
+        // ---- greedy parse of this block.  Every lane precomputes where the parse
+        // goes if it stands at its position: the first match at or after it
+        // (ballot mask) and that match's end.  The parse itself then only hops
+        // through these values with v_readlane (scalar code, no memory).
+        const uint64_t mall = (TYCHE_EABLATE & 4) ? 0ull : __ballot(ok);
+        uint32_t at = cursor > blk ? cursor - blk : 0u;        // parse position within the block
+        if ((mall >> at) == 0) continue;                       // no match starts at or after it
+        const uint64_t ahead = mall & ~((1ull << lane) - 1ull);
+        const uint32_t nml = ahead ? (uint32_t)__builtin_ctzll(ahead) : 64u;
+        const uint32_t nlen = __shfl(len | ((uint32_t)capped << 16), nml & 63u);
+        // hop word: bits 0..6 lane of the next match (64 = none), bit 7 capped, bits 8.. its end
+        const uint32_t hop = nml | ((nlen >> 16) << 7) | ((blk + nml + (nlen & 0xFFFFu)) << 8);
+        uint64_t sel = 0;
+        for (;;) {
+            const uint32_t hw = rdlane(hop, at);
+            const uint32_t li = hw & 127u;
+            if (li >= 64) break;                                 // no further match in this block
+            uint32_t end = hw >> 8;
+            if ((hw & 128u) && !(TYCHE_EABLATE & 8)) {
+                // reached the probe limit: extend with the whole wave
+                const uint32_t mp = blk + li, mc = rdlane(cand, li), ln0 = end - mp;
+                const uint32_t ln = ln0 + wave_extend(in, mp + ln0, mc + ln0, matchlimit, lane);
+                if (lane == li) len = ln;
+                end = mp + ln;
+            }
+            sel |= 1ull << li;
+            cursor = end;
+            if (cursor > mflimit) { done = true; break; }
+            if (cursor >= blk + kWave) break;
+            at = cursor - blk;
+        }
+        if (sel == 0) continue;
+        // ---- append this block's records (stream order)
+        const bool is_sel = (sel >> lane) & 1ull;
+        const uint32_t rank = nacc + (uint32_t)__popcll(sel & ((1ull << lane) - 1ull));
+        if (is_sel) rec[rank] = make_uint2(pos | (cand << 16), len | (back << 16));
+        nacc += (uint32_t)__popcll(sel);
+        // a block adds at most 16 records (each covers >= 4 positions)
+        if (nacc > kWave - 16 || done) {
+            __builtin_amdgcn_wave_barrier();
+            if (!sink(rec, nacc, anchor)) return 0xFFFFFFFFu;
+            anchor = cursor;
+            nacc = 0;
+        }
+    }
+    if (nacc) {
+        __builtin_amdgcn_wave_barrier();
+        if (!sink(rec, nacc, anchor)) return 0xFFFFFFFFu;
+        anchor = cursor;
+    }
+    return anchor;
+}
+
+}  // namespace lzp
+}  // namespace tyche

@@ -1,0 +1,514 @@
+// zstd_encode.hip -- gfx950 encoder for zstd frames, the codec behind
+// buffer__compress for ZSTD_COMPRESSOR_ID (src/buffer.c:203-212 -> ZSTD_compress
+// level 1, src/zstd/zstd_compress.c:2721).  The output is a standard zstd frame
+// that the reference's ZSTD_decompress (zstd_decompress.c:1459) restores
+// bit-exactly; it is not required to be the bytes zstd 1.1.2 emits (SURVEY §8a
+// A8), and its ratio is below level 1's: literals are stored raw and the
+// sequences use the predefined FSE distributions (Huffman literals and
+// per-block FSE tables are the §8f rank-4 follow-up).
+//
+// Frame layout (zstd_compress.c:2334-2376): magic, a single-segment frame
+// header with the content size (no checksum, no dictionary), then blocks of at
+// most kSeqCap sequences each (the last flagged).  Per block:
+//   literals section   Raw_Literals_Block header + the concatenated literal runs
+//                      (ZSTD_noCompressLiterals, zstd_compress.c:406-428)
+//   sequences section  nbSeq, mode byte 0 (LL/OF/ML predefined), and the FSE
+//                      bitstream written exactly as ZSTD_compressSequences does
+//                      (zstd_compress.c:695-735): last sequence first through
+//                      FSE_initCState2, the rest backwards with
+//                      FSE_encodeSymbol OF, ML, LL then the LL, ML, OF extra
+//                      bits, the three final states, the end mark
+//                      (bitstream.h BIT_addBits / BIT_flushBits / BIT_closeCStream)
+// A block whose encoding would not be smaller than its input is stored raw.
+//
+// One wave per page, looping over pages with the next page prefetched into
+// registers.  The match finder is the shared parse (lz_parse.h).  Sequence
+// codes and extra-bit values are computed lane-parallel; the FSE state chain
+// is serial, so it runs as wave-uniform code over 64 sequences held in lanes
+// (v_readlane), with the predefined CTables in constant memory (scalar loads),
+// flushing each sequence's bytes with one 8-lane byte store.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "engine.h"
+#include "lds_io.h"
+#include "lz_parse.h"
+
+namespace tyche {
+namespace {
+
+using lzp::kHashSize;
+using lzp::kWave;
+constexpr uint32_t kPad = 64;
+constexpr uint32_t kSeqCap = 1024;       // sequences buffered per block
+constexpr uint32_t kPrefetchVec = 16;
+
+// ------------------------------------------------------------ predefined FSE CTables
+// FSE_buildCTable_wksp (fse_compress.c) over the default distributions of
+// zstd_internal.h:118-136, evaluated at compile time.
+constexpr int16_t kLLNorm[36] = {4, 3, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 1, 1, 1, 2, 2, 2, 2, 2, 2, 2, 2, 2, 3, 2, 1,
+                                 1, 1, 1, 1, -1, -1, -1, -1};
+constexpr int16_t kMLNorm[53] = {1, 4, 3, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1,
+                                 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1, -1, -1};
+constexpr int16_t kOFNorm[29] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1,
+                                 -1, -1};
+constexpr uint8_t kLLBits[36] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 3, 3, 4, 6, 7, 8,
+                                 9, 10, 11, 12, 13, 14, 15, 16};
+constexpr uint8_t kMLBits[53] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
+                                 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 3, 3, 4, 4, 5, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
+constexpr uint32_t kLLBase[36] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 18, 20, 22, 24, 28, 32,
+                                  40, 48, 64, 0x80, 0x100, 0x200, 0x400, 0x800, 0x1000, 0x2000, 0x4000, 0x8000,
+                                  0x10000};
+constexpr uint32_t kMLBase[53] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24,
+                                  25, 26, 27, 28, 29, 30, 31, 32, 33, 34, 35, 37, 39, 41, 43, 47, 51, 59, 67, 83,
+                                  99, 0x83, 0x103, 0x203, 0x403, 0x803, 0x1003, 0x2003, 0x4003, 0x8003, 0x10003};
+
+struct CTab {
+    uint16_t state[64];      // stateTable (tableSize <= 64)
+    uint32_t dnb[53];        // symbolTT.deltaNbBits
+    int32_t dfs[53];         // symbolTT.deltaFindState
+    uint32_t log;
+};
+
+constexpr uint32_t ce_highbit(uint32_t v) {
+    uint32_t r = 0;
+    while (v >>= 1) r++;
+    return r;
+}
+
+constexpr CTab make_ctab(const int16_t *norm, uint32_t max_sv, uint32_t log) {
+    CTab t{};
+    const uint32_t size = 1u << log, mask = size - 1u, step = (size >> 1) + (size >> 3) + 3u;
+    uint8_t sym[64] = {};
+    uint32_t cumul[55] = {};
+    uint32_t high = size - 1u;
+    for (uint32_t u = 1; u <= max_sv + 1; u++) {
+        if (norm[u - 1] == -1) {
+            cumul[u] = cumul[u - 1] + 1;
+            sym[high--] = (uint8_t)(u - 1);
+        } else {
+            cumul[u] = cumul[u - 1] + (uint32_t)norm[u - 1];
+        }
+    }
+    cumul[max_sv + 1] = size + 1;
+    uint32_t pos = 0;
+    for (uint32_t s = 0; s <= max_sv; s++)
+        for (int i = 0; i < norm[s]; i++) {
+            sym[pos] = (uint8_t)s;
+            pos = (pos + step) & mask;
+            while (pos > high) pos = (pos + step) & mask;
+        }
+    for (uint32_t u = 0; u < size; u++) t.state[cumul[sym[u]]++] = (uint16_t)(size + u);
+    int32_t total = 0;
+    for (uint32_t s = 0; s <= max_sv; s++) {
+        const int32_t n = norm[s];
+        if (n == 0) continue;
+        if (n == -1 || n == 1) {
+            t.dnb[s] = (log << 16) - (1u << log);
+            t.dfs[s] = total - 1;
+            total++;
+        } else {
+            const uint32_t mbo = log - ce_highbit((uint32_t)n - 1u);
+            const uint32_t msp = (uint32_t)n << mbo;
+            t.dnb[s] = (mbo << 16) - msp;
+            t.dfs[s] = total - n;
+            total += n;
+        }
+    }
+    t.log = log;
+    return t;
+}
+
+// LL_Code / ML_Code (zstd_compress.c:515-533): the code whose base covers the value
+struct CodeTabs {
+    uint8_t ll[64];
+    uint8_t ml[128];
+};
+constexpr CodeTabs make_codes() {
+    CodeTabs c{};
+    for (uint32_t v = 0; v < 64; v++)
+        for (uint32_t k = 0; k < 36; k++)
+            if (kLLBase[k] <= v && v < kLLBase[k] + (1u << kLLBits[k])) c.ll[v] = (uint8_t)k;
+    for (uint32_t v = 0; v < 128; v++)
+        for (uint32_t k = 0; k < 53; k++)
+            if (kMLBase[k] - 3u <= v && v < kMLBase[k] - 3u + (1u << kMLBits[k])) c.ml[v] = (uint8_t)k;
+    return c;
+}
+
+__device__ __constant__ CTab c_ll_ct = make_ctab(kLLNorm, 35, 6);
+__device__ __constant__ CTab c_ml_ct = make_ctab(kMLNorm, 52, 6);
+__device__ __constant__ CTab c_of_ct = make_ctab(kOFNorm, 28, 5);
+__device__ __constant__ CodeTabs c_codes = make_codes();
+__device__ __constant__ uint8_t c_llbits[36] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 3, 3,
+                                                4, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
+__device__ __constant__ uint8_t c_mlbits[53] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
+                                                0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 3, 3, 4, 4, 5, 7, 8, 9,
+                                                10, 11, 12, 13, 14, 15, 16};
+
+__device__ __forceinline__ uint32_t hb(uint32_t v) { return 31u - (uint32_t)__builtin_clz(v); }
+
+// (code, extra bits) of one sequence -- ZSTD_seqToCodes (zstd_compress.c:535-556)
+struct SeqCode {
+    uint32_t llc, mlc, ofc;          // codes
+    uint32_t llv, mlv, ofv;          // extra-bit values (masked by BIT_addBits)
+    uint32_t llb, mlb;               // extra-bit counts (ofc for offsets)
+};
+__device__ __forceinline__ SeqCode seq_code(uint32_t ll, uint32_t ml, uint32_t off) {
+    SeqCode c;
+    const uint32_t mlbase = ml - 3u, ofcode = off + 3u;
+    c.llc = ll > 63u ? hb(ll) + 19u : c_codes.ll[ll];
+    c.mlc = mlbase > 127u ? hb(mlbase) + 36u : c_codes.ml[mlbase];
+    c.ofc = hb(ofcode);
+    c.llb = c_llbits[c.llc];
+    c.mlb = c_mlbits[c.mlc];
+    c.llv = ll & ((1u << c.llb) - 1u);
+    c.mlv = mlbase & ((1u << c.mlb) - 1u);
+    c.ofv = ofcode & ((1u << c.ofc) - 1u);
+    return c;
+}
+
+// ------------------------------------------------------------ backward-readable bit writer
+struct BitC {
+    uint64_t c;
+    uint32_t pos;     // bits in c
+    uint32_t ptr;     // output offset of the next byte
+};
+__device__ __forceinline__ void add_bits(BitC &b, uint32_t v, uint32_t nb) {
+    b.c |= (uint64_t)v << b.pos;      // v already masked to nb bits
+    b.pos += nb;
+}
+// BIT_flushBits: the whole bytes of c go out (8 lanes, one byte each)
+__device__ __forceinline__ void flush_bits(BitC &b, uint8_t *dst, uint32_t lane) {
+    const uint32_t nbytes = b.pos >> 3;
+    if (lane < nbytes) dst[b.ptr + lane] = (uint8_t)(b.c >> (8u * lane));
+    b.ptr += nbytes;
+    b.pos &= 7u;
+    b.c = nbytes >= 8u ? 0ull : b.c >> (8u * nbytes);
+}
+
+struct FseState {
+    uint32_t value;
+};
+__device__ __forceinline__ void fse_init2(FseState &s, const CTab &t, uint32_t sym) {
+    const uint32_t dnb = t.dnb[sym];
+    const uint32_t nbo = (dnb + (1u << 15)) >> 16;
+    const uint32_t v = (nbo << 16) - dnb;
+    s.value = t.state[(int32_t)(v >> nbo) + t.dfs[sym]];
+}
+__device__ __forceinline__ void fse_encode(BitC &b, FseState &s, const CTab &t, uint32_t sym) {
+    const uint32_t nbo = (s.value + t.dnb[sym]) >> 16;
+    add_bits(b, s.value & ((1u << nbo) - 1u), nbo);
+    s.value = t.state[(int32_t)(s.value >> nbo) + t.dfs[sym]];
+}
+
+// ------------------------------------------------------------ block emission
+// Sequences of the current block live in LDS: seq[i] = (ll | off << 16, ml).
+struct Enc {
+    const uint8_t *in;   // page (LDS)
+    uint8_t *dst;        // output (global)
+    uint32_t cap, op;    // capacity, bytes written
+    uint2 *seq;          // kSeqCap sequences
+    uint32_t nseq;       // sequences in the current block
+    uint32_t bstart;     // first page byte of the current block
+    uint32_t cursor;     // end of the last buffered sequence's match
+    uint8_t *map;        // 64-byte owner map
+    bool fail;
+};
+
+// Writes one block covering page bytes [s.bstart, bend) with the buffered
+// sequences; `last` sets Last_Block.  Returns false if it does not fit.
+__device__ bool emit_block(Enc &e, uint32_t bend, bool last, uint32_t lane) {
+    const uint32_t n = e.nseq, blen = bend - e.bstart;
+    // ---- per-sequence sizes (lane-parallel over 64-sequence groups)
+    uint32_t lit_sum = 0, span = 0, xbits = 0;
+    for (uint32_t g = 0; g < n; g += kWave) {
+        const uint32_t i = g + lane;
+        uint32_t ll = 0, ml = 0, xb = 0;
+        if (i < n) {
+            const uint2 r = e.seq[i];
+            ll = r.x & 0xFFFFu;
+            ml = r.y;
+            const SeqCode c = seq_code(ll, ml, r.x >> 16);
+            xb = c.llb + c.mlb + c.ofc;
+        }
+        lit_sum += rdlane((uint32_t)wave_incl_sum((int32_t)ll), kWave - 1);
+        span += rdlane((uint32_t)wave_incl_sum((int32_t)(ll + ml)), kWave - 1);
+        xbits += rdlane((uint32_t)wave_incl_sum((int32_t)xb), kWave - 1);
+    }
+    const uint32_t trail = bend - (e.bstart + span);       // literals after the last match
+    const uint32_t lit_total = lit_sum + trail;
+    const uint32_t fl = 1u + (lit_total > 31u) + (lit_total > 4095u);
+    const uint32_t nsh = n < 0x7Fu ? 1u : (n < 0x7F00u ? 2u : 3u);
+    // upper bound of the FSE bitstream: every state emits at most its table log
+    const uint32_t fse_bound = n ? (n * 17u + xbits + 17u + 8u + 7u) / 8u + 1u : 0u;
+    const uint32_t comp_bound = fl + lit_total + nsh + (n ? 1u : 0u) + fse_bound;
+    const uint32_t hdr = e.op;                              // block header position
+    if (comp_bound >= blen) {
+        // ---- raw block (Block_Type 0): header + the page bytes
+        if (e.op + 3u + blen > e.cap) return false;
+        const uint32_t bh = (last ? 1u : 0u) | (0u << 1) | (blen << 3);
+        if (lane < 3) e.dst[hdr + lane] = (uint8_t)(bh >> (8u * lane));
+        for (uint32_t j = lane; j < blen; j += kWave) e.dst[hdr + 3u + j] = e.in[e.bstart + j];
+        e.op += 3u + blen;
+        return true;
+    }
+    if (e.op + 3u + comp_bound > e.cap) return false;
+    uint32_t o = hdr + 3u;
+    // ---- literals section header (ZSTD_noCompressLiterals)
+    {
+        uint32_t h;
+        if (fl == 1u) h = lit_total << 3;
+        else if (fl == 2u) h = (1u << 2) | (lit_total << 4);
+        else h = (3u << 2) | (lit_total << 4);
+        if (lane < fl) e.dst[o + lane] = (uint8_t)(h >> (8u * lane));
+        o += fl;
+    }
+    // ---- literal bytes, 64 per store: output byte j belongs to the last run starting at or before j
+    {
+        uint32_t lo = 0, pstart = e.bstart;   // literal-section offset / page position of this group
+        for (uint32_t g = 0; g <= n; g += kWave) {
+            const uint32_t i = g + lane;
+            // runs: sequences g..g+63, plus the trailing literals as run n
+            uint32_t ll = 0, ml = 0;
+            if (i < n) {
+                const uint2 r = e.seq[i];
+                ll = r.x & 0xFFFFu;
+                ml = r.y;
+            } else if (i == n) {
+                ll = trail;
+            }
+            const bool run = i <= n;
+            const int32_t li = wave_incl_sum((int32_t)ll), si = wave_incl_sum((int32_t)(ll + ml));
+            const uint32_t rlo = lo + (uint32_t)li - ll;                   // run start in the literal section
+            const uint32_t rsrc = pstart + (uint32_t)si - (ll + ml);       // run start in the page
+            const uint32_t glen = rdlane((uint32_t)li, kWave - 1);
+            for (uint32_t j0 = 0; j0 < glen; j0 += kWave) {
+                const uint32_t j = lo + j0 + lane;
+                const uint64_t before = __ballot(run && ll && rlo <= lo + j0);
+                const int32_t owner0 = before ? 63 - (int32_t)__builtin_clzll(before) : 0;
+                e.map[lane] = 0xFF;
+                __builtin_amdgcn_wave_barrier();
+                if (run && ll && rlo > lo + j0 && rlo < lo + j0 + kWave) e.map[rlo - lo - j0] = (uint8_t)lane;
+                __builtin_amdgcn_wave_barrier();
+                const uint32_t mv = e.map[lane];
+                const uint32_t owner = (uint32_t)max(wave_incl_max(mv == 0xFF ? -1 : (int32_t)mv), owner0);
+                const uint32_t orlo = __shfl(rlo, owner), orsrc = __shfl(rsrc, owner);
+                if (j0 + lane < glen) e.dst[o + j] = e.in[orsrc + (j - orlo)];
+                __builtin_amdgcn_wave_barrier();
+            }
+            lo += glen;
+            pstart += rdlane((uint32_t)si, kWave - 1);
+        }
+        o += lit_total;
+    }
+    // ---- sequences section header
+    if (lane < nsh) {
+        uint32_t h;
+        if (nsh == 1u) h = n;
+        else if (nsh == 2u) h = ((n >> 8) + 0x80u) | ((n & 0xFFu) << 8);
+        else h = 0xFFu | ((n - 0x7F00u) << 8);
+        e.dst[o + lane] = (uint8_t)(h >> (8u * lane));
+    }
+    o += nsh;
+    if (n) {
+        if (lane == 0) e.dst[o] = 0;   // LL, OF, ML: predefined distributions (set_basic)
+        o += 1;
+        // ---- FSE bitstream: groups of 64 sequences from the last, serial inside a group
+        BitC b;
+        b.c = 0;
+        b.pos = 0;
+        b.ptr = o;
+        FseState sll, sml, sof;
+        sll.value = sml.value = sof.value = 0;
+        const uint32_t ng = (n + kWave - 1) / kWave;
+        for (uint32_t gi = ng; gi-- > 0;) {
+            const uint32_t g = gi * kWave;
+            const uint32_t i = g + lane;
+            uint32_t pk_code = 0, pk_ll = 0, pk_ml = 0, pk_of = 0;
+            if (i < n) {
+                const uint2 r = e.seq[i];
+                const SeqCode c = seq_code(r.x & 0xFFFFu, r.y, r.x >> 16);
+                pk_code = c.llc | (c.mlc << 8) | (c.ofc << 16);
+                pk_ll = c.llv | (c.llb << 24);
+                pk_ml = c.mlv | (c.mlb << 24);
+                pk_of = c.ofv;
+            }
+            const uint32_t top = min(n - g, kWave);
+            for (uint32_t k = top; k-- > 0;) {
+                const uint32_t code = rdlane(pk_code, k), xl = rdlane(pk_ll, k), xm = rdlane(pk_ml, k),
+                               xo = rdlane(pk_of, k);
+                const uint32_t llc = code & 0xFFu, mlc = (code >> 8) & 0xFFu, ofc = code >> 16;
+                const uint32_t llb = xl >> 24, mlb = xm >> 24;
+                if (g + k == n - 1) {
+                    // first symbols (zstd_compress.c:700-708)
+                    fse_init2(sml, c_ml_ct, mlc);
+                    fse_init2(sof, c_of_ct, ofc);
+                    fse_init2(sll, c_ll_ct, llc);
+                } else {
+                    fse_encode(b, sof, c_of_ct, ofc);
+                    fse_encode(b, sml, c_ml_ct, mlc);
+                    fse_encode(b, sll, c_ll_ct, llc);
+                    if (ofc + mlb + llb >= 64u - 7u - (9u + 9u + 8u)) flush_bits(b, e.dst, lane);
+                }
+                add_bits(b, xl & 0xFFFFFFu, llb);
+                add_bits(b, xm & 0xFFFFFFu, mlb);
+                add_bits(b, xo, ofc);
+                flush_bits(b, e.dst, lane);
+            }
+        }
+        // FSE_flushCState x3, BIT_closeCStream (end mark)
+        add_bits(b, sml.value & 63u, c_ml_ct.log);
+        flush_bits(b, e.dst, lane);
+        add_bits(b, sof.value & 31u, c_of_ct.log);
+        flush_bits(b, e.dst, lane);
+        add_bits(b, sll.value & 63u, c_ll_ct.log);
+        flush_bits(b, e.dst, lane);
+        add_bits(b, 1u, 1u);
+        flush_bits(b, e.dst, lane);
+        o = b.ptr + (b.pos > 0 ? 1u : 0u);
+        if (b.pos > 0 && lane == 0) e.dst[b.ptr] = (uint8_t)b.c;
+    }
+    const uint32_t csize = o - (hdr + 3u);
+    const uint32_t bh = (last ? 1u : 0u) | (2u << 1) | (csize << 3);
+    if (lane < 3) e.dst[hdr + lane] = (uint8_t)(bh >> (8u * lane));
+    e.op = o;
+    return true;
+}
+
+// Encodes one page held in LDS (in[0, L), 64 zero bytes after).  Returns the
+// frame size, or 0 if it does not fit in cap.
+__device__ int32_t encode_page(const uint8_t *in, uint32_t L, uint16_t *table, uint8_t *map, uint2 *rec, uint2 *seq,
+                               uint8_t *dst, uint32_t cap, uint32_t lane) {
+    // ---- frame header: magic, single-segment descriptor with the content size
+    const uint32_t fcs_id = L < 256u ? 0u : (L < 65536u + 256u ? 1u : 2u);
+    const uint32_t fcs_len = fcs_id == 0u ? 1u : (fcs_id == 1u ? 2u : 4u);
+    const uint32_t fh = 5u + fcs_len;
+    if (fh + 3u > cap) return 0;
+    {
+        const uint32_t fcs = fcs_id == 1u ? L - 256u : L;
+        uint32_t v = 0;
+        if (lane < 4) v = 0xFD2FB528u >> (8u * lane);
+        else if (lane == 4) v = 0x20u | (fcs_id << 6);
+        else if (lane < 5u + fcs_len) v = fcs >> (8u * (lane - 5u));
+        if (lane < fh) dst[lane] = (uint8_t)v;
+    }
+    Enc e;
+    e.in = in;
+    e.dst = dst;
+    e.cap = cap;
+    e.op = fh;
+    e.seq = seq;
+    e.nseq = 0;
+    e.bstart = 0;
+    e.cursor = 0;
+    e.map = map;
+    e.fail = false;
+    auto sink = [&](const uint2 *r, uint32_t n, uint32_t anchor) -> bool {
+        uint32_t ls, ll, ml, off;
+        lzp::decode_record(r, n, anchor, lane, ls, ll, ml, off);
+        if (lane < n) seq[e.nseq + lane] = make_uint2(ll | (off << 16), ml);
+        e.nseq += n;
+        const uint2 lastr = r[n - 1];
+        e.cursor = (lastr.x & 0xFFFFu) + (lastr.y & 0xFFFFu);
+        __builtin_amdgcn_wave_barrier();
+        if (e.nseq > kSeqCap - kWave) {
+            if (!emit_block(e, e.cursor, false, lane)) return false;
+            e.bstart = e.cursor;
+            e.nseq = 0;
+        }
+        return true;
+    };
+    const uint32_t anchor = lzp::parse_page(in, L, table, rec, lane, sink);
+    if (anchor == 0xFFFFFFFFu) return 0;
+    if (!emit_block(e, L, true, lane)) return 0;
+    return (int32_t)e.op;
+}
+
+__global__ __launch_bounds__(64) void zstd_encode_kernel(tyche_batch_t b, uint32_t in_cap) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint32_t lane = threadIdx.x;
+    uint16_t *table = (uint16_t *)smem;
+    uint8_t *map = smem + kHashSize * sizeof(uint16_t);                 // 64-byte owner map
+    uint2 *rec = (uint2 *)(map + kWave);                               // 64 parse records
+    uint2 *seq = rec + kWave;                                          // kSeqCap block sequences
+    uint8_t *stage = (uint8_t *)(seq + kSeqCap);
+    const size_t stride = gridDim.x;
+
+    size_t page = blockIdx.x;
+    if (page >= b.count) return;
+    PageRef p = batch_page(b, page);
+    uint32_t head = stage_in(p.src, p.src_len <= in_cap ? p.src_len : 0, stage, lane, kWave);
+    for (;;) {
+        const size_t next = page + stride;
+        PageRef pn;
+        u32x4 pf[kPrefetchVec];
+        uint32_t nhead = 0, nvec = 0;
+        if (next < b.count) {
+            pn = batch_page(b, next);
+            if (pn.src_len <= in_cap && pn.src_len > 0) {
+                uintptr_t a = (uintptr_t)pn.src;
+                nhead = (uint32_t)(a & 15u);
+                nvec = (nhead + pn.src_len + 15u) >> 4;
+                const u32x4 *g = (const u32x4 *)(a - nhead);
+#pragma unroll
+                for (uint32_t k = 0; k < kPrefetchVec; k++) {
+                    const uint32_t v = lane + k * kWave;
+                    if (v < nvec) pf[k] = __builtin_nontemporal_load(g + v);
+                }
+            }
+        }
+        int32_t rv;
+        if (p.src_len > in_cap) {
+            rv = kResultTooLarge;
+        } else {
+            uint8_t *in = stage + head;
+            for (uint32_t w = lane; w < kHashSize / 8; w += kWave) ((u32x4 *)table)[w] = u32x4{0, 0, 0, 0};
+            __syncthreads();
+            in[p.src_len + lane] = 0;
+            __syncthreads();
+            rv = encode_page(in, p.src_len, table, map, rec, seq, p.dst, p.dst_cap, lane);
+        }
+        if (lane == 0) b.results[page] = rv;
+        if (next >= b.count) break;
+        __syncthreads();
+        page = next;
+        p = pn;
+        head = nhead;
+        if (p.src_len <= in_cap && p.src_len > 0) {
+            u32x4 *l = (u32x4 *)stage;
+#pragma unroll
+            for (uint32_t k = 0; k < kPrefetchVec; k++) {
+                const uint32_t v = lane + k * kWave;
+                if (v < nvec) l[v] = pf[k];
+            }
+            const u32x4 *g = (const u32x4 *)((uintptr_t)p.src - nhead);
+            for (uint32_t v = lane + kPrefetchVec * kWave; v < nvec; v += kWave) l[v] = __builtin_nontemporal_load(g + v);
+        }
+    }
+}
+
+}  // namespace
+
+hipError_t launch_zstd_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream_t s) {
+    if (b.count == 0) return hipSuccess;
+    if (in_cap > 65535u) return hipErrorInvalidValue;    // 16-bit positions in the parse and sequence records
+    const size_t lds = kHashSize * sizeof(uint16_t) + kWave + kWave * 8 + kSeqCap * 8 +
+                       ((in_cap + 16u + kPad + 15u) & ~15u);
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    static int cus[64] = {0};
+    if (dev < 64 && cus[dev] == 0) {
+        (void)hipFuncSetAttribute((const void *)zstd_encode_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
+        int n = 0;
+        (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+        cus[dev] = n > 0 ? n : 256;
+    }
+    const size_t per_cu = std::max<size_t>(1, std::min<size_t>(32, (160 * 1024) / lds));
+    const size_t grid = std::min<size_t>(b.count, (size_t)(dev < 64 ? cus[dev] : 256) * per_cu);
+    hipLaunchKernelGGL(zstd_encode_kernel, dim3((unsigned)grid), dim3(kWave), lds, s, b, in_cap);
+    return hipGetLastError();
+}
+
+}  // namespace tyche
