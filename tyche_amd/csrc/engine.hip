@@ -63,7 +63,16 @@ int ensure_device() {
 }
 
 // codecs with a gfx950 kernel, per direction
-bool valid_codec(int id) { return id == TYCHE_LZ4_COMPRESSOR_ID || id == TYCHE_ZSTD_COMPRESSOR_ID; }
+bool valid_codec(int id) {
+    return id == TYCHE_LZ4_COMPRESSOR_ID || id == TYCHE_ZLIB_COMPRESSOR_ID || id == TYCHE_ZSTD_COMPRESSOR_ID;
+}
+
+// the encoder kernel for a codec id (valid_codec)
+hipError_t launch_encode(int id, const tyche_batch_t &b, uint32_t in_cap, hipStream_t s) {
+    if (id == TYCHE_ZSTD_COMPRESSOR_ID) return launch_zstd_encode(b, in_cap, s);
+    if (id == TYCHE_ZLIB_COMPRESSOR_ID) return launch_zlib_deflate(b, in_cap, s);
+    return launch_lz4_encode(b, in_cap, s);
+}
 bool valid_decode_codec(int id) {
     return id == TYCHE_LZ4_COMPRESSOR_ID || id == TYCHE_ZLIB_COMPRESSOR_ID || id == TYCHE_ZSTD_COMPRESSOR_ID;
 }
@@ -234,8 +243,7 @@ int tyche_compress_batch(int compressor_id, int compressor_level, const tyche_ba
     uint32_t in_cap = batch->src_lengths ? batch->max_src_length : batch->src_length;
     if (batch->src_lengths && in_cap == 0) in_cap = 65535;
     if (in_cap > 65535) { t_error = "pages above 64 KiB are not supported by the device encoders"; return TYCHE_E_BAD_ARGS; }
-    hipError_t e = compressor_id == TYCHE_ZSTD_COMPRESSOR_ID ? launch_zstd_encode(*batch, in_cap, (hipStream_t)stream)
-                                                              : launch_lz4_encode(*batch, in_cap, (hipStream_t)stream);
+    hipError_t e = launch_encode(compressor_id, *batch, in_cap, (hipStream_t)stream);
     if (e != hipSuccess) return fail("encode launch", e);
     return TYCHE_E_OK;
 }
@@ -271,14 +279,9 @@ int tyche_compress_host(int compressor_id, int compressor_level, size_t n, const
     if (n == 0) return TYCHE_E_OK;
     for (size_t i = 0; i < n; i++)
         if (src_lengths[i] > 65535u) { t_error = "pages above 64 KiB are not supported by the device encoders"; return TYCHE_E_BAD_ARGS; }
-    if (compressor_id == TYCHE_ZSTD_COMPRESSOR_ID)
-        return run_host_batch(n, src, src_lengths, dst, dst_capacities, results, true,
-                              [](const tyche_batch_t &b, hipStream_t s) {
-                                  return launch_zstd_encode(b, std::max(b.max_src_length, 1u), s);
-                              });
     return run_host_batch(n, src, src_lengths, dst, dst_capacities, results, true,
-                          [](const tyche_batch_t &b, hipStream_t s) {
-                              return launch_lz4_encode(b, std::max(b.max_src_length, 1u), s);
+                          [compressor_id](const tyche_batch_t &b, hipStream_t s) {
+                              return launch_encode(compressor_id, b, std::max(b.max_src_length, 1u), s);
                           });
 }
 
@@ -411,8 +414,7 @@ int tyche_buffers_compress(Buffer **bufs, void **compressed, int *status, size_t
         Buffer *b = bufs[idx[k]];
         src[k] = b->data;
         slen[k] = b->data_length;
-        dcap[k] = compressor_id == TYCHE_ZSTD_COMPRESSOR_ID ? zstd_bound(b->data_length)   // buffer.c:204
-                                                             : lz4_bound(b->data_length);   // LZ4_compressBound (buffer.c:179)
+        dcap[k] = tyche_compress_bound(compressor_id, b->data_length);   // the codec's bound (buffer.c:179, 191, 204)
         dst[k] = malloc(dcap[k]);
         if (!dst[k]) {
             for (size_t j = 0; j < k; j++) free(dst[j]);

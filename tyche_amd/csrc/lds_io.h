@@ -92,4 +92,24 @@ __device__ __forceinline__ void stage_out(uint8_t *dst, const uint8_t *lds, uint
     }
 }
 
+// adler32 (adler32.c:65) of out[0..n) in LDS: A = 1 + sum b_i, B = n + sum (n - i) b_i, mod 65521
+__device__ __forceinline__ uint32_t lds_adler32(const uint8_t *out, uint32_t n, uint32_t lane) {
+    uint32_t A = 0;
+    uint64_t B = 0;
+    for (uint32_t i = lane * 4u; i < n; i += 4u * 64u) {
+        uint32_t w = lds_ld32(out + i);
+        const uint32_t rem = n - i;
+        if (rem < 4u) w &= (1u << (8u * rem)) - 1u;
+        const uint32_t b0 = w & 255u, b1 = (w >> 8) & 255u, b2 = (w >> 16) & 255u, b3 = w >> 24;
+        const uint32_t s = b0 + b1 + b2 + b3;
+        A += s;
+        B += (uint64_t)rem * s - (b1 + 2u * b2 + 3u * b3);
+    }
+    const int32_t a = wave_incl_sum((int32_t)(A % 65521u));
+    const int32_t b = wave_incl_sum((int32_t)(uint32_t)(B % 65521u));
+    const uint32_t at = (1u + rdlane((uint32_t)a, 64u - 1)) % 65521u;
+    const uint32_t bt = (n % 65521u + rdlane((uint32_t)b, 64u - 1)) % 65521u;
+    return (bt << 16) | at;
+}
+
 }  // namespace tyche

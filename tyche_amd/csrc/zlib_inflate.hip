@@ -335,26 +335,6 @@ __device__ __forceinline__ void flush_matches(Pending &q, uint8_t *out, uint32_t
     }
 }
 
-// adler32 (adler32.c:65) of out[0..n) in LDS: A = 1 + sum b_i, B = n + sum (n - i) b_i, mod 65521
-__device__ __forceinline__ uint32_t adler_lds(const uint8_t *out, uint32_t n, uint32_t lane) {
-    uint32_t A = 0;
-    uint64_t B = 0;
-    for (uint32_t i = lane * 4u; i < n; i += 4u * kWave) {
-        uint32_t w = *(const uint32_t *)(out + i);
-        const uint32_t rem = n - i;
-        if (rem < 4u) w &= (1u << (8u * rem)) - 1u;
-        const uint32_t b0 = w & 255u, b1 = (w >> 8) & 255u, b2 = (w >> 16) & 255u, b3 = w >> 24;
-        const uint32_t s = b0 + b1 + b2 + b3;
-        A += s;
-        B += (uint64_t)rem * s - (b1 + 2u * b2 + 3u * b3);
-    }
-    const int32_t a = wave_incl_sum((int32_t)(A % 65521u));
-    const int32_t b = wave_incl_sum((int32_t)(uint32_t)(B % 65521u));
-    const uint32_t at = (1u + rdlane((uint32_t)a, kWave - 1)) % 65521u;
-    const uint32_t bt = (n % 65521u + rdlane((uint32_t)b, kWave - 1)) % 65521u;
-    return (bt << 16) | at;
-}
-
 // code-length code order (RFC 1951 3.2.7), 5 bits per entry
 __device__ __forceinline__ uint32_t cl_order(uint32_t i) {
     // 16 17 18 0 8 7 9 6 10 5 11 4 | 12 3 13 2 14 1 15
@@ -502,7 +482,7 @@ __device__ __forceinline__ int32_t inflate_page(BitReader &r, const uint8_t *src
     const uint32_t want = __builtin_bswap32(take(r, 32));
     flush_literals(q, out, lane);
     flush_matches(q, out, lane);
-    if (adler_lds(out, (uint32_t)op, lane) != want) return kZData;
+    if (lds_adler32(out, (uint32_t)op, lane) != want) return kZData;
     return op;
 }
 
