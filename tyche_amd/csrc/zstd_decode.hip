@@ -48,10 +48,10 @@ constexpr uint32_t kStreamPad = 32;    // zero bytes after the staged frame (8-b
 constexpr uint32_t kWinPad = 32;       // slack after the window (4X streams may run 3 bytes past)
 
 // ------------------------------------------------------------ constant tables
-__device__ __constant__ uint8_t c_ll_bits[36] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
+__device__ __constant__ uint32_t c_ll_bits[36] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
                                                  1, 1, 1, 1, 2, 2, 3, 3, 4, 6, 7, 8, 9, 10, 11, 12,
                                                  13, 14, 15, 16};
-__device__ __constant__ uint8_t c_ml_bits[53] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
+__device__ __constant__ uint32_t c_ml_bits[53] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
                                                  0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
                                                  1, 1, 1, 1, 2, 2, 3, 3, 4, 4, 5, 7, 8, 9, 10, 11,
                                                  12, 13, 14, 15, 16};
@@ -66,16 +66,54 @@ __device__ __constant__ uint32_t c_of_base[29] = {0, 1, 1, 5, 0xD, 0x1D, 0x3D, 0
                                                   0xFFD, 0x1FFD, 0x3FFD, 0x7FFD, 0xFFFD, 0x1FFFD, 0x3FFFD, 0x7FFFD,
                                                   0xFFFFD, 0x1FFFFD, 0x3FFFFD, 0x7FFFFD, 0xFFFFFD, 0x1FFFFFD,
                                                   0x3FFFFFD, 0x7FFFFFD, 0xFFFFFFD};
-// default distributions (zstd_internal.h:118-136)
-__device__ __constant__ int8_t c_ll_norm[36] = {4, 3, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 1, 1, 1,
-                                                2, 2, 2, 2, 2, 2, 2, 2, 2, 3, 2, 1, 1, 1, 1, 1,
-                                                -1, -1, -1, -1};
-__device__ __constant__ int8_t c_ml_norm[53] = {1, 4, 3, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1,
-                                                1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1,
-                                                1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1,
-                                                -1, -1, -1, -1, -1};
-__device__ __constant__ int8_t c_of_norm[29] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1,
-                                                1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1};
+// The predefined decoding tables (ZSTD_buildSeqTable set_basic ->
+// LL/OF/ML_defaultDTable, zstd_decompress.c:517-687) are FSE_buildDTable over
+// the default distributions; built here at compile time.
+constexpr int8_t kLLNormH[36] = {4, 3, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 1, 1, 1, 2, 2, 2, 2, 2, 2, 2, 2, 2, 3, 2, 1,
+                                 1, 1, 1, 1, -1, -1, -1, -1};
+constexpr int8_t kMLNormH[53] = {1, 4, 3, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1,
+                                 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1, -1, -1};
+constexpr int8_t kOFNormH[29] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1,
+                                 -1, -1};
+struct DTab {
+    uint32_t cell[64];   // newState | symbol << 16 | nbBits << 24
+};
+constexpr uint32_t ce_hb(uint32_t v) {
+    uint32_t r = 0;
+    while (v >>= 1) r++;
+    return r;
+}
+constexpr DTab make_dtab(const int8_t *norm, uint32_t max_sv, uint32_t log) {
+    DTab t{};
+    const uint32_t size = 1u << log, mask = size - 1u, step = (size >> 1) + (size >> 3) + 3u;
+    uint32_t high = size - 1u;
+    uint32_t next[64] = {};
+    uint32_t sym[64] = {};
+    for (uint32_t s = 0; s <= max_sv; s++) {
+        if (norm[s] == -1) {
+            sym[high--] = s;
+            next[s] = 1;
+        } else {
+            next[s] = (uint32_t)norm[s];
+        }
+    }
+    uint32_t pos = 0;
+    for (uint32_t s = 0; s <= max_sv; s++)
+        for (int i = 0; i < norm[s]; i++) {
+            sym[pos] = s;
+            pos = (pos + step) & mask;
+            while (pos > high) pos = (pos + step) & mask;
+        }
+    for (uint32_t u = 0; u < size; u++) {
+        const uint32_t sy = sym[u], ns = next[sy]++;
+        const uint32_t nb = log - ce_hb(ns);
+        t.cell[u] = ((ns << nb) - size) | (sy << 16) | (nb << 24);
+    }
+    return t;
+}
+__device__ __constant__ DTab c_ll_def = make_dtab(kLLNormH, 35, 6);
+__device__ __constant__ DTab c_of_def = make_dtab(kOFNormH, 28, 5);
+__device__ __constant__ DTab c_ml_def = make_dtab(kMLNormH, 52, 6);
 
 // ------------------------------------------------------------ LDS workspace
 struct Work {
@@ -128,6 +166,37 @@ __device__ __forceinline__ bool bitd_init(BitD &b, const uint8_t *in, int32_t st
     }
     return true;
 }
+// Wave-uniform variants: the loaded container goes through v_readfirstlane so
+// the whole reader (and every table index derived from it) lives in SGPRs and
+// constant-table lookups become scalar loads.
+__device__ __forceinline__ uint64_t ld64u(const uint8_t *p) {
+    return (uint64_t)rfl(lds_ld32(p)) | ((uint64_t)rfl(lds_ld32(p + 4)) << 32);
+}
+__device__ __forceinline__ bool bitd_init_u(BitD &b, const uint8_t *in, int32_t start, int32_t n) {
+    b.start = start;
+    b.c = 0;
+    b.used = 0;
+    b.ptr = start;
+    if (n < 1) return false;
+    const uint32_t last = rfl(in[start + n - 1]);
+    if (last == 0) return false;
+    const uint32_t mark = 8u - highbit(last);
+    if (n >= 8) {
+        b.ptr = start + n - 8;
+        b.c = ld64u(in + b.ptr);
+        b.used = mark;
+    } else {
+        uint64_t c = rfl(in[start]);
+        for (int32_t k = 1; k < n; k++) {
+            const uint32_t sh = k <= 3 ? 8u * (uint32_t)k : 64u - 8u * (8u - (uint32_t)k);
+            c += (uint64_t)rfl(in[start + k]) << sh;
+        }
+        b.c = c;
+        b.used = mark + (uint32_t)(8 - n) * 8u;
+    }
+    return true;
+}
+
 __device__ __forceinline__ uint64_t bitd_look(const BitD &b, uint32_t nb) {
     return ((b.c << (b.used & 63u)) >> 1) >> ((63u - nb) & 63u);
 }
@@ -165,6 +234,27 @@ __device__ __forceinline__ uint32_t bitd_reload(BitD &b, const uint8_t *in) {
     return r;
 }
 
+__device__ __forceinline__ uint32_t bitd_reload_u(BitD &b, const uint8_t *in) {
+    if (b.used > 64u) return kOverflow;
+    if (b.ptr >= b.start + 8) {
+        b.ptr -= (int32_t)(b.used >> 3);
+        b.used &= 7u;
+        b.c = ld64u(in + b.ptr);
+        return kUnfinished;
+    }
+    if (b.ptr == b.start) return b.used < 64u ? kEndOfBuffer : kCompleted;
+    int32_t nbytes = (int32_t)(b.used >> 3);
+    uint32_t r = kUnfinished;
+    if (b.ptr - nbytes < b.start) {
+        nbytes = b.ptr - b.start;
+        r = kEndOfBuffer;
+    }
+    b.ptr -= nbytes;
+    b.used -= (uint32_t)nbytes * 8u;
+    b.c = ld64u(in + b.ptr);
+    return r;
+}
+
 // ------------------------------------------------------------ FSE (uniform code)
 // FSE_readNCount (entropy_common.c:65-157) over in[ip0, ip0+n).  Returns header
 // bytes or < 0; max_sv in/out, table_log out.
@@ -173,7 +263,7 @@ __device__ int32_t read_ncount(const uint8_t *in, int32_t ip0, int32_t n, int16_
     if (n < 4) return kErr;
     const int32_t iend = ip0 + n;
     int32_t ip = ip0;
-    uint32_t bits = lds_ld32(in + ip);
+    uint32_t bits = rfl(lds_ld32(in + ip));
     int32_t nb = (int32_t)(bits & 0xFu) + 5;
     if (nb > 15) return kErr;
     bits >>= 4;
@@ -190,7 +280,7 @@ __device__ int32_t read_ncount(const uint8_t *in, int32_t ip0, int32_t n, int16_
                 n0 += 24;
                 if (ip < iend - 5) {
                     ip += 2;
-                    bits = lds_ld32(in + ip) >> (bitcount & 31);
+                    bits = rfl(lds_ld32(in + ip)) >> (bitcount & 31);
                 } else {
                     bits >>= 16;
                     bitcount += 16;
@@ -208,7 +298,7 @@ __device__ int32_t read_ncount(const uint8_t *in, int32_t ip0, int32_t n, int16_
             if ((ip <= iend - 7) || (ip + (bitcount >> 3) <= iend - 4)) {
                 ip += bitcount >> 3;
                 bitcount &= 7;
-                bits = lds_ld32(in + ip) >> bitcount;
+                bits = rfl(lds_ld32(in + ip)) >> bitcount;
             } else {
                 bits >>= 2;
             }
@@ -238,7 +328,7 @@ __device__ int32_t read_ncount(const uint8_t *in, int32_t ip0, int32_t n, int16_
             bitcount -= 8 * (iend - 4 - ip);
             ip = iend - 4;
         }
-        bits = lds_ld32(in + ip) >> (bitcount & 31);
+        bits = rfl(lds_ld32(in + ip)) >> (bitcount & 31);
     }
     if (remaining != 1) return kErr;
     if (bitcount > 32) return kErr;
@@ -317,14 +407,6 @@ __device__ bool build_dtable(uint32_t *cells, const int16_t *norm, uint32_t max_
     return true;
 }
 
-// default tables (ZSTD_buildSeqTable set_basic), from the constant norms
-__device__ void build_default(uint32_t *cells, const int8_t *cnorm, uint32_t max_sv, uint32_t log, int16_t *norm,
-                              uint16_t *next, uint32_t lane) {
-    if (lane <= max_sv) norm[lane] = cnorm[lane];
-    __builtin_amdgcn_wave_barrier();
-    build_dtable(cells, norm, max_sv, log, next, lane);
-}
-
 // ------------------------------------------------------------ Huffman (HUF_readStats + HUF_readDTableX2)
 // Reads the table description at in[ip, ip+n).  Returns header bytes or < 0;
 // fills W.huf and sets tlog.
@@ -357,22 +439,22 @@ __device__ int32_t huf_read_table(const Work &W, int32_t ip, int32_t n, uint32_t
             if (W.norm[s] >= large) fast = false;
         // FSE_decompress_usingDTable_generic (fse_decompress.c:218-275)
         BitD b;
-        if (!bitd_init(b, in, ip + 1 + hs, isize - hs)) return kErr;
+        if (!bitd_init_u(b, in, ip + 1 + hs, isize - hs)) return kErr;
         uint32_t s1 = bitd_read(b, flog);
-        bitd_reload(b, in);
+        bitd_reload_u(b, in);
         uint32_t s2 = bitd_read(b, flog);
-        bitd_reload(b, in);
+        bitd_reload_u(b, in);
         uint32_t op = 0;
         const uint32_t omax = 255, olimit = omax - 3;
         auto sym = [&](uint32_t &st) -> uint32_t {
-            const uint32_t c = W.wt[st];
+            const uint32_t c = rfl(W.wt[st]);
             const uint32_t nbb = cell_nb(c);
             const uint32_t low = fast ? bitd_read_fast(b, nbb) : bitd_read(b, nbb);
             st = cell_state(c) + low;
             return cell_sym(c);
         };
         for (;;) {
-            const uint32_t st = bitd_reload(b, in);
+            const uint32_t st = bitd_reload_u(b, in);
             if (!((st == kUnfinished) & (op < olimit))) break;
             const uint32_t a0 = sym(s1), a1 = sym(s2), a2 = sym(s1), a3 = sym(s2);
             if (lane == 0) {
@@ -388,7 +470,7 @@ __device__ int32_t huf_read_table(const Work &W, int32_t ip, int32_t n, uint32_t
             uint32_t a = sym(s1);
             if (lane == 0) W.w[op] = (uint8_t)a;
             op++;
-            if (bitd_reload(b, in) == kOverflow) {
+            if (bitd_reload_u(b, in) == kOverflow) {
                 a = sym(s2);
                 if (lane == 0) W.w[op] = (uint8_t)a;
                 op++;
@@ -398,7 +480,7 @@ __device__ int32_t huf_read_table(const Work &W, int32_t ip, int32_t n, uint32_t
             a = sym(s2);
             if (lane == 0) W.w[op] = (uint8_t)a;
             op++;
-            if (bitd_reload(b, in) == kOverflow) {
+            if (bitd_reload_u(b, in) == kOverflow) {
                 a = sym(s1);
                 if (lane == 0) W.w[op] = (uint8_t)a;
                 op++;
@@ -689,7 +771,7 @@ struct SeqTables {
 
 // ZSTD_buildSeqTable (zstd_decompress.c:693-724).  Returns bytes read or < 0.
 __device__ int32_t seq_table(const Work &W, uint32_t *cells, uint32_t &log, uint32_t type, uint32_t max,
-                             uint32_t max_log, int32_t ip, int32_t n, const int8_t *cnorm, uint32_t def_log,
+                             uint32_t max_log, int32_t ip, int32_t n, const DTab &def, uint32_t def_log,
                              bool flag_repeat, uint32_t lane) {
     if (type == 1) {   // set_rle
         if (n < 1) return kErr;
@@ -700,7 +782,7 @@ __device__ int32_t seq_table(const Work &W, uint32_t *cells, uint32_t &log, uint
         return 1;
     }
     if (type == 0) {   // set_basic
-        build_default(cells, cnorm, max, def_log, W.norm, W.next, lane);
+        if (lane < (1u << def_log)) cells[lane] = def.cell[lane];
         log = def_log;
         return 0;
     }
@@ -815,35 +897,35 @@ __device__ int32_t decode_block(const Work &W, SeqTables &T, int32_t ip, int32_t
         }
         if (sp + 4 > send) return kErr;
         const uint32_t modes = in[sp++];
-        int32_t r = seq_table(W, W.ll, T.ll_log, modes >> 6, 35, 9, sp, send - sp, c_ll_norm, 6, T.fse_entropy, lane);
+        int32_t r = seq_table(W, W.ll, T.ll_log, modes >> 6, 35, 9, sp, send - sp, c_ll_def, 6, T.fse_entropy, lane);
         if (r < 0) return kErr;
         sp += r;
-        r = seq_table(W, W.of, T.of_log, (modes >> 4) & 3u, 28, 8, sp, send - sp, c_of_norm, 5, T.fse_entropy, lane);
+        r = seq_table(W, W.of, T.of_log, (modes >> 4) & 3u, 28, 8, sp, send - sp, c_of_def, 5, T.fse_entropy, lane);
         if (r < 0) return kErr;
         sp += r;
-        r = seq_table(W, W.ml, T.ml_log, (modes >> 2) & 3u, 52, 9, sp, send - sp, c_ml_norm, 6, T.fse_entropy, lane);
+        r = seq_table(W, W.ml, T.ml_log, (modes >> 2) & 3u, 52, 9, sp, send - sp, c_ml_def, 6, T.fse_entropy, lane);
         if (r < 0) return kErr;
         sp += r;
         __builtin_amdgcn_wave_barrier();
         // ---- sequence loop (ZSTD_decompressSequences)
         T.fse_entropy = true;
         BitD b;
-        if (!bitd_init(b, in, sp, send - sp)) return kErr;
+        if (!bitd_init_u(b, in, sp, send - sp)) return kErr;
         uint32_t sll = bitd_read(b, T.ll_log);
-        bitd_reload(b, in);
+        bitd_reload_u(b, in);
         uint32_t sof = bitd_read(b, T.of_log);
-        bitd_reload(b, in);
+        bitd_reload_u(b, in);
         uint32_t sml = bitd_read(b, T.ml_log);
-        bitd_reload(b, in);
+        bitd_reload_u(b, in);
         uint32_t rep0 = T.rep0, rep1 = T.rep1, rep2 = T.rep2;
         bool more = true;
         while (more) {
             // decode up to 64 sequences into lanes
             uint32_t vll = 0, vml = 0, voff = 0, k = 0;
             for (; k < kWave; k++) {
-                if (!((bitd_reload(b, in) <= kCompleted) && nbseq)) { more = false; break; }
+                if (!((bitd_reload_u(b, in) <= kCompleted) && nbseq)) { more = false; break; }
                 nbseq--;
-                const uint32_t cl = W.ll[sll], cm = W.ml[sml], co = W.of[sof];
+                const uint32_t cl = rfl(W.ll[sll]), cm = rfl(W.ml[sml]), co = rfl(W.of[sof]);
                 const uint32_t llc = cell_sym(cl), mlc = cell_sym(cm), ofc = cell_sym(co);
                 uint32_t offv;
                 if (!ofc) offv = 0;
@@ -867,7 +949,7 @@ __device__ int32_t decode_block(const Work &W, SeqTables &T, int32_t ip, int32_t
                 const uint32_t mlb = c_ml_bits[mlc], llb = c_ll_bits[llc];
                 const uint32_t mlv = c_ml_base[mlc] + (mlc > 31u ? bitd_read_fast(b, mlb) : 0u);
                 const uint32_t llv = c_ll_base[llc] + (llc > 15u ? bitd_read_fast(b, llb) : 0u);
-                if (llb + mlb + ofc > 31u) bitd_reload(b, in);
+                if (llb + mlb + ofc > 31u) bitd_reload_u(b, in);
                 sll = cell_state(cl) + bitd_read(b, cell_nb(cl));
                 sml = cell_state(cm) + bitd_read(b, cell_nb(cm));
                 sof = cell_state(co) + bitd_read(b, cell_nb(co));

@@ -53,19 +53,8 @@ constexpr int16_t kMLNorm[53] = {1, 4, 3, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1,
                                  1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1, -1, -1};
 constexpr int16_t kOFNorm[29] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1,
                                  -1, -1};
-constexpr uint8_t kLLBits[36] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 3, 3, 4, 6, 7, 8,
-                                 9, 10, 11, 12, 13, 14, 15, 16};
-constexpr uint8_t kMLBits[53] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
-                                 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 3, 3, 4, 4, 5, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
-constexpr uint32_t kLLBase[36] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 18, 20, 22, 24, 28, 32,
-                                  40, 48, 64, 0x80, 0x100, 0x200, 0x400, 0x800, 0x1000, 0x2000, 0x4000, 0x8000,
-                                  0x10000};
-constexpr uint32_t kMLBase[53] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24,
-                                  25, 26, 27, 28, 29, 30, 31, 32, 33, 34, 35, 37, 39, 41, 43, 47, 51, 59, 67, 83,
-                                  99, 0x83, 0x103, 0x203, 0x403, 0x803, 0x1003, 0x2003, 0x4003, 0x8003, 0x10003};
-
 struct CTab {
-    uint16_t state[64];      // stateTable (tableSize <= 64)
+    uint32_t state[64];      // stateTable (tableSize <= 64); 32-bit so uniform lookups are scalar loads
     uint32_t dnb[53];        // symbolTT.deltaNbBits
     int32_t dfs[53];         // symbolTT.deltaFindState
     uint32_t log;
@@ -99,7 +88,7 @@ constexpr CTab make_ctab(const int16_t *norm, uint32_t max_sv, uint32_t log) {
             pos = (pos + step) & mask;
             while (pos > high) pos = (pos + step) & mask;
         }
-    for (uint32_t u = 0; u < size; u++) t.state[cumul[sym[u]]++] = (uint16_t)(size + u);
+    for (uint32_t u = 0; u < size; u++) t.state[cumul[sym[u]]++] = size + u;
     int32_t total = 0;
     for (uint32_t s = 0; s <= max_sv; s++) {
         const int32_t n = norm[s];
@@ -120,35 +109,14 @@ constexpr CTab make_ctab(const int16_t *norm, uint32_t max_sv, uint32_t log) {
     return t;
 }
 
-// LL_Code / ML_Code (zstd_compress.c:515-533): the code whose base covers the value
-struct CodeTabs {
-    uint8_t ll[64];
-    uint8_t ml[128];
-};
-constexpr CodeTabs make_codes() {
-    CodeTabs c{};
-    for (uint32_t v = 0; v < 64; v++)
-        for (uint32_t k = 0; k < 36; k++)
-            if (kLLBase[k] <= v && v < kLLBase[k] + (1u << kLLBits[k])) c.ll[v] = (uint8_t)k;
-    for (uint32_t v = 0; v < 128; v++)
-        for (uint32_t k = 0; k < 53; k++)
-            if (kMLBase[k] - 3u <= v && v < kMLBase[k] - 3u + (1u << kMLBits[k])) c.ml[v] = (uint8_t)k;
-    return c;
-}
-
 __device__ __constant__ CTab c_ll_ct = make_ctab(kLLNorm, 35, 6);
 __device__ __constant__ CTab c_ml_ct = make_ctab(kMLNorm, 52, 6);
 __device__ __constant__ CTab c_of_ct = make_ctab(kOFNorm, 28, 5);
-__device__ __constant__ CodeTabs c_codes = make_codes();
-__device__ __constant__ uint8_t c_llbits[36] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 3, 3,
-                                                4, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
-__device__ __constant__ uint8_t c_mlbits[53] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
-                                                0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 3, 3, 4, 4, 5, 7, 8, 9,
-                                                10, 11, 12, 13, 14, 15, 16};
-
 __device__ __forceinline__ uint32_t hb(uint32_t v) { return 31u - (uint32_t)__builtin_clz(v); }
 
-// (code, extra bits) of one sequence -- ZSTD_seqToCodes (zstd_compress.c:535-556)
+// (code, extra bits) of one sequence -- ZSTD_seqToCodes (zstd_compress.c:535-556).
+// LL_Code / ML_Code are evaluated with compares against the code bases
+// (zstd_decompress.c:864-873) instead of table gathers.
 struct SeqCode {
     uint32_t llc, mlc, ofc;          // codes
     uint32_t llv, mlv, ofv;          // extra-bit values (masked by BIT_addBits)
@@ -156,14 +124,32 @@ struct SeqCode {
 };
 __device__ __forceinline__ SeqCode seq_code(uint32_t ll, uint32_t ml, uint32_t off) {
     SeqCode c;
-    const uint32_t mlbase = ml - 3u, ofcode = off + 3u;
-    c.llc = ll > 63u ? hb(ll) + 19u : c_codes.ll[ll];
-    c.mlc = mlbase > 127u ? hb(mlbase) + 36u : c_codes.ml[mlbase];
+    const uint32_t m = ml - 3u, ofcode = off + 3u;
+    if (ll < 16u) {
+        c.llc = ll;
+        c.llb = 0;
+    } else if (ll < 64u) {
+        c.llc = 16u + (ll >= 18u) + (ll >= 20u) + (ll >= 22u) + (ll >= 24u) + (ll >= 28u) + (ll >= 32u) +
+                (ll >= 40u) + (ll >= 48u);
+        c.llb = 1u + (ll >= 24u) + (ll >= 32u) + (ll >= 48u);
+    } else {
+        c.llb = hb(ll);
+        c.llc = c.llb + 19u;
+    }
+    if (m < 32u) {
+        c.mlc = m;
+        c.mlb = 0;
+    } else if (m < 128u) {
+        c.mlc = 32u + (m >= 34u) + (m >= 36u) + (m >= 38u) + (m >= 40u) + (m >= 44u) + (m >= 48u) + (m >= 56u) +
+                (m >= 64u) + (m >= 80u) + (m >= 96u);
+        c.mlb = 1u + (m >= 40u) + (m >= 48u) + (m >= 64u) + (m >= 96u);
+    } else {
+        c.mlb = hb(m);
+        c.mlc = c.mlb + 36u;
+    }
     c.ofc = hb(ofcode);
-    c.llb = c_llbits[c.llc];
-    c.mlb = c_mlbits[c.mlc];
     c.llv = ll & ((1u << c.llb) - 1u);
-    c.mlv = mlbase & ((1u << c.mlb) - 1u);
+    c.mlv = m & ((1u << c.mlb) - 1u);
     c.ofv = ofcode & ((1u << c.ofc) - 1u);
     return c;
 }
