@@ -48,6 +48,9 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--e2e-pages", type=int, default=32768, help="host-buffer (PCIe-inclusive) sample; 0 = skip")
+    ap.add_argument("--no-extra", action="store_true", help="skip the secondary C3 (zstd) measurement")
+    ap.add_argument("--extra-pages", type=int, default=1 << 20, help="pages for the C3 zstd measurement")
+    ap.add_argument("--extra-steps", type=int, default=2)
     return ap.parse_args()
 
 
@@ -115,6 +118,104 @@ def cpu_baseline(pages_dev: torch.Tensor, n: int, threads: int) -> dict:
     }
 
 
+def zstd_cpu_baseline(pages_dev: torch.Tensor, n: int, threads: int) -> dict:
+    """The reference's vendored zstd 1.1.2 (oracle/_ref) at level 1 on the host, one call per page."""
+    import ctypes
+
+    import numpy as np
+
+    from oracle import oracle as O
+
+    if not O.have_ref():
+        return None
+    lib = O._Lib.ref()
+    host = pages_dev[:n].cpu().numpy()
+    plen = host.shape[1]
+    cap = int(lib.ZSTD_compressBound(plen))
+    comp = np.zeros((n, cap), dtype=np.uint8)
+    clen = np.zeros(n, dtype=np.int64)
+    out = np.zeros_like(host)
+    rv = np.zeros(n, dtype=np.int64)
+    u8p = ctypes.POINTER(ctypes.c_uint8)
+    base_in, base_c, base_o = host.ctypes.data, comp.ctypes.data, out.ctypes.data
+    chunks = [(i * n // threads, (i + 1) * n // threads) for i in range(threads)]
+
+    def comp_range(a, b):
+        for i in range(a, b):
+            clen[i] = lib.ZSTD_compress(ctypes.cast(base_c + i * cap, u8p), cap, ctypes.cast(base_in + i * plen, u8p),
+                                        plen, 1)
+
+    def dec_range(a, b):
+        for i in range(a, b):
+            rv[i] = lib.ZSTD_decompress(ctypes.cast(base_o + i * plen, u8p), plen, ctypes.cast(base_c + i * cap, u8p),
+                                        int(clen[i]))
+
+    best_c = best_d = float("inf")
+    with cf.ThreadPoolExecutor(max_workers=threads) as ex:
+        for _ in range(2):
+            t0 = time.perf_counter()
+            list(ex.map(lambda r: comp_range(*r), chunks))
+            t1 = time.perf_counter()
+            list(ex.map(lambda r: dec_range(*r), chunks))
+            t2 = time.perf_counter()
+            best_c, best_d = min(best_c, t1 - t0), min(best_d, t2 - t1)
+    assert (rv == plen).all() and np.array_equal(out, host), "zstd CPU baseline round trip failed"
+    nbytes = n * plen
+    return {"value": round(nbytes / (best_c + best_d) / GIB, 3), "unit": "GiB/s", "cores": threads,
+            "kind": "reference",
+            "sample": f"first {n} of the same pages ({nbytes / GIB:.2f} GiB), ZSTD_compress(level 1)/ZSTD_decompress "
+                      f"from oracle/_ref (vendored zstd 1.1.2), one call per page, {threads} threads, best of 2",
+            "compress_gib_s": round(nbytes / best_c / GIB, 3), "decompress_gib_s": round(nbytes / best_d / GIB, 3),
+            "ratio": round(nbytes / float(clen.sum()), 4)}
+
+
+def measure_codec(cid: int, name: str, n: int, plen: int, steps: int, warmup: int, dev, seed: int, first: int,
+                  dist: int) -> dict:
+    """Device-resident compress+decompress of n resident pages with codec `cid` (HIP events on the stream)."""
+    pages = codec.pagegen(n, plen, seed=seed, first=first, dist=dist, device=dev)
+    slot = codec.slot_size(plen, cid)
+    comp = torch.empty((n, slot), dtype=torch.uint8, device=dev)
+    clen = torch.empty((n,), dtype=torch.int32, device=dev)
+    out = torch.empty((n, plen), dtype=torch.uint8, device=dev)
+    rv = torch.empty((n,), dtype=torch.int32, device=dev)
+    codec.compress_pages(pages, compressor_id=cid, out=comp, out_len=clen)
+    torch.cuda.synchronize()
+    mx = int(clen.max().item())
+    for _ in range(max(warmup, 1)):
+        codec.compress_pages(pages, compressor_id=cid, out=comp, out_len=clen)
+        codec.decompress_pages(comp, clen, plen, compressor_id=cid, out=out, rv=rv, max_comp_len=mx)
+    torch.cuda.synchronize()
+    if not (bool((rv == plen).all().item()) and bool((clen > 0).all().item()) and torch.equal(out, pages)):
+        raise SystemExit(f"{name}: round trip failed on the benchmark pages")
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        ev[k][0].record()
+        codec.compress_pages(pages, compressor_id=cid, out=comp, out_len=clen)
+        ev[k][1].record()
+        codec.decompress_pages(comp, clen, plen, compressor_id=cid, out=out, rv=rv, max_comp_len=mx)
+        ev[k][2].record()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    c_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / steps
+    d_ms = sum(e[1].elapsed_time(e[2]) for e in ev) / steps
+    nbytes = n * plen
+    cbytes = int(clen.to(torch.int64).sum().item())
+    algo = nbytes + cbytes
+    res = {"pages": n, "page_len": plen, "steps": steps, "ms_per_step": round(wall / steps * 1e3, 3),
+           "value": round(nbytes * steps / wall / GIB, 3), "unit": "GiB/s",
+           "compress_gib_s": round(nbytes / (c_ms * 1e-3) / GIB, 3),
+           "decompress_gib_s": round(nbytes / (d_ms * 1e-3) / GIB, 3),
+           "kernel_ms": {f"{name}_encode": round(c_ms, 3), f"{name}_decode": round(d_ms, 3)},
+           "roofline_by_kernel": {f"{name}_encode": round(algo / (c_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                  f"{name}_decode": round(algo / (d_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+           "algorithmic_bytes_per_launch": algo, "ratio": round(nbytes / cbytes, 4)}
+    tr = {k: pmc_traffic(k, n, plen) for k in res["kernel_ms"]}
+    res["traffic"] = {k: (v["bytes"] if v else None) for k, v in tr.items()}
+    return res, pages
+
+
 def e2e_host(pages_dev: torch.Tensor, n: int) -> dict:
     """PCIe-inclusive rate through the host batch API (malloc'd pages -> pinned -> H2D -> kernels -> D2H)."""
     import ctypes
@@ -160,7 +261,7 @@ def pmc_traffic(kernel: str, pages: int, page_len: int):
     (profiles/rNN_traffic.json, made by tools/pmc_traffic.py from separate
     FETCH_SIZE / WRITE_SIZE rocprofv3 passes of the same kernels), scaled from
     bytes per page to this launch's page count; None when no summary matches."""
-    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r*_traffic.json")))
+    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r*_traffic*.json")))
     for f in reversed(files):
         t = json.load(open(f))
         if t.get("page_len") == page_len and kernel in t.get("bytes_per_page", {}):
@@ -257,11 +358,24 @@ def main():
         "ratio": round(page_bytes / comp_bytes, 4),
     }
     if info.rank == 0 and info.world == 1:
+        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
         if args.e2e_pages > 0:
             result["e2e_host_path"] = e2e_host(pages, min(args.e2e_pages, n))
         if not args.no_cpu:
-            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
             result["cpu_baseline"] = cpu_baseline(pages, min(args.cpu_pages, n), threads)
+        if not args.no_extra:
+            # C3 (configs[2]): zstd level-1 compress+decompress, 1M x 32 KiB pages, 1 GPU -- reported
+            # beside the headline line, never as `value`
+            del pages, comp, clen, out, rv
+            torch.cuda.empty_cache()
+            c3, zpages = measure_codec(3, "zstd", args.extra_pages, 32768, args.extra_steps, 1, dev, args.seed, 0,
+                                       args.dist)
+            c3["workload"] = "C3: zstd level-1 compress+decompress, 1M x 32 KiB pages, 1 GPU, device-resident"
+            if not args.no_cpu:
+                c3["cpu_baseline"] = zstd_cpu_baseline(zpages, min(16384, args.extra_pages), threads)
+            result["configs"] = {"C3_zstd": c3}
+            del zpages
+            torch.cuda.empty_cache()
     if info.rank == 0:
         print(json.dumps(result), flush=True)
     runner.shutdown(info)

@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round measurement on the GPU box: bench line, kernel-trace stats of the same
-# workload, and the two HBM PMC passes (FETCH_SIZE / WRITE_SIZE kept apart).
+# workload, and the HBM PMC passes (FETCH_SIZE / WRITE_SIZE kept apart) for the
+# C2 LZ4 kernels and the C3 zstd kernels.
 # Usage (via gpurun): bash tools/gpu_round_profile.sh r01
 set -e
 TAG=${1:-r01}
@@ -13,9 +14,12 @@ cat $OUT/bench_$TAG.json
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o bench \
     -- python3 $R/bench.py --no-cpu --e2e-pages 0 > $OUT/prof_bench_$TAG.log 2>&1
-export PAGES=262144 REPS=1
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_$TAG/fetch -o run \
-    -- python3 $R/tools/run_codec.py > $OUT/pmc_fetch_$TAG.log 2>&1
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_$TAG/write -o run \
-    -- python3 $R/tools/run_codec.py > $OUT/pmc_write_$TAG.log 2>&1
+for spec in lz4:16384 zstd:32768; do
+  c=${spec%%:*}; p=${spec##*:}
+  export CODEC=$c PLEN=$p PAGES=262144 REPS=1
+  timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_$TAG/${c}_fetch -o run \
+      -- python3 $R/tools/run_codec.py > $OUT/pmc_fetch_${c}_$TAG.log 2>&1
+  timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_$TAG/${c}_write -o run \
+      -- python3 $R/tools/run_codec.py > $OUT/pmc_write_${c}_$TAG.log 2>&1
+done
 echo DONE
