@@ -103,10 +103,16 @@ int tyche_buffers_decompress(Buffer **bufs, int *status, size_t n, int compresso
  * most dst_capacities[i] (or dst_capacity) bytes to dst + dst_offsets[i] (or
  * i*dst_stride).  All pointers are device pointers on the current device.
  * results[i] (device int32):
- *   compress   -- the codec's return: compressed size, or 0 on failure
- *                 (LZ4_compress_default semantics, lz4.c:697)
- *   decompress -- LZ4_decompress_safe semantics (lz4.c:1251): decoded size,
- *                 or -(input bytes consumed)-1 for a malformed stream.
+ *   compress   -- compressed size, or 0 when the output does not fit
+ *                 (LZ4_compress_default semantics, lz4.c:697, for every codec)
+ *   decompress -- the codec's own verdict:
+ *                 LZ4  LZ4_decompress_safe (lz4.c:1251): decoded size, or
+ *                      -(input bytes consumed)-1 for a malformed stream;
+ *                 zlib uncompress (uncompr.c:22): decoded length, or -3
+ *                      (Z_DATA_ERROR) / -5 (Z_BUF_ERROR);
+ *                 zstd ZSTD_decompress (zstd_decompress.c:1459): decoded size,
+ *                      or a negative value wherever ZSTD_isError holds.
+ *   INT32_MIN marks a page larger than the launch's declared maximum.
  * max_src_length (0 = unknown) bounds src lengths for LDS sizing.
  * `stream` is a hipStream_t (NULL = default stream); the call is asynchronous. */
 typedef struct tyche_batch {
@@ -127,7 +133,8 @@ typedef struct tyche_batch {
 
 int tyche_compress_batch(int compressor_id, int compressor_level, const tyche_batch_t *batch, void *stream);
 int tyche_decompress_batch(int compressor_id, const tyche_batch_t *batch, void *stream);
-/* worst-case compressed size for n input bytes (LZ4_compressBound, lz4.h:148) */
+/* worst-case compressed size for n input bytes: LZ4_compressBound (lz4.h:148),
+ * compressBound (zlib compress.c:74-78) or ZSTD_compressBound (zstd_compress.c:37) */
 uint32_t tyche_compress_bound(int compressor_id, uint32_t n);
 
 /* ---- host batch API (pinned staging + H2D -> kernels -> D2H) ------------- */
