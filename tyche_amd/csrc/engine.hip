@@ -18,7 +18,12 @@
 #include <time.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "engine.h"
@@ -96,13 +101,20 @@ inline uint32_t decode_in_cap(const tyche_batch_t &b, uint32_t fallback) {
 }
 
 // ---------------------------------------------------------------- host batches
-// One context per calling thread (tyche calls the codec from its compressor
-// pool and from worker threads concurrently, src/list.c:1051, 572): its own
-// stream, pinned staging and device buffers, grown on demand.
+// The Buffer API and the host batch entry points start and end in host memory
+// (tyche's Buffer->data is malloc'd, src/buffer.c:181, 246).  A batch is cut
+// into chunks of ~kChunkBytes of input that flow through a ring of kSlots
+// staging slots, one HIP stream each:
+//
+//   host gather (thread pool memcpy into pinned) -> H2D -> kernel -> D2H -> host scatter
+//
+// so chunk c's gather overlaps chunk c-1's copies and kernel and chunk c-2's
+// scatter; the two copy directions and the kernels of different slots run
+// concurrently.  One context per calling thread (tyche calls the codec from its
+// compressor pool and from worker threads concurrently, src/list.c:1051, 572).
 struct Arena {
     void *p = nullptr;
     size_t cap = 0;
-    bool pinned = false;
     int grow(size_t need, bool host) {
         if (need <= cap) return TYCHE_E_OK;
         size_t n = std::max(need, cap * 2);
@@ -119,15 +131,26 @@ struct Arena {
     }
 };
 
-struct HostCtx {
-    int device = -1;
+constexpr int kSlots = 3;
+constexpr size_t kChunkBytes = size_t(64) << 20;
+
+struct Slot {
     hipStream_t stream = nullptr;
     Arena h_in, h_out, h_meta, d_in, d_out, d_meta;
+    size_t first = 0, count = 0;   // pages of the chunk in flight
+    bool busy = false;
+};
+
+struct HostCtx {
+    int device = -1;
+    Slot slot[kSlots];
     int init(int dev) {
-        if (device == dev && stream) return TYCHE_E_OK;
+        if (device == dev && slot[0].stream) return TYCHE_E_OK;
         device = dev;
-        hipError_t e = hipStreamCreateWithFlags(&stream, hipStreamNonBlocking);
-        if (e != hipSuccess) return fail("hipStreamCreate", e);
+        for (Slot &s : slot) {
+            hipError_t e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
+            if (e != hipSuccess) return fail("hipStreamCreate", e);
+        }
         return TYCHE_E_OK;
     }
 };
@@ -135,73 +158,185 @@ thread_local HostCtx t_ctx[16];
 
 inline size_t up16(size_t x) { return (x + 15) & ~size_t(15); }
 
-// Moves n host pages to the device, runs `launch`, brings results and outputs back.
+// A small persistent worker pool for the host-side page copies (memcpy of
+// scattered malloc'd pages into and out of pinned staging).  One job at a
+// time; concurrent callers queue on the mutex.
+class CopyPool {
+  public:
+    static CopyPool &get() {
+        // never destroyed: its detached workers wait on its condition variable until exit
+        static CopyPool *p = new CopyPool;
+        return *p;
+    }
+    // runs f(i) for i in [0, n), in contiguous ranges, on the pool and the caller
+    template <typename F>
+    void run(size_t n, F f) {
+        if (n < 64 || workers_.empty()) {
+            for (size_t i = 0; i < n; i++) f(i);
+            return;
+        }
+        std::lock_guard<std::mutex> job_lock(job_mu_);
+        std::function<void(size_t, size_t)> body = [&f](size_t a, size_t b) {
+            for (size_t i = a; i < b; i++) f(i);
+        };
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            body_ = &body;
+            n_ = n;
+            next_.store(0);
+            pending_ = workers_.size();
+            gen_++;
+        }
+        cv_.notify_all();
+        work();
+        std::unique_lock<std::mutex> g(mu_);
+        done_cv_.wait(g, [this] { return pending_ == 0; });
+        body_ = nullptr;
+    }
+
+  private:
+    static constexpr size_t kGrain = 32;
+    CopyPool() {
+        unsigned t = std::thread::hardware_concurrency();
+        const char *env = getenv("TYCHE_HOST_THREADS");
+        unsigned want = env ? (unsigned)atoi(env) : std::min(16u, t ? t : 1u);
+        for (unsigned i = 1; i < want; i++) workers_.emplace_back([this] { loop(); });
+        for (auto &w : workers_) w.detach();
+    }
+    void work() {
+        for (;;) {
+            const size_t a = next_.fetch_add(kGrain);
+            if (a >= n_) break;
+            (*body_)(a, std::min(n_, a + kGrain));
+        }
+    }
+    void loop() {
+        uint64_t seen = 0;
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> g(mu_);
+                cv_.wait(g, [&] { return gen_ != seen; });
+                seen = gen_;
+            }
+            work();
+            std::lock_guard<std::mutex> g(mu_);
+            if (--pending_ == 0) done_cv_.notify_all();
+        }
+    }
+    std::vector<std::thread> workers_;
+    std::mutex job_mu_, mu_;
+    std::condition_variable cv_, done_cv_;
+    const std::function<void(size_t, size_t)> *body_ = nullptr;
+    size_t n_ = 0;
+    std::atomic<size_t> next_{0};
+    size_t pending_ = 0;
+    uint64_t gen_ = 0;
+};
+
+// Moves n host pages through `launch` chunk by chunk (see above).  results[i]
+// gets the kernel's per-page result; for results in (0, dst_cap[i]] that many
+// output bytes land in dst[i].
 template <typename Launch>
 int run_host_batch(size_t n, const void *const *src, const uint32_t *src_len, void *const *dst,
-                   const uint32_t *dst_cap, int32_t *results, bool copy_out_positive, Launch launch) {
+                   const uint32_t *dst_cap, int32_t *results, Launch launch) {
     int rc = ensure_device();
     if (rc) return rc;
     if (t_device >= 16) return fail_msg("device index too large");
     HostCtx &c = t_ctx[t_device];
     if ((rc = c.init(t_device))) return rc;
-    size_t in_bytes = 0, out_bytes = 0;
-    uint32_t max_in = 0, max_out = 0;
-    for (size_t i = 0; i < n; i++) {
-        in_bytes += up16(src_len[i]);
-        out_bytes += up16(dst_cap[i]);
-        max_in = std::max(max_in, src_len[i]);
-        max_out = std::max(max_out, dst_cap[i]);
-    }
-    size_t meta_bytes = n * (8 + 8 + 4 + 4 + 4) + 64;
-    if ((rc = c.h_in.grow(in_bytes + 16, true)) || (rc = c.h_out.grow(out_bytes + 16, true)) ||
-        (rc = c.h_meta.grow(meta_bytes, true)) || (rc = c.d_in.grow(in_bytes + 16, false)) ||
-        (rc = c.d_out.grow(out_bytes + 16, false)) || (rc = c.d_meta.grow(meta_bytes, false)))
-        return rc;
-    uint8_t *hin = (uint8_t *)c.h_in.p;
-    uint64_t *m_soff = (uint64_t *)c.h_meta.p;
-    uint64_t *m_doff = m_soff + n;
-    uint32_t *m_slen = (uint32_t *)(m_doff + n);
-    uint32_t *m_dcap = m_slen + n;
-    int32_t *m_res = (int32_t *)(m_dcap + n);
-    size_t so = 0, dof = 0;
-    for (size_t i = 0; i < n; i++) {
-        m_soff[i] = so;
-        m_doff[i] = dof;
-        m_slen[i] = src_len[i];
-        m_dcap[i] = dst_cap[i];
-        if (src_len[i]) memcpy(hin + so, src[i], src_len[i]);
-        so += up16(src_len[i]);
-        dof += up16(dst_cap[i]);
-    }
-    uint8_t *dmeta = (uint8_t *)c.d_meta.p;
-    size_t head_bytes = (uint8_t *)m_res - (uint8_t *)m_soff;
+    CopyPool &pool = CopyPool::get();
     hipError_t e;
-    if ((e = hipMemcpyAsync(dmeta, c.h_meta.p, head_bytes, hipMemcpyHostToDevice, c.stream)) != hipSuccess)
-        return fail("hipMemcpyAsync(meta)", e);
-    if (so && (e = hipMemcpyAsync(c.d_in.p, hin, so, hipMemcpyHostToDevice, c.stream)) != hipSuccess)
-        return fail("hipMemcpyAsync(in)", e);
-    tyche_batch_t b{};
-    b.count = n;
-    b.src = c.d_in.p;
-    b.src_offsets = (const uint64_t *)dmeta;
-    b.src_lengths = (const uint32_t *)(dmeta + ((uint8_t *)m_slen - (uint8_t *)m_soff));
-    b.max_src_length = max_in;
-    b.dst = c.d_out.p;
-    b.dst_offsets = (const uint64_t *)(dmeta + ((uint8_t *)m_doff - (uint8_t *)m_soff));
-    b.dst_capacities = (const uint32_t *)(dmeta + ((uint8_t *)m_dcap - (uint8_t *)m_soff));
-    b.dst_capacity = max_out;
-    b.results = (int32_t *)(dmeta + head_bytes);
-    if ((e = launch(b, c.stream)) != hipSuccess) return fail("kernel launch", e);
-    if ((e = hipMemcpyAsync(m_res, b.results, n * 4, hipMemcpyDeviceToHost, c.stream)) != hipSuccess)
-        return fail("hipMemcpyAsync(results)", e);
-    if (dof && (e = hipMemcpyAsync(c.h_out.p, c.d_out.p, dof, hipMemcpyDeviceToHost, c.stream)) != hipSuccess)
-        return fail("hipMemcpyAsync(out)", e);
-    if ((e = hipStreamSynchronize(c.stream)) != hipSuccess) return fail("hipStreamSynchronize", e);
-    for (size_t i = 0; i < n; i++) {
-        results[i] = m_res[i];
-        if (copy_out_positive && m_res[i] > 0 && (uint32_t)m_res[i] <= dst_cap[i])
-            memcpy(dst[i], (uint8_t *)c.h_out.p + m_doff[i], (size_t)m_res[i]);
+
+    // completes the chunk held by slot s: wait for its stream, scatter its outputs
+    auto finish = [&](Slot &S) -> int {
+        if (!S.busy) return TYCHE_E_OK;
+        S.busy = false;
+        if ((e = hipStreamSynchronize(S.stream)) != hipSuccess) return fail("hipStreamSynchronize", e);
+        const size_t k = S.count;
+        const uint64_t *m_doff = (const uint64_t *)S.h_meta.p + k;
+        const int32_t *m_res = (const int32_t *)((const uint8_t *)S.h_meta.p + k * 24);
+        const uint8_t *hout = (const uint8_t *)S.h_out.p;
+        const size_t f0 = S.first;
+        pool.run(k, [&](size_t j) {
+            const int32_t r = m_res[j];
+            results[f0 + j] = r;
+            if (r > 0 && (uint32_t)r <= dst_cap[f0 + j]) memcpy(dst[f0 + j], hout + m_doff[j], (size_t)r);
+        });
+        return TYCHE_E_OK;
+    };
+
+    size_t first = 0;
+    int si = 0;
+    while (first < n) {
+        // ---- chunk [first, last): ~kChunkBytes of input
+        size_t last = first, in_bytes = 0, out_bytes = 0;
+        uint32_t max_in = 0, max_out = 0;
+        while (last < n && (last == first || in_bytes + up16(src_len[last]) <= kChunkBytes)) {
+            in_bytes += up16(src_len[last]);
+            out_bytes += up16(dst_cap[last]);
+            max_in = std::max(max_in, src_len[last]);
+            max_out = std::max(max_out, dst_cap[last]);
+            last++;
+        }
+        const size_t k = last - first;
+        Slot &S = c.slot[si];
+        if ((rc = finish(S))) return rc;   // the slot's previous chunk
+        // meta layout: soff[k] u64, doff[k] u64, slen[k] u32, dcap[k] u32, res[k] i32
+        const size_t meta_bytes = k * 28 + 64;
+        if ((rc = S.h_in.grow(in_bytes + 16, true)) || (rc = S.h_out.grow(out_bytes + 16, true)) ||
+            (rc = S.h_meta.grow(meta_bytes, true)) || (rc = S.d_in.grow(in_bytes + 16, false)) ||
+            (rc = S.d_out.grow(out_bytes + 16, false)) || (rc = S.d_meta.grow(meta_bytes, false)))
+            return rc;
+        uint64_t *m_soff = (uint64_t *)S.h_meta.p;
+        uint64_t *m_doff = m_soff + k;
+        uint32_t *m_slen = (uint32_t *)(m_doff + k);
+        uint32_t *m_dcap = m_slen + k;
+        int32_t *m_res = (int32_t *)(m_dcap + k);
+        size_t so = 0, dof = 0;
+        for (size_t j = 0; j < k; j++) {
+            m_soff[j] = so;
+            m_doff[j] = dof;
+            m_slen[j] = src_len[first + j];
+            m_dcap[j] = dst_cap[first + j];
+            so += up16(src_len[first + j]);
+            dof += up16(dst_cap[first + j]);
+        }
+        uint8_t *hin = (uint8_t *)S.h_in.p;
+        pool.run(k, [&](size_t j) {
+            if (m_slen[j]) memcpy(hin + m_soff[j], src[first + j], m_slen[j]);
+        });
+        // ---- H2D -> kernel -> D2H on the slot's stream
+        uint8_t *dmeta = (uint8_t *)S.d_meta.p;
+        const size_t head_bytes = (uint8_t *)m_res - (uint8_t *)m_soff;
+        if ((e = hipMemcpyAsync(dmeta, S.h_meta.p, head_bytes, hipMemcpyHostToDevice, S.stream)) != hipSuccess)
+            return fail("hipMemcpyAsync(meta)", e);
+        if (so && (e = hipMemcpyAsync(S.d_in.p, hin, so, hipMemcpyHostToDevice, S.stream)) != hipSuccess)
+            return fail("hipMemcpyAsync(in)", e);
+        tyche_batch_t b{};
+        b.count = k;
+        b.src = S.d_in.p;
+        b.src_offsets = (const uint64_t *)dmeta;
+        b.src_lengths = (const uint32_t *)(dmeta + ((uint8_t *)m_slen - (uint8_t *)m_soff));
+        b.max_src_length = max_in;
+        b.dst = S.d_out.p;
+        b.dst_offsets = (const uint64_t *)(dmeta + ((uint8_t *)m_doff - (uint8_t *)m_soff));
+        b.dst_capacities = (const uint32_t *)(dmeta + ((uint8_t *)m_dcap - (uint8_t *)m_soff));
+        b.dst_capacity = max_out;
+        b.results = (int32_t *)(dmeta + head_bytes);
+        if ((e = launch(b, S.stream)) != hipSuccess) return fail("kernel launch", e);
+        if ((e = hipMemcpyAsync(m_res, b.results, k * 4, hipMemcpyDeviceToHost, S.stream)) != hipSuccess)
+            return fail("hipMemcpyAsync(results)", e);
+        if (dof && (e = hipMemcpyAsync(S.h_out.p, S.d_out.p, dof, hipMemcpyDeviceToHost, S.stream)) != hipSuccess)
+            return fail("hipMemcpyAsync(out)", e);
+        S.first = first;
+        S.count = k;
+        S.busy = true;
+        first = last;
+        si = (si + 1) % kSlots;
     }
+    // drain in issue order
+    for (int j = 0; j < kSlots; j++)
+        if ((rc = finish(c.slot[(si + j) % kSlots]))) return rc;
     return TYCHE_E_OK;
 }
 
@@ -279,7 +414,7 @@ int tyche_compress_host(int compressor_id, int compressor_level, size_t n, const
     if (n == 0) return TYCHE_E_OK;
     for (size_t i = 0; i < n; i++)
         if (src_lengths[i] > 65535u) { t_error = "pages above 64 KiB are not supported by the device encoders"; return TYCHE_E_BAD_ARGS; }
-    return run_host_batch(n, src, src_lengths, dst, dst_capacities, results, true,
+    return run_host_batch(n, src, src_lengths, dst, dst_capacities, results,
                           [compressor_id](const tyche_batch_t &b, hipStream_t s) {
                               return launch_encode(compressor_id, b, std::max(b.max_src_length, 1u), s);
                           });
@@ -290,16 +425,16 @@ int tyche_decompress_host(int compressor_id, size_t n, const void *const *src, c
     if (!valid_decode_codec(compressor_id)) { t_error = codec_msg(compressor_id); return TYCHE_E_BAD_ARGS; }
     if (n == 0) return TYCHE_E_OK;
     if (compressor_id == TYCHE_ZLIB_COMPRESSOR_ID)
-        return run_host_batch(n, src, src_lengths, dst, dst_capacities, results, true,
+        return run_host_batch(n, src, src_lengths, dst, dst_capacities, results,
                               [](const tyche_batch_t &b, hipStream_t s) {
                                   return launch_zlib_inflate(b, b.dst_capacity, s);
                               });
     if (compressor_id == TYCHE_ZSTD_COMPRESSOR_ID)
-        return run_host_batch(n, src, src_lengths, dst, dst_capacities, results, true,
+        return run_host_batch(n, src, src_lengths, dst, dst_capacities, results,
                               [](const tyche_batch_t &b, hipStream_t s) {
                                   return launch_zstd_decode(b, b.max_src_length, b.dst_capacity, s);
                               });
-    return run_host_batch(n, src, src_lengths, dst, dst_capacities, results, true,
+    return run_host_batch(n, src, src_lengths, dst, dst_capacities, results,
                           [](const tyche_batch_t &b, hipStream_t s) {
                               return launch_lz4_decode(b, b.max_src_length, b.dst_capacity, s);
                           });
