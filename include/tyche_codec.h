@@ -97,6 +97,21 @@ int tyche_buffers_compress(Buffer **bufs, void **compressed, int *status, size_t
  * src/list.c:563-589, coalesced); status[i] as buffer__decompress. */
 int tyche_buffers_decompress(Buffer **bufs, int *status, size_t n, int compressor_id);
 
+/* ---- restore queue: coalesced per-hit restores (src/list.c:563-589) ------- */
+/* Starts a dispatcher thread (on the calling thread's device) that batches
+ * concurrent tyche_buffer_restore calls: once a request arrives it waits up to
+ * max_wait_us for up to max_batch requests, then runs one GPU decompress batch
+ * per codec.  Idempotent. */
+int tyche_restore_queue_start(int max_batch, int max_wait_us);
+/* Drains and stops the dispatcher. */
+void tyche_restore_queue_stop(void);
+/* Drop-in for buffer__decompress at the list__search restore site
+ * (src/list.c:572): same status and side effects, but concurrent callers share
+ * GPU launches.  Without a running queue it is buffer__decompress. */
+int tyche_buffer_restore(Buffer *buf, int compressor_id);
+/* Launches and buffers served so far. */
+void tyche_restore_queue_stats(uint64_t *batches, uint64_t *buffers);
+
 /* ---- device-resident batch API ------------------------------------------- */
 /* Page i of the batch reads src + src_offsets[i] (or i*src_stride when
  * src_offsets is NULL) for src_lengths[i] (or src_length) bytes and writes at

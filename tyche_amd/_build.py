@@ -62,6 +62,24 @@ def build(force: bool = False, verbose: bool = False, profile: bool = False, abl
     return lib_path
 
 
+def build_tools(verbose: bool = False) -> str:
+    """tools/bin/cycle: the tyche-shaped C harness (tools/cycle.c) linked against the engine."""
+    root = os.path.abspath(os.path.join(HERE, ".."))
+    src = os.path.join(root, "tools", "cycle.c")
+    out_dir = os.path.join(root, "tools", "bin")
+    out = os.path.join(out_dir, "cycle")
+    os.makedirs(out_dir, exist_ok=True)
+    deps = [src, os.path.join(root, "include", "tyche_codec.h"), os.path.join(CSRC, "pagegen.h"), LIB]
+    if _newer(out, deps):
+        return out
+    cmd = ["gcc", "-O2", "-std=gnu99", "-Wall", "-o", out, src, "-I" + os.path.join(root, "include"),
+           "-L" + HERE, "-ltyche_codec", "-Wl,-rpath,$ORIGIN/../../tyche_amd", "-lpthread"]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.check_call(cmd)
+    return out
+
+
 if __name__ == "__main__":
     import sys
     abl = [int(a.split("=")[1]) for a in sys.argv if a.startswith("--ablate=")]

@@ -109,6 +109,10 @@ SIGNATURES = {
     "tyche_compress_host": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_size_t, _vpp, _u32p, _vpp, _u32p,
                                            _i32p]),
     "tyche_decompress_host": (ctypes.c_int, [ctypes.c_int, ctypes.c_size_t, _vpp, _u32p, _vpp, _u32p, _i32p]),
+    "tyche_restore_queue_start": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
+    "tyche_restore_queue_stop": (None, []),
+    "tyche_buffer_restore": (ctypes.c_int, [_BufP, ctypes.c_int]),
+    "tyche_restore_queue_stats": (None, [ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
     "tyche_device_count": (ctypes.c_int, []),
     "tyche_set_device": (ctypes.c_int, [ctypes.c_int]),
     "tyche_last_error": (ctypes.c_char_p, []),

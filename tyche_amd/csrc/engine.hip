@@ -19,6 +19,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <functional>
 #include <mutex>
@@ -654,6 +655,116 @@ int buffer__decompress(Buffer *buf, int compressor_id) {
     int status = TYCHE_E_OK;
     tyche_buffers_decompress(&buf, &status, 1, compressor_id);
     return status;
+}
+
+// ---------------------------------------------------------- restore queue
+// list__search restores one page per hit, synchronously, under the buffer's
+// lock (src/list.c:563-589).  The queue lets those concurrent per-hit restores
+// share GPU launches: a caller enqueues its Buffer and blocks; a dispatcher
+// thread takes whatever is queued (up to max_batch, after waiting at most
+// max_wait_us for company once the first request arrives), runs one
+// tyche_buffers_decompress per codec over the batch, and wakes each caller with
+// its buffer__decompress status.  Per-buffer semantics are unchanged.
+namespace {
+struct RestoreReq {
+    Buffer *buf;
+    int codec;
+    int status;
+    bool done;
+};
+struct RestoreQueue {
+    std::mutex mu;
+    std::condition_variable cv, done_cv;
+    std::vector<RestoreReq *> q;
+    bool running = false, stop = false;
+    int max_batch = 1024, max_wait_us = 50, device = 0;
+    uint64_t batches = 0, buffers = 0;
+    std::thread th;
+    void loop() {
+        (void)tyche_set_device(device);
+        std::vector<RestoreReq *> take;
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> g(mu);
+                cv.wait(g, [&] { return stop || !q.empty(); });
+                if (stop && q.empty()) return;
+                if ((int)q.size() < max_batch && max_wait_us > 0)
+                    cv.wait_for(g, std::chrono::microseconds(max_wait_us),
+                                [&] { return stop || (int)q.size() >= max_batch; });
+                const size_t k = std::min(q.size(), (size_t)max_batch);
+                take.assign(q.begin(), q.begin() + k);
+                q.erase(q.begin(), q.begin() + k);
+            }
+            // one batch per codec id present
+            for (int codec = 0; codec <= 3; codec++) {
+                std::vector<Buffer *> bufs;
+                std::vector<RestoreReq *> reqs;
+                for (RestoreReq *r : take)
+                    if (r->codec == codec) { bufs.push_back(r->buf); reqs.push_back(r); }
+                if (bufs.empty()) continue;
+                std::vector<int> st(bufs.size());
+                tyche_buffers_decompress(bufs.data(), st.data(), bufs.size(), codec);
+                for (size_t i = 0; i < reqs.size(); i++) reqs[i]->status = st[i];
+            }
+            for (RestoreReq *r : take)
+                if (r->codec < 0 || r->codec > 3) r->status = buffer__decompress(r->buf, r->codec);
+            {
+                std::lock_guard<std::mutex> g(mu);
+                batches++;
+                buffers += take.size();
+                for (RestoreReq *r : take) r->done = true;
+            }
+            done_cv.notify_all();
+        }
+    }
+};
+RestoreQueue g_rq;
+}  // namespace
+
+int tyche_restore_queue_start(int max_batch, int max_wait_us) {
+    std::lock_guard<std::mutex> g(g_rq.mu);
+    if (g_rq.running) return TYCHE_E_OK;
+    g_rq.max_batch = max_batch > 0 ? max_batch : 1024;
+    g_rq.max_wait_us = max_wait_us >= 0 ? max_wait_us : 50;
+    g_rq.device = t_device;
+    g_rq.stop = false;
+    g_rq.running = true;
+    g_rq.th = std::thread([] { g_rq.loop(); });
+    return TYCHE_E_OK;
+}
+
+void tyche_restore_queue_stop(void) {
+    {
+        std::lock_guard<std::mutex> g(g_rq.mu);
+        if (!g_rq.running) return;
+        g_rq.stop = true;
+    }
+    g_rq.cv.notify_all();
+    g_rq.th.join();
+    std::lock_guard<std::mutex> g(g_rq.mu);
+    g_rq.running = false;
+}
+
+int tyche_buffer_restore(Buffer *buf, int compressor_id) {
+    RestoreReq r{buf, compressor_id, TYCHE_E_OK, false};
+    {
+        std::unique_lock<std::mutex> g(g_rq.mu);
+        if (!g_rq.running || g_rq.stop) {
+            g.unlock();
+            return buffer__decompress(buf, compressor_id);   // no queue: the direct path
+        }
+        g_rq.q.push_back(&r);
+    }
+    g_rq.cv.notify_one();
+    std::unique_lock<std::mutex> g(g_rq.mu);
+    g_rq.done_cv.wait(g, [&] { return r.done; });
+    return r.status;
+}
+
+void tyche_restore_queue_stats(uint64_t *batches, uint64_t *buffers) {
+    std::lock_guard<std::mutex> g(g_rq.mu);
+    if (batches) *batches = g_rq.batches;
+    if (buffers) *buffers = g_rq.buffers;
 }
 
 // ---------------------------------------------------------- synthetic input
