@@ -30,16 +30,31 @@ struct PageRef {
     uint32_t dst_cap;
 };
 
+// Per-page metadata is never written by a kernel: read it through the constant
+// address space so a wave-uniform index becomes a scalar load (s_load, its own
+// lgkmcnt counter) instead of a vector load whose in-order vmcnt wait would also
+// drain the previous page's output stores.
+template <typename T>
+__device__ __forceinline__ T ld_meta(const T *p, size_t i) {
+    return ((const __attribute__((address_space(4))) T *)(uintptr_t)p)[i];
+}
+
 __device__ inline PageRef batch_page(const tyche_batch_t &b, size_t i) {
     PageRef r;
-    uint64_t so = b.src_offsets ? b.src_offsets[i] : (uint64_t)i * b.src_stride;
-    uint64_t dof = b.dst_offsets ? b.dst_offsets[i] : (uint64_t)i * b.dst_stride;
+    uint64_t so = b.src_offsets ? ld_meta(b.src_offsets, i) : (uint64_t)i * b.src_stride;
+    uint64_t dof = b.dst_offsets ? ld_meta(b.dst_offsets, i) : (uint64_t)i * b.dst_stride;
     r.src = (const uint8_t *)b.src + so;
-    r.src_len = b.src_lengths ? b.src_lengths[i] : b.src_length;
+    r.src_len = b.src_lengths ? ld_meta(b.src_lengths, i) : b.src_length;
     r.dst = (uint8_t *)b.dst + dof;
-    r.dst_cap = b.dst_capacities ? b.dst_capacities[i] : b.dst_capacity;
+    r.dst_cap = b.dst_capacities ? ld_meta(b.dst_capacities, i) : b.dst_capacity;
     return r;
 }
+
+// The codec kernels run one 64-lane wave per workgroup: LDS ordering between
+// lanes needs no s_barrier, and __syncthreads()'s workgroup fence would wait for
+// every outstanding global load (the next page's prefetch) -- a code-motion
+// barrier is all that is required.
+#define WAVE_SYNC() __builtin_amdgcn_wave_barrier()
 
 hipError_t launch_lz4_decode(const tyche_batch_t &b, uint32_t in_cap, uint32_t out_cap, hipStream_t s);
 hipError_t launch_lz4_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream_t s);

@@ -17,6 +17,14 @@ __device__ __forceinline__ uint32_t lds_ld16(const uint8_t *p) { return *(const 
 __device__ __forceinline__ void lds_st32(uint8_t *p, uint32_t v) { *(u32_ua *)p = v; }
 
 __device__ __forceinline__ uint32_t rfl(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+
+// Streaming loads from HBM through the global address space: a generic pointer
+// would compile to flat_load, which counts in both vmcnt and lgkmcnt (so every
+// later LDS wait would also wait for it) and is waited out of order.
+typedef const __attribute__((address_space(1))) u32x4 g_u32x4;
+typedef const __attribute__((address_space(1))) uint32_t g_u32;
+__device__ __forceinline__ u32x4 gload_nt(const u32x4 *p) { return __builtin_nontemporal_load((g_u32x4 *)(uintptr_t)p); }
+__device__ __forceinline__ uint32_t gload_nt(const uint32_t *p) { return __builtin_nontemporal_load((g_u32 *)(uintptr_t)p); }
 __device__ __forceinline__ uint32_t rdlane(uint32_t v, uint32_t lane) { return __builtin_amdgcn_readlane(v, lane); }
 
 // inclusive prefix sum over the 64 lanes with DPP row shifts + row broadcasts
@@ -55,16 +63,16 @@ __device__ __forceinline__ uint32_t stage_in(const uint8_t *src, uint32_t n, uin
     u32x4 *l = (u32x4 *)lds;
     uint32_t v = tid;
     for (; v + 3 * nthreads < nvec; v += 4 * nthreads) {   // 4 loads in flight per lane
-        u32x4 x0 = __builtin_nontemporal_load(g + v);
-        u32x4 x1 = __builtin_nontemporal_load(g + v + nthreads);
-        u32x4 x2 = __builtin_nontemporal_load(g + v + 2 * nthreads);
-        u32x4 x3 = __builtin_nontemporal_load(g + v + 3 * nthreads);
+        u32x4 x0 = gload_nt(g + v);
+        u32x4 x1 = gload_nt(g + v + nthreads);
+        u32x4 x2 = gload_nt(g + v + 2 * nthreads);
+        u32x4 x3 = gload_nt(g + v + 3 * nthreads);
         l[v] = x0;
         l[v + nthreads] = x1;
         l[v + 2 * nthreads] = x2;
         l[v + 3 * nthreads] = x3;
     }
-    for (; v < nvec; v += nthreads) l[v] = __builtin_nontemporal_load(g + v);
+    for (; v < nvec; v += nthreads) l[v] = gload_nt(g + v);
     return head;
 }
 

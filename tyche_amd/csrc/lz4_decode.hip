@@ -119,13 +119,13 @@ __device__ uint32_t parse_chain(const uint8_t *in, int32_t L, uint8_t *owner, ui
     const uint32_t seg0 = lane * S;
     const uint32_t seg1 = min(seg0 + S, (uint32_t)L);
     for (uint32_t w = lane; w < ((uint32_t)L + 3) / 4; w += kWave) ((uint32_t *)owner)[w] = 0;
-    __syncthreads();
+    WAVE_SYNC();
     uint32_t p = seg0;
     while (p < seg1) {
         owner[p] = (uint8_t)(lane + 1);
         p = next_token(in, L, p);
     }
-    __syncthreads();
+    WAVE_SYNC();
     PROF_MARK(2);
     uint32_t y = p, o = 0;                        // hand-off position and its stamp (0 = chain ends)
     if (seg0 < seg1) {
@@ -154,7 +154,7 @@ __device__ uint32_t parse_chain(const uint8_t *in, int32_t L, uint8_t *owner, ui
     uint32_t base = (uint32_t)incl - cnt;
     for (uint32_t q = entry; q < (uint32_t)L && q != y; q = next_token(in, L, q)) seqpos[base++] = (uint16_t)q;
     const uint32_t total = rdlane((uint32_t)incl, kWave - 1);
-    __syncthreads();
+    WAVE_SYNC();
     PROF_MARK(5);
     PROF_ADD(11, total);
     return total;
@@ -416,11 +416,11 @@ __global__ __launch_bounds__(64) void lz4_decode_serial_kernel(tyche_batch_t b, 
     uint8_t *stage = smem + ((out_cap + 15u) & ~15u);
     uint32_t head = stage_in(p.src, p.src_len, stage, lane, kWave);
     uint8_t *in = stage + head;
-    __syncthreads();
+    WAVE_SYNC();
     in[p.src_len + lane] = 0;
-    __syncthreads();
+    WAVE_SYNC();
     int32_t rv = decode_page_serial(in, (int32_t)p.src_len, out, (int32_t)p.dst_cap, lane);
-    __syncthreads();
+    WAVE_SYNC();
     if (rv > 0) stage_out(p.dst, out, (uint32_t)rv, lane, kWave);
     if (lane == 0) b.results[page] = rv;
 }
@@ -460,7 +460,7 @@ __global__ __launch_bounds__(64) void lz4_decode_wave_kernel(tyche_batch_t b, ui
 #pragma unroll
                 for (uint32_t k = 0; k < kPrefetchVec; k++) {
                     const uint32_t v = lane + k * kWave;
-                    if (v < nvec) pf[k] = __builtin_nontemporal_load(g + v);
+                    pf[k] = gload_nt(g + min(v, nvec - 1u));   // clamped: no branch, always in bounds
                 }
             }
         }
@@ -470,20 +470,20 @@ __global__ __launch_bounds__(64) void lz4_decode_wave_kernel(tyche_batch_t b, ui
             rv = kResultTooLarge;
         } else {
             uint8_t *in = stage + head;
-            __syncthreads();
+            WAVE_SYNC();
             in[p.src_len + lane] = 0;                           // kPad zero bytes past the end
-            __syncthreads();
+            WAVE_SYNC();
             PROF_MARK(1);
             PROF_ADD(0, 1);
             rv = decode_page(in, (int32_t)p.src_len, out, (int32_t)p.dst_cap, seqpos, slots, lane);
-            __syncthreads();
+            WAVE_SYNC();
             PROF_MARK(13);
             if (rv > 0 && !(TYCHE_ABLATE & 4)) stage_out(p.dst, out, (uint32_t)rv, lane, kWave);
         }
         if (lane == 0) b.results[page] = rv;
         if (next >= b.count) break;
         // ---- install the prefetched stream (and load any remainder past 8 KiB)
-        __syncthreads();
+        WAVE_SYNC();
         page = next;
         p = pn;
         head = nhead;
@@ -495,7 +495,7 @@ __global__ __launch_bounds__(64) void lz4_decode_wave_kernel(tyche_batch_t b, ui
                 if (v < nvec) l[v] = pf[k];
             }
             const u32x4 *g = (const u32x4 *)((uintptr_t)p.src - nhead);
-            for (uint32_t v = lane + kPrefetchVec * kWave; v < nvec; v += kWave) l[v] = __builtin_nontemporal_load(g + v);
+            for (uint32_t v = lane + kPrefetchVec * kWave; v < nvec; v += kWave) l[v] = gload_nt(g + v);
         }
         PROF_MARK(12);
     }

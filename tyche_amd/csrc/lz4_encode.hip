@@ -11,7 +11,7 @@
 // capacity (limitedOutput semantics: 0 when it would not fit).
 //
 // One 64-lane wave per page, looping over pages with the next page prefetched
-// into registers.  The page is staged in LDS next to a table of 2^12 16-bit
+// into registers.  The page is staged in LDS next to a table of 2^11 16-bit
 // positions (the byU16 scheme of lz4.c:402-408, hash 2654435761 of 4 bytes).
 // The page is scanned in blocks of 64 positions:
 //   * every lane hashes its position, takes the candidate left by earlier
@@ -174,7 +174,7 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel(tyche_batch_t b, uint32_
 #pragma unroll
                 for (uint32_t k = 0; k < kPrefetchVec; k++) {
                     const uint32_t v = lane + k * kWave;
-                    if (v < nvec) pf[k] = __builtin_nontemporal_load(g + v);
+                    pf[k] = gload_nt(g + min(v, nvec - 1u));   // clamped: no branch, always in bounds
                 }
             }
         }
@@ -184,14 +184,14 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel(tyche_batch_t b, uint32_
         } else {
             uint8_t *in = stage + head;
             for (uint32_t w = lane; w < kHashSize / 8; w += kWave) ((u32x4 *)table)[w] = u32x4{0, 0, 0, 0};
-            __syncthreads();
+            WAVE_SYNC();
             in[p.src_len + lane] = 0;
-            __syncthreads();
+            WAVE_SYNC();
             rv = encode_page(in, p.src_len, table, map, rec, p.dst, p.dst_cap, lane);
         }
         if (lane == 0) b.results[page] = rv;
         if (next >= b.count) break;
-        __syncthreads();
+        WAVE_SYNC();
         page = next;
         p = pn;
         head = nhead;
@@ -203,7 +203,7 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel(tyche_batch_t b, uint32_
                 if (v < nvec) l[v] = pf[k];
             }
             const u32x4 *g = (const u32x4 *)((uintptr_t)p.src - nhead);
-            for (uint32_t v = lane + kPrefetchVec * kWave; v < nvec; v += kWave) l[v] = __builtin_nontemporal_load(g + v);
+            for (uint32_t v = lane + kPrefetchVec * kWave; v < nvec; v += kWave) l[v] = gload_nt(g + v);
         }
     }
 }

@@ -219,7 +219,7 @@ struct BitReader {
 
 __device__ __forceinline__ uint32_t load_win(const BitReader &r, uint32_t base, uint32_t lane) {
     const uint32_t q = (base >> 2) + lane;
-    return q < r.nd ? __builtin_nontemporal_load(r.s4 + q) : 0u;
+    return q < r.nd ? gload_nt(r.s4 + q) : 0u;
 }
 
 __device__ __forceinline__ void refill(BitReader &r, uint32_t lane) {
@@ -530,12 +530,12 @@ __global__ __launch_bounds__(64) void zlib_inflate_kernel(tyche_batch_t b, uint3
             rv = kResultTooLarge;
         } else {
             rv = inflate_page(r, p.src, out, (int32_t)p.dst_cap, lens, sortL, sortD, lane);
-            __syncthreads();
+            WAVE_SYNC();
             if (rv > 0) stage_out(p.dst, out, (uint32_t)rv, lane, kWave);
         }
         if (lane == 0) b.results[page] = rv;
         if (next >= b.count) break;
-        __syncthreads();
+        WAVE_SYNC();
         page = next;
         p = pn;
         r = rn;

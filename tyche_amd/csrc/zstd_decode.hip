@@ -1107,15 +1107,15 @@ __global__ __launch_bounds__(64) void zstd_decode_kernel(tyche_batch_t b, uint32
         if (p.src_len > in_cap || p.dst_cap > out_cap) {
             rv = kResultTooLarge;
         } else {
-            __syncthreads();
+            WAVE_SYNC();
             const uint32_t head = stage_in(p.src, p.src_len, stage, lane, kWave);
             uint8_t *in = stage + head;
-            __syncthreads();
+            WAVE_SYNC();
             if (lane < kStreamPad / 4) lds_st32(in + p.src_len + lane * 4, 0u);
-            __syncthreads();
+            WAVE_SYNC();
             W.in = in;
             rv = decode_frame(W, (int32_t)p.src_len, (int32_t)p.dst_cap, lane);
-            __syncthreads();
+            WAVE_SYNC();
             if (rv > 0) stage_out(p.dst, W.win, (uint32_t)rv, lane, kWave);
         }
         if (lane == 0) b.results[page] = rv;

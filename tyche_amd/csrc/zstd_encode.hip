@@ -440,7 +440,7 @@ __global__ __launch_bounds__(64) void zstd_encode_kernel(tyche_batch_t b, uint32
 #pragma unroll
                 for (uint32_t k = 0; k < kPrefetchVec; k++) {
                     const uint32_t v = lane + k * kWave;
-                    if (v < nvec) pf[k] = __builtin_nontemporal_load(g + v);
+                    pf[k] = gload_nt(g + min(v, nvec - 1u));   // clamped: no branch, always in bounds
                 }
             }
         }
@@ -450,14 +450,14 @@ __global__ __launch_bounds__(64) void zstd_encode_kernel(tyche_batch_t b, uint32
         } else {
             uint8_t *in = stage + head;
             for (uint32_t w = lane; w < kHashSize / 8; w += kWave) ((u32x4 *)table)[w] = u32x4{0, 0, 0, 0};
-            __syncthreads();
+            WAVE_SYNC();
             in[p.src_len + lane] = 0;
-            __syncthreads();
+            WAVE_SYNC();
             rv = encode_page(in, p.src_len, table, map, rec, seq, p.dst, p.dst_cap, lane);
         }
         if (lane == 0) b.results[page] = rv;
         if (next >= b.count) break;
-        __syncthreads();
+        WAVE_SYNC();
         page = next;
         p = pn;
         head = nhead;
@@ -469,7 +469,7 @@ __global__ __launch_bounds__(64) void zstd_encode_kernel(tyche_batch_t b, uint32
                 if (v < nvec) l[v] = pf[k];
             }
             const u32x4 *g = (const u32x4 *)((uintptr_t)p.src - nhead);
-            for (uint32_t v = lane + kPrefetchVec * kWave; v < nvec; v += kWave) l[v] = __builtin_nontemporal_load(g + v);
+            for (uint32_t v = lane + kPrefetchVec * kWave; v < nvec; v += kWave) l[v] = gload_nt(g + v);
         }
     }
 }
