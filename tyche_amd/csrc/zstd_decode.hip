@@ -41,6 +41,9 @@ namespace tyche {
 namespace {
 
 constexpr uint32_t kWave = 64;
+#ifndef TYCHE_ZABLATE
+#define TYCHE_ZABLATE 0
+#endif
 constexpr int32_t kErr = -20;          // corruption_detected (any error: buffer.c only tests ZSTD_isError)
 constexpr int32_t kErrDst = -70;       // dstSize_tooSmall
 constexpr uint32_t kBlockMax = 128u * 1024u;
@@ -66,6 +69,37 @@ __device__ __constant__ uint32_t c_of_base[29] = {0, 1, 1, 5, 0xD, 0x1D, 0x3D, 0
                                                   0xFFD, 0x1FFD, 0x3FFD, 0x7FFD, 0xFFFD, 0x1FFFD, 0x3FFFD, 0x7FFFD,
                                                   0xFFFFD, 0x1FFFFD, 0x3FFFFD, 0x7FFFFD, 0xFFFFFD, 0x1FFFFFD,
                                                   0x3FFFFFD, 0x7FFFFFD, 0xFFFFFFD};
+// Base value and extra-bit count of a code (LL_base/LL_bits, ML_base/ML_bits,
+// OF_base of zstd_decompress.c:864-879, zstd_internal.h:115-127), computed
+// instead of loaded so the serial sequence chain carries no memory waits.
+__device__ __forceinline__ uint32_t of_base(uint32_t c) { return c < 2u ? c : (1u << c) - 3u; }
+__device__ __forceinline__ void ll_code(uint32_t c, uint32_t &base, uint32_t &bits) {
+    if (c < 16u) { base = c; bits = 0; return; }
+    if (c < 24u) {
+        // codes 16..23: bases 16 18 20 22 24 28 32 40, bits 1 1 1 1 2 2 3 3
+        const uint32_t k = c - 16u;
+        bits = k < 4u ? 1u : (k < 6u ? 2u : 3u);
+        base = k < 4u ? 16u + 2u * k : (k < 6u ? 24u + 4u * (k - 4u) : 32u + 8u * (k - 6u));
+        return;
+    }
+    if (c == 24u) { base = 48u; bits = 4u; return; }
+    bits = c - 19u;
+    base = 1u << bits;
+}
+__device__ __forceinline__ void ml_code(uint32_t c, uint32_t &base, uint32_t &bits) {
+    if (c < 32u) { base = c + 3u; bits = 0; return; }
+    if (c < 43u) {
+        // codes 32..42: bases 35 37 39 41 43 47 51 59 67 83 99, bits 1 1 1 1 2 2 3 3 4 4 5
+        const uint32_t k = c - 32u;
+        bits = k < 4u ? 1u : (k < 6u ? 2u : (k < 8u ? 3u : (k < 10u ? 4u : 5u)));
+        base = k < 4u ? 35u + 2u * k : (k < 6u ? 43u + 4u * (k - 4u) : (k < 8u ? 51u + 8u * (k - 6u)
+                                                                          : (k < 10u ? 67u + 16u * (k - 8u) : 99u)));
+        return;
+    }
+    bits = c - 36u;
+    base = (1u << bits) + 3u;
+}
+
 // The predefined decoding tables (ZSTD_buildSeqTable set_basic ->
 // LL/OF/ML_defaultDTable, zstd_decompress.c:517-687) are FSE_buildDTable over
 // the default distributions; built here at compile time.
@@ -132,6 +166,13 @@ __device__ __forceinline__ uint64_t ld64(const uint8_t *p) {
 }
 __device__ __forceinline__ uint32_t highbit(uint32_t v) { return 31u - (uint32_t)__builtin_clz(v); }
 
+// Wave-uniform reads of the staged frame: the value goes through
+// v_readfirstlane so everything computed from it stays in SGPRs.
+__device__ __forceinline__ uint32_t u8u(const uint8_t *in, int32_t i) { return rfl(in[i]); }
+__device__ __forceinline__ uint32_t u16u(const uint8_t *in, int32_t i) { return rfl(lds_ld16(in + i)); }
+__device__ __forceinline__ uint32_t u32u(const uint8_t *in, int32_t i) { return rfl(lds_ld32(in + i)); }
+__device__ __forceinline__ int32_t ru(int32_t v) { return (int32_t)rfl((uint32_t)v); }
+
 // ------------------------------------------------------------ bit reader (bitstream.h:260-408)
 enum : uint32_t { kUnfinished = 0, kEndOfBuffer = 1, kCompleted = 2, kOverflow = 3 };
 
@@ -173,6 +214,8 @@ __device__ __forceinline__ uint64_t ld64u(const uint8_t *p) {
     return (uint64_t)rfl(lds_ld32(p)) | ((uint64_t)rfl(lds_ld32(p + 4)) << 32);
 }
 __device__ __forceinline__ bool bitd_init_u(BitD &b, const uint8_t *in, int32_t start, int32_t n) {
+    start = ru(start);
+    n = ru(n);
     b.start = start;
     b.c = 0;
     b.used = 0;
@@ -413,7 +456,7 @@ __device__ bool build_dtable(uint32_t *cells, const int16_t *norm, uint32_t max_
 __device__ int32_t huf_read_table(const Work &W, int32_t ip, int32_t n, uint32_t &tlog, uint32_t lane) {
     const uint8_t *in = W.in;
     if (n < 1) return kErr;
-    int32_t isize = in[ip];
+    int32_t isize = (int32_t)u8u(in, ip);
     uint32_t osize;
     if (isize >= 128) {
         osize = (uint32_t)isize - 127u;
@@ -775,7 +818,7 @@ __device__ int32_t seq_table(const Work &W, uint32_t *cells, uint32_t &log, uint
                              bool flag_repeat, uint32_t lane) {
     if (type == 1) {   // set_rle
         if (n < 1) return kErr;
-        const uint32_t sym = W.in[ip];
+        const uint32_t sym = u8u(W.in, ip);
         if (sym > max) return kErr;
         if (lane == 0) cells[0] = cell(0, sym, 0);
         log = 0;
@@ -801,10 +844,14 @@ __device__ int32_t seq_table(const Work &W, uint32_t *cells, uint32_t &log, uint
 __device__ int32_t decode_block(const Work &W, SeqTables &T, int32_t ip, int32_t n, int32_t op, int32_t cap,
                                 uint32_t lane) {
     const uint8_t *in = W.in;
+    ip = ru(ip);
+    n = ru(n);
+    op = ru(op);
+    cap = ru(cap);
     if (n >= (int32_t)kBlockMax) return kErr;
     // ---- literals section (ZSTD_decodeLiteralsBlock)
     if (n < 3) return kErr;
-    const uint32_t b0 = in[ip];
+    const uint32_t b0 = u8u(in, ip);
     const uint32_t ltype = b0 & 3u, lhl = (b0 >> 2) & 3u;
     const uint8_t *lit;
     bool lit_in_window;
@@ -812,12 +859,12 @@ __device__ int32_t decode_block(const Work &W, SeqTables &T, int32_t ip, int32_t
     if (ltype >= 2u) {
         if (ltype == 3u && !T.lit_entropy) return kErr;
         if (n < 5) return kErr;
-        const uint32_t lhc = lds_ld32(in + ip);
+        const uint32_t lhc = u32u(in, ip);
         int32_t lh, csize;
         bool single = false;
         if (lhl <= 1u) { single = lhl == 0; lh = 3; lsize = (int32_t)((lhc >> 4) & 0x3FFu); csize = (int32_t)((lhc >> 14) & 0x3FFu); }
         else if (lhl == 2u) { lh = 4; lsize = (int32_t)((lhc >> 4) & 0x3FFFu); csize = (int32_t)(lhc >> 18); }
-        else { lh = 5; lsize = (int32_t)((lhc >> 4) & 0x3FFFFu); csize = (int32_t)((lhc >> 22) + ((uint32_t)in[ip + 4] << 10)); }
+        else { lh = 5; lsize = (int32_t)((lhc >> 4) & 0x3FFFFu); csize = (int32_t)((lhc >> 22) + (u8u(in, ip + 4) << 10)); }
         if (lsize > (int32_t)kBlockMax) return kErr;
         if (csize + lh > n) return kErr;
         // the block's output is lsize + sum(ml) bytes: a section that cannot fit the
@@ -856,8 +903,8 @@ __device__ int32_t decode_block(const Work &W, SeqTables &T, int32_t ip, int32_t
         lcons = lh + csize;
     } else {
         int32_t lh;
-        if (lhl == 1u) { lh = 2; lsize = (int32_t)(lds_ld16(in + ip) >> 4); }
-        else if (lhl == 3u) { lh = 3; lsize = (int32_t)((lds_ld32(in + ip) & 0xFFFFFFu) >> 4); }
+        if (lhl == 1u) { lh = 2; lsize = (int32_t)(u16u(in, ip) >> 4); }
+        else if (lhl == 3u) { lh = 3; lsize = (int32_t)((u32u(in, ip) & 0xFFFFFFu) >> 4); }
         else { lh = 1; lsize = (int32_t)(b0 >> 3); }
         if (ltype == 0u) {   // raw
             if (lh + lsize > n) return kErr;
@@ -882,21 +929,21 @@ __device__ int32_t decode_block(const Work &W, SeqTables &T, int32_t ip, int32_t
     int32_t sp = ip + lcons;
     const int32_t send = ip + n;
     if (send - sp < 1) return kErr;
-    int32_t nbseq = in[sp++];
+    int32_t nbseq = (int32_t)u8u(in, sp++);
     int32_t op0 = op, lp = 0;
     if (nbseq) {
         if (nbseq > 0x7F) {
             if (nbseq == 0xFF) {
                 if (sp + 2 > send) return kErr;
-                nbseq = (int32_t)lds_ld16(in + sp) + 0x7F00;
+                nbseq = (int32_t)u16u(in, sp) + 0x7F00;
                 sp += 2;
             } else {
                 if (sp >= send) return kErr;
-                nbseq = ((nbseq - 0x80) << 8) + in[sp++];
+                nbseq = ((nbseq - 0x80) << 8) + (int32_t)u8u(in, sp++);
             }
         }
         if (sp + 4 > send) return kErr;
-        const uint32_t modes = in[sp++];
+        const uint32_t modes = u8u(in, sp++);
         int32_t r = seq_table(W, W.ll, T.ll_log, modes >> 6, 35, 9, sp, send - sp, c_ll_def, 6, T.fse_entropy, lane);
         if (r < 0) return kErr;
         sp += r;
@@ -929,7 +976,7 @@ __device__ int32_t decode_block(const Work &W, SeqTables &T, int32_t ip, int32_t
                 const uint32_t llc = cell_sym(cl), mlc = cell_sym(cm), ofc = cell_sym(co);
                 uint32_t offv;
                 if (!ofc) offv = 0;
-                else offv = c_of_base[ofc] + bitd_read_fast(b, ofc);
+                else offv = of_base(ofc) + bitd_read_fast(b, ofc);
                 if (ofc <= 1u) {
                     offv += llc == 0;
                     if (offv) {
@@ -946,13 +993,16 @@ __device__ int32_t decode_block(const Work &W, SeqTables &T, int32_t ip, int32_t
                     rep1 = rep0;
                     rep0 = offv;
                 }
-                const uint32_t mlb = c_ml_bits[mlc], llb = c_ll_bits[llc];
-                const uint32_t mlv = c_ml_base[mlc] + (mlc > 31u ? bitd_read_fast(b, mlb) : 0u);
-                const uint32_t llv = c_ll_base[llc] + (llc > 15u ? bitd_read_fast(b, llb) : 0u);
+                uint32_t mlbase, mlb, llbase, llb;
+                ml_code(mlc, mlbase, mlb);
+                ll_code(llc, llbase, llb);
+                const uint32_t mlv = mlbase + (mlc > 31u ? bitd_read_fast(b, mlb) : 0u);
+                const uint32_t llv = llbase + (llc > 15u ? bitd_read_fast(b, llb) : 0u);
                 if (llb + mlb + ofc > 31u) bitd_reload_u(b, in);
                 sll = cell_state(cl) + bitd_read(b, cell_nb(cl));
                 sml = cell_state(cm) + bitd_read(b, cell_nb(cm));
                 sof = cell_state(co) + bitd_read(b, cell_nb(co));
+
                 if (lane == k) {
                     vll = llv;
                     vml = mlv;
@@ -960,8 +1010,14 @@ __device__ int32_t decode_block(const Work &W, SeqTables &T, int32_t ip, int32_t
                 }
             }
             if (k == 0) break;
+#if TYCHE_ZABLATE & 1
+            // timing-only: skip execution (output wrong), keep the positions moving
+            op += (int32_t)rdlane((uint32_t)wave_incl_sum(lane < k ? (int32_t)(vll + vml) : 0), kWave - 1);
+            lp += (int32_t)rdlane((uint32_t)wave_incl_sum(lane < k ? (int32_t)vll : 0), kWave - 1);
+#else
             if (!exec_batch(W.win, lit, lit_in_window, lit_win_base, k, vll, vml, voff, op, lp, lsize, cap, lane))
                 return kErr;
+#endif
         }
         if (nbseq) return kErr;
         T.rep0 = rep0;
@@ -987,8 +1043,8 @@ __device__ int32_t decode_block(const Work &W, SeqTables &T, int32_t ip, int32_t
 __device__ int32_t decode_frame(const Work &W, int32_t L, int32_t cap, uint32_t lane) {
     const uint8_t *in = W.in;
     if (L < 9) return kErr;
-    const uint32_t magic = lds_ld32(in);
-    const uint32_t fhd = in[4];
+    const uint32_t magic = u32u(in, 0);
+    const uint32_t fhd = u8u(in, 4);
     const uint32_t did = fhd & 3u, single = (fhd >> 5) & 1u, fcs_id = fhd >> 6;
     bool checksum = (fhd >> 2) & 1u;
     const int32_t fh = 5 + (int32_t)!single + (int32_t)(did == 3 ? 4 : did) + (int32_t)(fcs_id == 0 ? 0 : 1u << fcs_id) +
@@ -1005,19 +1061,19 @@ __device__ int32_t decode_frame(const Work &W, int32_t L, int32_t cap, uint32_t 
         uint64_t window = 0, fcs = 0;
         uint32_t dict_id = 0;
         if (!single) {
-            const uint32_t wl = in[pos++];
+            const uint32_t wl = u8u(in, pos++);
             const uint32_t wlog = (wl >> 3) + 10u;
             if (wlog > 27u) return kErr;
             window = 1ull << wlog;
             window += (window >> 3) * (wl & 7u);
         }
-        if (did == 1) { dict_id = in[pos]; pos += 1; }
-        else if (did == 2) { dict_id = lds_ld16(in + pos); pos += 2; }
-        else if (did == 3) { dict_id = lds_ld32(in + pos); pos += 4; }
-        if (fcs_id == 0) { if (single) fcs = in[pos]; }
-        else if (fcs_id == 1) fcs = (uint64_t)lds_ld16(in + pos) + 256u;
-        else if (fcs_id == 2) fcs = lds_ld32(in + pos);
-        else fcs = ld64(in + pos);
+        if (did == 1) { dict_id = u8u(in, pos); pos += 1; }
+        else if (did == 2) { dict_id = u16u(in, pos); pos += 2; }
+        else if (did == 3) { dict_id = u32u(in, pos); pos += 4; }
+        if (fcs_id == 0) { if (single) fcs = u8u(in, pos); }
+        else if (fcs_id == 1) fcs = (uint64_t)u16u(in, pos) + 256u;
+        else if (fcs_id == 2) fcs = u32u(in, pos);
+        else fcs = ld64u(in + pos);
         if (!window) window = (uint32_t)fcs;
         if (window > (1ull << 27)) return kErr;
         if (dict_id) return kErr;
@@ -1032,7 +1088,7 @@ __device__ int32_t decode_frame(const Work &W, int32_t L, int32_t cap, uint32_t 
     int32_t ip = fh, remaining = L - fh, op = 0;
     for (;;) {
         if (remaining < 3) return kErr;
-        const uint32_t bh = (uint32_t)in[ip] | ((uint32_t)in[ip + 1] << 8) | ((uint32_t)in[ip + 2] << 16);
+        const uint32_t bh = u8u(in, ip) | (u8u(in, ip + 1) << 8) | (u8u(in, ip + 2) << 16);
         const uint32_t last = bh & 1u, btype = (bh >> 1) & 3u, csize0 = bh >> 3;
         if (btype == 3u) return kErr;
         const int32_t csize = btype == 1u ? 1 : (int32_t)csize0;
