@@ -34,7 +34,11 @@ constexpr uint32_t kWave = 64;
 #endif
 constexpr uint32_t kHashLog = TYCHE_HASH_LOG;
 constexpr uint32_t kHashSize = 1u << kHashLog;
-constexpr uint32_t kProbe = 16;          // bytes probed per lane beyond MINMATCH
+#ifndef TYCHE_PROBE_WORDS
+#define TYCHE_PROBE_WORDS 4
+#endif
+constexpr uint32_t kProbeWords = TYCHE_PROBE_WORDS;   // 4-byte words probed per lane beyond MINMATCH
+constexpr uint32_t kProbe = 4 * kProbeWords;
 
 // Timing-only ablation builds (-DTYCHE_EABLATE=mask; outputs are wrong):
 //   1 skip the byte emission loop (sizes still computed), 2 no probes (every match 4 bytes),
@@ -105,67 +109,75 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
     for (; !done && blk <= mflimit; blk = max(blk + kWave, cursor & ~(kWave - 1))) {
         const uint32_t pos = blk + lane;
         const bool live = pos <= mflimit;
-        // ---- candidates from earlier blocks, then insert this block's positions
+        // ---- candidates from earlier blocks, then insert this block's positions.
+        // Every lane takes part, branch-free: lanes past mflimit only exist in the
+        // last block, and no lookup follows their inserts.
         const uint32_t v = lds_ld32(in + pos);
         const uint32_t h = hash4(v);
-        const uint32_t cand = live ? table[h] : 0u;
+        const uint32_t cand = table[h];
         __builtin_amdgcn_wave_barrier();
-        if (live) table[h] = (uint16_t)pos;
-        const bool ok = live && cand < pos && lds_ld32(in + cand) == v;
-        // ---- forward probe (MINMATCH + up to kProbe bytes) and backward probe (up to 4 bytes)
-        uint32_t len = (TYCHE_EABLATE & 2) ? 4u : 0u, back = 0;
-        bool capped = false;
-        if (ok && !(TYCHE_EABLATE & 2)) {
-            // four unaligned dword compares, no branches; clamp to the match limit
-            const uint32_t e = min(matchlimit, pos + kMinMatch + kProbe);
-            const uint32_t x0 = lds_ld32(in + pos + 4) ^ lds_ld32(in + cand + 4);
-            const uint32_t x1 = lds_ld32(in + pos + 8) ^ lds_ld32(in + cand + 8);
-            const uint32_t x2 = lds_ld32(in + pos + 12) ^ lds_ld32(in + cand + 12);
-            const uint32_t x3 = lds_ld32(in + pos + 16) ^ lds_ld32(in + cand + 16);
-            uint32_t n = x0 ? 4 + (__builtin_ctz(x0) >> 3)
-                       : x1 ? 8 + (__builtin_ctz(x1) >> 3)
-                       : x2 ? 12 + (__builtin_ctz(x2) >> 3)
-                       : x3 ? 16 + (__builtin_ctz(x3) >> 3) : 20u;
-            n = min(n, e - pos);
-            len = n;
-            capped = pos + n == e && e < matchlimit;
-            if (pos >= 4 && cand >= 4) {
-                const uint32_t x = lds_ld32(in + pos - 4) ^ lds_ld32(in + cand - 4);
-                back = x ? (__builtin_clz(x) >> 3) : 4u;
-            }
-        }
-        // ---- greedy parse of this block.  Every lane precomputes where the parse
-        // goes if it stands at its position: the first match at or after it
-        // (ballot mask) and that match's end.  The parse itself then only hops
-        // through these values with v_readlane (scalar code, no memory).
+        table[h] = (uint16_t)pos;
+        const bool ok = live & (cand < pos) & (lds_ld32(in + cand) == v);
+        // ---- forward probe (MINMATCH + up to kProbe bytes) and backward probe (up
+        // to 4 bytes): unaligned dword compares issued together, addresses clamped
+        // so lanes without a match read in bounds; only matched lanes' values are used
+        const uint32_t pa = ok ? pos : 0u, ca = ok ? cand : 0u;
+        uint32_t x[kProbeWords];
+#pragma unroll
+        for (uint32_t k = 0; k < kProbeWords; k++)
+            x[k] = lds_ld32(in + pa + 4 + 4 * k) ^ lds_ld32(in + ca + 4 + 4 * k);
+        const uint32_t xb = lds_ld32(in + max(pa, 4u) - 4) ^ lds_ld32(in + max(ca, 4u) - 4);
+        uint32_t n = 4u + kProbe;
+#pragma unroll
+        for (int k = (int)kProbeWords - 1; k >= 0; k--)
+            if (x[k]) n = 4u + 4u * (uint32_t)k + ((uint32_t)__builtin_ctz(x[k]) >> 3);
+        const uint32_t e = min(matchlimit, pos + kMinMatch + kProbe);
+        n = min(n, e - pos);
+        uint32_t len = (TYCHE_EABLATE & 2) ? 4u : n;
+        const bool capped = !(TYCHE_EABLATE & 2) && pos + n == e && e < matchlimit;
+        const uint32_t back = (TYCHE_EABLATE & 2) || pos < 4 || cand < 4 ? 0u : xb ? (__builtin_clz(xb) >> 3) : 4u;
+        // ---- greedy parse of this block.  Every lane first finds the next match
+        // lane at or after its own match's end (64: none in this block; 128: the
+        // match reached the probe limit, end not known yet), so the walk from the
+        // parse position is one v_readlane per selected match.  The parse
+        // position is always inside the block (blk >= cursor & ~63), and no mask
+        // bit lies past mflimit, so a match ending there ends the walk.
         const uint64_t mall = (TYCHE_EABLATE & 4) ? 0ull : __ballot(ok);
-        uint32_t at = cursor > blk ? cursor - blk : 0u;        // parse position within the block
-        if ((mall >> at) == 0) continue;                       // no match starts at or after it
-        const uint64_t ahead = mall & ~((1ull << lane) - 1ull);
-        const uint32_t nml = ahead ? (uint32_t)__builtin_ctzll(ahead) : 64u;
-        const uint32_t nlen = __shfl(len | ((uint32_t)capped << 16), nml & 63u);
-        // hop word: bits 0..6 lane of the next match (64 = none), bit 7 capped, bits 8.. its end
-        const uint32_t hop = nml | ((nlen >> 16) << 7) | ((blk + nml + (nlen & 0xFFFFu)) << 8);
+        const uint32_t at = cursor > blk ? cursor - blk : 0u;
+        const uint64_t rem = mall & (~0ull << at);
+        if (rem == 0) continue;                                // no match starts at or after it
+        const uint32_t endp = pos + len;
+        const uint32_t rl = endp - blk;
+        const uint64_t after = rl < kWave ? mall & (~0ull << rl) : 0ull;
+        const uint32_t nxt = (capped && !(TYCHE_EABLATE & 8)) ? 2u * kWave
+                           : after ? (uint32_t)__builtin_ctzll(after) : kWave;
         uint64_t sel = 0;
+        uint32_t li = (uint32_t)__builtin_ctzll(rem);
+        uint32_t end;
         for (;;) {
-            const uint32_t hw = rdlane(hop, at);
-            const uint32_t li = hw & 127u;
-            if (li >= 64) break;                                 // no further match in this block
-            uint32_t end = hw >> 8;
-            if ((hw & 128u) && !(TYCHE_EABLATE & 8)) {
-                // reached the probe limit: extend with the whole wave
-                const uint32_t mp = blk + li, mc = rdlane(cand, li), ln0 = end - mp;
-                const uint32_t ln = ln0 + wave_extend(in, mp + ln0, mc + ln0, matchlimit, lane);
-                if (lane == li) len = ln;
-                end = mp + ln;
-            }
             sel |= 1ull << li;
-            cursor = end;
-            if (cursor > mflimit) { done = true; break; }
-            if (cursor >= blk + kWave) break;
-            at = cursor - blk;
+            const uint32_t nl = rdlane(nxt, li);
+            if (nl < kWave) {
+                li = nl;
+                continue;
+            }
+            if (nl == kWave) {
+                end = rdlane(endp, li);
+                break;
+            }
+            // reached the probe limit: extend with the whole wave, then look for
+            // the next match after the extended end
+            const uint32_t mp = blk + li, mc = rdlane(cand, li), ln0 = rdlane(endp, li) - mp;
+            const uint32_t ln = ln0 + wave_extend(in, mp + ln0, mc + ln0, matchlimit, lane);
+            if (lane == li) len = ln;
+            end = mp + ln;
+            const uint32_t rel = end - blk;
+            const uint64_t r = rel < kWave ? mall & (~0ull << rel) : 0ull;
+            if (r == 0) break;
+            li = (uint32_t)__builtin_ctzll(r);
         }
-        if (sel == 0) continue;
+        cursor = end;
+        done = cursor > mflimit;
         // ---- append this block's records (stream order)
         const bool is_sel = (sel >> lane) & 1ull;
         const uint32_t rank = nacc + (uint32_t)__popcll(sel & ((1ull << lane) - 1ull));
