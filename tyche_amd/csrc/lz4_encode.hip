@@ -27,6 +27,8 @@
 //     written 64 per store instruction, contiguous.
 #include <hip/hip_runtime.h>
 
+#define TYCHE_PHASES_OWNER   // only used by -DTYCHE_PHASES profiling builds
+
 #include <algorithm>
 
 #include "engine.h"
@@ -229,5 +231,14 @@ hipError_t launch_lz4_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream_
     hipLaunchKernelGGL(lz4_encode_kernel, dim3((unsigned)grid), dim3(kWave), lds, s, b, in_cap);
     return hipGetLastError();
 }
+
+#ifdef TYCHE_PHASES
+// profiling builds only: per-phase parse cycles summed since the last call (then cleared)
+extern "C" int tyche_phase_read(unsigned long long *out) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(lzp::g_phase), 8 * sizeof(unsigned long long)) != hipSuccess) return -1;
+    static const unsigned long long zero[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(lzp::g_phase), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 }  // namespace tyche

@@ -48,6 +48,25 @@ constexpr uint32_t kProbe = 4 * kProbeWords;
 #define TYCHE_EABLATE 0
 #endif
 
+// Profiling-only builds (-DTYCHE_PHASES, tools/phase_prof.py): per-phase wave
+// cycles of the parse (s_memtime; each read waits for outstanding LDS ops),
+// summed over pages into g_phase.  Only the LZ4 encoder's translation unit
+// (TYCHE_PHASES_OWNER) is instrumented.
+#if defined(TYCHE_PHASES) && defined(TYCHE_PHASES_OWNER)
+__device__ unsigned long long g_phase[8];
+__device__ __forceinline__ uint32_t phase_clock() { return (uint32_t)__builtin_amdgcn_s_memtime(); }
+#define PHASE_INIT() uint32_t ph_t_ = phase_clock(), ph_[7] = {0, 0, 0, 0, 0, 0, 0}
+#define PHASE(i) do { const uint32_t t_ = phase_clock(); ph_[i] += t_ - ph_t_; ph_t_ = t_; } while (0)
+#define PHASE_COUNT() ph_[6]++
+#define PHASE_FLUSH() do { if (lane == 0) for (int i_ = 0; i_ < 7; i_++) atomicAdd(&g_phase[i_], (unsigned long long)ph_[i_]); \
+                           if (lane == 0) atomicAdd(&g_phase[7], 1ull); } while (0)
+#else
+#define PHASE_INIT() do {} while (0)
+#define PHASE(i) do {} while (0)
+#define PHASE_COUNT() do {} while (0)
+#define PHASE_FLUSH() do {} while (0)
+#endif
+
 __device__ __forceinline__ uint32_t hash4(uint32_t v) { return (v * 2654435761u) >> (32 - kHashLog); }
 
 // equal bytes at a and b going forward, a stopping before `limit` (whole wave, 256 bytes per step)
@@ -106,6 +125,7 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
     uint32_t nacc = 0;       // records accumulated since the last hand-off
     uint32_t blk = 0;        // current 64-position block
     bool done = false;
+    PHASE_INIT();
     for (; !done && blk <= mflimit; blk = max(blk + kWave, cursor & ~(kWave - 1))) {
         const uint32_t pos = blk + lane;
         const bool live = pos <= mflimit;
@@ -143,6 +163,7 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
         // position is always inside the block (blk >= cursor & ~63), and no mask
         // bit lies past mflimit, so a match ending there ends the walk.
         const uint64_t mall = (TYCHE_EABLATE & 4) ? 0ull : __ballot(ok);
+        PHASE(0);
         const uint32_t at = cursor > blk ? cursor - blk : 0u;
         const uint64_t rem = mall & (~0ull << at);
         if (rem == 0) continue;                                // no match starts at or after it
@@ -168,7 +189,10 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
             // reached the probe limit: extend with the whole wave, then look for
             // the next match after the extended end
             const uint32_t mp = blk + li, mc = rdlane(cand, li), ln0 = rdlane(endp, li) - mp;
+            PHASE(1);
             const uint32_t ln = ln0 + wave_extend(in, mp + ln0, mc + ln0, matchlimit, lane);
+            PHASE(5);
+            PHASE_COUNT();
             if (lane == li) len = ln;
             end = mp + ln;
             const uint32_t rel = end - blk;
@@ -178,24 +202,30 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
         }
         cursor = end;
         done = cursor > mflimit;
+        PHASE(1);
         // ---- append this block's records (stream order)
         const bool is_sel = (sel >> lane) & 1ull;
         const uint32_t rank = nacc + (uint32_t)__popcll(sel & ((1ull << lane) - 1ull));
         if (is_sel) rec[rank] = make_uint2(pos | (cand << 16), len | (back << 16));
         nacc += (uint32_t)__popcll(sel);
         // a block adds at most 16 records (each covers >= 4 positions)
+        PHASE(2);
         if (nacc > kWave - 16 || done) {
             __builtin_amdgcn_wave_barrier();
             if (!sink(rec, nacc, anchor)) return 0xFFFFFFFFu;
             anchor = cursor;
             nacc = 0;
+            PHASE(3);
         }
     }
+    PHASE(4);
     if (nacc) {
         __builtin_amdgcn_wave_barrier();
         if (!sink(rec, nacc, anchor)) return 0xFFFFFFFFu;
         anchor = cursor;
     }
+    PHASE(3);
+    PHASE_FLUSH();
     return anchor;
 }
 
