@@ -69,13 +69,48 @@ __device__ __forceinline__ uint32_t phase_clock() { return (uint32_t)__builtin_a
 
 __device__ __forceinline__ uint32_t hash4(uint32_t v) { return (v * 2654435761u) >> (32 - kHashLog); }
 
-// equal bytes at a and b going forward, a stopping before `limit` (whole wave, 256 bytes per step)
-__device__ inline uint32_t wave_extend(const uint8_t *in, uint32_t a, uint32_t b, uint32_t limit, uint32_t lane) {
+// The page is read as aligned dwords only: an LDS read off its natural
+// alignment (a 4-byte read at an odd address, a b64/b128 off 8/16) is replayed
+// at ~64 LDS cycles per wave instruction, which made the parse LDS-bound
+// (SQ_LDS_UNALIGNED_STALL ~90 % of LDS-active cycles).  A is the page's base
+// rounded down to 4 bytes and q a byte offset from it (position + (in & 3)).
+__device__ __forceinline__ uint32_t word_at(uint32_t lo, uint32_t hi, uint32_t s) {
+    return __builtin_amdgcn_alignbyte(hi, lo, s);   // bytes s..s+3 of hi:lo
+}
+__device__ __forceinline__ uint32_t lds_word(const uint32_t *A, uint32_t q) {
+    return word_at(A[q >> 2], A[(q >> 2) + 1], q & 3u);
+}
+
+// A 28-byte window around byte offset q (q - 4 .. q + 23, within 7 aligned
+// dwords): the word at q - 4 (backward probe), at q (MINMATCH verify) and the
+// kProbeWords words after it (forward probe).
+struct Window {
+    uint32_t back, w0, fw[kProbeWords];
+};
+__device__ __forceinline__ Window lds_window(const uint32_t *A, uint32_t q) {
+    static_assert(kProbeWords == 4, "the window holds four probe words");
+    const uint32_t i = q >> 2, s = q & 3u;
+    const uint32_t dm = A[max(i, 1u) - 1];   // q < 4 only at positions < 4, whose backward probe is unused
+    uint32_t d[6];
+#pragma unroll
+    for (int j = 0; j < 6; j++) d[j] = A[i + j];
+    Window r;
+    r.back = word_at(dm, d[0], s);
+    r.w0 = word_at(d[0], d[1], s);
+#pragma unroll
+    for (int k = 0; k < 4; k++) r.fw[k] = word_at(d[k + 1], d[k + 2], s);
+    return r;
+}
+
+// equal bytes at a and b going forward, a stopping before `limit` (whole wave,
+// 256 bytes per step); a, b, limit are positions, ib = (in & 3)
+__device__ inline uint32_t wave_extend(const uint8_t *in, const uint32_t *A, uint32_t ib, uint32_t a, uint32_t b,
+                                       uint32_t limit, uint32_t lane) {
     uint32_t n = 0;
     for (;;) {
         const uint32_t pa = a + n + 4 * lane;
         const bool full = pa + 4 <= limit;
-        const uint32_t x = full ? (lds_ld32(in + pa) ^ lds_ld32(in + b + n + 4 * lane)) : 1u;
+        const uint32_t x = full ? (lds_word(A, pa + ib) ^ lds_word(A, b + n + 4 * lane + ib)) : 1u;
         const uint64_t bad = __ballot(x != 0);
         if (bad == 0) {
             n += 4 * kWave;
@@ -121,6 +156,8 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
     if (L < (uint32_t)(kMfLimit + 1)) return 0;
     const uint32_t mflimit = L - kMfLimit;          // last position a match may start
     const uint32_t matchlimit = L - kLastLiterals;  // matches end at or before this
+    const uint32_t ib = (uint32_t)(uintptr_t)in & 3u;               // in's offset from a dword boundary
+    const uint32_t *A = (const uint32_t *)(in - ib);                // the page as aligned dwords
     uint32_t cursor = 0;     // matches may start here (end of the last match)
     uint32_t nacc = 0;       // records accumulated since the last hand-off
     uint32_t blk = 0;        // current 64-position block
@@ -129,28 +166,29 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
     for (; !done && blk <= mflimit; blk = max(blk + kWave, cursor & ~(kWave - 1))) {
         const uint32_t pos = blk + lane;
         const bool live = pos <= mflimit;
-        // ---- candidates from earlier blocks, then insert this block's positions.
-        // Every lane takes part, branch-free: lanes past mflimit only exist in the
-        // last block, and no lookup follows their inserts.
-        const uint32_t v = lds_ld32(in + pos);
+        // ---- this position's window (lanes past mflimit read mflimit's: their
+        // values are unused), its hash and the candidate left by earlier blocks,
+        // then insert this block's positions.  Every lane takes part, branch-free:
+        // lanes past mflimit only exist in the last block, and no lookup follows
+        // their inserts.
+        const Window pw = lds_window(A, (live ? pos : mflimit) + ib);
+        const uint32_t v = pw.w0;
         const uint32_t h = hash4(v);
         const uint32_t cand = table[h];
         __builtin_amdgcn_wave_barrier();
         table[h] = (uint16_t)pos;
-        const bool ok = live & (cand < pos) & (lds_ld32(in + cand) == v);
-        // ---- forward probe (MINMATCH + up to kProbe bytes) and backward probe (up
-        // to 4 bytes): unaligned dword compares issued together, addresses clamped
-        // so lanes without a match read in bounds; only matched lanes' values are used
-        const uint32_t pa = ok ? pos : 0u, ca = ok ? cand : 0u;
-        uint32_t x[kProbeWords];
-#pragma unroll
-        for (uint32_t k = 0; k < kProbeWords; k++)
-            x[k] = lds_ld32(in + pa + 4 + 4 * k) ^ lds_ld32(in + ca + 4 + 4 * k);
-        const uint32_t xb = lds_ld32(in + max(pa, 4u) - 4) ^ lds_ld32(in + max(ca, 4u) - 4);
+        // ---- the candidate's window: 4-byte verify, forward probe (MINMATCH + up
+        // to kProbe bytes) and backward probe (up to 4 bytes).  A candidate is a
+        // position <= mflimit, so the window stays inside the page's zero pad.
+        const Window cw = lds_window(A, cand + ib);
+        const bool ok = live & (cand < pos) & (cw.w0 == v);
         uint32_t n = 4u + kProbe;
 #pragma unroll
-        for (int k = (int)kProbeWords - 1; k >= 0; k--)
-            if (x[k]) n = 4u + 4u * (uint32_t)k + ((uint32_t)__builtin_ctz(x[k]) >> 3);
+        for (int k = (int)kProbeWords - 1; k >= 0; k--) {
+            const uint32_t x = pw.fw[k] ^ cw.fw[k];
+            if (x) n = 4u + 4u * (uint32_t)k + ((uint32_t)__builtin_ctz(x) >> 3);
+        }
+        const uint32_t xb = pw.back ^ cw.back;
         const uint32_t e = min(matchlimit, pos + kMinMatch + kProbe);
         n = min(n, e - pos);
         uint32_t len = (TYCHE_EABLATE & 2) ? 4u : n;
@@ -190,7 +228,7 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
             // the next match after the extended end
             const uint32_t mp = blk + li, mc = rdlane(cand, li), ln0 = rdlane(endp, li) - mp;
             PHASE(1);
-            const uint32_t ln = ln0 + wave_extend(in, mp + ln0, mc + ln0, matchlimit, lane);
+            const uint32_t ln = ln0 + wave_extend(in, A, ib, mp + ln0, mc + ln0, matchlimit, lane);
             PHASE(5);
             PHASE_COUNT();
             if (lane == li) len = ln;
