@@ -21,7 +21,7 @@ pages = codec.pagegen(n, plen)
 comp, clen = codec.compress_pages(pages)
 torch.cuda.synchronize()
 lib = _lib.load()
-buf = (ctypes.c_ulonglong * 8)()
+buf = (ctypes.c_ulonglong * 16)()
 assert lib.tyche_phase_read(buf) == 0, "tyche_phase_read failed"
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 e0.record()
@@ -34,5 +34,5 @@ names = ["block scan", "greedy walk", "record append", "sink/emit", "exit", "wav
 tot = sum(buf[i] for i in range(6))
 for i, nm in enumerate(names):
     print(f"{nm:14s} {buf[i] / npg:10.0f} cycles/page  {100.0 * buf[i] / tot:5.1f} %")
-print(f"extensions     {buf[6] / npg:10.1f} per page")
+print(f"extensions     {buf[6] / npg:10.1f} per page; blocks {buf[8] / npg:.1f}, with a match {buf[10] / npg:.1f}, matches {buf[9] / npg:.1f}")
 print(f"parse total    {tot / npg:10.0f} cycles/page; kernel {e0.elapsed_time(e1):.2f} ms for {n} pages; pages seen {npg}")

@@ -235,8 +235,8 @@ hipError_t launch_lz4_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream_
 #ifdef TYCHE_PHASES
 // profiling builds only: per-phase parse cycles summed since the last call (then cleared)
 extern "C" int tyche_phase_read(unsigned long long *out) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(lzp::g_phase), 8 * sizeof(unsigned long long)) != hipSuccess) return -1;
-    static const unsigned long long zero[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(lzp::g_phase), 16 * sizeof(unsigned long long)) != hipSuccess) return -1;
+    static const unsigned long long zero[16] = {};
     return hipMemcpyToSymbol(HIP_SYMBOL(lzp::g_phase), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
 }
 #endif

@@ -53,17 +53,17 @@ constexpr uint32_t kProbe = 4 * kProbeWords;
 // summed over pages into g_phase.  Only the LZ4 encoder's translation unit
 // (TYCHE_PHASES_OWNER) is instrumented.
 #if defined(TYCHE_PHASES) && defined(TYCHE_PHASES_OWNER)
-__device__ unsigned long long g_phase[8];
+__device__ unsigned long long g_phase[16];
 __device__ __forceinline__ uint32_t phase_clock() { return (uint32_t)__builtin_amdgcn_s_memtime(); }
-#define PHASE_INIT() uint32_t ph_t_ = phase_clock(), ph_[7] = {0, 0, 0, 0, 0, 0, 0}
+#define PHASE_INIT() uint32_t ph_t_ = phase_clock(), ph_[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}
 #define PHASE(i) do { const uint32_t t_ = phase_clock(); ph_[i] += t_ - ph_t_; ph_t_ = t_; } while (0)
-#define PHASE_COUNT() ph_[6]++
-#define PHASE_FLUSH() do { if (lane == 0) for (int i_ = 0; i_ < 7; i_++) atomicAdd(&g_phase[i_], (unsigned long long)ph_[i_]); \
+#define PHASE_COUNT(i) ph_[i]++
+#define PHASE_FLUSH() do { if (lane == 0) for (int i_ = 0; i_ < 12; i_++) if (i_ != 7) atomicAdd(&g_phase[i_], (unsigned long long)ph_[i_]); \
                            if (lane == 0) atomicAdd(&g_phase[7], 1ull); } while (0)
 #else
 #define PHASE_INIT() do {} while (0)
 #define PHASE(i) do {} while (0)
-#define PHASE_COUNT() do {} while (0)
+#define PHASE_COUNT(i) do {} while (0)
 #define PHASE_FLUSH() do {} while (0)
 #endif
 
@@ -202,9 +202,11 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
         // bit lies past mflimit, so a match ending there ends the walk.
         const uint64_t mall = (TYCHE_EABLATE & 4) ? 0ull : __ballot(ok);
         PHASE(0);
+        PHASE_COUNT(8);
         const uint32_t at = cursor > blk ? cursor - blk : 0u;
         const uint64_t rem = mall & (~0ull << at);
         if (rem == 0) continue;                                // no match starts at or after it
+        PHASE_COUNT(10);
         const uint32_t endp = pos + len;
         const uint32_t rl = endp - blk;
         const uint64_t after = rl < kWave ? mall & (~0ull << rl) : 0ull;
@@ -214,24 +216,26 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
         uint32_t li = (uint32_t)__builtin_ctzll(rem);
         uint32_t end;
         for (;;) {
-            sel |= 1ull << li;
-            const uint32_t nl = rdlane(nxt, li);
-            if (nl < kWave) {
-                li = nl;
-                continue;
-            }
-            if (nl == kWave) {
-                end = rdlane(endp, li);
+            // the hop loop proper: one v_readlane and one taken branch per match
+            uint32_t at_li;
+            do {
+                at_li = li;
+                sel |= 1ull << li;
+                PHASE_COUNT(9);
+                li = rdlane(nxt, li);
+            } while (li < kWave);
+            if (li == kWave) {
+                end = rdlane(endp, at_li);
                 break;
             }
             // reached the probe limit: extend with the whole wave, then look for
             // the next match after the extended end
-            const uint32_t mp = blk + li, mc = rdlane(cand, li), ln0 = rdlane(endp, li) - mp;
+            const uint32_t mp = blk + at_li, mc = rdlane(cand, at_li), ln0 = rdlane(endp, at_li) - mp;
             PHASE(1);
             const uint32_t ln = ln0 + wave_extend(in, A, ib, mp + ln0, mc + ln0, matchlimit, lane);
             PHASE(5);
-            PHASE_COUNT();
-            if (lane == li) len = ln;
+            PHASE_COUNT(6);
+            if (lane == at_li) len = ln;
             end = mp + ln;
             const uint32_t rel = end - blk;
             const uint64_t r = rel < kWave ? mall & (~0ull << rel) : 0ull;
