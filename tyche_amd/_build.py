@@ -19,12 +19,12 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 FLAGS = ["--offload-arch=" + ARCH, "-O3", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-variable",
          "-munsafe-fp-atomics", "-I" + os.path.join(HERE, "..", "include")]
-# The encoders read their pages as aligned dwords (lz_parse.h): LLVM's IR
+# The encoders and the zstd decoder read LDS as aligned dwords (lz_parse.h, ld64): LLVM's IR
 # load/store vectorizer would fuse neighbouring dwords into ds_read_b64/b128 at
 # 4-byte-aligned addresses, which the LDS replays at ~64 cycles per instruction.
 # Without it, pairs still become ds_read2_b32 (4-byte alignment suffices).
 NO_LSV = ["-mllvm", "-amdgpu-load-store-vectorizer=false"]
-SOURCE_FLAGS = {"lz4_encode.hip": NO_LSV, "zstd_encode.hip": NO_LSV, "zlib_deflate.hip": NO_LSV}
+SOURCE_FLAGS = {"lz4_encode.hip": NO_LSV, "zstd_encode.hip": NO_LSV, "zlib_deflate.hip": NO_LSV, "zstd_decode.hip": NO_LSV}
 
 
 def _newer(target: str, deps: list[str]) -> bool:

@@ -161,8 +161,15 @@ struct Work {
     uint8_t *w;          // 256 Huffman weights
 };
 
+// 8 bytes at any LDS byte address from three aligned dwords: an unaligned LDS
+// read is replayed at ~64 LDS cycles per wave instruction (this file builds
+// without the IR load/store vectorizer, so the dwords are not re-fused into a
+// misaligned ds_read_b96; _build.py)
 __device__ __forceinline__ uint64_t ld64(const uint8_t *p) {
-    return (uint64_t)lds_ld32(p) | ((uint64_t)lds_ld32(p + 4) << 32);
+    const uint32_t s = (uint32_t)(uintptr_t)p & 3u;
+    const uint32_t *A = (const uint32_t *)(p - s);
+    const uint32_t d0 = A[0], d1 = A[1], d2 = A[2];
+    return (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, s) | ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, s) << 32);
 }
 __device__ __forceinline__ uint32_t highbit(uint32_t v) { return 31u - (uint32_t)__builtin_clz(v); }
 
@@ -211,7 +218,8 @@ __device__ __forceinline__ bool bitd_init(BitD &b, const uint8_t *in, int32_t st
 // the whole reader (and every table index derived from it) lives in SGPRs and
 // constant-table lookups become scalar loads.
 __device__ __forceinline__ uint64_t ld64u(const uint8_t *p) {
-    return (uint64_t)rfl(lds_ld32(p)) | ((uint64_t)rfl(lds_ld32(p + 4)) << 32);
+    const uint64_t v = ld64(p);
+    return (uint64_t)rfl((uint32_t)v) | ((uint64_t)rfl((uint32_t)(v >> 32)) << 32);
 }
 __device__ __forceinline__ bool bitd_init_u(BitD &b, const uint8_t *in, int32_t start, int32_t n) {
     start = ru(start);
