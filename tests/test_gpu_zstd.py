@@ -20,6 +20,7 @@ incompressible pages; the encoder is deterministic.
 """
 import ctypes
 import hashlib
+import zlib
 
 import numpy as np
 import pytest
@@ -333,3 +334,107 @@ def test_encode_buffer_api(tc, oracle_mod):
     for i, b in enumerate(bufs):
         assert B.buffer_bytes(b) == pages[i].tobytes()
         B.destroy(b)
+
+
+# ----------------------------------------------------------------- Huffman literals (§8f rank 4)
+def _first_lit_type(frame):
+    """Literals_Block_Type of the first block (None for a raw/RLE block), RFC 8878 3.1.1."""
+    fhd = frame[4]
+    single, did, fcs_id = (fhd >> 5) & 1, fhd & 3, fhd >> 6
+    pos = 5 + (0 if single else 1) + (0, 1, 2, 4)[did] + ((1 if single else 0), 2, 4, 8)[fcs_id]
+    bh = frame[pos] | frame[pos + 1] << 8 | frame[pos + 2] << 16
+    if (bh >> 1) & 3 != 2:
+        return None
+    return frame[pos + 3] & 3
+
+
+@pytest.mark.parametrize("plen", [16384, 32768])
+def test_encode_huffman_literals_bench_pages(tc, oracle_mod, plen):
+    """Bench-distribution pages get Huffman-coded literals (Literals_Block_Type 2) and decode with the
+    reference; the ratio is well above the raw-literal encoder's ~2.9."""
+    O = oracle_mod
+    n = 64
+    pages = tc.pagegen(n, plen, seed=11, dist=0, device=DEV)
+    comp, clen = tc.compress_pages(pages, compressor_id=ZSTD)
+    out, rv = tc.decompress_pages(comp, clen, plen, compressor_id=ZSTD)
+    torch.cuda.synchronize()
+    assert torch.equal(out, pages) and bool((rv == plen).all())
+    total = _check_frames(O, comp, clen, pages.cpu().numpy(), plen)
+    ch, lh = comp.cpu().numpy(), clen.cpu().numpy()
+    types = [_first_lit_type(ch[i, :lh[i]].tobytes()) for i in range(n)]
+    assert types.count(2) == n, types
+    assert n * plen / total > 3.1
+
+
+def _literal_heavy_page(rng, plen, draw):
+    """Half the bytes drawn from `draw` (literals), half 8-byte copies of earlier bytes (matches)."""
+    out = bytearray()
+    while len(out) < plen:
+        if len(out) > 64 and rng.random() < 0.5:
+            p = int(rng.integers(0, len(out) - 8))
+            out += out[p:p + 8]
+        else:
+            out += bytes(draw(int(rng.integers(1, 12))))
+    return np.frombuffer(bytes(out[:plen]), np.uint8)
+
+
+@pytest.mark.parametrize("alphabet", ["two", "16", "100", "256", "geo0.9", "geo0.97", "skew99"])
+@pytest.mark.parametrize("plen", [4096, 16384, 32768])
+def test_encode_huffman_literal_alphabets(tc, oracle_mod, alphabet, plen):
+    """Literal alphabets from 2 symbols to all 256 with heavy skew (lengths hit the 11-bit limit,
+    weights need the FSE header or fit raw nibbles): every frame decodes with the reference, the
+    restatement and the device decoder."""
+    O = oracle_mod
+    rng = np.random.default_rng(zlib.crc32(f"{alphabet}:{plen}".encode()))
+    if alphabet == "two":
+        draw = lambda k: rng.choice(np.array([65, 200], np.uint8), k)
+    elif alphabet in ("16", "100", "256"):
+        m = int(alphabet)
+        draw = lambda k: rng.integers(256 - m, 256, k, dtype=np.uint8)
+    elif alphabet.startswith("geo"):
+        q = float(alphabet[3:])
+        p = q ** np.arange(256)
+        p /= p.sum()
+        draw = lambda k: rng.choice(256, k, p=p).astype(np.uint8)
+    else:
+        draw = lambda k: np.where(rng.random(k) < 0.99, 7, rng.integers(0, 256, k)).astype(np.uint8)
+    host = np.stack([_literal_heavy_page(rng, plen, draw) for _ in range(8)])
+    d = torch.from_numpy(host).to(DEV)
+    comp, clen = tc.compress_pages(d, compressor_id=ZSTD)
+    out, rv = tc.decompress_pages(comp, clen, plen, compressor_id=ZSTD)
+    torch.cuda.synchronize()
+    assert bool((rv == plen).all()) and torch.equal(out, d)
+    _check_frames(O, comp, clen, host, plen)
+
+
+@pytest.mark.parametrize("slack", [0, 16, 200, 2000])
+def test_encode_tight_capacity(tc, oracle_mod, slack):
+    """Output capacity just above the frame size: the literal scratch at the buffer's tail no longer
+    fits, so blocks fall back to raw literals (or the page reports 'does not fit', 0); whatever is
+    returned decodes with the reference."""
+    from tyche_amd import _lib
+    import ctypes
+    O = oracle_mod
+    plen, n = 16384, 16
+    pages = tc.pagegen(n, plen, seed=21, dist=0, device=DEV)
+    comp, clen = tc.compress_pages(pages, compressor_id=ZSTD)
+    torch.cuda.synchronize()
+    cap = int(clen.max()) + slack
+    slot = tc.slot_size(plen, ZSTD)
+    comp2 = torch.zeros((n, slot), dtype=torch.uint8, device=DEV)
+    clen2 = torch.zeros(n, dtype=torch.int32, device=DEV)
+    b = _lib.Batch(count=n, src=pages.data_ptr(), src_stride=plen, src_length=plen, max_src_length=plen,
+                   dst=comp2.data_ptr(), dst_stride=slot, dst_capacity=cap, results=clen2.data_ptr())
+    _lib.check(_lib.load().tyche_compress_batch(ZSTD, 1, ctypes.byref(b), torch.cuda.current_stream().cuda_stream),
+               "compress")
+    torch.cuda.synchronize()
+    ch, lh, host = comp2.cpu().numpy(), clen2.cpu().numpy(), pages.cpu().numpy()
+    for i in range(n):
+        assert 0 <= lh[i] <= cap
+        if lh[i] == 0:
+            continue
+        r, dec = O.zstd_decompress(ch[i, :lh[i]].tobytes(), plen)
+        assert r == plen and dec == host[i].tobytes()
+        if O.have_ref():
+            r2, dec2 = O.ref_zstd_decompress(ch[i, :lh[i]].tobytes(), plen)
+            assert r2 == plen and dec2 == host[i].tobytes()

@@ -33,6 +33,7 @@
 
 #include "engine.h"
 #include "lds_io.h"
+#include "huf_enc.h"
 #include "lz_parse.h"
 
 namespace tyche {
@@ -199,8 +200,200 @@ struct Enc {
     uint32_t bstart;     // first page byte of the current block
     uint32_t cursor;     // end of the last buffered sequence's match
     uint8_t *map;        // 64-byte owner map
+    uint32_t *htab;      // 256 entries: literal histogram, then Huffman code | length << 16
+    uint8_t *wts;        // 256 Huffman weights
+    uint32_t *stage;     // 128 dwords of pending stream bits (the parse's record area, free here)
     bool fail;
 };
+
+// Calls f(j, byte) for every literal j of the block (literal-section order),
+// 64 per step: literal j belongs to the last run starting at or before it
+// (sequences 0..n-1, then the trailing literals as run n).
+template <typename F>
+__device__ void for_each_literal(const Enc &e, uint32_t n, uint32_t trail, uint32_t lane, F &&f) {
+    uint32_t lo = 0, pstart = e.bstart;   // literal-section offset / page position of this group
+    for (uint32_t g = 0; g <= n; g += kWave) {
+        const uint32_t i = g + lane;
+        uint32_t ll = 0, ml = 0;
+        if (i < n) {
+            const uint2 r = e.seq[i];
+            ll = r.x & 0xFFFFu;
+            ml = r.y;
+        } else if (i == n) {
+            ll = trail;
+        }
+        const bool run = i <= n;
+        const int32_t li = wave_incl_sum((int32_t)ll), si = wave_incl_sum((int32_t)(ll + ml));
+        const uint32_t rlo = lo + (uint32_t)li - ll;                   // run start in the literal section
+        const uint32_t rsrc = pstart + (uint32_t)si - (ll + ml);       // run start in the page
+        const uint32_t glen = rdlane((uint32_t)li, kWave - 1);
+        for (uint32_t j0 = 0; j0 < glen; j0 += kWave) {
+            const uint32_t j = lo + j0 + lane;
+            const uint64_t before = __ballot(run && ll && rlo <= lo + j0);
+            const int32_t owner0 = before ? 63 - (int32_t)__builtin_clzll(before) : 0;
+            e.map[lane] = 0xFF;
+            __builtin_amdgcn_wave_barrier();
+            if (run && ll && rlo > lo + j0 && rlo < lo + j0 + kWave) e.map[rlo - lo - j0] = (uint8_t)lane;
+            __builtin_amdgcn_wave_barrier();
+            const uint32_t mv = e.map[lane];
+            const uint32_t owner = (uint32_t)max(wave_incl_max(mv == 0xFF ? -1 : (int32_t)mv), owner0);
+            const uint32_t orlo = __shfl(rlo, owner), orsrc = __shfl(rsrc, owner);
+            if (j0 + lane < glen) f(j, (uint32_t)e.in[orsrc + (j - orlo)]);
+            __builtin_amdgcn_wave_barrier();
+        }
+        lo += glen;
+        pstart += rdlane((uint32_t)si, kWave - 1);
+    }
+}
+
+constexpr uint32_t kHufMinLit = 64;      // fewer literals stay raw (ZSTD_compressLiterals' minimum is 63)
+constexpr uint32_t kHufMaxBits = 11;     // HUF_TABLELOG_DEFAULT
+
+// Huffman-compressed literals section (ZSTD_compressLiterals, zstd_compress.c:459-514,
+// with HUF_compress4X / 1X_usingCTable): the literals are first scattered to
+// the tail of the output buffer as scratch while an LDS histogram is built;
+// after the code is chosen the streams are written at o, below the scratch.
+// Returns the section size, or 0 when raw literals are to be used instead.
+__device__ uint32_t huf_literals(Enc &e, uint32_t n, uint32_t trail, uint32_t lit_total, uint32_t o, uint32_t lane) {
+    const uint32_t lh = 3u + (lit_total >= 1024u) + (lit_total >= 16384u);
+    const bool single = lit_total < 256u;
+    if (e.cap < lit_total || e.cap - lit_total < o + lh + 272u) return 0;   // room for header + weights below the scratch
+    const uint32_t scr = e.cap - lit_total;
+    // ---- pass 1: scatter to scratch, histogram
+    for (uint32_t k = lane; k < 256u; k += kWave) e.htab[k] = 0;
+    __builtin_amdgcn_wave_barrier();
+    uint8_t *dst = e.dst;
+    uint32_t *hist = e.htab;
+    for_each_literal(e, n, trail, lane, [&](uint32_t j, uint32_t v) {
+        dst[scr + j] = (uint8_t)v;
+        atomicAdd(&hist[v], 1u);
+    });
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");   // scratch stores visible, L1 invalidated
+    __builtin_amdgcn_wave_barrier();
+    uint32_t c[4], l[4], code[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) c[j] = e.htab[lane + 64u * j];
+    const uint32_t maxlen = huf::code_lengths(c, lit_total, kHufMaxBits, l, lane);
+    if (maxlen == 0) {
+        // a single distinct byte: RLE literals (set_rle)
+        const uint32_t fl = 1u + (lit_total > 31u) + (lit_total > 4095u);
+        uint32_t h;
+        if (fl == 1u) h = 1u | (lit_total << 3);
+        else if (fl == 2u) h = 1u | (1u << 2) | (lit_total << 4);
+        else h = 1u | (3u << 2) | (lit_total << 4);
+        int32_t sym = -1;
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+            if (c[j]) sym = (int32_t)(lane + 64u * j);
+        sym = huf::wave_max(sym);
+        if (lane < fl) e.dst[o + lane] = (uint8_t)(h >> (8u * lane));
+        if (lane == 0) e.dst[o + fl] = (uint8_t)sym;
+        return fl + 1u;
+    }
+    int32_t msv = -1;
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+        if (c[j]) msv = (int32_t)(lane + 64u * j);
+    const uint32_t max_sv = (uint32_t)huf::wave_max(msv);
+    // ---- weights of symbols 0..max_sv-1 (the last one is implied), HUF_writeCTable
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const uint32_t sv = lane + 64u * j;
+        e.wts[sv] = (uint8_t)(l[j] ? maxlen + 1u - l[j] : 0u);
+    }
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t wpos = o + lh;
+    uint32_t whdr;
+    const uint32_t hs = huf::compress_weights(e.wts, max_sv, e.dst, wpos + 1u, lane);
+    if (hs > 1u && hs < 128u) {
+        if (lane == 0) e.dst[wpos] = (uint8_t)hs;
+        whdr = hs + 1u;
+    } else if (max_sv <= 128u) {
+        // raw 4-bit weights
+        if (lane == 0) e.dst[wpos] = (uint8_t)(127u + max_sv);
+        for (uint32_t k = lane; 2u * k < max_sv; k += kWave) {
+            const uint32_t a = e.wts[2u * k], b = 2u * k + 1u < max_sv ? e.wts[2u * k + 1u] : 0u;
+            e.dst[wpos + 1u + k] = (uint8_t)((a << 4) | b);
+        }
+        whdr = (max_sv + 1u) / 2u + 1u;
+    } else {
+        return 0;
+    }
+    // ---- size check against the raw form and the scratch
+    uint32_t bits = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) bits += c[j] * l[j];
+    const uint32_t total_bits = huf::wave_sum(bits);
+    const uint32_t nst = single ? 1u : 4u;
+    const uint32_t bound = whdr + (single ? 0u : 6u) + total_bits / 8u + 2u * nst;
+    const uint32_t min_gain = (lit_total >> 6) + 2u;
+    if (bound + min_gain >= lit_total || o + lh + bound > scr) return 0;
+    // ---- codes: htab[s] = code | length << 16
+    huf::canonical_codes(l, maxlen, code, lane);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int j = 0; j < 4; j++) e.htab[lane + 64u * j] = code[j] | (l[j] << 16);
+    __builtin_amdgcn_wave_barrier();
+    // ---- streams: symbols last to first, bits LSB first (HUF_compress1X_usingCTable), end mark
+    uint32_t sp = wpos + whdr + (single ? 0u : 6u);
+    const uint32_t seg = (lit_total + 3u) / 4u;
+    for (uint32_t st = 0; st < nst; st++) {
+        const uint32_t a = single ? 0u : st * seg;
+        const uint32_t bnd = single ? lit_total : (st == 3u ? lit_total : min(lit_total, (st + 1u) * seg));
+        const uint32_t s0 = sp;
+        uint32_t nbits = 0;
+        for (uint32_t k = lane; k < 128u; k += kWave) e.stage[k] = 0;
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t k0 = 0; a + k0 < bnd; k0 += kWave) {
+            const bool act = a + k0 + lane < bnd;
+            uint32_t ent = 0;
+            if (act) ent = e.htab[e.dst[scr + bnd - 1u - (k0 + lane)]];
+            const uint32_t len = ent >> 16, cv = ent & 0xFFFFu;
+            const int32_t bi = wave_incl_sum((int32_t)len);
+            const uint32_t b = nbits + (uint32_t)bi - len;
+            if (len) {
+                const uint32_t w = b >> 5, sh = b & 31u;
+                atomicOr(&e.stage[w], cv << sh);
+                if (sh + len > 32u) atomicOr(&e.stage[w + 1u], cv >> (32u - sh));
+            }
+            __builtin_amdgcn_wave_barrier();
+            nbits += rdlane((uint32_t)bi, kWave - 1);
+            // drain the complete bytes, keep the partial one in word 0
+            const uint32_t nb = nbits >> 3;
+            const uint8_t *sb = (const uint8_t *)e.stage;
+            for (uint32_t j = lane; j < nb; j += kWave) e.dst[sp + j] = sb[j];
+            const uint32_t part = (nbits & 7u) ? (uint32_t)sb[nb] : 0u;
+            __builtin_amdgcn_wave_barrier();
+            const uint32_t used = (nbits + 31u) >> 5;
+            for (uint32_t w = lane; w <= used && w < 128u; w += kWave) e.stage[w] = w == 0 ? part : 0u;
+            __builtin_amdgcn_wave_barrier();
+            sp += nb;
+            nbits &= 7u;
+        }
+        // BIT_closeCStream: end mark, last partial byte
+        const uint32_t last = (e.stage[0] & ((1u << nbits) - 1u)) | (1u << nbits);
+        if (lane == 0) e.dst[sp] = (uint8_t)last;
+        sp += 1u;
+        if (!single && st < 3u) {
+            const uint32_t ssz = sp - s0;
+            if (lane < 2) e.dst[wpos + whdr + 2u * st + lane] = (uint8_t)(ssz >> (8u * lane));
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    const uint32_t clit = sp - (o + lh);
+    // ---- literals section header (set_compressed)
+    if (lh == 3u) {
+        const uint32_t h = 2u | ((single ? 0u : 1u) << 2) | (lit_total << 4) | (clit << 14);
+        if (lane < 3) e.dst[o + lane] = (uint8_t)(h >> (8u * lane));
+    } else if (lh == 4u) {
+        const uint32_t h = 2u | (2u << 2) | (lit_total << 4) | (clit << 18);
+        if (lane < 4) e.dst[o + lane] = (uint8_t)(h >> (8u * lane));
+    } else {
+        const uint64_t h = 2ull | (3ull << 2) | ((uint64_t)lit_total << 4) | ((uint64_t)clit << 22);
+        if (lane < 5) e.dst[o + lane] = (uint8_t)(h >> (8u * lane));
+    }
+    return sp - o;
+}
 
 // Writes one block covering page bytes [s.bstart, bend) with the buffered
 // sequences; `last` sets Last_Block.  Returns false if it does not fit.
@@ -241,53 +434,20 @@ __device__ bool emit_block(Enc &e, uint32_t bend, bool last, uint32_t lane) {
     }
     if (e.op + 3u + comp_bound > e.cap) return false;
     uint32_t o = hdr + 3u;
-    // ---- literals section header (ZSTD_noCompressLiterals)
-    {
+    // ---- literals section: Huffman-compressed when it pays, else raw (ZSTD_noCompressLiterals)
+    uint32_t lsec = lit_total >= kHufMinLit ? huf_literals(e, n, trail, lit_total, o, lane) : 0u;
+    if (lsec == 0) {
         uint32_t h;
         if (fl == 1u) h = lit_total << 3;
         else if (fl == 2u) h = (1u << 2) | (lit_total << 4);
         else h = (3u << 2) | (lit_total << 4);
         if (lane < fl) e.dst[o + lane] = (uint8_t)(h >> (8u * lane));
-        o += fl;
+        uint8_t *dst = e.dst;
+        const uint32_t lo0 = o + fl;
+        for_each_literal(e, n, trail, lane, [&](uint32_t j, uint32_t v) { dst[lo0 + j] = (uint8_t)v; });
+        lsec = fl + lit_total;
     }
-    // ---- literal bytes, 64 per store: output byte j belongs to the last run starting at or before j
-    {
-        uint32_t lo = 0, pstart = e.bstart;   // literal-section offset / page position of this group
-        for (uint32_t g = 0; g <= n; g += kWave) {
-            const uint32_t i = g + lane;
-            // runs: sequences g..g+63, plus the trailing literals as run n
-            uint32_t ll = 0, ml = 0;
-            if (i < n) {
-                const uint2 r = e.seq[i];
-                ll = r.x & 0xFFFFu;
-                ml = r.y;
-            } else if (i == n) {
-                ll = trail;
-            }
-            const bool run = i <= n;
-            const int32_t li = wave_incl_sum((int32_t)ll), si = wave_incl_sum((int32_t)(ll + ml));
-            const uint32_t rlo = lo + (uint32_t)li - ll;                   // run start in the literal section
-            const uint32_t rsrc = pstart + (uint32_t)si - (ll + ml);       // run start in the page
-            const uint32_t glen = rdlane((uint32_t)li, kWave - 1);
-            for (uint32_t j0 = 0; j0 < glen; j0 += kWave) {
-                const uint32_t j = lo + j0 + lane;
-                const uint64_t before = __ballot(run && ll && rlo <= lo + j0);
-                const int32_t owner0 = before ? 63 - (int32_t)__builtin_clzll(before) : 0;
-                e.map[lane] = 0xFF;
-                __builtin_amdgcn_wave_barrier();
-                if (run && ll && rlo > lo + j0 && rlo < lo + j0 + kWave) e.map[rlo - lo - j0] = (uint8_t)lane;
-                __builtin_amdgcn_wave_barrier();
-                const uint32_t mv = e.map[lane];
-                const uint32_t owner = (uint32_t)max(wave_incl_max(mv == 0xFF ? -1 : (int32_t)mv), owner0);
-                const uint32_t orlo = __shfl(rlo, owner), orsrc = __shfl(rsrc, owner);
-                if (j0 + lane < glen) e.dst[o + j] = e.in[orsrc + (j - orlo)];
-                __builtin_amdgcn_wave_barrier();
-            }
-            lo += glen;
-            pstart += rdlane((uint32_t)si, kWave - 1);
-        }
-        o += lit_total;
-    }
+    o += lsec;
     // ---- sequences section header
     if (lane < nsh) {
         uint32_t h;
@@ -365,7 +525,7 @@ __device__ bool emit_block(Enc &e, uint32_t bend, bool last, uint32_t lane) {
 // Encodes one page held in LDS (in[0, L), 64 zero bytes after).  Returns the
 // frame size, or 0 if it does not fit in cap.
 __device__ int32_t encode_page(const uint8_t *in, uint32_t L, uint16_t *table, uint8_t *map, uint2 *rec, uint2 *seq,
-                               uint8_t *dst, uint32_t cap, uint32_t lane) {
+                               uint32_t *htab, uint8_t *wts, uint8_t *dst, uint32_t cap, uint32_t lane) {
     // ---- frame header: magic, single-segment descriptor with the content size
     const uint32_t fcs_id = L < 256u ? 0u : (L < 65536u + 256u ? 1u : 2u);
     const uint32_t fcs_len = fcs_id == 0u ? 1u : (fcs_id == 1u ? 2u : 4u);
@@ -389,6 +549,9 @@ __device__ int32_t encode_page(const uint8_t *in, uint32_t L, uint16_t *table, u
     e.bstart = 0;
     e.cursor = 0;
     e.map = map;
+    e.htab = htab;
+    e.wts = wts;
+    e.stage = (uint32_t *)rec;
     e.fail = false;
     auto sink = [&](const uint2 *r, uint32_t n, uint32_t anchor) -> bool {
         uint32_t ls, ll, ml, off;
@@ -418,7 +581,9 @@ __global__ __launch_bounds__(64) void zstd_encode_kernel(tyche_batch_t b, uint32
     uint8_t *map = smem + kHashSize * sizeof(uint16_t);                 // 64-byte owner map
     uint2 *rec = (uint2 *)(map + kWave);                               // 64 parse records
     uint2 *seq = rec + kWave;                                          // kSeqCap block sequences
-    uint8_t *stage = (uint8_t *)(seq + kSeqCap);
+    uint32_t *htab = (uint32_t *)(seq + kSeqCap);                      // literal histogram / Huffman codes
+    uint8_t *wts = (uint8_t *)(htab + 256);                            // Huffman weights
+    uint8_t *stage = wts + 256;
     const size_t stride = gridDim.x;
 
     size_t page = blockIdx.x;
@@ -453,7 +618,7 @@ __global__ __launch_bounds__(64) void zstd_encode_kernel(tyche_batch_t b, uint32
             WAVE_SYNC();
             in[p.src_len + lane] = 0;
             WAVE_SYNC();
-            rv = encode_page(in, p.src_len, table, map, rec, seq, p.dst, p.dst_cap, lane);
+            rv = encode_page(in, p.src_len, table, map, rec, seq, htab, wts, p.dst, p.dst_cap, lane);
         }
         if (lane == 0) b.results[page] = rv;
         if (next >= b.count) break;
@@ -479,7 +644,7 @@ __global__ __launch_bounds__(64) void zstd_encode_kernel(tyche_batch_t b, uint32
 hipError_t launch_zstd_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream_t s) {
     if (b.count == 0) return hipSuccess;
     if (in_cap > 65535u) return hipErrorInvalidValue;    // 16-bit positions in the parse and sequence records
-    const size_t lds = kHashSize * sizeof(uint16_t) + kWave + kWave * 8 + kSeqCap * 8 +
+    const size_t lds = kHashSize * sizeof(uint16_t) + kWave + kWave * 8 + kSeqCap * 8 + 256 * 4 + 256 +
                        ((in_cap + 16u + kPad + 15u) & ~15u);
     int dev = 0;
     (void)hipGetDevice(&dev);
