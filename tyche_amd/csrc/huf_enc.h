@@ -166,22 +166,31 @@ struct SmallCT {
     uint32_t log;
 };
 
-// FSE_buildCTable_wksp (fse_compress.c) for norm[] (no -1 entries), log <= 6.
+// FSE_buildCTable_wksp (fse_compress.c) for norm[], log <= 6; -1 entries
+// (low-probability symbols) take one cell each at the top of the table.
 // norm_l: lane s holds norm[s] (0 beyond max_sv).
 __device__ SmallCT build_small_ct(int32_t norm_l, uint32_t max_sv, uint32_t log, uint32_t lane) {
     const uint32_t size = 1u << log, mask = size - 1u, step = (size >> 1) + (size >> 3) + 3u;
-    // spread symbols (uniform serial walk); lane u ends up with tableSymbol[u]
-    uint32_t tsym = 0, pos = 0;
+    // low-probability cells from the top, then the spread (uniform serial walk);
+    // lane u ends up with tableSymbol[u]
+    uint32_t tsym = 0, pos = 0, high = size - 1u;
+    for (uint32_t s = 0; s <= max_sv; s++)
+        if ((int32_t)rdlane((uint32_t)norm_l, s) == -1) {
+            if (lane == high) tsym = s;
+            high--;
+        }
     for (uint32_t s = 0; s <= max_sv; s++) {
         const int32_t n = (int32_t)rdlane((uint32_t)norm_l, s);
         for (int32_t i = 0; i < n; i++) {
             if (lane == pos) tsym = s;
             pos = (pos + step) & mask;
+            while (pos > high) pos = (pos + step) & mask;
         }
     }
-    // cumul of norm (exclusive), per symbol, in lanes
-    const int32_t incl = wave_incl_sum(lane <= max_sv ? norm_l : 0);
-    const uint32_t cum_l = (uint32_t)(incl - (lane <= max_sv ? norm_l : 0));
+    // cumul of norm (exclusive, -1 counting as 1), per symbol, in lanes
+    const int32_t cells = lane <= max_sv ? (norm_l == -1 ? 1 : norm_l) : 0;
+    const int32_t incl = wave_incl_sum(cells);
+    const uint32_t cum_l = (uint32_t)(incl - cells);
     // stateTable[cumul[s] + rank of u among cells of s] = size + u
     const uint64_t lt = lane ? (~0ull >> (64u - lane)) : 0ull;
     uint32_t idx = lane;   // lanes past the table permute onto themselves
@@ -196,8 +205,8 @@ __device__ SmallCT build_small_ct(int32_t norm_l, uint32_t max_sv, uint32_t log,
     // symbol transforms
     t.dnb = 0;
     t.dfs = 0;
-    if (lane <= max_sv && norm_l > 0) {
-        if (norm_l == 1) {
+    if (lane <= max_sv && norm_l != 0) {
+        if (norm_l == 1 || norm_l == -1) {
             t.dnb = (log << 16) - (1u << log);
             t.dfs = (int32_t)cum_l - 1;
         } else {
@@ -279,6 +288,30 @@ __device__ uint32_t write_ncount(int32_t norm_l, uint32_t max_sv, uint32_t log, 
     return out - o;
 }
 
+// Normalized counts for an FSE table of 2^log cells (FSE_normalizeCount's
+// contract, simpler rounding): lane s holds count cnt of `total`; each used
+// symbol gets >= 1 cell, the rest is proportional, and the rounding remainder
+// goes to (or is taken from) the largest entries.  At most 64 symbols, and no
+// more used symbols than cells.  Returns false only on a logic error.
+__device__ bool normalize(uint32_t cnt, uint32_t total, uint32_t log, int32_t &norm, uint32_t lane) {
+    const uint32_t size = 1u << log;
+    norm = cnt ? max(1, (int32_t)(((uint64_t)cnt * size + total / 2u) / total)) : 0;
+    int32_t diff = (int32_t)size - (int32_t)wave_sum((uint32_t)norm);
+    for (uint32_t it = 0; diff != 0; it++) {
+        if (it >= 64u) return false;
+        // give to / take from the symbol with the largest normalized count (> 1 when taking)
+        const int32_t key = (norm > (diff < 0 ? 1 : 0)) ? (norm << 8) | (int32_t)lane : -1;
+        const int32_t bk = wave_max(key);
+        if (bk < 0) return false;
+        const uint32_t s = (uint32_t)bk & 255u;
+        const int32_t have = (int32_t)rdlane((uint32_t)norm, s);
+        const int32_t d = diff > 0 ? diff : max(diff, 1 - have);
+        if (lane == s) norm += d;
+        diff -= d;
+    }
+    return true;
+}
+
 // HUF_compressWeights (huf_compress.c, 1.1.2): FSE table log 6 at most,
 // FSE_optimalTableLog, normalized counts, NCount header, two interleaved states
 // (FSE_compress_usingCTable_generic).  w[0, n) are the weights (LDS bytes,
@@ -308,21 +341,8 @@ __device__ uint32_t compress_weights(const uint8_t *w, uint32_t n, uint8_t *dst,
     if (max_bits_src < log) log = max_bits_src;
     if (min_bits > log) log = min_bits;
     log = min(max(log, 5u), 12u);
-    // normalize: proportional, each used symbol >= 1, the remainder to the largest
-    const uint32_t size = 1u << log;
-    int32_t norm = 0;
-    if (lane <= max_sv && cnt) norm = max(1, (int32_t)(((uint64_t)cnt * size + n / 2u) / n));
-    int32_t diff = (int32_t)size - (int32_t)wave_sum((uint32_t)norm);
-    for (uint32_t it = 0; diff != 0; it++) {
-        if (it >= 64u) return 0;
-        // give to / take from the symbol with the largest normalized count (> 1 when taking)
-        const int32_t key = (norm > (diff < 0 ? 1 : 0)) ? (norm << 8) | (int32_t)lane : -1;
-        const uint32_t s = (uint32_t)wave_max(key) & 255u;
-        const int32_t have = (int32_t)rdlane((uint32_t)norm, s);
-        const int32_t d = diff > 0 ? diff : max(diff, 1 - have);
-        if (lane == s) norm += d;
-        diff -= d;
-    }
+    int32_t norm;
+    if (!normalize(cnt, n, log, norm, lane)) return 0;
     uint32_t op = o + write_ncount(norm, max_sv, log, dst, o, lane);
     const SmallCT t = build_small_ct(norm, max_sv, log, lane);
     // FSE_compress_usingCTable_generic, 64-bit container (4 symbols per flush)

@@ -110,6 +110,12 @@ constexpr CTab make_ctab(const int16_t *norm, uint32_t max_sv, uint32_t log) {
     return t;
 }
 
+__device__ __constant__ int16_t c_ll_norm[36] = {4, 3, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 1, 1, 1, 2, 2, 2, 2, 2, 2, 2, 2,
+                                                 2, 3, 2, 1, 1, 1, 1, 1, -1, -1, -1, -1};
+__device__ __constant__ int16_t c_ml_norm[53] = {1, 4, 3, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1,
+                                                 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1, -1, -1};
+__device__ __constant__ int16_t c_of_norm[29] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1,
+                                                 -1, -1};
 __device__ __constant__ CTab c_ll_ct = make_ctab(kLLNorm, 35, 6);
 __device__ __constant__ CTab c_ml_ct = make_ctab(kMLNorm, 52, 6);
 __device__ __constant__ CTab c_of_ct = make_ctab(kOFNorm, 28, 5);
@@ -123,9 +129,9 @@ struct SeqCode {
     uint32_t llv, mlv, ofv;          // extra-bit values (masked by BIT_addBits)
     uint32_t llb, mlb;               // extra-bit counts (ofc for offsets)
 };
-__device__ __forceinline__ SeqCode seq_code(uint32_t ll, uint32_t ml, uint32_t off) {
+__device__ __forceinline__ SeqCode seq_code(uint32_t ll, uint32_t ml, uint32_t ofcode) {
     SeqCode c;
-    const uint32_t m = ml - 3u, ofcode = off + 3u;
+    const uint32_t m = ml - 3u;
     if (ll < 16u) {
         c.llc = ll;
         c.llb = 0;
@@ -203,8 +209,21 @@ struct Enc {
     uint32_t *htab;      // 256 entries: literal histogram, then Huffman code | length << 16
     uint8_t *wts;        // 256 Huffman weights
     uint32_t *stage;     // 128 dwords of pending stream bits (the parse's record area, free here)
+    uint32_t rep;        // repeat offset 1 of the frame so far (initial {1, 4, 8}, zstd_internal.h:73)
     bool fail;
 };
+
+// Codes of sequence i of the block.  Only repeat offset 1 is used, and only
+// with a nonzero literal length (Offset_Value 1, history unchanged); any other
+// offset is sent as Offset_Value = offset + 3 and becomes repeat offset 1.  So
+// repeat offset 1 before sequence i is always the previous sequence's offset
+// (or the frame's, across blocks) and the choice is lane-parallel.
+__device__ __forceinline__ SeqCode seq_code_at(const Enc &e, uint32_t i) {
+    const uint2 r = e.seq[i];
+    const uint32_t ll = r.x & 0xFFFFu, off = r.x >> 16;
+    const uint32_t prev = i ? (e.seq[i - 1].x >> 16) : e.rep;
+    return seq_code(ll, r.y, (ll > 0u && off == prev) ? 1u : off + 3u);
+}
 
 // Calls f(j, byte) for every literal j of the block (literal-section order),
 // 64 per step: literal j belongs to the last run starting at or before it
@@ -397,7 +416,7 @@ __device__ uint32_t huf_literals(Enc &e, uint32_t n, uint32_t trail, uint32_t li
 
 // Writes one block covering page bytes [s.bstart, bend) with the buffered
 // sequences; `last` sets Last_Block.  Returns false if it does not fit.
-__device__ bool emit_block(Enc &e, uint32_t bend, bool last, uint32_t lane) {
+__device__ __forceinline__ bool emit_block(Enc &e, uint32_t bend, bool last, uint32_t lane) {
     const uint32_t n = e.nseq, blen = bend - e.bstart;
     // ---- per-sequence sizes (lane-parallel over 64-sequence groups)
     uint32_t lit_sum = 0, span = 0, xbits = 0;
@@ -408,7 +427,7 @@ __device__ bool emit_block(Enc &e, uint32_t bend, bool last, uint32_t lane) {
             const uint2 r = e.seq[i];
             ll = r.x & 0xFFFFu;
             ml = r.y;
-            const SeqCode c = seq_code(ll, ml, r.x >> 16);
+            const SeqCode c = seq_code(ll, ml, (r.x >> 16) + 3u);   // bound: no repeat offsets
             xb = c.llb + c.mlb + c.ofc;
         }
         lit_sum += rdlane((uint32_t)wave_incl_sum((int32_t)ll), kWave - 1);
@@ -421,7 +440,7 @@ __device__ bool emit_block(Enc &e, uint32_t bend, bool last, uint32_t lane) {
     const uint32_t nsh = n < 0x7Fu ? 1u : (n < 0x7F00u ? 2u : 3u);
     // upper bound of the FSE bitstream: every state emits at most its table log
     const uint32_t fse_bound = n ? (n * 17u + xbits + 17u + 8u + 7u) / 8u + 1u : 0u;
-    const uint32_t comp_bound = fl + lit_total + nsh + (n ? 1u : 0u) + fse_bound;
+    const uint32_t comp_bound = fl + lit_total + nsh + (n ? 1u + 3u * 48u : 0u) + fse_bound;   // + NCount headers
     const uint32_t hdr = e.op;                              // block header position
     if (comp_bound >= blen) {
         // ---- raw block (Block_Type 0): header + the page bytes
@@ -458,23 +477,66 @@ __device__ bool emit_block(Enc &e, uint32_t bend, bool last, uint32_t lane) {
     }
     o += nsh;
     if (n) {
-        if (lane == 0) e.dst[o] = 0;   // LL, OF, ML: predefined distributions (set_basic)
-        o += 1;
+        // ---- code histograms (htab is free once the literals are out): LL at 0, ML at 64, OF at 128
+        for (uint32_t k = lane; k < 192u; k += kWave) e.htab[k] = 0;
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t g = 0; g < n; g += kWave) {
+            if (g + lane < n) {
+                const SeqCode c = seq_code_at(e, g + lane);
+                atomicAdd(&e.htab[c.llc], 1u);
+                atomicAdd(&e.htab[64u + c.mlc], 1u);
+                atomicAdd(&e.htab[128u + c.ofc], 1u);
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        // ---- tables: per-block distributions at the predefined accuracy (LL 6, OF 5,
+        // ML 6 -- one cell per lane) from 64 sequences on (MIN_SEQ_FOR_DYNAMIC_FSE),
+        // the predefined ones below (ZSTD_compressSequences, zstd_compress.c:595-660);
+        // NCount headers follow the mode byte in LL, OF, ML order
+        const uint32_t mpos = o;
+        o += 1u;
+        const bool dyn = n >= 64u;
+        huf::SmallCT tll, tof, tml;
+        {
+            int32_t nll, nof, nml;
+            uint32_t mll, mof, mml;
+            if (dyn) {
+                const uint32_t cll = e.htab[lane], cml = e.htab[64u + lane], cof = lane < 32u ? e.htab[128u + lane] : 0u;
+                mll = (uint32_t)huf::wave_max(cll ? (int32_t)lane : -1);
+                mml = (uint32_t)huf::wave_max(cml ? (int32_t)lane : -1);
+                mof = (uint32_t)huf::wave_max(cof ? (int32_t)lane : -1);
+                if (!huf::normalize(cll, n, 6, nll, lane) || !huf::normalize(cof, n, 5, nof, lane) ||
+                    !huf::normalize(cml, n, 6, nml, lane))
+                    return false;
+                o += huf::write_ncount(nll, mll, 6, e.dst, o, lane);
+                o += huf::write_ncount(nof, mof, 5, e.dst, o, lane);
+                o += huf::write_ncount(nml, mml, 6, e.dst, o, lane);
+            } else {
+                nll = lane <= 35u ? (int32_t)c_ll_norm[min(lane, 35u)] : 0;
+                nml = lane <= 52u ? (int32_t)c_ml_norm[min(lane, 52u)] : 0;
+                nof = lane <= 28u ? (int32_t)c_of_norm[min(lane, 28u)] : 0;
+                mll = 35;
+                mml = 52;
+                mof = 28;
+            }
+            tll = huf::build_small_ct(nll, mll, 6, lane);
+            tof = huf::build_small_ct(nof, mof, 5, lane);
+            tml = huf::build_small_ct(nml, mml, 6, lane);
+        }
+        if (lane == 0) e.dst[mpos] = dyn ? (uint8_t)((2u << 6) | (2u << 4) | (2u << 2)) : 0u;
         // ---- FSE bitstream: groups of 64 sequences from the last, serial inside a group
-        BitC b;
+        huf::BitW b;
         b.c = 0;
         b.pos = 0;
         b.ptr = o;
-        FseState sll, sml, sof;
-        sll.value = sml.value = sof.value = 0;
+        uint32_t sll = 0, sml = 0, sof = 0;
         const uint32_t ng = (n + kWave - 1) / kWave;
         for (uint32_t gi = ng; gi-- > 0;) {
             const uint32_t g = gi * kWave;
             const uint32_t i = g + lane;
             uint32_t pk_code = 0, pk_ll = 0, pk_ml = 0, pk_of = 0;
             if (i < n) {
-                const uint2 r = e.seq[i];
-                const SeqCode c = seq_code(r.x & 0xFFFFu, r.y, r.x >> 16);
+                const SeqCode c = seq_code_at(e, i);
                 pk_code = c.llc | (c.mlc << 8) | (c.ofc << 16);
                 pk_ll = c.llv | (c.llb << 24);
                 pk_ml = c.mlv | (c.mlb << 24);
@@ -488,32 +550,33 @@ __device__ bool emit_block(Enc &e, uint32_t bend, bool last, uint32_t lane) {
                 const uint32_t llb = xl >> 24, mlb = xm >> 24;
                 if (g + k == n - 1) {
                     // first symbols (zstd_compress.c:700-708)
-                    fse_init2(sml, c_ml_ct, mlc);
-                    fse_init2(sof, c_of_ct, ofc);
-                    fse_init2(sll, c_ll_ct, llc);
+                    sml = huf::ct_init2(tml, mlc);
+                    sof = huf::ct_init2(tof, ofc);
+                    sll = huf::ct_init2(tll, llc);
                 } else {
-                    fse_encode(b, sof, c_of_ct, ofc);
-                    fse_encode(b, sml, c_ml_ct, mlc);
-                    fse_encode(b, sll, c_ll_ct, llc);
-                    if (ofc + mlb + llb >= 64u - 7u - (9u + 9u + 8u)) flush_bits(b, e.dst, lane);
+                    huf::ct_encode(b, sof, tof, ofc);
+                    huf::ct_encode(b, sml, tml, mlc);
+                    huf::ct_encode(b, sll, tll, llc);
+                    if (ofc + mlb + llb >= 64u - 7u - (9u + 9u + 8u)) huf::bw_flush(b, e.dst, lane);
                 }
-                add_bits(b, xl & 0xFFFFFFu, llb);
-                add_bits(b, xm & 0xFFFFFFu, mlb);
-                add_bits(b, xo, ofc);
-                flush_bits(b, e.dst, lane);
+                huf::bw_add(b, xl & 0xFFFFFFu, llb);
+                huf::bw_add(b, xm & 0xFFFFFFu, mlb);
+                huf::bw_add(b, xo, ofc);
+                huf::bw_flush(b, e.dst, lane);
             }
         }
         // FSE_flushCState x3, BIT_closeCStream (end mark)
-        add_bits(b, sml.value & 63u, c_ml_ct.log);
-        flush_bits(b, e.dst, lane);
-        add_bits(b, sof.value & 31u, c_of_ct.log);
-        flush_bits(b, e.dst, lane);
-        add_bits(b, sll.value & 63u, c_ll_ct.log);
-        flush_bits(b, e.dst, lane);
-        add_bits(b, 1u, 1u);
-        flush_bits(b, e.dst, lane);
+        huf::bw_add(b, sml, tml.log);
+        huf::bw_flush(b, e.dst, lane);
+        huf::bw_add(b, sof, tof.log);
+        huf::bw_flush(b, e.dst, lane);
+        huf::bw_add(b, sll, tll.log);
+        huf::bw_flush(b, e.dst, lane);
+        huf::bw_add(b, 1u, 1u);
+        huf::bw_flush(b, e.dst, lane);
         o = b.ptr + (b.pos > 0 ? 1u : 0u);
         if (b.pos > 0 && lane == 0) e.dst[b.ptr] = (uint8_t)b.c;
+        e.rep = e.seq[n - 1].x >> 16;   // the decoder's repeat offset 1 after this block
     }
     const uint32_t csize = o - (hdr + 3u);
     const uint32_t bh = (last ? 1u : 0u) | (2u << 1) | (csize << 3);
@@ -524,7 +587,7 @@ __device__ bool emit_block(Enc &e, uint32_t bend, bool last, uint32_t lane) {
 
 // Encodes one page held in LDS (in[0, L), 64 zero bytes after).  Returns the
 // frame size, or 0 if it does not fit in cap.
-__device__ int32_t encode_page(const uint8_t *in, uint32_t L, uint16_t *table, uint8_t *map, uint2 *rec, uint2 *seq,
+__device__ __forceinline__ int32_t encode_page(const uint8_t *in, uint32_t L, uint16_t *table, uint8_t *map, uint2 *rec, uint2 *seq,
                                uint32_t *htab, uint8_t *wts, uint8_t *dst, uint32_t cap, uint32_t lane) {
     // ---- frame header: magic, single-segment descriptor with the content size
     const uint32_t fcs_id = L < 256u ? 0u : (L < 65536u + 256u ? 1u : 2u);
@@ -549,6 +612,7 @@ __device__ int32_t encode_page(const uint8_t *in, uint32_t L, uint16_t *table, u
     e.bstart = 0;
     e.cursor = 0;
     e.map = map;
+    e.rep = 1u;
     e.htab = htab;
     e.wts = wts;
     e.stage = (uint32_t *)rec;
