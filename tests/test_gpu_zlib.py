@@ -308,3 +308,91 @@ def test_deflate_buffer_api(tc, oracle_mod):
     for i, b in enumerate(bufs):
         assert B.buffer_bytes(b) == pages[i].tobytes()
         B.destroy(b)
+
+
+# ----------------------------------------------------------------- dynamic trees (§8f rank 4)
+@pytest.mark.parametrize("plen", [8192, 16384, 32768])
+def test_deflate_dynamic_bench_pages(tc, oracle_mod, plen):
+    """Bench-distribution pages are coded as one dynamic-Huffman block (BFINAL 1, BTYPE 10 in the
+    first stream bits), inflate everywhere, and compress well beyond the fixed-code ratio (~3.1)."""
+    n = 48
+    pages = tc.pagegen(n, plen, seed=404, dist=0, device=DEV)
+    comp, clen = tc.compress_pages(pages, compressor_id=ZLIB)
+    out, rv = tc.decompress_pages(comp, clen, plen, compressor_id=ZLIB)
+    torch.cuda.synchronize()
+    assert torch.equal(out, pages) and bool((rv == plen).all())
+    total = _check_zlib_streams(oracle_mod, comp, clen, pages.cpu().numpy())
+    ch, lh = comp.cpu().numpy(), clen.cpu().numpy()
+    assert all(ch[i, 2] & 7 == 5 for i in range(n))
+    assert n * plen / total > 3.3
+
+
+def _literal_heavy_page(rng, plen, draw):
+    out = bytearray()
+    while len(out) < plen:
+        if len(out) > 64 and rng.random() < 0.5:
+            p = int(rng.integers(0, len(out) - 8))
+            out += out[p:p + int(rng.integers(3, 300))]
+        else:
+            out += bytes(draw(int(rng.integers(1, 12))))
+    return np.frombuffer(bytes(out[:plen]), np.uint8)
+
+
+@pytest.mark.parametrize("alphabet", ["two", "16", "256", "geo0.97", "skew99", "runs"])
+@pytest.mark.parametrize("plen", [1024, 16384, 65535])
+def test_deflate_dynamic_alphabets(tc, oracle_mod, alphabet, plen):
+    """Skewed and tiny literal alphabets, long matches (258-byte chunks, many length codes), a page of
+    runs only (a single distance code: the forced two-code distance tree): every stream inflates
+    with the reference, the oracle, host zlib and the device."""
+    rng = np.random.default_rng(zlib.crc32(f"{alphabet}:{plen}".encode()))
+    if alphabet == "two":
+        draw = lambda k: rng.choice(np.array([65, 200], np.uint8), k)
+    elif alphabet in ("16", "256"):
+        m = int(alphabet)
+        draw = lambda k: rng.integers(256 - m, 256, k, dtype=np.uint8)
+    elif alphabet == "geo0.97":
+        p = 0.97 ** np.arange(256)
+        p /= p.sum()
+        draw = lambda k: rng.choice(256, k, p=p).astype(np.uint8)
+    elif alphabet == "skew99":
+        draw = lambda k: np.where(rng.random(k) < 0.99, 7, rng.integers(0, 256, k)).astype(np.uint8)
+    if alphabet == "runs":
+        host = np.stack([np.repeat(rng.integers(0, 256, plen // 500 + 1, dtype=np.uint8), 500)[:plen]
+                         for _ in range(4)])
+    else:
+        host = np.stack([_literal_heavy_page(rng, plen, draw) for _ in range(4)])
+    d = torch.from_numpy(host).to(DEV)
+    comp, clen = tc.compress_pages(d, compressor_id=ZLIB)
+    out, rv = tc.decompress_pages(comp, clen, plen, compressor_id=ZLIB)
+    torch.cuda.synchronize()
+    assert bool((rv == plen).all()) and torch.equal(out, d)
+    _check_zlib_streams(oracle_mod, comp, clen, host)
+
+
+@pytest.mark.parametrize("slack", [0, 16, 300, 3000])
+def test_deflate_tight_capacity(tc, oracle_mod, slack):
+    """Capacity just above the stream size: the parse records no longer fit below the stream, so the
+    page is re-coded in one pass with the fixed codes, stored, or reported as not fitting (0)."""
+    from tyche_amd import _lib
+    plen, n = 16384, 16
+    pages = tc.pagegen(n, plen, seed=77, dist=0, device=DEV)
+    comp, clen = tc.compress_pages(pages, compressor_id=ZLIB)
+    torch.cuda.synchronize()
+    cap = int(clen.max()) + slack
+    slot = tc.slot_size(plen, ZLIB)
+    comp2 = torch.zeros((n, slot), dtype=torch.uint8, device=DEV)
+    clen2 = torch.zeros(n, dtype=torch.int32, device=DEV)
+    b = _lib.Batch(count=n, src=pages.data_ptr(), src_stride=plen, src_length=plen, max_src_length=plen,
+                   dst=comp2.data_ptr(), dst_stride=slot, dst_capacity=cap, results=clen2.data_ptr())
+    _lib.check(_lib.load().tyche_compress_batch(ZLIB, 1, ctypes.byref(b), torch.cuda.current_stream().cuda_stream),
+               "compress")
+    torch.cuda.synchronize()
+    ch, lh, host = comp2.cpu().numpy(), clen2.cpu().numpy(), pages.cpu().numpy()
+    for i in range(n):
+        assert 0 <= lh[i] <= cap
+        if lh[i]:
+            s = ch[i, :lh[i]].tobytes()
+            assert zlib.decompress(s) == host[i].tobytes()
+            if oracle_mod.have_ref():
+                r2, dec2 = oracle_mod.ref_zlib_uncompress(s, plen)
+                assert r2 == plen and dec2 == host[i].tobytes()

@@ -27,9 +27,18 @@ __device__ __forceinline__ uint32_t hb(uint32_t v) { return 31u - (uint32_t)__bu
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) { return rdlane((uint32_t)wave_incl_sum((int32_t)v), kWave - 1); }
 __device__ __forceinline__ int32_t wave_max(int32_t v) { return (int32_t)rdlane((uint32_t)wave_incl_max(v), kWave - 1); }
 
-// register j of a 4-register per-lane array, j uniform
-__device__ __forceinline__ uint32_t pick(const uint32_t (&r)[4], uint32_t j) {
-    return j == 0 ? r[0] : j == 1 ? r[1] : j == 2 ? r[2] : r[3];
+// Element (j, lane) of an R-register per-lane array, j and lane uniform: every
+// register is read and the scalar result selected (a dynamically indexed
+// register array would go through scratch memory).
+template <int R>
+__device__ __forceinline__ uint32_t pick_lane(const uint32_t (&r)[R], uint32_t j, uint32_t ln) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int k = 0; k < R; k++) {
+        const uint32_t t = rdlane(r[k], ln);
+        v = j == (uint32_t)k ? t : v;
+    }
+    return v;
 }
 
 // Smallest l >= 0 with c << l >= total (c >= 1, total < 2^24).
@@ -41,13 +50,15 @@ __device__ __forceinline__ uint32_t shannon_len(uint32_t c, uint32_t total) {
 }
 
 // Code lengths for counts c[j] (symbol lane + 64 j; 0 = unused) of `total`
-// symbols, limited to maxbits (<= 11, so 256 symbols always fit).  Returns the
+// symbols, limited to maxbits (64 R symbols must fit in 2^maxbits; R <= 8 and
+// total < 2^22, so a count and a symbol share one 31-bit selection key).  Returns the
 // longest length, or 0 when fewer than two symbols are used (no code needed).
-__device__ uint32_t code_lengths(const uint32_t (&c)[4], uint32_t total, uint32_t maxbits, uint32_t (&l)[4],
+template <int R>
+__device__ uint32_t code_lengths(const uint32_t (&c)[R], uint32_t total, uint32_t maxbits, uint32_t (&l)[R],
                                  uint32_t lane) {
     uint32_t units = 0, used = 0;
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
+    for (int j = 0; j < R; j++) {
         l[j] = c[j] ? min(max(shannon_len(c[j], total), 1u), maxbits) : 0u;
         units += c[j] ? 1u << (maxbits - l[j]) : 0u;
         used += c[j] ? 1u : 0u;
@@ -61,16 +72,16 @@ __device__ uint32_t code_lengths(const uint32_t (&c)[4], uint32_t total, uint32_
         if (it >= 4096u) return 0;
         int32_t best = -1;
 #pragma unroll
-        for (int j = 0; j < 4; j++)
-            if (c[j] && l[j] < maxbits) best = max(best, (int32_t)(0x7FFFFFFFu - ((c[j] << 8) | (lane + 64u * j))));
+        for (int j = 0; j < R; j++)
+            if (c[j] && l[j] < maxbits) best = max(best, (int32_t)(0x7FFFFFFFu - ((c[j] << 9) | (lane + 64u * j))));
         const int32_t bk = wave_max(best);
         if (bk < 0) return 0;
-        const uint32_t s = (0x7FFFFFFFu - (uint32_t)bk) & 255u;
-        const uint32_t js = s >> 6, lo = rdlane(pick(l, js), s & 63u);
+        const uint32_t s = (0x7FFFFFFFu - (uint32_t)bk) & 511u;
+        const uint32_t js = s >> 6, lo = pick_lane<R>(l, js, s & 63u);
         K -= 1u << (maxbits - lo - 1u);
         if (lane == (s & 63u)) {
 #pragma unroll
-            for (int j = 0; j < 4; j++)
+            for (int j = 0; j < R; j++)
                 if ((uint32_t)j == js) l[j]++;
         }
     }
@@ -81,23 +92,23 @@ __device__ uint32_t code_lengths(const uint32_t (&c)[4], uint32_t total, uint32_
         const uint32_t slack = T - K;
         int32_t best = -1;
 #pragma unroll
-        for (int j = 0; j < 4; j++)
+        for (int j = 0; j < R; j++)
             if (c[j] && l[j] > 1u && (1u << (maxbits - l[j])) <= slack)
-                best = max(best, (int32_t)((c[j] << 8) | (lane + 64u * j)));
+                best = max(best, (int32_t)((c[j] << 9) | (lane + 64u * j)));
         const int32_t bk = wave_max(best);
         if (bk < 0) return 0;
-        const uint32_t s = (uint32_t)bk & 255u;
-        const uint32_t js = s >> 6, lo = rdlane(pick(l, js), s & 63u);
+        const uint32_t s = (uint32_t)bk & 511u;
+        const uint32_t js = s >> 6, lo = pick_lane<R>(l, js, s & 63u);
         K += 1u << (maxbits - lo);
         if (lane == (s & 63u)) {
 #pragma unroll
-            for (int j = 0; j < 4; j++)
+            for (int j = 0; j < R; j++)
                 if ((uint32_t)j == js) l[j]--;
         }
     }
     int32_t m = 0;
 #pragma unroll
-    for (int j = 0; j < 4; j++) m = max(m, (int32_t)l[j]);
+    for (int j = 0; j < R; j++) m = max(m, (int32_t)l[j]);
     return (uint32_t)wave_max(m);
 }
 
@@ -134,6 +145,38 @@ __device__ void canonical_codes(const uint32_t (&l)[4], uint32_t maxlen, uint32_
             if (l[j] == (uint32_t)L) code[j] = start[L] + (uint32_t)__popcll(m & lt);
             start[L] += (uint32_t)__popcll(m);
         }
+    }
+}
+
+// Deflate's canonical codes (RFC 1951 3.2.2): shorter codes first, symbol
+// order within a length; returned bit-reversed (deflate sends codes MSB first
+// into an LSB-first stream).
+template <int R>
+__device__ void deflate_codes(const uint32_t (&l)[R], uint32_t (&rcode)[R], uint32_t lane) {
+    uint32_t next[16];
+    {
+        uint32_t code = 0, prev = 0;
+#pragma unroll
+        for (int L = 1; L <= 15; L++) {
+            code = (code + prev) << 1;
+            next[L] = code;
+            uint32_t k = 0;
+#pragma unroll
+            for (int j = 0; j < R; j++) k += (uint32_t)__popcll(__ballot(l[j] == (uint32_t)L));
+            prev = k;
+        }
+    }
+    const uint64_t lt = lane ? (~0ull >> (64u - lane)) : 0ull;
+#pragma unroll
+    for (int j = 0; j < R; j++) {
+        uint32_t c = 0;
+#pragma unroll
+        for (int L = 1; L <= 15; L++) {
+            const uint64_t m = __ballot(l[j] == (uint32_t)L);
+            if (l[j] == (uint32_t)L) c = next[L] + (uint32_t)__popcll(m & lt);
+            next[L] += (uint32_t)__popcll(m);
+        }
+        rcode[j] = l[j] ? __builtin_bitreverse32(c) >> (32u - l[j]) : 0u;
     }
 }
 
