@@ -3,17 +3,20 @@
 // level 1, src/zstd/zstd_compress.c:2721).  The output is a standard zstd frame
 // that the reference's ZSTD_decompress (zstd_decompress.c:1459) restores
 // bit-exactly; it is not required to be the bytes zstd 1.1.2 emits (SURVEY §8a
-// A8), and its ratio is below level 1's: literals are stored raw and the
-// sequences use the predefined FSE distributions (Huffman literals and
-// per-block FSE tables are the §8f rank-4 follow-up).
+// A8).  Its ratio is below level 1's because of the parse (greedy, one hash
+// candidate), not the entropy stage: literals are Huffman-coded and the
+// sequences get per-block FSE tables and repeat offsets (§8f rank 4).
 //
 // Frame layout (zstd_compress.c:2334-2376): magic, a single-segment frame
 // header with the content size (no checksum, no dictionary), then blocks of at
 // most kSeqCap sequences each (the last flagged).  Per block:
-//   literals section   Raw_Literals_Block header + the concatenated literal runs
+//   literals section   Huffman-compressed (1 or 4 streams, FSE-compressed
+//                      weights; huf_literals below), else RLE or raw
 //                      (ZSTD_noCompressLiterals, zstd_compress.c:406-428)
-//   sequences section  nbSeq, mode byte 0 (LL/OF/ML predefined), and the FSE
-//                      bitstream written exactly as ZSTD_compressSequences does
+//   sequences section  nbSeq, the mode byte (per-block FSE tables from 64
+//                      sequences on, predefined below) with their NCount
+//                      headers, and the FSE bitstream written exactly as
+//                      ZSTD_compressSequences does
 //                      (zstd_compress.c:695-735): last sequence first through
 //                      FSE_initCState2, the rest backwards with
 //                      FSE_encodeSymbol OF, ML, LL then the LL, ML, OF extra
@@ -25,8 +28,8 @@
 // registers.  The match finder is the shared parse (lz_parse.h).  Sequence
 // codes and extra-bit values are computed lane-parallel; the FSE state chain
 // is serial, so it runs as wave-uniform code over 64 sequences held in lanes
-// (v_readlane), with the predefined CTables in constant memory (scalar loads),
-// flushing each sequence's bytes with one 8-lane byte store.
+// (v_readlane), with each table held in one VGPR (huf::SmallCT), flushing each
+// sequence's bytes with one 8-lane byte store.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -45,80 +48,14 @@ constexpr uint32_t kPad = 64;
 constexpr uint32_t kSeqCap = 1024;       // sequences buffered per block
 constexpr uint32_t kPrefetchVec = 16;
 
-// ------------------------------------------------------------ predefined FSE CTables
-// FSE_buildCTable_wksp (fse_compress.c) over the default distributions of
-// zstd_internal.h:118-136, evaluated at compile time.
-constexpr int16_t kLLNorm[36] = {4, 3, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 1, 1, 1, 2, 2, 2, 2, 2, 2, 2, 2, 2, 3, 2, 1,
-                                 1, 1, 1, 1, -1, -1, -1, -1};
-constexpr int16_t kMLNorm[53] = {1, 4, 3, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1,
-                                 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1, -1, -1};
-constexpr int16_t kOFNorm[29] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1,
-                                 -1, -1};
-struct CTab {
-    uint32_t state[64];      // stateTable (tableSize <= 64); 32-bit so uniform lookups are scalar loads
-    uint32_t dnb[53];        // symbolTT.deltaNbBits
-    int32_t dfs[53];         // symbolTT.deltaFindState
-    uint32_t log;
-};
-
-constexpr uint32_t ce_highbit(uint32_t v) {
-    uint32_t r = 0;
-    while (v >>= 1) r++;
-    return r;
-}
-
-constexpr CTab make_ctab(const int16_t *norm, uint32_t max_sv, uint32_t log) {
-    CTab t{};
-    const uint32_t size = 1u << log, mask = size - 1u, step = (size >> 1) + (size >> 3) + 3u;
-    uint8_t sym[64] = {};
-    uint32_t cumul[55] = {};
-    uint32_t high = size - 1u;
-    for (uint32_t u = 1; u <= max_sv + 1; u++) {
-        if (norm[u - 1] == -1) {
-            cumul[u] = cumul[u - 1] + 1;
-            sym[high--] = (uint8_t)(u - 1);
-        } else {
-            cumul[u] = cumul[u - 1] + (uint32_t)norm[u - 1];
-        }
-    }
-    cumul[max_sv + 1] = size + 1;
-    uint32_t pos = 0;
-    for (uint32_t s = 0; s <= max_sv; s++)
-        for (int i = 0; i < norm[s]; i++) {
-            sym[pos] = (uint8_t)s;
-            pos = (pos + step) & mask;
-            while (pos > high) pos = (pos + step) & mask;
-        }
-    for (uint32_t u = 0; u < size; u++) t.state[cumul[sym[u]]++] = size + u;
-    int32_t total = 0;
-    for (uint32_t s = 0; s <= max_sv; s++) {
-        const int32_t n = norm[s];
-        if (n == 0) continue;
-        if (n == -1 || n == 1) {
-            t.dnb[s] = (log << 16) - (1u << log);
-            t.dfs[s] = total - 1;
-            total++;
-        } else {
-            const uint32_t mbo = log - ce_highbit((uint32_t)n - 1u);
-            const uint32_t msp = (uint32_t)n << mbo;
-            t.dnb[s] = (mbo << 16) - msp;
-            t.dfs[s] = total - n;
-            total += n;
-        }
-    }
-    t.log = log;
-    return t;
-}
-
+// ------------------------------------------------------------ predefined distributions
+// zstd_internal.h:118-136 (LL, ML: log 6; OF: log 5), used below 64 sequences
 __device__ __constant__ int16_t c_ll_norm[36] = {4, 3, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 1, 1, 1, 2, 2, 2, 2, 2, 2, 2, 2,
                                                  2, 3, 2, 1, 1, 1, 1, 1, -1, -1, -1, -1};
 __device__ __constant__ int16_t c_ml_norm[53] = {1, 4, 3, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1,
                                                  1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1, -1, -1};
 __device__ __constant__ int16_t c_of_norm[29] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1,
                                                  -1, -1};
-__device__ __constant__ CTab c_ll_ct = make_ctab(kLLNorm, 35, 6);
-__device__ __constant__ CTab c_ml_ct = make_ctab(kMLNorm, 52, 6);
-__device__ __constant__ CTab c_of_ct = make_ctab(kOFNorm, 28, 5);
 __device__ __forceinline__ uint32_t hb(uint32_t v) { return 31u - (uint32_t)__builtin_clz(v); }
 
 // (code, extra bits) of one sequence -- ZSTD_seqToCodes (zstd_compress.c:535-556).
@@ -159,40 +96,6 @@ __device__ __forceinline__ SeqCode seq_code(uint32_t ll, uint32_t ml, uint32_t o
     c.mlv = m & ((1u << c.mlb) - 1u);
     c.ofv = ofcode & ((1u << c.ofc) - 1u);
     return c;
-}
-
-// ------------------------------------------------------------ backward-readable bit writer
-struct BitC {
-    uint64_t c;
-    uint32_t pos;     // bits in c
-    uint32_t ptr;     // output offset of the next byte
-};
-__device__ __forceinline__ void add_bits(BitC &b, uint32_t v, uint32_t nb) {
-    b.c |= (uint64_t)v << b.pos;      // v already masked to nb bits
-    b.pos += nb;
-}
-// BIT_flushBits: the whole bytes of c go out (8 lanes, one byte each)
-__device__ __forceinline__ void flush_bits(BitC &b, uint8_t *dst, uint32_t lane) {
-    const uint32_t nbytes = b.pos >> 3;
-    if (lane < nbytes) dst[b.ptr + lane] = (uint8_t)(b.c >> (8u * lane));
-    b.ptr += nbytes;
-    b.pos &= 7u;
-    b.c = nbytes >= 8u ? 0ull : b.c >> (8u * nbytes);
-}
-
-struct FseState {
-    uint32_t value;
-};
-__device__ __forceinline__ void fse_init2(FseState &s, const CTab &t, uint32_t sym) {
-    const uint32_t dnb = t.dnb[sym];
-    const uint32_t nbo = (dnb + (1u << 15)) >> 16;
-    const uint32_t v = (nbo << 16) - dnb;
-    s.value = t.state[(int32_t)(v >> nbo) + t.dfs[sym]];
-}
-__device__ __forceinline__ void fse_encode(BitC &b, FseState &s, const CTab &t, uint32_t sym) {
-    const uint32_t nbo = (s.value + t.dnb[sym]) >> 16;
-    add_bits(b, s.value & ((1u << nbo) - 1u), nbo);
-    s.value = t.state[(int32_t)(s.value >> nbo) + t.dfs[sym]];
 }
 
 // ------------------------------------------------------------ block emission
