@@ -99,9 +99,10 @@ __device__ __forceinline__ uint32_t next_token(const uint8_t *in, int32_t L, uin
     return (uint32_t)q;
 }
 
-// Parallel token-chain parse.  Writes the ordered token positions to seqpos and
-// returns their number.  owner: L bytes of scratch (the page window, unused
-// until the copy phases).
+// Parallel token-chain parse.  Writes the ordered token positions to the top
+// of the page window (seqpos = the last `total` u16 slots below win_end) and
+// returns their number.  owner: L bytes of scratch at the window's start
+// (unused until the copy phases; no stamp is read once positions are written).
 //
 //  1. lane k walks the chain from its segment start k*S to the segment end,
 //     stamping owner[p] = k+1 on every position it visits;
@@ -113,7 +114,8 @@ __device__ __forceinline__ uint32_t next_token(const uint8_t *in, int32_t L, uin
 //     code) gives every on-chain lane its entry point;
 //  4. each on-chain lane re-walks entry -> hand-off position to count and then
 //     write its positions.
-__device__ uint32_t parse_chain(const uint8_t *in, int32_t L, uint8_t *owner, uint16_t *seqpos, uint32_t lane) {
+__device__ uint32_t parse_chain(const uint8_t *in, int32_t L, uint8_t *owner, uint16_t *win_end, uint16_t *&seqpos,
+                                uint32_t lane) {
     PROF_DECL
     const uint32_t S = ((uint32_t)L + kWave - 1) / kWave;
     const uint32_t seg0 = lane * S;
@@ -152,8 +154,9 @@ __device__ uint32_t parse_chain(const uint8_t *in, int32_t L, uint8_t *owner, ui
     for (uint32_t q = entry; q < (uint32_t)L && q != y; q = next_token(in, L, q)) cnt++;
     const int32_t incl = wave_incl_sum((int32_t)cnt);
     uint32_t base = (uint32_t)incl - cnt;
-    for (uint32_t q = entry; q < (uint32_t)L && q != y; q = next_token(in, L, q)) seqpos[base++] = (uint16_t)q;
     const uint32_t total = rdlane((uint32_t)incl, kWave - 1);
+    seqpos = win_end - total;
+    for (uint32_t q = entry; q < (uint32_t)L && q != y; q = next_token(in, L, q)) seqpos[base++] = (uint16_t)q;
     WAVE_SYNC();
     PROF_MARK(5);
     PROF_ADD(11, total);
@@ -170,13 +173,21 @@ __device__ __forceinline__ uint32_t mod_small(uint32_t i, uint32_t m) {
 }
 
 // Decodes one page held in LDS.  in: stream of L bytes (kPad zero bytes after),
-// out: C-byte LDS window.  slots: 4 x 8 bytes of scratch.  Returns
-// LZ4_decompress_safe's value.
-__device__ int32_t decode_page(const uint8_t *in, int32_t L, uint8_t *out, int32_t C, uint16_t *seqpos,
-                               uint2 *slots, uint32_t lane) {
+// out: LDS window of W >= C + 16 bytes whose top holds the token positions.
+// Returns LZ4_decompress_safe's value.
+//
+// The positions of batches not yet read sit above the output: every sequence
+// but the last writes >= 4 bytes and takes 2 bytes of positions, so a valid
+// stream's output never reaches them.  A malformed one could (its sequences
+// need not fit in C), so each batch checks its write extent first and hands
+// the page to the sequential decoder, which gives the same result, when it
+// would overlap.
+__device__ int32_t decode_page_serial(const uint8_t *in, int32_t L, uint8_t *out, int32_t C, uint32_t lane);
+__device__ int32_t decode_page(const uint8_t *in, int32_t L, uint8_t *out, int32_t C, uint32_t W, uint32_t lane) {
     if (C == 0) return (L == 1 && in[0] == 0) ? 0 : -1;
     if (L <= 0) return -1;
-    const uint32_t nseq = parse_chain(in, L, out, seqpos, lane);
+    uint16_t *seqpos;
+    const uint32_t nseq = parse_chain(in, L, out, (uint16_t *)(out + W), seqpos, lane);
     PROF_DECL
     const uint32_t grp = lane >> 4, gl = lane & 15;
     const uint64_t lt_mask = (1ull << lane) - 1ull;
@@ -248,6 +259,11 @@ __device__ int32_t decode_page(const uint8_t *in, int32_t L, uint8_t *out, int32
             if (final_rv < 0) return final_rv;                 // output is discarded on error
         }
         const bool term_lane = finished && lane == n_ok;       // terminal literal run
+        if (b0 + kWave < nseq) {
+            // writes reach op_base + (this batch's output) + 3 (dword literal overrun)
+            const int64_t wend = (int64_t)op_base + (int64_t)rdlane((uint32_t)incl, kWave - 1) + 3;
+            if (wend > (int64_t)W - 2 * (int64_t)(nseq - b0 - kWave)) return decode_page_serial(in, L, out, C, lane);
+        }
         PROF_MARK(6);
         // ---- literals: short ones per lane (4 bytes per step), long ones by the whole wave
         const bool do_lit = (lane < n_ok && active) || term_lane;
@@ -430,13 +446,11 @@ constexpr uint32_t kPrefetchVec = 8;   // 16-byte vectors per lane prefetched fo
 // One wave per page, looping over pages; the next page's stream is prefetched
 // into registers while the current one is decoded.
 __global__ __launch_bounds__(64) void lz4_decode_wave_kernel(tyche_batch_t b, uint32_t in_cap, uint32_t out_cap,
-                                                             uint32_t off_in, uint32_t off_seq, uint32_t off_slots) {
+                                                             uint32_t off_in) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t lane = threadIdx.x;
-    uint8_t *out = smem;
+    uint8_t *out = smem;                 // page window [0, off_in): output, parse stamps, token positions
     uint8_t *stage = smem + off_in;
-    uint16_t *seqpos = (uint16_t *)(smem + off_seq);
-    uint2 *slots = (uint2 *)(smem + off_slots);
     const size_t stride = gridDim.x;
 
     size_t page = blockIdx.x;
@@ -475,7 +489,7 @@ __global__ __launch_bounds__(64) void lz4_decode_wave_kernel(tyche_batch_t b, ui
             WAVE_SYNC();
             PROF_MARK(1);
             PROF_ADD(0, 1);
-            rv = decode_page(in, (int32_t)p.src_len, out, (int32_t)p.dst_cap, seqpos, slots, lane);
+            rv = decode_page(in, (int32_t)p.src_len, out, (int32_t)p.dst_cap, off_in, lane);
             WAVE_SYNC();
             PROF_MARK(13);
             if (rv > 0 && !(TYCHE_ABLATE & 4)) stage_out(p.dst, out, (uint32_t)rv, lane, kWave);
@@ -505,12 +519,14 @@ __global__ __launch_bounds__(64) void lz4_decode_wave_kernel(tyche_batch_t b, ui
 
 hipError_t launch_lz4_decode(const tyche_batch_t &b, uint32_t in_cap, uint32_t out_cap, hipStream_t s) {
     if (b.count == 0) return hipSuccess;
-    // page window (also the parse's owner stamps, so at least in_cap bytes), stream, token list, slots
+    // page window (output; the parse's owner stamps, so at least in_cap bytes;
+    // the token positions at its top, <= in_cap / 3 + 1 of them, which always
+    // fit: W >= in_cap + 20), then the staged stream
     const uint32_t off_in = (std::max(out_cap, in_cap + 4u) + 16u + 15u) & ~15u;
-    const uint32_t off_seq = off_in + ((in_cap + 16u + kPad + 15u) & ~15u);
-    const uint32_t max_seq = in_cap / 3u + 2u;
-    const uint32_t off_slots = off_seq + ((max_seq * 2u + 15u) & ~15u);
-    const size_t lds = off_slots + 64;
+#ifndef TYCHE_LDS_EXTRA
+#define TYCHE_LDS_EXTRA 0
+#endif
+    const size_t lds = off_in + ((in_cap + 16u + kPad + 15u) & ~15u) + TYCHE_LDS_EXTRA;   // EXTRA: occupancy experiments
     if (lds > 160 * 1024) {
         // large pages: sequential decoder, LDS = page window + stream only
         const size_t lds2 = ((out_cap + 15u) & ~15u) + ((in_cap + 16u + kPad + 15u) & ~15u);
@@ -537,8 +553,7 @@ hipError_t launch_lz4_decode(const tyche_batch_t &b, uint32_t in_cap, uint32_t o
     }
     const size_t per_cu = std::max<size_t>(1, std::min<size_t>(32, (160 * 1024) / lds));
     const size_t grid = std::min<size_t>(b.count, (size_t)(dev < 64 ? cus[dev] : 256) * per_cu);
-    hipLaunchKernelGGL(lz4_decode_wave_kernel, dim3((unsigned)grid), dim3(kWave), lds, s, b, in_cap, out_cap, off_in,
-                       off_seq, off_slots);
+    hipLaunchKernelGGL(lz4_decode_wave_kernel, dim3((unsigned)grid), dim3(kWave), lds, s, b, in_cap, out_cap, off_in);
     return hipGetLastError();
 }
 
