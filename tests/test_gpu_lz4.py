@@ -220,3 +220,25 @@ def test_buffer_batch_api(tc, oracle_mod):
     for i, b in enumerate(bufs):
         assert B.buffer_bytes(b) == pages[i].tobytes()
         B.destroy(b)
+
+
+def _seq_stream(nseq, tail):
+    body = bytes([0x10, 0x41, 0x01, 0x00])                     # 1 literal 'A', match 4 at offset 1
+    body += bytes([0x00, 0x01, 0x00]) * (nseq - 1)             # matches of 4 at offset 1
+    return body + bytes([0x50]) + b"B" * 5 if tail else body   # 5 trailing literals (or none)
+
+
+@pytest.mark.parametrize("nseq,cap,tail", [(6000, 16384, True), (6000, 8192, True), (3000, 16384, True),
+                                           (20000, 65535, True), (4094, 16384, True), (4094, 16384, False),
+                                           (2000, 8192, True)])
+def test_decode_token_list_near_output(tc, oracle_mod, nseq, cap, tail):
+    """Streams of thousands of 3-byte sequences (4 output bytes each): the token positions kept at the
+    top of the page window would be reached by the output of a stream whose sequences overrun the
+    capacity, so such pages restart on the sequential decoder.  Verdict and output equal the
+    oracle's either way; (4094, 16384) exactly fills the page."""
+    s = _seq_stream(nseq, tail)
+    r, dec = oracle_mod.lz4_decompress(s, cap)
+    rv, outs = ragged_decode(tc, [s], [cap])
+    assert rv[0] == r, (rv[0], r)
+    if r > 0:
+        assert outs[0] == dec
