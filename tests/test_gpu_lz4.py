@@ -242,3 +242,23 @@ def test_decode_token_list_near_output(tc, oracle_mod, nseq, cap, tail):
     assert rv[0] == r, (rv[0], r)
     if r > 0:
         assert outs[0] == dec
+
+
+def test_decode_size_classes(tc):
+    """A 16K-page batch whose streams span 2 KB .. 16 KB (compressible, half-random, random pages in
+    a seeded shuffle): the launch splits into a short-stream class sized for one more wave per CU
+    and a long-stream class; every page is decoded exactly once, in either."""
+    n, plen = 16384, 16384
+    pages = tc.pagegen(n, plen, seed=17, dist=0, device=DEV)
+    g = torch.Generator(device="cpu").manual_seed(3)
+    noisy = torch.randperm(n, generator=g)[: n // 8].to(DEV)
+    rnd = torch.randint(0, 256, (noisy.numel(), plen), dtype=torch.uint8, generator=None, device=DEV)
+    half = torch.arange(noisy.numel(), device=DEV) % 2 == 0
+    pages[noisy[half]] = rnd[half]                       # incompressible: streams > page
+    pages[noisy[~half], : plen // 3] = rnd[~half][:, : plen // 3]   # a third random: mid-size streams
+    comp, clen = tc.compress_pages(pages)
+    mx = int(clen.max())
+    assert mx > 16384 and int(clen.min()) < 7000
+    out, rv = tc.decompress_pages(comp, clen, plen, max_comp_len=mx)
+    torch.cuda.synchronize()
+    assert bool((rv == plen).all()) and torch.equal(out, pages)
