@@ -14,6 +14,7 @@ cat $OUT/bench_$TAG.json
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o bench \
     -- python3 $R/bench.py --no-cpu --e2e-pages 0 > $OUT/prof_bench_$TAG.log 2>&1
+# reduce with tools/pmc_traffic.py (--calls lz4_decode=1: two size-class launches per call)
 for spec in lz4:16384 zstd:32768; do
   c=${spec%%:*}; p=${spec##*:}
   export CODEC=$c PLEN=$p PAGES=262144 REPS=1

@@ -6,7 +6,10 @@
 Correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE and WRITE_SIZE are in
 KiB; on gfx950 FETCH_SIZE reports half the bytes of a 16-B/lane streaming read,
 so HBM bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.  Each kernel's figure is
-the mean over its dispatches, divided by the pages one dispatch processes.
+its bytes per codec call divided by the pages of a call.  A call is one
+dispatch, except where --calls says how many calls the kernel's dispatches
+make up (the LZ4 decoder runs two size-class launches per call:
+--calls lz4_decode=1 for tools/run_codec.py with REPS=1).
 bench.py scales the per-page figure to its own launch for `roofline.traffic`.
 """
 import argparse
@@ -42,17 +45,20 @@ def main():
     ap.add_argument("--pages", type=int, required=True)
     ap.add_argument("--page-len", type=int, default=16384)
     ap.add_argument("-o", "--out", required=True)
+    ap.add_argument("--calls", action="append", default=[], help="kernel=N: its dispatches make up N codec calls")
     a = ap.parse_args()
+    calls = {kv.split("=")[0]: int(kv.split("=")[1]) for kv in a.calls}
     f = per_dispatch(a.fetch, "FETCH_SIZE")
     w = per_dispatch(a.write, "WRITE_SIZE")
-    res = {"pages_per_dispatch": a.pages, "page_len": a.page_len,
+    res = {"pages_per_call": a.pages, "page_len": a.page_len, "calls": calls,
            "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024 / pages (gfx950 FETCH_SIZE half-count corrected)",
            "bytes_per_page": {}, "read_bytes_per_page": {}, "write_bytes_per_page": {}}
     for k in KERNELS:
         if not f.get(k) or not w.get(k):
             continue
-        rd = 2 * 1024 * sum(f[k]) / len(f[k]) / a.pages
-        wr = 1024 * sum(w[k]) / len(w[k]) / a.pages
+        nf, nw = calls.get(k, len(f[k])), calls.get(k, len(w[k]))
+        rd = 2 * 1024 * sum(f[k]) / nf / a.pages
+        wr = 1024 * sum(w[k]) / nw / a.pages
         res["read_bytes_per_page"][k] = round(rd, 1)
         res["write_bytes_per_page"][k] = round(wr, 1)
         res["bytes_per_page"][k] = round(rd + wr, 1)
