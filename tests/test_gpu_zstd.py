@@ -438,3 +438,62 @@ def test_encode_tight_capacity(tc, oracle_mod, slack):
         if O.have_ref():
             r2, dec2 = O.ref_zstd_decompress(ch[i, :lh[i]].tobytes(), plen)
             assert r2 == plen and dec2 == host[i].tobytes()
+
+
+def _huff12_frame(lits):
+    """A one-block frame whose literals use a tableLog-12 Huffman table (two 12-bit codes), raw
+    4-bit weights, single stream, no sequences -- zstd 1.1.2's own encoder never goes past 11."""
+    w = [11, 11, 10, 10, 9, 9, 1, 1, 8, 7, 6, 5, 4, 3, 2]          # symbol 15 implied: weight 9
+    weights = w + [9]
+    tlog = 12
+    nb = [tlog + 1 - x for x in weights]
+    # HUF_buildCTable: starting value per length from the longest down, symbol order within a length
+    per = [0] * 13
+    for b in nb:
+        per[b] += 1
+    start, mn = [0] * 13, 0
+    for b in range(12, 0, -1):
+        start[b] = mn
+        mn = (mn + per[b]) >> 1
+    code = []
+    for b in nb:
+        code.append(start[b])
+        start[b] += 1
+    acc, nbits = 0, 0
+    for s in reversed(lits):                                    # last symbol first, LSB first
+        acc |= code[s] << nbits
+        nbits += nb[s]
+    acc |= 1 << nbits                                           # end mark
+    stream = acc.to_bytes(nbits // 8 + 1, "little")
+    hdr = bytes([127 + len(w)]) + bytes((w[i] << 4) | (w[i + 1] if i + 1 < len(w) else 0) for i in range(0, len(w), 2))
+    lit_sec_body = hdr + stream
+    n, c = len(lits), len(lit_sec_body)
+    assert n < 256 and c < 1024
+    lh = (2 | (0 << 2) | (n << 4) | (c << 14)).to_bytes(3, "little")
+    block = lh + lit_sec_body + b"\x00"                         # nbSeq = 0
+    bh = (1 | (2 << 1) | (len(block) << 3)).to_bytes(3, "little")
+    return b"\x28\xb5\x2f\xfd" + bytes([0x20, n]) + bh + block
+
+
+def test_decode_huffman_tablelog12(tc, oracle_mod):
+    """The device decoder's 11-bit Huffman table with the 12-bit side table: a frame with two 12-bit
+    codes decodes exactly like the reference and the oracle."""
+    rng = np.random.default_rng(12)
+    lits = [int(x) for x in rng.integers(0, 16, 200)]
+    lits[::17] = [6] * len(lits[::17])
+    lits[5::19] = [7] * len(lits[5::19])
+    frame = _huff12_frame(lits)
+    want = bytes(lits)
+    r, dec = oracle_mod.zstd_decompress(frame, 200)
+    assert r == 200 and dec == want
+    if oracle_mod.have_ref():
+        r2, dec2 = oracle_mod.ref_zstd_decompress(frame, 200)
+        assert r2 == 200 and dec2 == want
+    slots = torch.zeros((4, 512), dtype=torch.uint8)
+    for i in range(4):
+        slots[i, :len(frame)] = torch.from_numpy(np.frombuffer(frame, np.uint8).copy())
+    clen = torch.full((4,), len(frame), dtype=torch.int32)
+    out, rv = tc.decompress_pages(slots.to(DEV), clen.to(DEV), 200, compressor_id=ZSTD)
+    torch.cuda.synchronize()
+    assert bool((rv == 200).all())
+    assert all(out[i].cpu().numpy().tobytes() == want for i in range(4))

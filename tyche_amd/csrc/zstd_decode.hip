@@ -153,7 +153,8 @@ __device__ __constant__ DTab c_ml_def = make_dtab(kMLNormH, 52, 6);
 struct Work {
     uint8_t *win;        // page window (cap + kWinPad)
     const uint8_t *in;   // staged frame (len + kStreamPad zero bytes)
-    uint16_t *huf;       // 4096 entries: symbol | nbBits << 8
+    uint16_t *huf;       // 2048 entries: symbol | nbBits << 8, indexed by the next min(tableLog, 11) bits
+    uint8_t *hpair;      // tableLog 12 only: the symbols of the 12-bit codes, by 12-bit index
     uint32_t *ll, *of, *ml;   // FSE cells: newState | symbol << 16 | nbBits << 24
     uint32_t *wt;        // 64 cells for the Huffman-weight FSE table
     int16_t *norm;       // 256 normalized counts
@@ -593,8 +594,23 @@ __device__ int32_t huf_read_table(const Work &W, int32_t ip, int32_t n, uint32_t
             if (wv == k) at = start[k] + (__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0)) << (k - 1));
             start[k] += (uint32_t)__builtin_popcountll(m) << (k - 1);
         }
-        const uint32_t len = s < nsym && wv ? (1u << wv) >> 1 : 0u;
+        // tableLog 12: the table is indexed by 11 bits.  Symbols of weight >= 2
+        // start at even 12-bit positions and cover an even number of them, so
+        // they halve exactly; the weight-1 symbols (12-bit codes, an even number
+        // of them, first in the table) go to hpair and their 11-bit entries say
+        // "12 bits, see hpair".
+        const bool t12 = tlog == 12u;
+        uint32_t len = s < nsym && wv ? (1u << wv) >> 1 : 0u;
         const uint16_t e = (uint16_t)(s | ((tlog + 1u - wv) << 8));
+        if (t12) {
+            if (len == 1u) {
+                W.hpair[at] = (uint8_t)s;
+                W.huf[at >> 1] = (uint16_t)(12u << 8);
+                len = 0;
+            }
+            at >>= 1;
+            len >>= 1;
+        }
         if (len <= 16) {
             for (uint32_t i = 0; i < len; i++) W.huf[at + i] = e;
         }
@@ -648,7 +664,8 @@ __device__ bool huf_decode(const Work &W, int32_t cs, int32_t n, bool single, ui
         if (lane < act_n && i < cnt) {
             if (b.used > 52u) bitd_reload(b, in);
             const uint32_t v = (uint32_t)bitd_look_fast(b, tlog);
-            const uint32_t e = W.huf[v];
+            uint32_t e = W.huf[tlog == 12u ? v >> 1 : v];
+            if ((e >> 8) == 12u) e = W.hpair[v] | (12u << 8);   // a 12-bit code (tableLog 12 only)
             out[o0 + i] = (uint8_t)e;
             b.used += e >> 8;
         }
@@ -1133,21 +1150,22 @@ __device__ int32_t decode_frame(const Work &W, int32_t L, int32_t cap, uint32_t 
 }
 
 struct Layout {
-    uint32_t off_in, off_huf, off_ll, off_of, off_ml, off_wt, off_norm, off_next, off_w, total;
+    uint32_t off_in, off_huf, off_ll, off_of, off_ml, off_wt, off_norm, off_next, off_w, off_hp, total;
 };
 
 __host__ __device__ inline Layout make_layout(uint32_t in_cap, uint32_t out_cap) {
     Layout l;
     l.off_in = (out_cap + kWinPad + 15u) & ~15u;
     l.off_huf = l.off_in + ((in_cap + 16u + kStreamPad + 15u) & ~15u);
-    l.off_ll = l.off_huf + 4096u * 2u;
+    l.off_ll = l.off_huf + 2048u * 2u;
     l.off_of = l.off_ll + 512u * 4u;
     l.off_ml = l.off_of + 256u * 4u;
     l.off_wt = l.off_ml + 512u * 4u;
     l.off_norm = l.off_wt + 64u * 4u;
     l.off_next = l.off_norm + 256u * 2u;
     l.off_w = l.off_next + 256u * 2u;
-    l.total = l.off_w + 256u + 16u;
+    l.off_hp = l.off_w + 256u + 16u;
+    l.total = l.off_hp + 256u;
     return l;
 }
 
@@ -1157,6 +1175,7 @@ __global__ __launch_bounds__(64) void zstd_decode_kernel(tyche_batch_t b, uint32
     Work W;
     W.win = smem;
     W.huf = (uint16_t *)(smem + lay.off_huf);
+    W.hpair = smem + lay.off_hp;
     W.ll = (uint32_t *)(smem + lay.off_ll);
     W.of = (uint32_t *)(smem + lay.off_of);
     W.ml = (uint32_t *)(smem + lay.off_ml);
