@@ -38,7 +38,7 @@ def main():
     pg = max(v[0], 1)
     tot = sum(v[k] for k in (1, 2, 3, 5, 6, 7, 8, 12))
     print(f"pages {v[0]}  seq/page {v[11] / pg:.0f}  hand-offs/page {v[4] / pg:.2f}  batches/page {v[10] / pg:.1f}"
-          f"  groups/page {v[9] / pg:.0f}  max_comp {mx}")
+          f"  groups/page {v[9] / pg:.0f}  ready/round {v[14] / max(v[9], 1):.2f}  max_comp {mx}")
     for k in (1, 2, 3, 5, 6, 7, 8, 12):
         print(f"  {NAMES[k]:14s} {v[k] / pg:10.0f} cyc/page  {100.0 * v[k] / tot:5.1f}%")
 

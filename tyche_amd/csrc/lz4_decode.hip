@@ -314,6 +314,7 @@ __device__ int32_t decode_page(const uint8_t *in, int32_t L, uint8_t *out, int32
             // up to four ready short matches, in stream order, go to the four 16-lane
             // groups; their fields are fetched with v_readlane (scalar picks, no LDS trip)
             uint64_t ready = pending & shortm & __ballot(src_end <= F);
+            PROF_ADD(14, __builtin_popcountll(ready));
             uint32_t gpk = 0, gml = 0;          // this group's packed (d | off << 16) and length
 #pragma unroll
             for (uint32_t k = 0; k < 4; k++) {
