@@ -149,7 +149,13 @@ __device__ __forceinline__ void decode_record(const uint2 *rec, uint32_t n, uint
 // consumes n >= 1 records whose literal runs start at `anchor`, and returns
 // false to abort.  Returns the anchor where the last literal run starts, or
 // 0xFFFFFFFF if the sink aborted.
-template <typename Sink>
+//
+// kRepCand (zstd): every position also tries the repeat-offset candidate
+// pos - R, R = the offset of the last match selected before this block (zstd's
+// fast parse checks the repeat offset first, zstd_compress.c:951-958), and
+// takes it when it verifies and is at least as long as the hash candidate's
+// match: a repeat offset costs a few bits instead of ~10 (zstd_encode.hip).
+template <bool kRepCand = false, typename Sink>
 __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *table, uint2 *rec, uint32_t lane,
                                       Sink &sink) {
     uint32_t anchor = 0;
@@ -161,6 +167,7 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
     uint32_t cursor = 0;     // matches may start here (end of the last match)
     uint32_t nacc = 0;       // records accumulated since the last hand-off
     uint32_t blk = 0;        // current 64-position block
+    uint32_t R = 1;          // repeat offset (kRepCand): zstd's initial repeat offset 1
     bool done = false;
     PHASE_INIT();
     for (; !done && blk <= mflimit; blk = max(blk + kWave, cursor & ~(kWave - 1))) {
@@ -174,19 +181,37 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
         const Window pw = lds_window(A, (live ? pos : mflimit) + ib);
         const uint32_t v = pw.w0;
         const uint32_t h = hash4(v);
-        const uint32_t cand = table[h];
+        uint32_t cand = table[h];
         __builtin_amdgcn_wave_barrier();
         table[h] = (uint16_t)pos;
         // ---- the candidate's window: 4-byte verify, forward probe (MINMATCH + up
         // to kProbe bytes) and backward probe (up to 4 bytes).  A candidate is a
         // position <= mflimit, so the window stays inside the page's zero pad.
-        const Window cw = lds_window(A, cand + ib);
-        const bool ok = live & (cand < pos) & (cw.w0 == v);
+        Window cw = lds_window(A, cand + ib);
+        bool ok = live & (cand < pos) & (cw.w0 == v);
         uint32_t n = 4u + kProbe;
 #pragma unroll
         for (int k = (int)kProbeWords - 1; k >= 0; k--) {
             const uint32_t x = pw.fw[k] ^ cw.fw[k];
             if (x) n = 4u + 4u * (uint32_t)k + ((uint32_t)__builtin_ctz(x) >> 3);
+        }
+        if (kRepCand) {
+            // the repeat-offset candidate (consecutive windows: cheap loads)
+            const uint32_t rc = pos >= R ? pos - R : 0u;
+            const Window rw = lds_window(A, min(rc, mflimit) + ib);
+            const bool rok = live & (pos >= R) & (rw.w0 == v);
+            uint32_t rn = 4u + kProbe;
+#pragma unroll
+            for (int k = (int)kProbeWords - 1; k >= 0; k--) {
+                const uint32_t x = pw.fw[k] ^ rw.fw[k];
+                if (x) rn = 4u + 4u * (uint32_t)k + ((uint32_t)__builtin_ctz(x) >> 3);
+            }
+            if (rok && (!ok || rn >= n)) {
+                cand = rc;
+                cw = rw;
+                n = rn;
+                ok = true;
+            }
         }
         const uint32_t xb = pw.back ^ cw.back;
         const uint32_t e = min(matchlimit, pos + kMinMatch + kProbe);
@@ -226,6 +251,7 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
             } while (li < kWave);
             if (li == kWave) {
                 end = rdlane(endp, at_li);
+                if (kRepCand) R = blk + at_li - rdlane(cand, at_li);
                 break;
             }
             // reached the probe limit: extend with the whole wave, then look for
@@ -237,6 +263,7 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
             PHASE_COUNT(6);
             if (lane == at_li) len = ln;
             end = mp + ln;
+            if (kRepCand) R = mp - mc;
             const uint32_t rel = end - blk;
             const uint64_t r = rel < kWave ? mall & (~0ull << rel) : 0ull;
             if (r == 0) break;

@@ -535,7 +535,7 @@ __device__ __forceinline__ int32_t encode_page(const uint8_t *in, uint32_t L, ui
         }
         return true;
     };
-    const uint32_t anchor = lzp::parse_page(in, L, table, rec, lane, sink);
+    const uint32_t anchor = lzp::parse_page<true>(in, L, table, rec, lane, sink);
     if (anchor == 0xFFFFFFFFu) return 0;
     if (!emit_block(e, L, true, lane)) return 0;
     return (int32_t)e.op;
