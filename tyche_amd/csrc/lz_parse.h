@@ -206,7 +206,10 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
                 const uint32_t x = pw.fw[k] ^ rw.fw[k];
                 if (x) rn = 4u + 4u * (uint32_t)k + ((uint32_t)__builtin_ctz(x) >> 3);
             }
-            if (rok && (!ok || rn >= n)) {
+#ifndef TYCHE_REP_SLACK
+#define TYCHE_REP_SLACK 0
+#endif
+            if (rok && (!ok || rn + TYCHE_REP_SLACK >= n)) {
                 cand = rc;
                 cw = rw;
                 n = rn;
