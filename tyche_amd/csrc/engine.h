@@ -2,6 +2,8 @@
 // gfx950 kernels (lz4_decode.hip, lz4_encode.hip, pagegen.hip).
 #pragma once
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 #include <stdint.h>
 
 #include "../../include/tyche_codec.h"
@@ -56,12 +58,37 @@ __device__ inline PageRef batch_page(const tyche_batch_t &b, size_t i) {
 // barrier is all that is required.
 #define WAVE_SYNC() __builtin_amdgcn_wave_barrier()
 
+// Resident one-wave workgroups per CU for a kernel at `lds` bytes of dynamic
+// LDS, as the runtime computes it (LDS granules, VGPRs, the per-CU limits).
+// The page loops size their grids to exactly this: one more workgroup per CU
+// than fits would run after a resident one finished its whole share of pages.
+inline size_t waves_per_cu(const void *kernel, size_t lds) {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kernel, 64, lds) == hipSuccess && n > 0) return (size_t)n;
+    const size_t granted = (lds + 511u) & ~(size_t)511u;
+    return granted ? std::max<size_t>(1, std::min<size_t>(32, (160 * 1024) / granted)) : 32;
+}
+
 hipError_t launch_lz4_decode(const tyche_batch_t &b, uint32_t in_cap, uint32_t out_cap, hipStream_t s);
 hipError_t launch_lz4_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream_t s);
 hipError_t launch_zstd_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream_t s);
 hipError_t launch_zlib_deflate(const tyche_batch_t &b, uint32_t in_cap, hipStream_t s);
 hipError_t launch_zlib_inflate(const tyche_batch_t &b, uint32_t out_cap, hipStream_t s);
 hipError_t launch_zstd_decode(const tyche_batch_t &b, uint32_t in_cap, uint32_t out_cap, hipStream_t s);
+// Dynamic page assignment.  The codec kernels run one-wave workgroups that loop
+// over pages; when a CU holds a number of waves that is not a multiple of its 4
+// SIMDs, the waves sharing a SIMD run slower than the lone ones, and static
+// striding (page += gridDim.x) leaves the lone waves idle at the end.  Instead
+// each wave starts at blockIdx.x and then claims pages from a per-launch
+// counter.  work_counter() hands out a zeroed counter for a launch on stream s
+// (a ring of device counters, reset with an async memset on that stream).
+unsigned *work_counter(hipStream_t s);
+__device__ __forceinline__ size_t claim_page(unsigned *counter, uint32_t lane) {
+    unsigned v = 0;
+    if (lane == 0) v = atomicAdd(counter, 1u);
+    return (size_t)__builtin_amdgcn_readfirstlane(v) + gridDim.x;
+}
+
 hipError_t launch_pagegen(void *dst, uint64_t stride, uint32_t page_len, uint64_t seed, uint64_t first,
                           size_t count, uint32_t dist, hipStream_t s);
 

@@ -31,6 +31,21 @@
 
 using namespace tyche;
 
+unsigned *tyche::work_counter(hipStream_t s) {
+    constexpr int kRing = 256;   // launches in flight at once stay far below this
+    static std::mutex mu;
+    static unsigned *ring[64] = {nullptr};
+    static unsigned next_slot[64] = {0};
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (dev < 0 || dev >= 64) return nullptr;
+    std::lock_guard<std::mutex> g(mu);
+    if (!ring[dev] && hipMalloc((void **)&ring[dev], kRing * sizeof(unsigned)) != hipSuccess) return nullptr;
+    unsigned *c = ring[dev] + (next_slot[dev]++ % kRing);
+    if (hipMemsetAsync(c, 0, sizeof(unsigned), s) != hipSuccess) return nullptr;
+    return c;
+}
+
 namespace {
 
 thread_local int t_device = 0;

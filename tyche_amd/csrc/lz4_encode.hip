@@ -148,7 +148,7 @@ __device__ int32_t encode_page(const uint8_t *in, uint32_t L, uint16_t *table, u
     return (int32_t)(op + total);
 }
 
-__global__ __launch_bounds__(64) void lz4_encode_kernel(tyche_batch_t b, uint32_t in_cap) {
+__global__ __launch_bounds__(64) void lz4_encode_kernel(tyche_batch_t b, uint32_t in_cap, unsigned *ctr) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t lane = threadIdx.x;
     uint16_t *table = (uint16_t *)smem;
@@ -162,7 +162,7 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel(tyche_batch_t b, uint32_
     PageRef p = batch_page(b, page);
     uint32_t head = stage_in(p.src, p.src_len <= in_cap ? p.src_len : 0, stage, lane, kWave);
     for (;;) {
-        const size_t next = page + stride;
+        const size_t next = ctr ? claim_page(ctr, lane) : page + stride;   // dynamic assignment (engine.h)
         PageRef pn;
         u32x4 pf[kPrefetchVec];
         uint32_t nhead = 0, nvec = 0;
@@ -226,9 +226,9 @@ hipError_t launch_lz4_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream_
         (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
         cus[dev] = n > 0 ? n : 256;
     }
-    const size_t per_cu = std::max<size_t>(1, std::min<size_t>(32, (160 * 1024) / lds));
+    const size_t per_cu = waves_per_cu((const void *)lz4_encode_kernel, lds);
     const size_t grid = std::min<size_t>(b.count, (size_t)(dev < 64 ? cus[dev] : 256) * per_cu);
-    hipLaunchKernelGGL(lz4_encode_kernel, dim3((unsigned)grid), dim3(kWave), lds, s, b, in_cap);
+    hipLaunchKernelGGL(lz4_encode_kernel, dim3((unsigned)grid), dim3(kWave), lds, s, b, in_cap, work_counter(s));
     return hipGetLastError();
 }
 

@@ -499,7 +499,8 @@ __device__ __forceinline__ void reader_init(BitReader &r, const PageRef &p, uint
     (void)lane;
 }
 
-__global__ __launch_bounds__(64) void zlib_inflate_kernel(tyche_batch_t b, uint32_t out_cap, uint32_t off_lens) {
+__global__ __launch_bounds__(64) void zlib_inflate_kernel(tyche_batch_t b, uint32_t out_cap, uint32_t off_lens,
+                                                          unsigned *ctr) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t lane = threadIdx.x;
     uint8_t *out = smem;
@@ -515,7 +516,7 @@ __global__ __launch_bounds__(64) void zlib_inflate_kernel(tyche_batch_t b, uint3
     r.wa = load_win(r, 0, lane);
     r.wb = load_win(r, 256, lane);
     for (;;) {
-        const size_t next = page + stride;
+        const size_t next = ctr ? claim_page(ctr, lane) : page + stride;   // dynamic assignment (engine.h)
         // the next page's first 512 stream bytes are loaded behind this page's decode
         PageRef pn;
         BitReader rn;
@@ -559,12 +560,10 @@ hipError_t launch_zlib_inflate(const tyche_batch_t &b, uint32_t out_cap, hipStre
         (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
         cus[dev] = n > 0 ? n : 256;
     }
-    int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)zlib_inflate_kernel, kWave, lds) !=
-            hipSuccess || per_cu <= 0)
-        per_cu = std::max<int>(1, (int)std::min<size_t>(32, (160 * 1024) / lds));
+    const size_t per_cu = waves_per_cu((const void *)zlib_inflate_kernel, lds);
     const size_t grid = std::min<size_t>(b.count, (size_t)(dev < 64 ? cus[dev] : 256) * (size_t)per_cu);
-    hipLaunchKernelGGL(zlib_inflate_kernel, dim3((unsigned)grid), dim3(kWave), lds, s, b, out_cap, off_lens);
+    hipLaunchKernelGGL(zlib_inflate_kernel, dim3((unsigned)grid), dim3(kWave), lds, s, b, out_cap, off_lens,
+                       work_counter(s));
     return hipGetLastError();
 }
 

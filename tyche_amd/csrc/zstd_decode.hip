@@ -660,12 +660,15 @@ __device__ bool huf_decode(const Work &W, int32_t cs, int32_t n, bool single, ui
     if (__ballot(lane < (single ? 1u : 4u) && !ok)) return false;
     const uint32_t act_n = single ? 1u : 4u;
     const uint32_t mc = rdlane(cnt, 0);   // stream 1 holds the most symbols
+    const uint32_t hsh = tlog == 12u ? 1u : 0u;   // the table is indexed by at most 11 bits
     for (uint32_t i = 0; i < mc; i++) {
         if (lane < act_n && i < cnt) {
             if (b.used > 52u) bitd_reload(b, in);
             const uint32_t v = (uint32_t)bitd_look_fast(b, tlog);
-            uint32_t e = W.huf[tlog == 12u ? v >> 1 : v];
-            if ((e >> 8) == 12u) e = W.hpair[v] | (12u << 8);   // a 12-bit code (tableLog 12 only)
+            // branch-free: both reads go out together; hpair only matters for a
+            // 12-bit code (tableLog 12), the mask keeps the other reads in bounds
+            const uint32_t e0 = W.huf[v >> hsh], ep = W.hpair[v & 255u];
+            const uint32_t e = (e0 >> 8) == 12u ? (ep | (12u << 8)) : e0;
             out[o0 + i] = (uint8_t)e;
             b.used += e >> 8;
         }
@@ -1169,7 +1172,8 @@ __host__ __device__ inline Layout make_layout(uint32_t in_cap, uint32_t out_cap)
     return l;
 }
 
-__global__ __launch_bounds__(64) void zstd_decode_kernel(tyche_batch_t b, uint32_t in_cap, uint32_t out_cap, Layout lay) {
+__global__ __launch_bounds__(64) void zstd_decode_kernel(tyche_batch_t b, uint32_t in_cap, uint32_t out_cap, Layout lay,
+                                                         unsigned *ctr) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t lane = threadIdx.x;
     Work W;
@@ -1184,7 +1188,8 @@ __global__ __launch_bounds__(64) void zstd_decode_kernel(tyche_batch_t b, uint32
     W.next = (uint16_t *)(smem + lay.off_next);
     W.w = smem + lay.off_w;
     uint8_t *stage = smem + lay.off_in;
-    for (size_t page = blockIdx.x; page < b.count; page += gridDim.x) {
+    for (size_t page = blockIdx.x; page < b.count;
+         page = ctr ? claim_page(ctr, lane) : page + gridDim.x) {   // dynamic assignment (engine.h)
         const PageRef p = batch_page(b, page);
         int32_t rv;
         if (p.src_len > in_cap || p.dst_cap > out_cap) {
@@ -1221,9 +1226,10 @@ hipError_t launch_zstd_decode(const tyche_batch_t &b, uint32_t in_cap, uint32_t 
         (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
         cus[dev] = n > 0 ? n : 256;
     }
-    const size_t per_cu = std::max<size_t>(1, std::min<size_t>(32, (160 * 1024) / lay.total));
+    const size_t per_cu = waves_per_cu((const void *)zstd_decode_kernel, lay.total);
     const size_t grid = std::min<size_t>(b.count, (size_t)(dev < 64 ? cus[dev] : 256) * per_cu);
-    hipLaunchKernelGGL(zstd_decode_kernel, dim3((unsigned)grid), dim3(kWave), lay.total, s, b, in_cap, out_cap, lay);
+    hipLaunchKernelGGL(zstd_decode_kernel, dim3((unsigned)grid), dim3(kWave), lay.total, s, b, in_cap, out_cap, lay,
+                       work_counter(s));
     return hipGetLastError();
 }
 

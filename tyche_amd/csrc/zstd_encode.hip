@@ -541,7 +541,7 @@ __device__ __forceinline__ int32_t encode_page(const uint8_t *in, uint32_t L, ui
     return (int32_t)e.op;
 }
 
-__global__ __launch_bounds__(64) void zstd_encode_kernel(tyche_batch_t b, uint32_t in_cap) {
+__global__ __launch_bounds__(64) void zstd_encode_kernel(tyche_batch_t b, uint32_t in_cap, unsigned *ctr) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t lane = threadIdx.x;
     uint16_t *table = (uint16_t *)smem;
@@ -558,7 +558,7 @@ __global__ __launch_bounds__(64) void zstd_encode_kernel(tyche_batch_t b, uint32
     PageRef p = batch_page(b, page);
     uint32_t head = stage_in(p.src, p.src_len <= in_cap ? p.src_len : 0, stage, lane, kWave);
     for (;;) {
-        const size_t next = page + stride;
+        const size_t next = ctr ? claim_page(ctr, lane) : page + stride;   // dynamic assignment (engine.h)
         PageRef pn;
         u32x4 pf[kPrefetchVec];
         uint32_t nhead = 0, nvec = 0;
@@ -623,9 +623,9 @@ hipError_t launch_zstd_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream
         (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
         cus[dev] = n > 0 ? n : 256;
     }
-    const size_t per_cu = std::max<size_t>(1, std::min<size_t>(32, (160 * 1024) / lds));
+    const size_t per_cu = waves_per_cu((const void *)zstd_encode_kernel, lds);
     const size_t grid = std::min<size_t>(b.count, (size_t)(dev < 64 ? cus[dev] : 256) * per_cu);
-    hipLaunchKernelGGL(zstd_encode_kernel, dim3((unsigned)grid), dim3(kWave), lds, s, b, in_cap);
+    hipLaunchKernelGGL(zstd_encode_kernel, dim3((unsigned)grid), dim3(kWave), lds, s, b, in_cap, work_counter(s));
     return hipGetLastError();
 }
 
