@@ -445,15 +445,34 @@ __global__ __launch_bounds__(64) void lz4_decode_serial_kernel(tyche_batch_t b, 
 
 constexpr uint32_t kPrefetchVec = 8;   // 16-byte vectors per lane prefetched for the next page (8 KiB)
 
-// Next claimed page whose stream length is in [lo, hi] (claims skip the others).
-__device__ __forceinline__ size_t next_claimed(const tyche_batch_t &b, unsigned *ctr, uint32_t lane, uint32_t lo,
-                                               uint32_t hi) {
-    for (;;) {
-        const size_t i = claim_page(ctr, lane);
-        if (i >= b.count || !b.src_lengths) return i;
+// Dynamic assignment in chunks of K <= 64 pages: chunk c is pages [c*K, c*K+K),
+// the first chunk of a wave is blockIdx.x, later ones are claimed (engine.h).
+// A chunk's pages whose stream length is in [lo, hi] are taken one by one
+// (mask); the others belong to the other size class.
+struct Claims {
+    size_t base;
+    uint64_t mask;
+};
+__device__ __forceinline__ void load_chunk(const tyche_batch_t &b, size_t c, uint32_t K, uint32_t lo, uint32_t hi,
+                                           uint32_t lane, Claims &cl) {
+    cl.base = c * K;
+    const size_t i = cl.base + lane;
+    bool take = lane < K && i < b.count;
+    if (take && b.src_lengths) {
         const uint32_t l = ld_meta(b.src_lengths, i);
-        if (l >= lo && l <= hi) return i;
+        take = l >= lo && l <= hi;
     }
+    cl.mask = __ballot(take);
+}
+__device__ __forceinline__ size_t next_chunked(const tyche_batch_t &b, unsigned *ctr, uint32_t K, uint32_t lo,
+                                               uint32_t hi, uint32_t lane, Claims &cl) {
+    while (cl.mask == 0) {
+        if (cl.base >= b.count) return b.count;
+        load_chunk(b, claim_page(ctr, lane), K, lo, hi, lane, cl);
+    }
+    const uint32_t j = (uint32_t)__builtin_ctzll(cl.mask);
+    cl.mask &= cl.mask - 1ull;
+    return cl.base + j;
 }
 
 // First page at or after i (step stride) whose stream length is in [lo, hi].
@@ -472,21 +491,18 @@ __device__ __forceinline__ size_t next_in_class(const tyche_batch_t &b, size_t i
 // length lies in [cls_lo, cls_hi] are taken (launch_lz4_decode's size classes).
 __global__ __launch_bounds__(64) void lz4_decode_wave_kernel(tyche_batch_t b, uint32_t in_cap, uint32_t out_cap,
                                                              uint32_t off_in, uint32_t cls_lo, uint32_t cls_hi,
-                                                             unsigned *ctr) {
+                                                             unsigned *ctr, uint32_t chunk) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t lane = threadIdx.x;
     uint8_t *out = smem;                 // page window [0, off_in): output, parse stamps, token positions
     uint8_t *stage = smem + off_in;
     const size_t stride = gridDim.x;
 
-    // the first page is blockIdx.x when it is in the class; claims start past the grid
     size_t page;
+    Claims cl;
     if (ctr) {
-        page = blockIdx.x;
-        if (page < b.count && b.src_lengths) {
-            const uint32_t l0 = ld_meta(b.src_lengths, page);
-            if (l0 < cls_lo || l0 > cls_hi) page = next_claimed(b, ctr, lane, cls_lo, cls_hi);
-        }
+        load_chunk(b, blockIdx.x, chunk, cls_lo, cls_hi, lane, cl);
+        page = next_chunked(b, ctr, chunk, cls_lo, cls_hi, lane, cl);
     } else {
         page = next_in_class(b, blockIdx.x, stride, cls_lo, cls_hi);
     }
@@ -495,9 +511,9 @@ __global__ __launch_bounds__(64) void lz4_decode_wave_kernel(tyche_batch_t b, ui
     uint32_t head = stage_in(p.src, p.src_len <= in_cap ? p.src_len : 0, stage, lane, kWave);
     for (;;) {
         PROF_DECL
-        // dynamic assignment (engine.h) for the launches that take (nearly) every page;
-        // the long-stream class keeps static striding (most of its claims would be skips)
-        const size_t next = ctr ? next_claimed(b, ctr, lane, cls_lo, cls_hi)
+        // dynamic assignment (engine.h): single pages for a launch that takes
+        // (nearly) every page, chunks for the long-stream class
+        const size_t next = ctr ? next_chunked(b, ctr, chunk, cls_lo, cls_hi, lane, cl)
                                 : next_in_class(b, page + stride, stride, cls_lo, cls_hi);
         // ---- prefetch the next page's stream (first 8 KiB) into registers
         PageRef pn;
@@ -596,13 +612,13 @@ hipError_t launch_lz4_decode(const tyche_batch_t &b, uint32_t in_cap, uint32_t o
         return ((std::max(out_cap, cap + 4u) + 16u + 15u) & ~15u) + ((cap + 16u + kPad + 15u) & ~15u) + TYCHE_LDS_EXTRA;
     };
     auto granted = [](size_t l) -> size_t { return (l + 511u) & ~(size_t)511u; };
-    auto launch = [&](uint32_t cap, uint32_t lo, uint32_t hi, bool dynamic) {
+    auto launch = [&](uint32_t cap, uint32_t lo, uint32_t hi, uint32_t chunk) {
         const size_t l = lds_for(cap);
         const uint32_t win = (std::max(out_cap, cap + 4u) + 16u + 15u) & ~15u;
         const size_t per_cu = waves_per_cu((const void *)lz4_decode_wave_kernel, l);
         const size_t grid = std::min<size_t>(b.count, ncu * per_cu);
         hipLaunchKernelGGL(lz4_decode_wave_kernel, dim3((unsigned)grid), dim3(kWave), l, s, b, cap, out_cap, win, lo, hi,
-                           dynamic ? work_counter(s) : nullptr);
+                           chunk ? work_counter(s) : nullptr, chunk);
     };
     // Size classes: the decoder is latency-bound and its residency is set by
     // the LDS per wave, i.e. by the longest stream of the batch.  When streams
@@ -612,6 +628,12 @@ hipError_t launch_lz4_decode(const tyche_batch_t &b, uint32_t in_cap, uint32_t o
     // instead of 6, 129.6 -> 121.8 ms per 1M pages).
     // Each wave skips the pages of the other class.  TYCHE_DECODE_CLASSES=0
     // turns the split off (A/B timing).
+#ifndef TYCHE_CLASS_CHUNK
+#define TYCHE_CLASS_CHUNK 1
+#endif
+    // chunk of the long-stream class (1M bench pages, ms: static 118.9, chunks of
+    // 64: 117.4, 8: 111.1, 2: 110.2, 1: 109.9 -- skipped claims are cheap)
+    constexpr uint32_t kClassChunk = TYCHE_CLASS_CHUNK;   // static striding when 0
     static const int split_env = getenv("TYCHE_DECODE_CLASSES") ? atoi(getenv("TYCHE_DECODE_CLASSES")) : 1;
     const size_t waves = split_env && b.src_lengths && b.count >= 8192
                              ? waves_per_cu((const void *)lz4_decode_wave_kernel, lds) : 32;
@@ -621,12 +643,12 @@ hipError_t launch_lz4_decode(const tyche_batch_t &b, uint32_t in_cap, uint32_t o
         while (T > 16u && granted(lds_for(T)) > target) T -= 16u;
         if (granted(lds_for(T)) <= target && T >= in_cap / 2u && T < in_cap &&
             waves_per_cu((const void *)lz4_decode_wave_kernel, lds_for(T)) > waves) {
-            launch(T, 0u, T, true);
-            launch(in_cap, T + 1u, 0xFFFFFFFFu, false);
+            launch(T, 0u, T, 1u);
+            launch(in_cap, T + 1u, 0xFFFFFFFFu, kClassChunk);
             return hipGetLastError();
         }
     }
-    launch(in_cap, 0u, 0xFFFFFFFFu, true);
+    launch(in_cap, 0u, 0xFFFFFFFFu, 1u);
     return hipGetLastError();
 }
 
