@@ -35,6 +35,9 @@
 #include <stdint.h>
 #include <string.h>
 #include "oracle.h"
+#ifdef ZSTD_SEQ_TRACE
+void zstd_seq_trace(uint32_t llc, uint32_t mlc, uint32_t ofc, size_t ll, size_t ml, size_t off);
+#endif
 
 #define ZE_GENERIC (-1)
 #define ZE_PREFIX (-10)
@@ -596,6 +599,9 @@ static int decode_sequences(dctx_t *d, uint8_t *ostart, uint8_t *op0, uint8_t *o
             }
             const size_t ml = ML_BASE[mlc] + ((mlc > 31) ? (size_t)bitd_read_fast(&b, ML_BITS[mlc]) : 0);
             const size_t ll = LL_BASE[llc] + ((llc > 15) ? (size_t)bitd_read_fast(&b, LL_BITS[llc]) : 0);
+#ifdef ZSTD_SEQ_TRACE   /* tools/zstd_seq_stats.c only */
+            zstd_seq_trace(llc, mlc, ofc, ll, ml, off);
+#endif
             if (LL_BITS[llc] + ML_BITS[mlc] + ofc > 64 - 7 - (9 + 9 + 8)) bitd_reload(&b);
             {   /* FSE_updateState x3 (LL, ML, OF) */
                 const fse_cell_t a = d->ll.cell[sll];

@@ -150,11 +150,14 @@ __device__ __forceinline__ void decode_record(const uint2 *rec, uint32_t n, uint
 // false to abort.  Returns the anchor where the last literal run starts, or
 // 0xFFFFFFFF if the sink aborted.
 //
-// kRepCand (zstd): every position also tries the repeat-offset candidate
-// pos - R, R = the offset of the last match selected before this block (zstd's
-// fast parse checks the repeat offset first, zstd_compress.c:951-958), and
-// takes it when it verifies and is at least as long as the hash candidate's
-// match: a repeat offset costs a few bits instead of ~10 (zstd_encode.hip).
+// kRepCand (zstd): every position also tries the repeat-offset candidates
+// pos - R and pos - R2, (R, R2) = the first two repeat offsets after the
+// matches selected before this block (zstd's fast parse checks repeat offset 1
+// at ip+1 before the hash candidate at ip, zstd_compress.c:951-958, and
+// repeat offset 2 right after each match, :985-994).  A repeat candidate is
+// taken when it verifies and is at least as long as the hash candidate's
+// match, and a position whose successor has a repeat match starts none of its
+// own: a repeat offset costs a few bits instead of ~10 (zstd_encode.hip).
 template <bool kRepCand = false, typename Sink>
 __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *table, uint2 *rec, uint32_t lane,
                                       Sink &sink) {
@@ -167,7 +170,7 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
     uint32_t cursor = 0;     // matches may start here (end of the last match)
     uint32_t nacc = 0;       // records accumulated since the last hand-off
     uint32_t blk = 0;        // current 64-position block
-    uint32_t R = 1;          // repeat offset (kRepCand): zstd's initial repeat offset 1
+    uint32_t R = 1, R2 = 4;  // repeat offsets 1 and 2 (kRepCand): zstd's initial {1, 4}
     bool done = false;
     PHASE_INIT();
     for (; !done && blk <= mflimit; blk = max(blk + kWave, cursor & ~(kWave - 1))) {
@@ -195,11 +198,12 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
             const uint32_t x = pw.fw[k] ^ cw.fw[k];
             if (x) n = 4u + 4u * (uint32_t)k + ((uint32_t)__builtin_ctz(x) >> 3);
         }
+        bool rok = false;
         if (kRepCand) {
             // the repeat-offset candidate (consecutive windows: cheap loads)
             const uint32_t rc = pos >= R ? pos - R : 0u;
             const Window rw = lds_window(A, min(rc, mflimit) + ib);
-            const bool rok = live & (pos >= R) & (rw.w0 == v);
+            rok = live & (pos >= R) & (rw.w0 == v);
             uint32_t rn = 4u + kProbe;
 #pragma unroll
             for (int k = (int)kProbeWords - 1; k >= 0; k--) {
@@ -209,12 +213,32 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
 #ifndef TYCHE_REP_SLACK
 #define TYCHE_REP_SLACK 0
 #endif
+            // repeat offset 2 (the other offset of two alternating ones)
+            const uint32_t rc2 = pos >= R2 ? pos - R2 : 0u;
+            const Window rw2 = lds_window(A, min(rc2, mflimit) + ib);
+#ifndef TYCHE_REP2
+#define TYCHE_REP2 1
+#endif
+            const bool rok2 = TYCHE_REP2 && live & (pos >= R2) & (rw2.w0 == v) & (R2 != R);
+            uint32_t rn2 = 4u + kProbe;
+#pragma unroll
+            for (int k = (int)kProbeWords - 1; k >= 0; k--) {
+                const uint32_t x = pw.fw[k] ^ rw2.fw[k];
+                if (x) rn2 = 4u + 4u * (uint32_t)k + ((uint32_t)__builtin_ctz(x) >> 3);
+            }
             if (rok && (!ok || rn + TYCHE_REP_SLACK >= n)) {
                 cand = rc;
                 cw = rw;
                 n = rn;
                 ok = true;
             }
+            if (rok2 && (!ok || rn2 + TYCHE_REP_SLACK >= n) && !(rok && rn >= rn2)) {
+                cand = rc2;
+                cw = rw2;
+                n = rn2;
+                ok = true;
+            }
+            rok |= rok2;
         }
         const uint32_t xb = pw.back ^ cw.back;
         const uint32_t e = min(matchlimit, pos + kMinMatch + kProbe);
@@ -228,7 +252,18 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
         // parse position is one v_readlane per selected match.  The parse
         // position is always inside the block (blk >= cursor & ~63), and no mask
         // bit lies past mflimit, so a match ending there ends the walk.
-        const uint64_t mall = (TYCHE_EABLATE & 4) ? 0ull : __ballot(ok);
+        uint64_t mall = (TYCHE_EABLATE & 4) ? 0ull : __ballot(ok);
+#ifndef TYCHE_REP_NEXT
+#define TYCHE_REP_NEXT 1
+#endif
+        if (kRepCand && TYCHE_REP_NEXT) {
+            // zstd's fast parse tries the repeat offset at ip+1 before the hash
+            // candidate at ip (zstd_compress.c:951-958): a position whose
+            // successor has a repeat match starts no match of its own unless
+            // it is a repeat match itself
+            const uint64_t mrep = __ballot(rok);
+            mall &= ~(mrep >> 1) | mrep;
+        }
         PHASE(0);
         PHASE_COUNT(8);
         const uint32_t at = cursor > blk ? cursor - blk : 0u;
@@ -250,11 +285,18 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
                 at_li = li;
                 sel |= 1ull << li;
                 PHASE_COUNT(9);
+                if (kRepCand) {
+                    // repeat history of the selected matches (a new offset shifts it)
+                    const uint32_t off = blk + li - rdlane(cand, li);
+                    if (off != R) {
+                        R2 = R;
+                        R = off;
+                    }
+                }
                 li = rdlane(nxt, li);
             } while (li < kWave);
             if (li == kWave) {
                 end = rdlane(endp, at_li);
-                if (kRepCand) R = blk + at_li - rdlane(cand, at_li);
                 break;
             }
             // reached the probe limit: extend with the whole wave, then look for
@@ -266,7 +308,6 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
             PHASE_COUNT(6);
             if (lane == at_li) len = ln;
             end = mp + ln;
-            if (kRepCand) R = mp - mc;
             const uint32_t rel = end - blk;
             const uint64_t r = rel < kWave ? mall & (~0ull << rel) : 0ull;
             if (r == 0) break;

@@ -3,9 +3,9 @@
 // level 1, src/zstd/zstd_compress.c:2721).  The output is a standard zstd frame
 // that the reference's ZSTD_decompress (zstd_decompress.c:1459) restores
 // bit-exactly; it is not required to be the bytes zstd 1.1.2 emits (SURVEY §8a
-// A8).  Its ratio is below level 1's because of the parse (greedy, one hash
-// candidate), not the entropy stage: literals are Huffman-coded and the
-// sequences get per-block FSE tables and repeat offsets (§8f rank 4).
+// A8).  Literals are Huffman-coded, the sequences get per-block FSE tables and
+// all three repeat offsets (§8f rank 4); the parse (lz_parse.h) tries both
+// leading repeat offsets beside the hash candidate.
 //
 // Frame layout (zstd_compress.c:2334-2376): magic, a single-segment frame
 // header with the content size (no checksum, no dictionary), then blocks of at
@@ -99,7 +99,8 @@ __device__ __forceinline__ SeqCode seq_code(uint32_t ll, uint32_t ml, uint32_t o
 }
 
 // ------------------------------------------------------------ block emission
-// Sequences of the current block live in LDS: seq[i] = (ll | off << 16, ml).
+// Sequences of the current block live in LDS: seq[i] = (ll | off << 16, ml | rc << 16),
+// rc = the repeat code chosen at emission (0: the offset is sent as off + 3).
 struct Enc {
     const uint8_t *in;   // page (LDS)
     uint8_t *dst;        // output (global)
@@ -112,20 +113,67 @@ struct Enc {
     uint32_t *htab;      // 256 entries: literal histogram, then Huffman code | length << 16
     uint8_t *wts;        // 256 Huffman weights
     uint32_t *stage;     // 128 dwords of pending stream bits (the parse's record area, free here)
-    uint32_t rep;        // repeat offset 1 of the frame so far (initial {1, 4, 8}, zstd_internal.h:73)
+    uint32_t r0, r1, r2; // the decoder's repeat offsets after the blocks emitted so far (initial {1, 4, 8},
+                         // zstd_internal.h:73); raw blocks leave them unchanged
     bool fail;
 };
 
-// Codes of sequence i of the block.  Only repeat offset 1 is used, and only
-// with a nonzero literal length (Offset_Value 1, history unchanged); any other
-// offset is sent as Offset_Value = offset + 3 and becomes repeat offset 1.  So
-// repeat offset 1 before sequence i is always the previous sequence's offset
-// (or the frame's, across blocks) and the choice is lane-parallel.
+// Codes of sequence i of the block, after resolve_repeats.
 __device__ __forceinline__ SeqCode seq_code_at(const Enc &e, uint32_t i) {
     const uint2 r = e.seq[i];
-    const uint32_t ll = r.x & 0xFFFFu, off = r.x >> 16;
-    const uint32_t prev = i ? (e.seq[i - 1].x >> 16) : e.rep;
-    return seq_code(ll, r.y, (ll > 0u && off == prev) ? 1u : off + 3u);
+    const uint32_t ll = r.x & 0xFFFFu, off = r.x >> 16, rc = r.y >> 16;
+    return seq_code(ll, r.y & 0xFFFFu, rc ? rc : off + 3u);
+}
+
+// Offset_Value of every sequence of the block against the repeat history
+// (ZSTD_decodeSequence's rules, zstd_decompress.c:897-915): with a literal
+// length, 1/2/3 name repeat offsets 1/2/3; without one, 1/2 name repeat offsets
+// 2/3 (zstd's "immediate repcode", zstd_compress.c:985-994).  Using repeat
+// offset 1 with a literal length changes nothing (event E), repeat 2 swaps the
+// first two, anything else shifts the history.  The scan is lane-parallel:
+//   r0 before i = off[i-1] (every case leaves the offset just used in front);
+//   r1 before i = off[p-1] for the last p < i that is not an E event (E keeps
+//                 r1, every other case sets it to the previous r0);
+//   r2 before i = r1 before q for the last q < i that shifted (!E and
+//                 off[q] != r1 before q; swaps and E keep r2).
+// Returns the history after the block through h0..h2 (committed only if the
+// block is emitted compressed: raw blocks leave the decoder's history alone).
+__device__ __forceinline__ void resolve_repeats(const Enc &e, uint32_t n, uint32_t lane, uint32_t &h0, uint32_t &h1,
+                                                uint32_t &h2) {
+    uint32_t c0 = e.r0, c1 = e.r1, c2 = e.r2;
+    const uint64_t below = (1ull << lane) - 1ull;
+    for (uint32_t g = 0; g < n; g += kWave) {
+        const uint32_t i = g + lane;
+        const uint2 r = i < n ? e.seq[i] : make_uint2(0u, 0u);
+        const uint32_t ll = r.x & 0xFFFFu, off = r.x >> 16;
+        const uint32_t up = (uint32_t)__shfl((int)off, (int)(lane ? lane - 1u : 0u));
+        const uint32_t r0b = lane ? up : c0;
+        const bool ev = ll > 0u && off == r0b;
+        const uint64_t ne = __ballot(!ev) & below;
+        const int p = ne ? 63 - __builtin_clzll(ne) : 0;
+        const uint32_t tp = (uint32_t)__shfl((int)r0b, p);
+        const uint32_t r1b = ne ? tp : c1;
+        const bool sh = !ev && off != r1b;
+        const uint64_t sm = __ballot(sh) & below;
+        const int q = sm ? 63 - __builtin_clzll(sm) : 0;
+        const uint32_t tq = (uint32_t)__shfl((int)r1b, q);
+        const uint32_t r2b = sm ? tq : c2;
+        uint32_t rc;
+        if (ll) rc = off == r0b ? 1u : off == r1b ? 2u : off == r2b ? 3u : 0u;
+        else rc = off == r1b ? 1u : off == r2b ? 2u : 0u;
+        if (i < n) e.seq[i].y = (r.y & 0xFFFFu) | (rc << 16);
+        // the history after the group's last sequence
+        const uint32_t last = min(n - g, kWave) - 1u;
+        const uint32_t o_l = rdlane(off, last), r0_l = rdlane(r0b, last), r1_l = rdlane(r1b, last),
+                       r2_l = rdlane(r2b, last);
+        const bool ev_l = rdlane((uint32_t)ev, last) != 0u, sh_l = rdlane((uint32_t)sh, last) != 0u;
+        c0 = o_l;
+        c1 = ev_l ? r1_l : r0_l;
+        c2 = sh_l ? r1_l : r2_l;
+    }
+    h0 = c0;
+    h1 = c1;
+    h2 = c2;
 }
 
 // Calls f(j, byte) for every literal j of the block (literal-section order),
@@ -140,7 +188,7 @@ __device__ void for_each_literal(const Enc &e, uint32_t n, uint32_t trail, uint3
         if (i < n) {
             const uint2 r = e.seq[i];
             ll = r.x & 0xFFFFu;
-            ml = r.y;
+            ml = r.y & 0xFFFFu;
         } else if (i == n) {
             ll = trail;
         }
@@ -329,7 +377,7 @@ __device__ __forceinline__ bool emit_block(Enc &e, uint32_t bend, bool last, uin
         if (i < n) {
             const uint2 r = e.seq[i];
             ll = r.x & 0xFFFFu;
-            ml = r.y;
+            ml = r.y & 0xFFFFu;
             const SeqCode c = seq_code(ll, ml, (r.x >> 16) + 3u);   // bound: no repeat offsets
             xb = c.llb + c.mlb + c.ofc;
         }
@@ -379,7 +427,14 @@ __device__ __forceinline__ bool emit_block(Enc &e, uint32_t bend, bool last, uin
         e.dst[o + lane] = (uint8_t)(h >> (8u * lane));
     }
     o += nsh;
+    uint32_t h0 = e.r0, h1 = e.r1, h2 = e.r2;
     if (n) {
+#ifndef TYCHE_NO_RESOLVE
+        resolve_repeats(e, n, lane, h0, h1, h2);
+#else
+        for (uint32_t i = lane; i < n; i += kWave) e.seq[i].y &= 0xFFFFu;   // timing ablation: raw offsets only
+#endif
+        __builtin_amdgcn_wave_barrier();
         // ---- code histograms (htab is free once the literals are out): LL at 0, ML at 64, OF at 128
         for (uint32_t k = lane; k < 192u; k += kWave) e.htab[k] = 0;
         __builtin_amdgcn_wave_barrier();
@@ -479,12 +534,14 @@ __device__ __forceinline__ bool emit_block(Enc &e, uint32_t bend, bool last, uin
         huf::bw_flush(b, e.dst, lane);
         o = b.ptr + (b.pos > 0 ? 1u : 0u);
         if (b.pos > 0 && lane == 0) e.dst[b.ptr] = (uint8_t)b.c;
-        e.rep = e.seq[n - 1].x >> 16;   // the decoder's repeat offset 1 after this block
     }
     const uint32_t csize = o - (hdr + 3u);
     const uint32_t bh = (last ? 1u : 0u) | (2u << 1) | (csize << 3);
     if (lane < 3) e.dst[hdr + lane] = (uint8_t)(bh >> (8u * lane));
     e.op = o;
+    e.r0 = h0;
+    e.r1 = h1;
+    e.r2 = h2;
     return true;
 }
 
@@ -515,7 +572,9 @@ __device__ __forceinline__ int32_t encode_page(const uint8_t *in, uint32_t L, ui
     e.bstart = 0;
     e.cursor = 0;
     e.map = map;
-    e.rep = 1u;
+    e.r0 = 1u;
+    e.r1 = 4u;
+    e.r2 = 8u;
     e.htab = htab;
     e.wts = wts;
     e.stage = (uint32_t *)rec;
