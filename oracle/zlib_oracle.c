@@ -20,6 +20,10 @@
 #include <stdint.h>
 #include <string.h>
 #include "oracle.h"
+#ifdef ZLIB_SYM_TRACE
+void zlib_sym_trace(int len, int dist);   /* tools/zlib_sym_stats.c only */
+void zlib_block_trace(const uint8_t *lens, int nlen, int ndist, int type);
+#endif
 
 #define Z_OK 0
 #define Z_DATA_ERROR (-3)
@@ -143,6 +147,9 @@ int oracle_zlib_uncompress(const uint8_t *src, int srclen, uint8_t *dst, int dst
             build(&lencode, lens, 288, 1);
             for (i = 0; i < 32; i++) lens[i] = 5;     /* 30, 31 complete the code; they decode as invalid */
             build(&distcode, lens, 32, 2);
+#ifdef ZLIB_SYM_TRACE
+            zlib_block_trace(lens, 288, 32, 1);
+#endif
         } else {
             static const uint8_t order[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
             int nlen = (int)need(&s, 5) + 257, ndist = (int)need(&s, 5) + 1, ncode = (int)need(&s, 4) + 4;
@@ -175,6 +182,9 @@ int oracle_zlib_uncompress(const uint8_t *src, int srclen, uint8_t *dst, int dst
             if (lens[256] == 0) return Z_DATA_ERROR;    /* no end-of-block code */
             if (build(&lencode, lens, nlen, 1)) return Z_DATA_ERROR;
             if (build(&distcode, lens + nlen, ndist, 2)) return Z_DATA_ERROR;
+#ifdef ZLIB_SYM_TRACE
+            zlib_block_trace(lens, nlen, ndist, 2);
+#endif
         }
         for (;;) {
             int sym = decode(&s, &lencode);
@@ -182,6 +192,9 @@ int oracle_zlib_uncompress(const uint8_t *src, int srclen, uint8_t *dst, int dst
             if (sym < 256) {
                 if (op >= dstcap) return Z_BUF_ERROR;
                 dst[op++] = (uint8_t)sym;
+#ifdef ZLIB_SYM_TRACE
+                zlib_sym_trace(0, sym);
+#endif
                 continue;
             }
             if (sym == 256) break;
@@ -193,6 +206,9 @@ int oracle_zlib_uncompress(const uint8_t *src, int srclen, uint8_t *dst, int dst
             int dist = kDistBase[ds] + (int)need(&s, kDistExtra[ds]);
             if (s.overrun) return Z_DATA_ERROR;
             if (dist > op) return Z_DATA_ERROR;         /* invalid distance too far back */
+#ifdef ZLIB_SYM_TRACE
+            zlib_sym_trace(len, dist);
+#endif
             for (int i = 0; i < len; i++) {
                 if (op >= dstcap) return Z_BUF_ERROR;
                 dst[op] = dst[op - dist];

@@ -49,17 +49,221 @@ __device__ __forceinline__ uint32_t shannon_len(uint32_t c, uint32_t total) {
     return l;
 }
 
+// Optimal (Huffman) code lengths of the used symbols, unlimited (at most 63).
+// Counts are ranked by (count, symbol) lane-parallel and placed in LDS in
+// ascending order, then the in-place minimum-redundancy construction of Moffat
+// and Katajainen runs on that array as wave-uniform code: pass 1 pairs the two
+// lightest items left to right (leaf or earlier internal node), storing parent
+// indices; pass 2 turns them into internal-node depths; pass 3 hands out leaf
+// depths from the heaviest leaf down.  Lengths are then limited to maxbits
+// (<= 15) on the per-length counts.  sc: 128 R words of LDS scratch.  Returns
+// false if the lengths could not be made (the caller falls back to Shannon's).
+template <int R>
+__device__ bool huffman_lengths(const uint32_t (&c)[R], uint32_t maxbits, uint32_t (&l)[R], uint32_t *sc,
+                                uint32_t lane) {
+    uint32_t key[R], rank[R];
+#pragma unroll
+    for (int j = 0; j < R; j++) {
+        key[j] = c[j] ? (c[j] << 9) | (lane + 64u * (uint32_t)j) : 0xFFFFFFFFu;
+        rank[j] = 0;
+    }
+    uint32_t n = 0;
+#pragma unroll
+    for (int jj = 0; jj < R; jj++) {
+        uint64_t m = __ballot(key[jj] != 0xFFFFFFFFu);
+        n += (uint32_t)__popcll(m);
+        while (m) {
+            const uint32_t ln = (uint32_t)__builtin_ctzll(m);
+            m &= m - 1ull;
+            const uint32_t k = rdlane(key[jj], ln);
+#pragma unroll
+            for (int j = 0; j < R; j++) rank[j] += k < key[j] ? 1u : 0u;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < R; j++)
+        if (c[j]) sc[rank[j]] = c[j];
+    __builtin_amdgcn_wave_barrier();
+    auto rd = [&](uint32_t i) { return __builtin_amdgcn_readfirstlane(sc[i]); };
+    auto wr = [&](uint32_t i, uint32_t v) {
+        if (lane == 0) sc[i] = v;
+        __builtin_amdgcn_wave_barrier();
+    };
+    if (n >= 2u) {
+        // pass 1: weights then parents
+        // (at the start of step nx, root <= nx - 1 and leaf >= nx + 1, so the
+        // cached leaf weight vl stays valid and A[nx] is written last)
+        wr(0, rd(0) + rd(1));
+        uint32_t root = 0, leaf = 2;
+        uint32_t vl = n > 2u ? rd(2) : 0u;
+        for (uint32_t nx = 1; nx < n - 1u; nx++) {
+            uint32_t vr = rd(root), w;
+            if (leaf >= n || vr < vl) {
+                w = vr;
+                wr(root, nx);
+                root++;
+                if (root < nx) vr = rd(root);
+            } else {
+                w = vl;
+                leaf++;
+                if (leaf < n) vl = rd(leaf);
+            }
+            if (leaf >= n || (root < nx && vr < vl)) {
+                w += vr;
+                wr(root, nx);
+                root++;
+            } else {
+                w += vl;
+                leaf++;
+                if (leaf < n) vl = rd(leaf);
+            }
+            wr(nx, w);
+        }
+        // pass 2: internal depths by pointer jumping (lane-parallel, 9 rounds
+        // cover any depth < 512): D[t] = depth so far, P[t] = ancestor
+        uint32_t *D = sc + 64u * R;
+        uint32_t d[R], pp[R];
+#pragma unroll
+        for (int k = 0; k < R; k++) {
+            const uint32_t t = lane + 64u * (uint32_t)k;
+            const bool in = t < n - 2u;                 // internal, not the root
+            pp[k] = in ? sc[t] : t;
+            d[k] = in ? 1u : 0u;
+        }
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int k = 0; k < R; k++) {
+            const uint32_t t = lane + 64u * (uint32_t)k;
+            if (t < n - 1u) {
+                D[t] = d[k];
+                sc[t] = pp[k];
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        for (int round = 0; round < 9; round++) {
+            uint32_t nd[R], np[R];
+#pragma unroll
+            for (int k = 0; k < R; k++) {
+                const uint32_t t = lane + 64u * (uint32_t)k;
+                const uint32_t a = t < n - 1u ? pp[k] : 0u;
+                nd[k] = d[k] + (t < n - 1u ? D[a] : 0u);
+                np[k] = t < n - 1u ? sc[a] : 0u;
+            }
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int k = 0; k < R; k++) {
+                const uint32_t t = lane + 64u * (uint32_t)k;
+                d[k] = nd[k];
+                pp[k] = np[k];
+                if (t < n - 1u) {
+                    D[t] = d[k];
+                    sc[t] = pp[k];
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+        // pass 3: leaves per depth from internal nodes per depth (a node at
+        // depth x has two children at x + 1), folded at maxbits
+        uint32_t *hist = D;                            // 64 words, D is read out
+        hist[lane] = 0;
+        __builtin_amdgcn_wave_barrier();
+        bool deep = false;
+#pragma unroll
+        for (int k = 0; k < R; k++) {
+            const uint32_t t = lane + 64u * (uint32_t)k;
+            if (t < n - 1u) {
+                deep |= d[k] > 62u;
+                atomicAdd(&hist[min(d[k], 62u)], 1u);
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (__ballot(deep)) return false;
+        const uint32_t ci = hist[lane];
+        const uint32_t cprev = (uint32_t)__shfl((int)ci, (int)(lane ? lane - 1u : 0u));
+        const uint32_t leaves = lane ? 2u * cprev - ci : 0u;  // leaves at depth = lane
+        uint32_t bl[16];
+        uint32_t over = 0;
+        {
+            uint32_t ov = lane > maxbits ? leaves : 0u;
+            over = (uint32_t)wave_sum(ov);
+        }
+#pragma unroll
+        for (int L = 0; L < 16; L++) bl[L] = (uint32_t)L <= maxbits ? rdlane(leaves, (uint32_t)L) : 0u;
+#pragma unroll
+        for (int L = 0; L < 16; L++)
+            if ((uint32_t)L == maxbits) bl[L] += over;
+        if (over) {
+            // Kraft repair on the per-length counts: lengthen a code of the deepest
+            // level below maxbits while over-subscribed, then shorten the deepest
+            // one whose gain fits while under-subscribed
+            const uint32_t T = 1u << maxbits;
+            uint32_t K = 0;
+#pragma unroll
+            for (int L = 1; L < 16; L++)
+                if ((uint32_t)L <= maxbits) K += bl[L] << (maxbits - (uint32_t)L);
+            for (uint32_t it = 0; K > T && it < 4096u; it++) {
+                int lv = -1;
+#pragma unroll
+                for (int L = 1; L < 16; L++)
+                    if ((uint32_t)L < maxbits && bl[L]) lv = L;
+                if (lv < 0) return false;
+#pragma unroll
+                for (int L = 1; L < 16; L++) {
+                    if (L == lv) bl[L]--;
+                    if (L == lv + 1) bl[L]++;
+                }
+                K -= 1u << (maxbits - (uint32_t)lv - 1u);
+            }
+            for (uint32_t it = 0; K < T && it < 4096u; it++) {
+                int lv = -1;
+#pragma unroll
+                for (int L = 2; L < 16; L++)
+                    if ((uint32_t)L <= maxbits && bl[L] && (1u << (maxbits - (uint32_t)L)) <= T - K) lv = L;
+                if (lv < 0) return false;
+#pragma unroll
+                for (int L = 1; L < 16; L++) {
+                    if (L == lv) bl[L]--;
+                    if (L == lv - 1) bl[L]++;
+                }
+                K += 1u << (maxbits - (uint32_t)lv);
+            }
+            if (K != T) return false;
+        }
+        // lengths by rank: the least frequent symbols take the longest codes
+#pragma unroll
+        for (int j = 0; j < R; j++) {
+            uint32_t r = rank[j], len = 0;
+#pragma unroll
+            for (int L = 15; L >= 1; L--) {
+                if (len == 0u && (uint32_t)L <= maxbits) {
+                    if (r < bl[L]) len = (uint32_t)L;
+                    else r -= bl[L];
+                }
+            }
+            l[j] = c[j] ? len : 0u;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < R; j++) l[j] = c[j] ? 1u : 0u;
+    }
+    __builtin_amdgcn_wave_barrier();
+    return true;
+}
+
 // Code lengths for counts c[j] (symbol lane + 64 j; 0 = unused) of `total`
 // symbols, limited to maxbits (64 R symbols must fit in 2^maxbits; R <= 8 and
 // total < 2^22, so a count and a symbol share one 31-bit selection key).  Returns the
 // longest length, or 0 when fewer than two symbols are used (no code needed).
 template <int R>
 __device__ uint32_t code_lengths(const uint32_t (&c)[R], uint32_t total, uint32_t maxbits, uint32_t (&l)[R],
-                                 uint32_t lane) {
+                                 uint32_t lane, uint32_t *sc = nullptr) {
     uint32_t units = 0, used = 0;
+    // start from the optimal lengths when LDS scratch is given (the loops below
+    // then only run when some length exceeds maxbits), else from Shannon's
+    const bool huff = sc && huffman_lengths<R>(c, maxbits, l, sc, lane);
 #pragma unroll
     for (int j = 0; j < R; j++) {
-        l[j] = c[j] ? min(max(shannon_len(c[j], total), 1u), maxbits) : 0u;
+        l[j] = c[j] ? min(max(huff ? l[j] : shannon_len(c[j], total), 1u), maxbits) : 0u;
         units += c[j] ? 1u << (maxbits - l[j]) : 0u;
         used += c[j] ? 1u : 0u;
     }

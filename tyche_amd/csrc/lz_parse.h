@@ -158,7 +158,14 @@ __device__ __forceinline__ void decode_record(const uint2 *rec, uint32_t n, uint
 // taken when it verifies and is at least as long as the hash candidate's
 // match, and a position whose successor has a repeat match starts none of its
 // own: a repeat offset costs a few bits instead of ~10 (zstd_encode.hip).
-template <bool kRepCand = false, typename Sink>
+//
+// kMin3 (deflate): matches from 3 bytes on (MIN_MATCH, deflate.h; deflate_fast
+// takes any match >= MIN_MATCH): candidates verify on 3 bytes, and every
+// position also tries distance 4 straight from its own window -- arrays of
+// 4-byte items that differ in one byte (page line pointers) are level 1's most
+// common 3-byte match (16 % of its matches on the bench pages).  A 3-byte
+// table of its own was tried: +0.3 % ratio for +8 % encode time.
+template <bool kRepCand = false, bool kMin3 = false, typename Sink>
 __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *table, uint2 *rec, uint32_t lane,
                                       Sink &sink) {
     uint32_t anchor = 0;
@@ -183,6 +190,7 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
         // their inserts.
         const Window pw = lds_window(A, (live ? pos : mflimit) + ib);
         const uint32_t v = pw.w0;
+        constexpr uint32_t vm = kMin3 ? 0xFFFFFFu : 0xFFFFFFFFu;   // the bytes a candidate must match
         const uint32_t h = hash4(v);
         uint32_t cand = table[h];
         __builtin_amdgcn_wave_barrier();
@@ -191,25 +199,46 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
         // to kProbe bytes) and backward probe (up to 4 bytes).  A candidate is a
         // position <= mflimit, so the window stays inside the page's zero pad.
         Window cw = lds_window(A, cand + ib);
-        bool ok = live & (cand < pos) & (cw.w0 == v);
+        bool ok = live & (cand < pos) & (((cw.w0 ^ v) & vm) == 0u);
         uint32_t n = 4u + kProbe;
 #pragma unroll
         for (int k = (int)kProbeWords - 1; k >= 0; k--) {
             const uint32_t x = pw.fw[k] ^ cw.fw[k];
             if (x) n = 4u + 4u * (uint32_t)k + ((uint32_t)__builtin_ctz(x) >> 3);
         }
+        if (kMin3 && cw.w0 != v) n = 3u;
+        if (kMin3) {
+            // distance 4 straight from this position's window (arrays of 4-byte
+            // items differing in one byte), taken when at least as long
+            const bool okd = live & (pos >= 4u) & (((pw.back ^ v) & vm) == 0u);
+            uint32_t nd = 4u + kProbe;
+#pragma unroll
+            for (int k = (int)kProbeWords - 1; k >= 0; k--) {
+                const uint32_t x = pw.fw[k] ^ (k ? pw.fw[k > 0 ? k - 1 : 0] : v);
+                if (x) nd = 4u + 4u * (uint32_t)k + ((uint32_t)__builtin_ctz(x) >> 3);
+            }
+            if (pw.back != v) nd = 3u;
+            if (okd && (!ok || nd >= n)) {
+                cand = pos - 4u;
+                cw.back = ~pw.back;   // no backward extension (the word before pos - 4 is not in the window)
+                cw.w0 = pw.back;
+                n = nd;
+                ok = true;
+            }
+        }
         bool rok = false;
         if (kRepCand) {
             // the repeat-offset candidate (consecutive windows: cheap loads)
             const uint32_t rc = pos >= R ? pos - R : 0u;
             const Window rw = lds_window(A, min(rc, mflimit) + ib);
-            rok = live & (pos >= R) & (rw.w0 == v);
+            rok = live & (pos >= R) & (((rw.w0 ^ v) & vm) == 0u);
             uint32_t rn = 4u + kProbe;
 #pragma unroll
             for (int k = (int)kProbeWords - 1; k >= 0; k--) {
                 const uint32_t x = pw.fw[k] ^ rw.fw[k];
                 if (x) rn = 4u + 4u * (uint32_t)k + ((uint32_t)__builtin_ctz(x) >> 3);
             }
+            if (kMin3 && rw.w0 != v) rn = 3u;
 #ifndef TYCHE_REP_SLACK
 #define TYCHE_REP_SLACK 0
 #endif
@@ -219,13 +248,14 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
 #ifndef TYCHE_REP2
 #define TYCHE_REP2 1
 #endif
-            const bool rok2 = TYCHE_REP2 && live & (pos >= R2) & (rw2.w0 == v) & (R2 != R);
+            const bool rok2 = TYCHE_REP2 && live & (pos >= R2) & (((rw2.w0 ^ v) & vm) == 0u) & (R2 != R);
             uint32_t rn2 = 4u + kProbe;
 #pragma unroll
             for (int k = (int)kProbeWords - 1; k >= 0; k--) {
                 const uint32_t x = pw.fw[k] ^ rw2.fw[k];
                 if (x) rn2 = 4u + 4u * (uint32_t)k + ((uint32_t)__builtin_ctz(x) >> 3);
             }
+            if (kMin3 && rw2.w0 != v) rn2 = 3u;
             if (rok && (!ok || rn + TYCHE_REP_SLACK >= n)) {
                 cand = rc;
                 cw = rw;
@@ -321,9 +351,9 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
         const uint32_t rank = nacc + (uint32_t)__popcll(sel & ((1ull << lane) - 1ull));
         if (is_sel) rec[rank] = make_uint2(pos | (cand << 16), len | (back << 16));
         nacc += (uint32_t)__popcll(sel);
-        // a block adds at most 16 records (each covers >= 4 positions)
+        // a block adds at most 16 records (each covers >= 4 positions; 22 of >= 3)
         PHASE(2);
-        if (nacc > kWave - 16 || done) {
+        if (nacc > kWave - (kMin3 ? 22u : 16u) || done) {
             __builtin_amdgcn_wave_barrier();
             if (!sink(rec, nacc, anchor)) return 0xFFFFFFFFu;
             anchor = cursor;

@@ -34,6 +34,12 @@
 #include "lds_io.h"
 #include "huf_enc.h"
 #include "lz_parse.h"
+#ifndef TYCHE_ZLIB_REP
+#define TYCHE_ZLIB_REP 0
+#endif
+#ifndef TYCHE_ZLIB_MIN3
+#define TYCHE_ZLIB_MIN3 1
+#endif
 
 namespace tyche {
 namespace {
@@ -276,7 +282,7 @@ __device__ int32_t encode_fixed1(const uint8_t *in, uint32_t L, uint32_t adler, 
             if (off > 32768u) { ll += ml; ml = 0; }     // beyond the deflate window: literals
             return code_runs(o, in, n, ls, ll, ml, off, map, lane);
         };
-        anchor = lzp::parse_page(in, L, table, rec, lane, sink);
+        anchor = lzp::parse_page<TYCHE_ZLIB_REP != 0, TYCHE_ZLIB_MIN3 != 0>(in, L, table, rec, lane, sink);
         ok = anchor != 0xFFFFFFFFu;
     }
     if (ok) ok = code_runs(o, in, 1, anchor, L - anchor, 0, 1, map, lane);   // last literals
@@ -366,13 +372,23 @@ __device__ int32_t encode_page(const uint8_t *in, uint32_t L, uint16_t *table, u
         nrec += n;
         return true;
     };
-    const uint32_t anchor = lzp::parse_page(in, L, table, rec, lane, sink);
+    const uint32_t anchor = lzp::parse_page<TYCHE_ZLIB_REP != 0, TYCHE_ZLIB_MIN3 != 0>(in, L, table, rec, lane, sink);
     if (anchor == 0xFFFFFFFFu || nrec + 1u > room)
         return encode_fixed1(in, L, adler, table, map, rec, stage, dst, cap, lane);
     if (lane == 0) recs[-1 - (int32_t)nrec] = make_uint2(anchor | ((L - anchor) << 16), 1u << 16);   // last literals
     nrec += 1;
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");   // records visible, L1 invalidated
     __builtin_amdgcn_wave_barrier();
+    // reverse them in place: record i at recf[i], the first ones nearest the
+    // stream, so the stream may grow over the records already coded (pass 3)
+    for (uint32_t i = lane; i < nrec / 2u; i += kWave) {
+        const uint2 a = recs[-1 - (int32_t)i], b = recs[-(int32_t)(nrec - i)];
+        recs[-1 - (int32_t)i] = b;
+        recs[-(int32_t)(nrec - i)] = a;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
+    __builtin_amdgcn_wave_barrier();
+    const uint2 *recf = (const uint2 *)top - nrec;
     // ---- pass 2: symbol histograms in the hash table's LDS (litlen 0..319, distance 320..351)
     uint32_t *H = (uint32_t *)table;
     for (uint32_t k = lane; k < 352u; k += kWave) H[k] = 0;
@@ -380,7 +396,7 @@ __device__ int32_t encode_page(const uint8_t *in, uint32_t L, uint16_t *table, u
     uint32_t xbits = 0;   // extra bits of lengths and distances (this lane's share)
     for (uint32_t r0 = 0; r0 < nrec; r0 += kWave) {
         const uint32_t cnt = min(nrec - r0, kWave);
-        const uint2 rv = lane < cnt ? recs[-1 - (int32_t)(r0 + lane)] : make_uint2(0, 1u << 16);
+        const uint2 rv = lane < cnt ? recf[r0 + lane] : make_uint2(0, 1u << 16);
         visit_runs(in, cnt, rv.x & 0xFFFFu, rv.x >> 16, rv.y & 0xFFFFu, rv.y >> 16, map, lane,
                    [&](bool valid, bool lit, uint32_t byte, uint32_t mlen, uint32_t dist) {
                        if (valid) {
@@ -416,8 +432,10 @@ __device__ int32_t encode_page(const uint8_t *in, uint32_t L, uint16_t *table, u
     totl = huf::wave_sum(totl);
     const uint32_t totd = huf::wave_sum(cd[0]);
     const uint32_t fixed_bits = 3u + huf::wave_sum(fixl) + 5u * totd + extra;
-    if (huf::code_lengths<5>(cll, totl, 15, lll, lane) == 0) two_symbol_code<5>(lll, 0u, 256u, lane);
-    if (huf::code_lengths<1>(cd, totd, 15, ld, lane) == 0) {
+    // (H is free once the counts are in registers: LDS scratch of the Huffman construction)
+    __builtin_amdgcn_wave_barrier();
+    if (huf::code_lengths<5>(cll, totl, 15, lll, lane, H) == 0) two_symbol_code<5>(lll, 0u, 256u, lane);
+    if (huf::code_lengths<1>(cd, totd, 15, ld, lane, H) == 0) {
         const int32_t u = huf::wave_max(cd[0] ? (int32_t)lane : -1);
         two_symbol_code<1>(ld, u > 0 ? 0u : 1u, u > 0 ? (uint32_t)u : 0u, lane);
     }
@@ -443,7 +461,7 @@ __device__ int32_t encode_page(const uint8_t *in, uint32_t L, uint16_t *table, u
     scan_tree(nlit, getl, count_cl);
     scan_tree(ndist, getd, count_cl);
     uint32_t ccl[1] = {clc}, lcl[1];
-    if (huf::code_lengths<1>(ccl, huf::wave_sum(lane < 19u ? clc : 0u), 7, lcl, lane) == 0) {
+    if (huf::code_lengths<1>(ccl, huf::wave_sum(lane < 19u ? clc : 0u), 7, lcl, lane, H) == 0) {
         const int32_t u = huf::wave_max(clc ? (int32_t)lane : -1);
         two_symbol_code<1>(lcl, u > 0 ? 0u : 1u, u > 0 ? (uint32_t)u : 0u, lane);
     }
@@ -456,7 +474,7 @@ __device__ int32_t encode_page(const uint8_t *in, uint32_t L, uint16_t *table, u
     const uint32_t size = 2u + (bits + 7u) / 8u + 4u;
     const uint32_t rec_lo = (uint32_t)(top - base) - 8u * nrec;
     if (size >= stored || size > cap) return emit_stored(in, L, dst, cap, adler, lane);
-    if (size > rec_lo) return encode_fixed1(in, L, adler, table, map, rec, stage, dst, cap, lane);
+    // (the stream may not reach records still to be read: checked as it grows, o.limit)
     // ---- codes (bit-reversed | length << 16) over the histograms
     uint32_t rll[5], rd[1], rcl[1];
     huf::deflate_codes<5>(lll, rll, lane);
@@ -503,7 +521,8 @@ __device__ int32_t encode_page(const uint8_t *in, uint32_t L, uint16_t *table, u
     bool ok = drain(o, lane);
     for (uint32_t r0 = 0; ok && r0 < nrec; r0 += kWave) {
         const uint32_t cnt = min(nrec - r0, kWave);
-        const uint2 rv = lane < cnt ? recs[-1 - (int32_t)(r0 + lane)] : make_uint2(0, 1u << 16);
+        const uint2 rv = lane < cnt ? recf[r0 + lane] : make_uint2(0, 1u << 16);
+        o.limit = min(cap, rec_lo + 8u * (r0 + cnt));   // this group's records are in registers now
         ok = visit_runs(in, cnt, rv.x & 0xFFFFu, rv.x >> 16, rv.y & 0xFFFFu, rv.y >> 16, map, lane,
                         [&](bool valid, bool lit, uint32_t byte, uint32_t mlen, uint32_t dist) {
                             uint64_t v = 0;
