@@ -46,6 +46,7 @@ using lzp::kHashSize;
 using lzp::kWave;
 constexpr uint32_t kPad = 64;
 constexpr uint32_t kSeqCap = 1024;       // sequences buffered per block
+constexpr uint32_t kHtab = 512;          // htab words
 constexpr uint32_t kPrefetchVec = 16;
 
 // ------------------------------------------------------------ predefined distributions
@@ -110,7 +111,8 @@ struct Enc {
     uint32_t bstart;     // first page byte of the current block
     uint32_t cursor;     // end of the last buffered sequence's match
     uint8_t *map;        // 64-byte owner map
-    uint32_t *htab;      // 256 entries: literal histogram, then Huffman code | length << 16
+    uint32_t *htab;      // 512 entries: literal histogram, then Huffman code | length << 16 (all 512:
+                         // scratch of the Huffman construction)
     uint8_t *wts;        // 256 Huffman weights
     uint32_t *stage;     // 128 dwords of pending stream bits (the parse's record area, free here)
     uint32_t r0, r1, r2; // the decoder's repeat offsets after the blocks emitted so far (initial {1, 4, 8},
@@ -243,7 +245,8 @@ __device__ uint32_t huf_literals(Enc &e, uint32_t n, uint32_t trail, uint32_t li
     uint32_t c[4], l[4], code[4];
 #pragma unroll
     for (int j = 0; j < 4; j++) c[j] = e.htab[lane + 64u * j];
-    const uint32_t maxlen = huf::code_lengths(c, lit_total, kHufMaxBits, l, lane);
+    __builtin_amdgcn_wave_barrier();   // htab (now in c) is the Huffman construction's scratch
+    const uint32_t maxlen = huf::code_lengths(c, lit_total, kHufMaxBits, l, lane, e.htab);
     if (maxlen == 0) {
         // a single distinct byte: RLE literals (set_rle)
         const uint32_t fl = 1u + (lit_total > 31u) + (lit_total > 4095u);
@@ -608,7 +611,7 @@ __global__ __launch_bounds__(64) void zstd_encode_kernel(tyche_batch_t b, uint32
     uint2 *rec = (uint2 *)(map + kWave);                               // 64 parse records
     uint2 *seq = rec + kWave;                                          // kSeqCap block sequences
     uint32_t *htab = (uint32_t *)(seq + kSeqCap);                      // literal histogram / Huffman codes
-    uint8_t *wts = (uint8_t *)(htab + 256);                            // Huffman weights
+    uint8_t *wts = (uint8_t *)(htab + kHtab);                          // Huffman weights
     uint8_t *stage = wts + 256;
     const size_t stride = gridDim.x;
 
@@ -670,7 +673,7 @@ __global__ __launch_bounds__(64) void zstd_encode_kernel(tyche_batch_t b, uint32
 hipError_t launch_zstd_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream_t s) {
     if (b.count == 0) return hipSuccess;
     if (in_cap > 65535u) return hipErrorInvalidValue;    // 16-bit positions in the parse and sequence records
-    const size_t lds = kHashSize * sizeof(uint16_t) + kWave + kWave * 8 + kSeqCap * 8 + 256 * 4 + 256 +
+    const size_t lds = kHashSize * sizeof(uint16_t) + kWave + kWave * 8 + kSeqCap * 8 + kHtab * 4 + 256 +
                        ((in_cap + 16u + kPad + 15u) & ~15u);
     int dev = 0;
     (void)hipGetDevice(&dev);
