@@ -26,6 +26,10 @@ typedef const __attribute__((address_space(1))) uint32_t g_u32;
 __device__ __forceinline__ u32x4 gload_nt(const u32x4 *p) { return __builtin_nontemporal_load((g_u32x4 *)(uintptr_t)p); }
 __device__ __forceinline__ uint32_t gload_nt(const uint32_t *p) { return __builtin_nontemporal_load((g_u32 *)(uintptr_t)p); }
 __device__ __forceinline__ uint32_t rdlane(uint32_t v, uint32_t lane) { return __builtin_amdgcn_readlane(v, lane); }
+// 4-byte store to global memory at any byte address (one global_store_dword in
+// unaligned access mode)
+typedef __attribute__((address_space(1))) u32_ua g_u32_ua;
+__device__ __forceinline__ void store_u32_unaligned(uint8_t *p, uint32_t v) { *(g_u32_ua *)(uintptr_t)p = v; }
 
 // inclusive prefix sum over the 64 lanes with DPP row shifts + row broadcasts
 __device__ __forceinline__ int32_t wave_incl_sum(int32_t v) {

@@ -44,30 +44,42 @@ using lzp::kHashSize;
 constexpr uint32_t kPad = 64;
 constexpr uint32_t kPrefetchVec = 16;    // 16-byte vectors per lane prefetched for the next page (16 KiB)
 
-// byte `rel` of a sequence's encoding: token, literal-length bytes, literals, offset, match-length bytes
+// a sequence's encoding: token, literal-length bytes, literals, offset, match-length bytes
 struct SeqFields {
     uint32_t lit, lext, anchor, off, mc, token, total;
 };
 
+// byte `rel` of a sequence's encoding, branch-free (the literal is read
+// unconditionally, from a clamped in-page position): the selects cost less than
+// the divergent branches of 64 lanes in different fields (134 -> 128 ms per 1M pages)
 __device__ __forceinline__ uint32_t seq_byte(const SeqFields &f, const uint8_t *in, uint32_t rel) {
-    if (rel == 0) return f.token;
-    if (rel <= f.lext) return rel == f.lext ? (f.lit - 15u) % 255u : 255u;
-    const uint32_t lb = 1 + f.lext;
-    if (rel < lb + f.lit) return in[f.anchor + rel - lb];
-    const uint32_t ob = lb + f.lit;
-    if (rel == ob) return f.off & 0xFFu;
-    if (rel == ob + 1) return f.off >> 8;
-    return rel == f.total - 1 ? (f.mc - 15u) % 255u : 255u;
+    const uint32_t lb = 1 + f.lext, ob = lb + f.lit;
+    const uint32_t li = f.anchor + min(rel - lb, f.lit - 1u);   // rel in [lb, ob) when used
+    const uint32_t litb = in[rel >= lb && f.lit ? li : 0u];
+    const uint32_t ext = rel == f.lext ? (f.lit - 15u) % 255u : 255u;
+    const uint32_t mext = rel == f.total - 1u ? (f.mc - 15u) % 255u : 255u;
+    uint32_t v = mext;
+    v = rel == ob + 1u ? f.off >> 8 : v;
+    v = rel == ob ? f.off & 0xFFu : v;
+    v = rel < ob ? litb : v;
+    v = rel <= f.lext ? ext : v;
+    v = rel == 0u ? f.token : v;
+    return v;
 }
+
 
 // Encodes n accumulated sequences (records in LDS, stream order) after the
 // literal run that starts at `anchor`, writing their bytes to dst + op.  One
 // record per lane: the previous record's end gives each sequence's literal run;
-// a DPP prefix sum places the encodings; output bytes go out 64 per store, each
-// lane finding its sequence through an LDS owner map and a max-scan.  Returns
-// false if the output would exceed cap.
+// a DPP prefix sum places the encodings.  Output goes out 256 bytes per step,
+// four consecutive bytes per lane and one dword store: sequence starts are
+// stamped into a 256-byte LDS map, each lane reads its four stamps as a dword,
+// and the owner of every byte is the last start at or before it (a wave
+// exclusive max-scan of the lanes' last stamps, then a running max over the
+// four).  Each sequence's packed fields sit in LDS (fld, 16 bytes), read once
+// per distinct owner.  Returns false if the output would exceed cap.
 __device__ bool emit_records(const uint2 *rec, uint32_t n, uint32_t anchor, const uint8_t *in, uint8_t *dst,
-                             uint32_t &op, uint32_t cap, uint8_t *map, uint32_t lane) {
+                             uint32_t &op, uint32_t cap, uint8_t *map, uint4 *fld, uint32_t lane) {
     const bool is_sel = lane < n;
     const uint2 r = rec[is_sel ? lane : 0];
     const uint2 rp = rec[lane > 0 && is_sel ? lane - 1 : 0];
@@ -91,32 +103,58 @@ __device__ bool emit_records(const uint2 *rec, uint32_t n, uint32_t anchor, cons
     const uint32_t eo = (uint32_t)incl - enc;
     const uint32_t et = rdlane((uint32_t)incl, 63);
     if (op + et > cap) return false;
-    // fields travel packed: 4 bpermutes per output chunk
-    const uint32_t pk0 = f.lit | (f.lext << 16), pk1 = f.anchor | (f.off << 16);
-    const uint32_t pk2 = f.mc | (f.total << 16), pk3 = eo | (f.token << 16);
-    for (uint32_t j0 = 0; j0 < ((TYCHE_EABLATE & 1) ? 0u : et); j0 += kWave) {
-        const uint32_t j = j0 + lane;
-        // owner of byte j: the last sequence whose encoding starts at or before j.
-        // Starts inside this chunk are stamped into a 64-byte map and max-scanned.
-        const uint64_t before = __ballot(is_sel && eo <= j0);
+    if (is_sel) fld[lane] = make_uint4(f.lit | (f.lext << 16), f.anchor | (f.off << 16), f.mc | (f.total << 16),
+                                       eo | (f.token << 16));
+    uint32_t *map32 = (uint32_t *)map;
+    for (uint32_t j0 = 0; j0 < ((TYCHE_EABLATE & 1) ? 0u : et); j0 += 4u * kWave) {
+        // the last sequence starting before this step, then the starts inside it
+        const uint64_t before = __ballot(is_sel && eo < j0);
         const int32_t owner0 = before ? 63 - (int32_t)__builtin_clzll(before) : 0;
-        map[lane] = 0xFF;
+        map32[lane] = 0xFFFFFFFFu;
         __builtin_amdgcn_wave_barrier();
-        if (is_sel && eo > j0 && eo < j0 + kWave) map[eo - j0] = (uint8_t)lane;
+        if (is_sel && eo >= j0 && eo < j0 + 4u * kWave) map[eo - j0] = (uint8_t)lane;
         __builtin_amdgcn_wave_barrier();
-        const uint32_t mv = map[lane];
-        const uint32_t owner = (uint32_t)max(wave_incl_max(mv == 0xFF ? -1 : (int32_t)mv), owner0);
-        const uint32_t g0 = __shfl(pk0, owner), g1 = __shfl(pk1, owner);
-        const uint32_t g2 = __shfl(pk2, owner), g3 = __shfl(pk3, owner);
-        SeqFields g;
-        g.lit = g0 & 0xFFFFu;
-        g.lext = g0 >> 16;
-        g.anchor = g1 & 0xFFFFu;
-        g.off = g1 >> 16;
-        g.mc = g2 & 0xFFFFu;
-        g.total = g2 >> 16;
-        g.token = g3 >> 16;
-        if (j < et) dst[op + j] = (uint8_t)seq_byte(g, in, j - (g3 & 0xFFFFu));
+        const uint32_t m = map32[lane];
+        int32_t last = -1;
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            const uint32_t st = (m >> (8 * t)) & 0xFFu;
+            if (st != 0xFFu) last = (int32_t)st;
+        }
+        // owner entering this lane's first byte: the last stamp of the lanes below
+        const int32_t incl_max = wave_incl_max(last);
+        int32_t cur = (int32_t)__shfl(incl_max, (int)(lane ? lane - 1u : 0u));
+        cur = max(lane ? cur : -1, owner0);
+        const uint32_t jb = j0 + 4u * lane;
+        uint32_t word = 0, prev_o = 0xFFFFFFFFu;
+        uint4 g = make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            const uint32_t st = (m >> (8 * t)) & 0xFFu;
+            if (st != 0xFFu) cur = (int32_t)st;
+            if (jb + (uint32_t)t < et) {
+                if ((uint32_t)cur != prev_o) {
+                    g = fld[cur];
+                    prev_o = (uint32_t)cur;
+                }
+                SeqFields q;
+                q.lit = g.x & 0xFFFFu;
+                q.lext = g.x >> 16;
+                q.anchor = g.y & 0xFFFFu;
+                q.off = g.y >> 16;
+                q.mc = g.z & 0xFFFFu;
+                q.total = g.z >> 16;
+                q.token = g.w >> 16;
+                word |= seq_byte(q, in, jb + (uint32_t)t - (g.w & 0xFFFFu)) << (8 * t);
+            }
+        }
+        if (jb + 4u <= et) {
+            store_u32_unaligned(dst + op + jb, word);
+        } else {
+#pragma unroll
+            for (int t = 0; t < 4; t++)
+                if (jb + (uint32_t)t < et) dst[op + jb + (uint32_t)t] = (uint8_t)(word >> (8 * t));
+        }
         __builtin_amdgcn_wave_barrier();
     }
     op += et;
@@ -126,10 +164,10 @@ __device__ bool emit_records(const uint2 *rec, uint32_t n, uint32_t anchor, cons
 // Encodes one page held in LDS into dst (global, capacity cap).  Returns the
 // compressed size, or 0 if it does not fit in cap.
 __device__ int32_t encode_page(const uint8_t *in, uint32_t L, uint16_t *table, uint8_t *map, uint2 *rec,
-                               uint8_t *dst, uint32_t cap, uint32_t lane) {
+                               uint4 *fld, uint8_t *dst, uint32_t cap, uint32_t lane) {
     uint32_t op = 0;
     auto sink = [&](const uint2 *r, uint32_t n, uint32_t anchor) -> bool {
-        return emit_records(r, n, anchor, in, dst, op, cap, map, lane);
+        return emit_records(r, n, anchor, in, dst, op, cap, map, fld, lane);
     };
     const uint32_t anchor = lzp::parse_page(in, L, table, rec, lane, sink);
     if (anchor == 0xFFFFFFFFu) return 0;
@@ -152,9 +190,10 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel(tyche_batch_t b, uint32_
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t lane = threadIdx.x;
     uint16_t *table = (uint16_t *)smem;
-    uint8_t *map = smem + kHashSize * sizeof(uint16_t);                 // 64-byte owner map
-    uint2 *rec = (uint2 *)(map + kWave);                               // 64 sequence records
-    uint8_t *stage = (uint8_t *)(rec + kWave);
+    uint8_t *map = smem + kHashSize * sizeof(uint16_t);                 // 256-byte owner map
+    uint2 *rec = (uint2 *)(map + 4 * kWave);                           // 64 sequence records
+    uint4 *fld = (uint4 *)(rec + kWave);                               // 64 packed sequence fields
+    uint8_t *stage = (uint8_t *)(fld + kWave);
     const size_t stride = gridDim.x;
 
     size_t page = blockIdx.x;
@@ -189,7 +228,7 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel(tyche_batch_t b, uint32_
             WAVE_SYNC();
             in[p.src_len + lane] = 0;
             WAVE_SYNC();
-            rv = encode_page(in, p.src_len, table, map, rec, p.dst, p.dst_cap, lane);
+            rv = encode_page(in, p.src_len, table, map, rec, fld, p.dst, p.dst_cap, lane);
         }
         if (lane == 0) b.results[page] = rv;
         if (next >= b.count) break;
@@ -215,7 +254,8 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel(tyche_batch_t b, uint32_
 hipError_t launch_lz4_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream_t s) {
     if (b.count == 0) return hipSuccess;
     if (in_cap > 65535u) return hipErrorInvalidValue;    // 16-bit positions (byU16 regime)
-    const size_t lds = kHashSize * sizeof(uint16_t) + kWave + kWave * 8 + ((in_cap + 16u + kPad + 15u) & ~15u);
+    const size_t lds = kHashSize * sizeof(uint16_t) + 4 * kWave + kWave * 8 + kWave * 16 +
+                       ((in_cap + 16u + kPad + 15u) & ~15u);
     int dev = 0;
     (void)hipGetDevice(&dev);
     static int cus[64] = {0};
