@@ -164,14 +164,6 @@ __device__ uint32_t parse_chain(const uint8_t *in, int32_t L, uint8_t *owner, ui
     return total;
 }
 
-__device__ __forceinline__ uint32_t mod_small(uint32_t i, uint32_t m) {
-    // i % m for i < 2^20, m >= 1 without an integer divide
-    uint32_t q = (uint32_t)((float)i * __frcp_rn((float)m));
-    int32_t r = (int32_t)i - (int32_t)(q * m);
-    if (r < 0) r += (int32_t)m;
-    if (r >= (int32_t)m) r -= (int32_t)m;
-    return (uint32_t)r;
-}
 
 // Decodes one page held in LDS.  in: stream of L bytes (kPad zero bytes after),
 // out: LDS window of W >= C + 16 bytes whose top holds the token positions.

@@ -263,14 +263,6 @@ __device__ __forceinline__ uint32_t put_lane(uint32_t v, uint32_t j, uint32_t x,
     return lane == j ? x : v;
 }
 
-__device__ __forceinline__ uint32_t mod_small(uint32_t i, uint32_t m) {
-    // i % m for i < 2^20, m >= 1 without an integer divide
-    uint32_t q = (uint32_t)((float)i * __frcp_rn((float)m));
-    int32_t r = (int32_t)i - (int32_t)(q * m);
-    if (r < 0) r += (int32_t)m;
-    if (r >= (int32_t)m) r -= (int32_t)m;
-    return (uint32_t)r;
-}
 
 // ------------------------------------------------------------- batched output
 struct Pending {

@@ -683,13 +683,6 @@ __device__ bool huf_decode(const Work &W, int32_t cs, int32_t n, bool single, ui
 }
 
 // ------------------------------------------------------------ sequence execution
-__device__ __forceinline__ uint32_t mod_small(uint32_t i, uint32_t m) {
-    uint32_t q = (uint32_t)((float)i * __frcp_rn((float)m));
-    int32_t r = (int32_t)i - (int32_t)(q * m);
-    if (r < 0) r += (int32_t)m;
-    if (r >= (int32_t)m) r -= (int32_t)m;
-    return (uint32_t)r;
-}
 
 // whole-wave forward copy out[d, d+ml) <- out[d-off, ...) (overlap semantics)
 __device__ __forceinline__ void wave_match(uint8_t *out, int32_t d, int32_t off, int32_t ml, uint32_t lane) {
