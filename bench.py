@@ -376,6 +376,15 @@ def main():
             result["configs"] = {"C3_zstd": c3}
             del zpages
             torch.cuda.empty_cache()
+            # C4 (configs[3]) per GPU: LZ4 decompress of 8M x 8 KiB pages over 8 GPUs is 1M x 8 KiB
+            # pages on each (page-range shards, no collective); its one-GPU shard, decode rate reported
+            c4, c4pages = measure_codec(1, "lz4", args.extra_pages, 8192, max(args.extra_steps, 3), 1, dev,
+                                        args.seed, 0, args.dist)
+            c4["workload"] = ("C4 shard: LZ4 compress+decompress of 1M x 8 KiB pages on one GPU (C4 = 8M pages "
+                              "over 8 GPUs, decompress_gib_s is its per-GPU rate)")
+            result["configs"]["C4_lz4_8k_shard"] = c4
+            del c4pages
+            torch.cuda.empty_cache()
     if info.rank == 0:
         print(json.dumps(result), flush=True)
     runner.shutdown(info)
