@@ -11,7 +11,7 @@
 // capacity (limitedOutput semantics: 0 when it would not fit).
 //
 // One 64-lane wave per page, looping over pages with the next page prefetched
-// into registers.  The page is staged in LDS next to a table of 2^11 16-bit
+// into registers.  The page is staged in LDS next to a table of 2^10 16-bit
 // positions (the byU16 scheme of lz4.c:402-408, hash 2654435761 of 4 bytes).
 // The page is scanned in blocks of 64 positions:
 //   * every lane hashes its position, takes the candidate left by earlier
@@ -28,6 +28,12 @@
 #include <hip/hip_runtime.h>
 
 #define TYCHE_PHASES_OWNER   // only used by -DTYCHE_PHASES profiling builds
+// 2^10 hash slots (2 KB): the wave's LDS (page 16.4 KB + table + records) drops
+// to 20 KB, one 512-byte granule under 160 KB / 8, so 8 waves per CU instead of
+// 7: 127.7 -> 111.6 ms per 1M pages for ratio 2.635 -> 2.621 (reference 2.647)
+#ifndef TYCHE_HASH_LOG
+#define TYCHE_HASH_LOG 10
+#endif
 
 #include <algorithm>
 

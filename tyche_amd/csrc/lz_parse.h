@@ -4,8 +4,8 @@
 // One 64-lane wave parses one page held in LDS next to a table of 2^11 16-bit
 // positions (the byU16 scheme of lz4.c:402-408, hash 2654435761 of 4 bytes; the
 // reference's table has 2^13 slots -- 2^11 keeps the ratio within 0.5 % on the
-// bench pages and raises residency from 6 to 7 waves per CU at 16 KiB pages,
-// 12 % faster encode; 2^10 would give 8 waves at a 0.6-1.9 % ratio cost).
+// bench pages and raises residency from 6 to 7 waves per CU at 16 KiB pages;
+// the LZ4 encoder takes 2^10 for 8 waves per CU, lz4_encode.hip).
 // The page is scanned in blocks of 64 positions:
 //   * every lane hashes its position, takes the candidate left by earlier
 //     blocks, verifies 4 bytes, probes the match length up to 20 bytes and the
