@@ -566,6 +566,8 @@ __global__ __launch_bounds__(64) void lz4_decode_wave_kernel(tyche_batch_t b, ui
 
 hipError_t launch_lz4_decode(const tyche_batch_t &b, uint32_t in_cap, uint32_t out_cap, hipStream_t s) {
     if (b.count == 0) return hipSuccess;
+    // large batches: one page per lane (lz4_decode_lane.hip)
+    if (lz4_lane_decode_wanted(b.count)) return launch_lz4_decode_lane(b, in_cap, out_cap, s);
     // page window (output; the parse's owner stamps, so at least in_cap bytes;
     // the token positions at its top, <= in_cap / 3 + 1 of them, which always
     // fit: W >= in_cap + 20), then the staged stream

@@ -1,0 +1,264 @@
+// lz4_decode_lane.hip -- throughput LZ4 block decode for large batches: one
+// page per LANE (64 pages per wave), decoded straight from the compressed
+// stream in HBM into the page's destination in HBM.
+//
+// The wave-per-page decoder (lz4_decode.hip) spends ~40 k wave instructions per
+// 16 KiB page reconstructing LZ4's two serial chains (token chain, match
+// dependencies) in parallel.  A lane that simply runs the reference's
+// sequential loop (lz4.c:1089-1248, restated in decode_page_serial) issues ~50
+// instructions per sequence, and with 64 pages per wave that is under 1/20th
+// of the instruction stream; the cost moves to the vector memory pipe (every
+// load/store touches 64 different lines) and to latency, which the batch
+// hides: a 1M-page batch keeps every lane of every resident wave busy.
+//
+// Copies are 16 bytes per access (unaligned global_load/store_dwordx4) and may
+// run past the sequence end ("wild copies", as lz4.c's LZ4_wildCopy) but never
+// past the page's capacity C; the bytes past the decoded end are overwritten by
+// later sequences before anything reads them.  A lane's store followed by its
+// own load of the same address returns the stored value (vector memory
+// operations of one wave are performed in order), which the forward semantics
+// of overlapping copies rely on.  Self-overlapping matches with offset < 16
+// (runs: offset 1 = a repeated byte) are expanded in registers to a 16-byte
+// pattern of period `offset` and stored with a stride that is a multiple of
+// the offset -- no read-after-write through memory at all.
+//
+// Results are LZ4_decompress_safe's, checks in the reference's order: the
+// decoded size, or -(input bytes consumed)-1 for a malformed stream (the
+// stream is read as if padded with zero bytes, like the staged stream of the
+// wave decoder; the reference reads the same positions).  On error the page's
+// destination holds partial output (the reference's does too).
+#include <hip/hip_runtime.h>
+
+#include "engine.h"
+#include "lds_io.h"
+
+#include <algorithm>
+#include <cstdlib>
+
+namespace tyche {
+
+namespace {
+
+typedef unsigned __int128 u128;
+typedef u32x4 u32x4_ua __attribute__((aligned(1)));
+typedef __attribute__((address_space(1))) u32x4_ua g_u32x4_ua;
+typedef __attribute__((address_space(1))) uint8_t g_u8;
+typedef __attribute__((address_space(1))) uint64_t g_u64_ua __attribute__((aligned(1)));
+
+__device__ __forceinline__ u128 ld16(const uint8_t *p) {
+    u32x4 v = *(const g_u32x4_ua *)(uintptr_t)p;
+    return __builtin_bit_cast(u128, v);
+}
+__device__ __forceinline__ uint64_t ld8(const uint8_t *p) { return *(const g_u64_ua *)(uintptr_t)p; }
+__device__ __forceinline__ void st16(uint8_t *p, u128 v) {
+    *(g_u32x4_ua *)(uintptr_t)p = __builtin_bit_cast(u32x4, v);
+}
+__device__ __forceinline__ uint32_t ld1(const uint8_t *p) { return *(const g_u8 *)(uintptr_t)p; }
+__device__ __forceinline__ void st1(uint8_t *p, uint32_t v) { *(g_u8 *)(uintptr_t)p = (uint8_t)v; }
+
+// 32-byte stream window at ip, zero past L.  The parse of a sequence reads
+// its token, length bytes, short literals and offset from the window; the
+// next sequence's window is loaded before the current one's copies, so one
+// load latency per sequence sits on the serial chain.
+struct Win {
+    u128 lo, hi;
+};
+__device__ __forceinline__ Win shr256(Win w, int32_t n) {   // by n bytes, 0 <= n < 32
+    Win r;
+    if (n >= 16) {
+        r.lo = w.hi >> (8 * (n - 16));
+        r.hi = 0;
+    } else if (n > 0) {
+        r.lo = (w.lo >> (8 * n)) | (w.hi << (128 - 8 * n));
+        r.hi = w.hi >> (8 * n);
+    } else {
+        r = w;
+    }
+    return r;
+}
+__device__ __forceinline__ Win window(const uint8_t *__restrict__ in, int32_t ip, int32_t L) {
+    Win w;
+    if (ip + 32 <= L) {
+        w.lo = ld16(in + ip);
+        w.hi = ld16(in + ip + 16);
+        return w;
+    }
+    if (L >= 32) {
+        w.lo = ld16(in + L - 32);
+        w.hi = ld16(in + L - 16);
+        return shr256(w, ip - (L - 32));
+    }
+    w.lo = 0;
+    w.hi = 0;
+    for (int32_t j = L - 1; j >= ip; j--) {
+        w.hi = (w.hi << 8) | (w.lo >> 120);
+        w.lo = (w.lo << 8) | ld1(in + j);
+    }
+    return w;
+}
+__device__ __forceinline__ uint32_t byte_at(const uint8_t *__restrict__ in, int32_t ip, int32_t L) {
+    return ip < L ? ld1(in + ip) : 0u;
+}
+// byte ip + rel of the stream (zero past L): from the window when rel < 32
+__device__ __forceinline__ uint32_t getb(const Win &w, const uint8_t *__restrict__ in, int32_t ip, int32_t rel,
+                                         int32_t L) {
+    if (rel < 16) return (uint32_t)(w.lo >> (8 * rel)) & 0xFFu;
+    if (rel < 32) return (uint32_t)(w.hi >> (8 * (rel - 16))) & 0xFFu;
+    return byte_at(in, ip + rel, L);
+}
+
+// n bytes from src to dst; room: bytes writable at dst, avail: readable at src
+__device__ __forceinline__ void copy_run(uint8_t *__restrict__ dst, const uint8_t *__restrict__ src, int32_t n,
+                                         int32_t room, int32_t avail) {
+    int32_t k = 0;
+    for (; k < n; k += 16) {
+        if (k + 16 > room || k + 16 > avail) break;
+        st16(dst + k, ld16(src + k));
+    }
+    for (; k < n; k++) st1(dst + k, ld1(src + k));
+}
+
+// Decode one page: LZ4_decompress_safe(in, out, L, C), as decode_page_serial.
+__device__ int32_t decode_lane(const uint8_t *__restrict__ in, int32_t L, uint8_t *__restrict__ out, int32_t C) {
+    if (C == 0) return (L == 1 && ld1(in) == 0) ? 0 : -1;
+    if (L <= 0) return -1;
+    int32_t ip = 0, op = 0;
+    Win w = window(in, 0, L);
+    for (;;) {
+        const uint32_t token = (uint32_t)w.lo & 0xFFu;
+        int32_t lit = (int32_t)(token >> 4);
+        int32_t pos = 1;   // stream position relative to ip
+        if (lit == kRunMask) {
+            uint32_t s;
+            do {
+                s = getb(w, in, ip, pos, L);
+                pos++;
+                lit += (int32_t)s;
+            } while (ip + pos < L - kRunMask && s == 255);
+        }
+        // terminal literal run, or error (lz4.c:1147-1163)
+        if (op + lit > C - kMfLimit || ip + pos + lit > L - 8) {
+            ip += pos;
+            if (ip + lit != L || op + lit > C) return -ip - 1;
+            copy_run(out + op, in + ip, lit, C - op, L - ip);
+            return op + lit;
+        }
+        // literals: from the window when short (pos <= 2 then), else from HBM
+        if (lit <= 16 && op + 16 <= C) {
+            st16(out + op, shr256(w, pos).lo);
+        } else {
+            copy_run(out + op, in + ip + pos, lit, C - op, L - ip - pos);
+        }
+        pos += lit;
+        const int32_t off = (int32_t)(getb(w, in, ip, pos, L) | (getb(w, in, ip, pos + 1, L) << 8));
+        pos += 2;
+        op += lit;
+        if (off > op) return -(ip + pos) - 1;                   // lz4.c:1168
+        int32_t ml = (int32_t)(token & 15u);
+        if (ml == 15) {
+            uint32_t s;
+            do {
+                s = getb(w, in, ip, pos, L);
+                pos++;
+                if (ip + pos > L - kLastLiterals) return -(ip + pos) - 1;   // lz4.c:1176
+                ml += (int32_t)s;
+            } while (s == 255);
+        }
+        ml += kMinMatch;
+        if (op + ml > C - kLastLiterals) return -(ip + pos) - 1;   // lz4.c:1225
+        uint8_t *dst = out + op;
+        const uint8_t *src = dst - off;
+        // first source chunk (after the literal store: it may overlap it), then
+        // the next window, then the copy
+        u128 m = off <= 8 ? (u128)ld8(src) : ld16(src);   // off >= 9: src + 16 <= op + 7 <= C; else src + 8 <= op + 8 - off
+        ip += pos;
+        w = window(in, ip, L);
+        if (off >= 16) {
+            // every 16-byte source chunk ends at or before its destination
+            int32_t k = 0;
+            if (op + 16 <= C) {
+                st16(dst, m);
+                for (k = 16; k < ml; k += 16) {
+                    if (op + k + 16 > C) break;
+                    st16(dst + k, ld16(src + k));
+                }
+            }
+            for (; k < ml; k++) st1(dst + k, ld1(src + k));
+        } else {
+            // period-`off` pattern of the off final bytes before dst, doubled
+            // (offset 0 passes the reference's checks and copies dst onto
+            // itself -- undefined bytes; zeros here, and no endless doubling)
+            u128 p = 0;
+            int32_t step = 16;
+            if (off > 0) {
+                p = m & ((((u128)1) << (8 * off)) - 1);
+                for (int32_t len = off; len < 16; len <<= 1) p |= p << (8 * len);
+                step = 16 - (int32_t)mod_small(16u, (uint32_t)off);   // largest multiple of off <= 16
+            }
+            int32_t k = 0;
+            for (; k < ml; k += step) {
+                if (op + k + 16 > C) break;
+                st16(dst + k, p);
+            }
+            for (int32_t j = k; j < ml; j++) st1(dst + j, (uint32_t)(p >> (8 * (j - k))) & 0xFFu);
+        }
+        op += ml;
+    }
+}
+
+// Pages are claimed per lane: lane g starts at page g, then takes the next
+// unclaimed one from the launch's counter (engine.h: work_counter).
+__global__ __launch_bounds__(64) void lz4_decode_lane_kernel(tyche_batch_t b, uint32_t in_cap, uint32_t out_cap,
+                                                              unsigned *ctr) {
+    const size_t nthreads = (size_t)gridDim.x * blockDim.x;
+    size_t page = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    while (page < b.count) {
+        const uint64_t so = b.src_offsets ? b.src_offsets[page] : (uint64_t)page * b.src_stride;
+        const uint64_t dof = b.dst_offsets ? b.dst_offsets[page] : (uint64_t)page * b.dst_stride;
+        const uint32_t L = b.src_lengths ? b.src_lengths[page] : b.src_length;
+        const uint32_t C = b.dst_capacities ? b.dst_capacities[page] : b.dst_capacity;
+        int32_t rv;
+        if (L > in_cap || C > out_cap) {
+            rv = kResultTooLarge;
+        } else {
+            rv = decode_lane((const uint8_t *)b.src + so, (int32_t)L, (uint8_t *)b.dst + dof, (int32_t)C);
+        }
+        b.results[page] = rv;
+        page = (size_t)atomicAdd(ctr, 1u) + nthreads;
+    }
+}
+
+}  // namespace
+
+// Threshold and residency (env, for A/B timing): TYCHE_LZ4_LANE_MIN pages per
+// batch (default 65536) switch the batch to this kernel, TYCHE_LZ4_LANE_WAVES
+// resident waves per CU (default kLaneWaves).
+bool lz4_lane_decode_wanted(size_t count) {
+    static const long min_pages = getenv("TYCHE_LZ4_LANE_MIN") ? atol(getenv("TYCHE_LZ4_LANE_MIN")) : 65536;
+    return min_pages >= 0 && count >= (size_t)min_pages;
+}
+
+// resident waves per CU (1M x 16 KiB pages, ms: 4 waves 88.9, 8: 98.7, 16: 105.3, all: 106.9)
+constexpr size_t kLaneWaves = 4;
+
+hipError_t launch_lz4_decode_lane(const tyche_batch_t &b, uint32_t in_cap, uint32_t out_cap, hipStream_t s) {
+    if (b.count == 0) return hipSuccess;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    static int cus[64] = {0};
+    if (dev < 64 && cus[dev] == 0) {
+        int n = 0;
+        (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+        cus[dev] = n > 0 ? n : 256;
+    }
+    const size_t ncu = dev < 64 ? cus[dev] : 256;
+    static const long env_waves = getenv("TYCHE_LZ4_LANE_WAVES") ? atol(getenv("TYCHE_LZ4_LANE_WAVES")) : 0;
+    size_t waves = waves_per_cu((const void *)lz4_decode_lane_kernel, 0);
+    waves = std::min<size_t>(waves, env_waves > 0 ? (size_t)env_waves : kLaneWaves);
+    const size_t grid = std::min<size_t>((b.count + 63) / 64, ncu * waves);
+    hipLaunchKernelGGL(lz4_decode_lane_kernel, dim3((unsigned)grid), dim3(64), 0, s, b, in_cap, out_cap,
+                       work_counter(s));
+    return hipGetLastError();
+}
+
+}  // namespace tyche
