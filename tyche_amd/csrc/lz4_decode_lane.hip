@@ -206,6 +206,163 @@ __device__ int32_t decode_lane(const uint8_t *__restrict__ in, int32_t L, uint8_
     }
 }
 
+// ---- ring variant: the page's output is assembled in a per-lane LDS ring of
+// the last kRing bytes and leaves for HBM only in whole 64-byte lines.
+//
+// Writing the page straight to HBM 16 bytes at a time (decode_lane) leaves
+// every line partially written for ~10 sequences; with 256 pages in flight per
+// CU the L2 evicts most of them half-full (PMC: 79 KiB written and ~1,000 L2
+// misses per 16 KiB page).  Here the stores to HBM are aligned full lines
+// written once, and matches whose source lies in the ring (70 % of them on the
+// bench pages: offset <= kRing - 48) never touch HBM; the others read the
+// page's already-flushed bytes back from HBM.
+constexpr int32_t kRing = 512;                 // power of two
+constexpr int32_t kRingStride = kRing + 48;    // 16 B front slack, 32 B tail slack
+constexpr int32_t kRingNear = kRing - 48;      // offsets up to this read the ring
+constexpr int32_t kLine = 64;
+
+typedef __attribute__((address_space(3))) u32x4_ua l_u32x4_ua;
+__device__ __forceinline__ u128 lds16(const uint8_t *p) {
+    return __builtin_bit_cast(u128, *(const l_u32x4_ua *)(const __attribute__((address_space(3))) uint8_t *)p);
+}
+__device__ __forceinline__ void lds16(uint8_t *p, u128 v) {
+    *(l_u32x4_ua *)(__attribute__((address_space(3))) uint8_t *)p = __builtin_bit_cast(u32x4, v);
+}
+// 16 bytes of the ring at page position x (valid for any x: the 16 bytes past
+// the ring's end mirror its first 16)
+__device__ __forceinline__ u128 ring_rd(uint8_t *rb, int32_t x) { return lds16(rb + (x & (kRing - 1))); }
+__device__ __forceinline__ void ring_wr(uint8_t *rb, int32_t x, u128 v) {
+    const int32_t q = x & (kRing - 1);
+    lds16(rb + q, v);
+    if (q + 16 > kRing) lds16(rb + q - kRing, v);   // wrapped part, to the ring's start
+    if (q < 16) lds16(rb + q + kRing, v);           // mirror of the start, past the end
+}
+// write out the whole lines of [fl, fin)
+__device__ __forceinline__ void ring_flush(uint8_t *rb, uint8_t *__restrict__ out, int32_t &fl, int32_t fin) {
+    while (fin - fl >= kLine) {
+#pragma unroll
+        for (int32_t j = 0; j < kLine; j += 16) st16(out + fl + j, ring_rd(rb, fl + j));
+        fl += kLine;
+    }
+}
+__device__ __forceinline__ void ring_flush_all(uint8_t *rb, uint8_t *__restrict__ out, int32_t &fl, int32_t fin) {
+    ring_flush(rb, out, fl, fin);
+    for (; fl + 16 <= fin; fl += 16) st16(out + fl, ring_rd(rb, fl));
+    if (fl < fin) {
+        const u128 v = ring_rd(rb, fl);
+        for (int32_t j = 0; fl + j < fin; j++) st1(out + fl + j, (uint32_t)(v >> (8 * j)) & 0xFFu);
+        fl = fin;
+    }
+}
+__device__ __forceinline__ u128 stream16(const uint8_t *__restrict__ in, int32_t a, int32_t L) {
+    return a + 16 <= L ? ld16(in + a) : window(in, a, L).lo;
+}
+
+// LZ4_decompress_safe(in, out, L, C) through the ring rb (as decode_lane)
+__device__ int32_t decode_ring(const uint8_t *__restrict__ in, int32_t L, uint8_t *__restrict__ out, int32_t C,
+                               uint8_t *rb) {
+    if (C == 0) return (L == 1 && ld1(in) == 0) ? 0 : -1;
+    if (L <= 0) return -1;
+    int32_t ip = 0, op = 0, fl = 0;   // fl: bytes of the page already in HBM
+    Win w = window(in, 0, L);
+    for (;;) {
+        const uint32_t token = (uint32_t)w.lo & 0xFFu;
+        int32_t lit = (int32_t)(token >> 4);
+        int32_t pos = 1;
+        if (lit == kRunMask) {
+            uint32_t s;
+            do {
+                s = getb(w, in, ip, pos, L);
+                pos++;
+                lit += (int32_t)s;
+            } while (ip + pos < L - kRunMask && s == 255);
+        }
+        if (op + lit > C - kMfLimit || ip + pos + lit > L - 8) {   // lz4.c:1147-1163
+            ip += pos;
+            if (ip + lit != L || op + lit > C) return -ip - 1;
+            ring_flush_all(rb, out, fl, op);
+            copy_run(out + op, in + ip, lit, C - op, L - ip);
+            return op + lit;
+        }
+        if (lit <= 16) {
+            ring_wr(rb, op, shr256(w, pos).lo);
+        } else {
+            for (int32_t k = 0; k < lit; k += 16) {
+                ring_wr(rb, op + k, stream16(in, ip + pos + k, L));
+                ring_flush(rb, out, fl, op + min(k + 16, lit));
+            }
+        }
+        pos += lit;
+        const int32_t off = (int32_t)(getb(w, in, ip, pos, L) | (getb(w, in, ip, pos + 1, L) << 8));
+        pos += 2;
+        op += lit;
+        if (off > op) return -(ip + pos) - 1;                   // lz4.c:1168
+        int32_t ml = (int32_t)(token & 15u);
+        if (ml == 15) {
+            uint32_t s;
+            do {
+                s = getb(w, in, ip, pos, L);
+                pos++;
+                if (ip + pos > L - kLastLiterals) return -(ip + pos) - 1;   // lz4.c:1176
+                ml += (int32_t)s;
+            } while (s == 255);
+        }
+        ml += kMinMatch;
+        if (op + ml > C - kLastLiterals) return -(ip + pos) - 1;   // lz4.c:1225
+        // the unflushed tail is < kLine + 32 bytes here, so a source at
+        // offset > kRingNear is already in HBM; a nearer one is in the ring
+        const bool far = off > kRingNear;
+        u128 m = far ? ld16(out + op - off) : ring_rd(rb, op - off);
+        ip += pos;
+        w = window(in, ip, L);
+        if (off >= 16) {
+            ring_wr(rb, op, m);
+            for (int32_t k = 16; k < ml; k += 16) {
+                ring_flush(rb, out, fl, op + k);
+                m = far ? ld16(out + op + k - off) : ring_rd(rb, op + k - off);
+                ring_wr(rb, op + k, m);
+            }
+        } else {
+            // period-`off` pattern (offset 0: undefined bytes, zeros here)
+            u128 p = 0;
+            int32_t step = 16;
+            if (off > 0) {
+                p = m & ((((u128)1) << (8 * off)) - 1);
+                for (int32_t len = off; len < 16; len <<= 1) p |= p << (8 * len);
+                step = 16 - (int32_t)mod_small(16u, (uint32_t)off);
+            }
+            for (int32_t k = 0; k < ml; k += step) {
+                ring_flush(rb, out, fl, op + k);
+                ring_wr(rb, op + k, p);
+            }
+        }
+        op += ml;
+        ring_flush(rb, out, fl, op);
+    }
+}
+
+__global__ __launch_bounds__(64) void lz4_decode_ring_kernel(tyche_batch_t b, uint32_t in_cap, uint32_t out_cap,
+                                                             unsigned *ctr) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint8_t *rb = smem + threadIdx.x * kRingStride + 16;
+    const size_t nthreads = (size_t)gridDim.x * blockDim.x;
+    size_t page = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    while (page < b.count) {
+        const uint64_t so = b.src_offsets ? b.src_offsets[page] : (uint64_t)page * b.src_stride;
+        const uint64_t dof = b.dst_offsets ? b.dst_offsets[page] : (uint64_t)page * b.dst_stride;
+        const uint32_t L = b.src_lengths ? b.src_lengths[page] : b.src_length;
+        const uint32_t C = b.dst_capacities ? b.dst_capacities[page] : b.dst_capacity;
+        int32_t rv;
+        if (L > in_cap || C > out_cap) {
+            rv = kResultTooLarge;
+        } else {
+            rv = decode_ring((const uint8_t *)b.src + so, (int32_t)L, (uint8_t *)b.dst + dof, (int32_t)C, rb);
+        }
+        b.results[page] = rv;
+        page = (size_t)atomicAdd(ctr, 1u) + nthreads;
+    }
+}
+
 // Pages are claimed per lane: lane g starts at page g, then takes the next
 // unclaimed one from the launch's counter (engine.h: work_counter).
 __global__ __launch_bounds__(64) void lz4_decode_lane_kernel(tyche_batch_t b, uint32_t in_cap, uint32_t out_cap,
@@ -253,6 +410,22 @@ hipError_t launch_lz4_decode_lane(const tyche_batch_t &b, uint32_t in_cap, uint3
     }
     const size_t ncu = dev < 64 ? cus[dev] : 256;
     static const long env_waves = getenv("TYCHE_LZ4_LANE_WAVES") ? atol(getenv("TYCHE_LZ4_LANE_WAVES")) : 0;
+    static const int ring = getenv("TYCHE_LZ4_LANE_RING") ? atoi(getenv("TYCHE_LZ4_LANE_RING")) : 1;
+    if (ring) {
+        const size_t lds = 64 * (size_t)kRingStride;
+        static bool attr = false;
+        if (!attr) {
+            (void)hipFuncSetAttribute((const void *)lz4_decode_ring_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      160 * 1024);
+            attr = true;
+        }
+        size_t waves = waves_per_cu((const void *)lz4_decode_ring_kernel, lds);
+        if (env_waves > 0) waves = std::min<size_t>(waves, (size_t)env_waves);
+        const size_t grid = std::min<size_t>((b.count + 63) / 64, ncu * waves);
+        hipLaunchKernelGGL(lz4_decode_ring_kernel, dim3((unsigned)grid), dim3(64), lds, s, b, in_cap, out_cap,
+                           work_counter(s));
+        return hipGetLastError();
+    }
     size_t waves = waves_per_cu((const void *)lz4_decode_lane_kernel, 0);
     waves = std::min<size_t>(waves, env_waves > 0 ? (size_t)env_waves : kLaneWaves);
     const size_t grid = std::min<size_t>((b.count + 63) / 64, ncu * waves);
