@@ -262,3 +262,41 @@ def test_decode_size_classes(tc):
     out, rv = tc.decompress_pages(comp, clen, plen, max_comp_len=mx)
     torch.cuda.synchronize()
     assert bool((rv == plen).all()) and torch.equal(out, pages)
+
+
+def test_decode_lane_path_fixtures(tc):
+    """Batches of >= 65,536 pages take the lane-per-page decoder (lz4_decode_lane.hip):
+    the reference-generated, sample and malformed fixtures, repeated to 64K pages, give
+    the reference's return values and bytes there too."""
+    gm, gg, gs = load_golden("lz4_malformed.npz"), load_golden("lz4_generated.npz"), load_golden("lz4_sample.npz")
+    streams, caps, want_rv, want_dig = [], [], [], []
+    for i in range(len(gm["cap"])):
+        streams.append(unpack(gm["comp"], gm["comp_off"], gm["comp_len"], i))
+        caps.append(int(gm["cap"][i]))
+        want_rv.append(int(gm["rv"][i]))
+        want_dig.append(gm["digest"][i].tobytes() if gm["defined"][i] else None)
+    for g, capf in ((gg, lambda i: int(gg["meta"][i][1])), (gs, lambda i: int(gs["size"][i]))):
+        m = len(g["digest"])
+        for i in range(m):
+            streams.append(unpack(g["comp"], g["comp_off"], g["comp_len"], i))
+            caps.append(capf(i))
+            want_rv.append(caps[-1])
+            want_dig.append(g["digest"][i].tobytes())
+    k = -(-65536 // len(streams))
+    rv, outs = ragged_decode(tc, streams * k, caps * k)
+    for j in range(len(streams) * k):
+        i = j % len(streams)
+        assert rv[j] == want_rv[i], (j, i, rv[j], want_rv[i])
+        if want_dig[i] is not None:
+            assert hashlib.sha256(outs[j]).digest() == want_dig[i], (j, i)
+
+
+@pytest.mark.parametrize("dist", [0, 1, 2, 3, 4, 5])
+def test_decode_lane_path_roundtrip(tc, dist):
+    """64K x 4 KiB pages of every pagegen distribution through the lane-per-page decoder."""
+    n, plen = 65536, 4096
+    pages = tc.pagegen(n, plen, seed=77, first=dist * 1000, dist=dist, device=DEV)
+    comp, clen = tc.compress_pages(pages)
+    out, rv = tc.decompress_pages(comp, clen, plen)
+    torch.cuda.synchronize()
+    assert bool((rv == plen).all()) and torch.equal(out, pages)

@@ -214,11 +214,10 @@ __device__ int32_t decode_lane(const uint8_t *__restrict__ in, int32_t L, uint8_
 // CU the L2 evicts most of them half-full (PMC: 79 KiB written and ~1,000 L2
 // misses per 16 KiB page).  Here the stores to HBM are aligned full lines
 // written once, and matches whose source lies in the ring (70 % of them on the
-// bench pages: offset <= kRing - 48) never touch HBM; the others read the
+// bench pages: offset <= kRing - 32) never touch HBM; the others read the
 // page's already-flushed bytes back from HBM.
-constexpr int32_t kRing = 512;                 // power of two
-constexpr int32_t kRingStride = kRing + 48;    // 16 B front slack, 32 B tail slack
-constexpr int32_t kRingNear = kRing - 48;      // offsets up to this read the ring
+// kRing (power of two): ring bytes per lane; stride adds 16 B front slack and
+// 32 B tail slack; offsets up to kRing - 32 read the ring
 constexpr int32_t kLine = 64;
 
 typedef __attribute__((address_space(3))) u32x4_ua l_u32x4_ua;
@@ -230,7 +229,9 @@ __device__ __forceinline__ void lds16(uint8_t *p, u128 v) {
 }
 // 16 bytes of the ring at page position x (valid for any x: the 16 bytes past
 // the ring's end mirror its first 16)
+template <int32_t kRing>
 __device__ __forceinline__ u128 ring_rd(uint8_t *rb, int32_t x) { return lds16(rb + (x & (kRing - 1))); }
+template <int32_t kRing>
 __device__ __forceinline__ void ring_wr(uint8_t *rb, int32_t x, u128 v) {
     const int32_t q = x & (kRing - 1);
     lds16(rb + q, v);
@@ -238,18 +239,20 @@ __device__ __forceinline__ void ring_wr(uint8_t *rb, int32_t x, u128 v) {
     if (q < 16) lds16(rb + q + kRing, v);           // mirror of the start, past the end
 }
 // write out the whole lines of [fl, fin)
+template <int32_t kRing>
 __device__ __forceinline__ void ring_flush(uint8_t *rb, uint8_t *__restrict__ out, int32_t &fl, int32_t fin) {
     while (fin - fl >= kLine) {
 #pragma unroll
-        for (int32_t j = 0; j < kLine; j += 16) st16(out + fl + j, ring_rd(rb, fl + j));
+        for (int32_t j = 0; j < kLine; j += 16) st16(out + fl + j, ring_rd<kRing>(rb, fl + j));
         fl += kLine;
     }
 }
+template <int32_t kRing>
 __device__ __forceinline__ void ring_flush_all(uint8_t *rb, uint8_t *__restrict__ out, int32_t &fl, int32_t fin) {
-    ring_flush(rb, out, fl, fin);
-    for (; fl + 16 <= fin; fl += 16) st16(out + fl, ring_rd(rb, fl));
+    ring_flush<kRing>(rb, out, fl, fin);
+    for (; fl + 16 <= fin; fl += 16) st16(out + fl, ring_rd<kRing>(rb, fl));
     if (fl < fin) {
-        const u128 v = ring_rd(rb, fl);
+        const u128 v = ring_rd<kRing>(rb, fl);
         for (int32_t j = 0; fl + j < fin; j++) st1(out + fl + j, (uint32_t)(v >> (8 * j)) & 0xFFu);
         fl = fin;
     }
@@ -259,6 +262,7 @@ __device__ __forceinline__ u128 stream16(const uint8_t *__restrict__ in, int32_t
 }
 
 // LZ4_decompress_safe(in, out, L, C) through the ring rb (as decode_lane)
+template <int32_t kRing>
 __device__ int32_t decode_ring(const uint8_t *__restrict__ in, int32_t L, uint8_t *__restrict__ out, int32_t C,
                                uint8_t *rb) {
     if (C == 0) return (L == 1 && ld1(in) == 0) ? 0 : -1;
@@ -280,16 +284,16 @@ __device__ int32_t decode_ring(const uint8_t *__restrict__ in, int32_t L, uint8_
         if (op + lit > C - kMfLimit || ip + pos + lit > L - 8) {   // lz4.c:1147-1163
             ip += pos;
             if (ip + lit != L || op + lit > C) return -ip - 1;
-            ring_flush_all(rb, out, fl, op);
+            ring_flush_all<kRing>(rb, out, fl, op);
             copy_run(out + op, in + ip, lit, C - op, L - ip);
             return op + lit;
         }
         if (lit <= 16) {
-            ring_wr(rb, op, shr256(w, pos).lo);
+            ring_wr<kRing>(rb, op, shr256(w, pos).lo);
         } else {
             for (int32_t k = 0; k < lit; k += 16) {
-                ring_wr(rb, op + k, stream16(in, ip + pos + k, L));
-                ring_flush(rb, out, fl, op + min(k + 16, lit));
+                ring_wr<kRing>(rb, op + k, stream16(in, ip + pos + k, L));
+                ring_flush<kRing>(rb, out, fl, op + min(k + 16, lit));
             }
         }
         pos += lit;
@@ -309,18 +313,19 @@ __device__ int32_t decode_ring(const uint8_t *__restrict__ in, int32_t L, uint8_
         }
         ml += kMinMatch;
         if (op + ml > C - kLastLiterals) return -(ip + pos) - 1;   // lz4.c:1225
-        // the unflushed tail is < kLine + 32 bytes here, so a source at
-        // offset > kRingNear is already in HBM; a nearer one is in the ring
-        const bool far = off > kRingNear;
-        u128 m = far ? ld16(out + op - off) : ring_rd(rb, op - off);
+        // the unflushed tail is < kLine + 16 bytes here and the ring holds every
+        // position above op + 16 - kRing, so a source at offset > kRing - 32
+        // (>= 96) is already in HBM and a nearer one is in the ring
+        const bool far = off > kRing - 32;
+        u128 m = far ? ld16(out + op - off) : ring_rd<kRing>(rb, op - off);
         ip += pos;
         w = window(in, ip, L);
         if (off >= 16) {
-            ring_wr(rb, op, m);
+            ring_wr<kRing>(rb, op, m);
             for (int32_t k = 16; k < ml; k += 16) {
-                ring_flush(rb, out, fl, op + k);
-                m = far ? ld16(out + op + k - off) : ring_rd(rb, op + k - off);
-                ring_wr(rb, op + k, m);
+                ring_flush<kRing>(rb, out, fl, op + k);
+                m = far ? ld16(out + op + k - off) : ring_rd<kRing>(rb, op + k - off);
+                ring_wr<kRing>(rb, op + k, m);
             }
         } else {
             // period-`off` pattern (offset 0: undefined bytes, zeros here)
@@ -332,19 +337,20 @@ __device__ int32_t decode_ring(const uint8_t *__restrict__ in, int32_t L, uint8_
                 step = 16 - (int32_t)mod_small(16u, (uint32_t)off);
             }
             for (int32_t k = 0; k < ml; k += step) {
-                ring_flush(rb, out, fl, op + k);
-                ring_wr(rb, op + k, p);
+                ring_flush<kRing>(rb, out, fl, op + k);
+                ring_wr<kRing>(rb, op + k, p);
             }
         }
         op += ml;
-        ring_flush(rb, out, fl, op);
+        ring_flush<kRing>(rb, out, fl, op);
     }
 }
 
+template <int32_t kRing>
 __global__ __launch_bounds__(64) void lz4_decode_ring_kernel(tyche_batch_t b, uint32_t in_cap, uint32_t out_cap,
                                                              unsigned *ctr) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    uint8_t *rb = smem + threadIdx.x * kRingStride + 16;
+    uint8_t *rb = smem + threadIdx.x * (kRing + 48) + 16;
     const size_t nthreads = (size_t)gridDim.x * blockDim.x;
     size_t page = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     while (page < b.count) {
@@ -356,7 +362,7 @@ __global__ __launch_bounds__(64) void lz4_decode_ring_kernel(tyche_batch_t b, ui
         if (L > in_cap || C > out_cap) {
             rv = kResultTooLarge;
         } else {
-            rv = decode_ring((const uint8_t *)b.src + so, (int32_t)L, (uint8_t *)b.dst + dof, (int32_t)C, rb);
+            rv = decode_ring<kRing>((const uint8_t *)b.src + so, (int32_t)L, (uint8_t *)b.dst + dof, (int32_t)C, rb);
         }
         b.results[page] = rv;
         page = (size_t)atomicAdd(ctr, 1u) + nthreads;
@@ -395,8 +401,10 @@ bool lz4_lane_decode_wanted(size_t count) {
     return min_pages >= 0 && count >= (size_t)min_pages;
 }
 
-// resident waves per CU (1M x 16 KiB pages, ms: 4 waves 88.9, 8: 98.7, 16: 105.3, all: 106.9)
+// ring-less kernel: resident waves per CU (1M x 16 KiB pages, ms: 4 waves 80.8, 8: 92.1, 2: 97.7)
 constexpr size_t kLaneWaves = 4;
+// ring bytes per lane (0: the ring-less kernel)
+constexpr int kDefaultRing = 256;
 
 hipError_t launch_lz4_decode_lane(const tyche_batch_t &b, uint32_t in_cap, uint32_t out_cap, hipStream_t s) {
     if (b.count == 0) return hipSuccess;
@@ -410,20 +418,25 @@ hipError_t launch_lz4_decode_lane(const tyche_batch_t &b, uint32_t in_cap, uint3
     }
     const size_t ncu = dev < 64 ? cus[dev] : 256;
     static const long env_waves = getenv("TYCHE_LZ4_LANE_WAVES") ? atol(getenv("TYCHE_LZ4_LANE_WAVES")) : 0;
-    static const int ring = getenv("TYCHE_LZ4_LANE_RING") ? atoi(getenv("TYCHE_LZ4_LANE_RING")) : 1;
+    static const int ring = getenv("TYCHE_LZ4_LANE_RING") ? atoi(getenv("TYCHE_LZ4_LANE_RING")) : kDefaultRing;
     if (ring) {
-        const size_t lds = 64 * (size_t)kRingStride;
+        const void *k = ring == 128   ? (const void *)lz4_decode_ring_kernel<128>
+                        : ring == 256 ? (const void *)lz4_decode_ring_kernel<256>
+                                      : (const void *)lz4_decode_ring_kernel<512>;
+        const int32_t rbytes = ring == 128 ? 128 : ring == 256 ? 256 : 512;
+        const size_t lds = 64 * (size_t)(rbytes + 48);
         static bool attr = false;
         if (!attr) {
-            (void)hipFuncSetAttribute((const void *)lz4_decode_ring_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      160 * 1024);
+            (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
             attr = true;
         }
-        size_t waves = waves_per_cu((const void *)lz4_decode_ring_kernel, lds);
+        size_t waves = waves_per_cu(k, lds);
         if (env_waves > 0) waves = std::min<size_t>(waves, (size_t)env_waves);
         const size_t grid = std::min<size_t>((b.count + 63) / 64, ncu * waves);
-        hipLaunchKernelGGL(lz4_decode_ring_kernel, dim3((unsigned)grid), dim3(64), lds, s, b, in_cap, out_cap,
-                           work_counter(s));
+        void *args[] = {(void *)&b, &in_cap, &out_cap, nullptr};
+        unsigned *ctr = work_counter(s);
+        args[3] = &ctr;
+        (void)hipLaunchKernel(k, dim3((unsigned)grid), dim3(64), args, lds, s);
         return hipGetLastError();
     }
     size_t waves = waves_per_cu((const void *)lz4_decode_lane_kernel, 0);
