@@ -262,13 +262,38 @@ __device__ __forceinline__ u128 stream16(const uint8_t *__restrict__ in, int32_t
 }
 
 // LZ4_decompress_safe(in, out, L, C) through the ring rb (as decode_lane)
-template <int32_t kRing>
+// kWin = 16: one 16-byte load per sequence (covers the token, literals and
+// offset of all but ~1 % of sequences; the rest read single bytes)
+template <int32_t kWin>
+__device__ __forceinline__ Win windowN(const uint8_t *__restrict__ in, int32_t ip, int32_t L) {
+    if (kWin == 32) return window(in, ip, L);
+    Win w;
+    w.hi = 0;
+    if (ip + 16 <= L) {
+        w.lo = ld16(in + ip);
+    } else if (L >= 16) {
+        w.lo = ld16(in + L - 16) >> (8 * (ip - (L - 16)));
+    } else {
+        w.lo = 0;
+        for (int32_t j = L - 1; j >= ip; j--) w.lo = (w.lo << 8) | ld1(in + j);
+    }
+    return w;
+}
+template <int32_t kWin>
+__device__ __forceinline__ uint32_t getbN(const Win &w, const uint8_t *__restrict__ in, int32_t ip, int32_t rel,
+                                          int32_t L) {
+    if (kWin == 32) return getb(w, in, ip, rel, L);
+    if (rel < 16) return (uint32_t)(w.lo >> (8 * rel)) & 0xFFu;
+    return byte_at(in, ip + rel, L);
+}
+
+template <int32_t kRing, int32_t kWin>
 __device__ int32_t decode_ring(const uint8_t *__restrict__ in, int32_t L, uint8_t *__restrict__ out, int32_t C,
                                uint8_t *rb) {
     if (C == 0) return (L == 1 && ld1(in) == 0) ? 0 : -1;
     if (L <= 0) return -1;
     int32_t ip = 0, op = 0, fl = 0;   // fl: bytes of the page already in HBM
-    Win w = window(in, 0, L);
+    Win w = windowN<kWin>(in, 0, L);
     for (;;) {
         const uint32_t token = (uint32_t)w.lo & 0xFFu;
         int32_t lit = (int32_t)(token >> 4);
@@ -276,7 +301,7 @@ __device__ int32_t decode_ring(const uint8_t *__restrict__ in, int32_t L, uint8_
         if (lit == kRunMask) {
             uint32_t s;
             do {
-                s = getb(w, in, ip, pos, L);
+                s = getbN<kWin>(w, in, ip, pos, L);
                 pos++;
                 lit += (int32_t)s;
             } while (ip + pos < L - kRunMask && s == 255);
@@ -288,7 +313,7 @@ __device__ int32_t decode_ring(const uint8_t *__restrict__ in, int32_t L, uint8_
             copy_run(out + op, in + ip, lit, C - op, L - ip);
             return op + lit;
         }
-        if (lit <= 16) {
+        if (kWin == 32 ? lit <= 16 : pos + lit <= 16) {
             ring_wr<kRing>(rb, op, shr256(w, pos).lo);
         } else {
             for (int32_t k = 0; k < lit; k += 16) {
@@ -297,7 +322,7 @@ __device__ int32_t decode_ring(const uint8_t *__restrict__ in, int32_t L, uint8_
             }
         }
         pos += lit;
-        const int32_t off = (int32_t)(getb(w, in, ip, pos, L) | (getb(w, in, ip, pos + 1, L) << 8));
+        const int32_t off = (int32_t)(getbN<kWin>(w, in, ip, pos, L) | (getbN<kWin>(w, in, ip, pos + 1, L) << 8));
         pos += 2;
         op += lit;
         if (off > op) return -(ip + pos) - 1;                   // lz4.c:1168
@@ -305,7 +330,7 @@ __device__ int32_t decode_ring(const uint8_t *__restrict__ in, int32_t L, uint8_
         if (ml == 15) {
             uint32_t s;
             do {
-                s = getb(w, in, ip, pos, L);
+                s = getbN<kWin>(w, in, ip, pos, L);
                 pos++;
                 if (ip + pos > L - kLastLiterals) return -(ip + pos) - 1;   // lz4.c:1176
                 ml += (int32_t)s;
@@ -319,7 +344,7 @@ __device__ int32_t decode_ring(const uint8_t *__restrict__ in, int32_t L, uint8_
         const bool far = off > kRing - 32;
         u128 m = far ? ld16(out + op - off) : ring_rd<kRing>(rb, op - off);
         ip += pos;
-        w = window(in, ip, L);
+        w = windowN<kWin>(in, ip, L);
         if (off >= 16) {
             ring_wr<kRing>(rb, op, m);
             for (int32_t k = 16; k < ml; k += 16) {
@@ -346,7 +371,7 @@ __device__ int32_t decode_ring(const uint8_t *__restrict__ in, int32_t L, uint8_
     }
 }
 
-template <int32_t kRing>
+template <int32_t kRing, int32_t kWin>
 __global__ __launch_bounds__(64) void lz4_decode_ring_kernel(tyche_batch_t b, uint32_t in_cap, uint32_t out_cap,
                                                              unsigned *ctr) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -362,7 +387,7 @@ __global__ __launch_bounds__(64) void lz4_decode_ring_kernel(tyche_batch_t b, ui
         if (L > in_cap || C > out_cap) {
             rv = kResultTooLarge;
         } else {
-            rv = decode_ring<kRing>((const uint8_t *)b.src + so, (int32_t)L, (uint8_t *)b.dst + dof, (int32_t)C, rb);
+            rv = decode_ring<kRing, kWin>((const uint8_t *)b.src + so, (int32_t)L, (uint8_t *)b.dst + dof, (int32_t)C, rb);
         }
         b.results[page] = rv;
         page = (size_t)atomicAdd(ctr, 1u) + nthreads;
@@ -405,6 +430,8 @@ bool lz4_lane_decode_wanted(size_t count) {
 constexpr size_t kLaneWaves = 4;
 // ring bytes per lane (0: the ring-less kernel)
 constexpr int kDefaultRing = 256;
+// stream window bytes per sequence (16 or 32; 1M x 16 KiB pages at 256-byte rings: 34.2 / 37.8 ms)
+constexpr int kDefaultWin = 16;
 
 hipError_t launch_lz4_decode_lane(const tyche_batch_t &b, uint32_t in_cap, uint32_t out_cap, hipStream_t s) {
     if (b.count == 0) return hipSuccess;
@@ -420,9 +447,13 @@ hipError_t launch_lz4_decode_lane(const tyche_batch_t &b, uint32_t in_cap, uint3
     static const long env_waves = getenv("TYCHE_LZ4_LANE_WAVES") ? atol(getenv("TYCHE_LZ4_LANE_WAVES")) : 0;
     static const int ring = getenv("TYCHE_LZ4_LANE_RING") ? atoi(getenv("TYCHE_LZ4_LANE_RING")) : kDefaultRing;
     if (ring) {
-        const void *k = ring == 128   ? (const void *)lz4_decode_ring_kernel<128>
-                        : ring == 256 ? (const void *)lz4_decode_ring_kernel<256>
-                                      : (const void *)lz4_decode_ring_kernel<512>;
+        static const int win = getenv("TYCHE_LZ4_LANE_WIN") ? atoi(getenv("TYCHE_LZ4_LANE_WIN")) : kDefaultWin;
+        const void *k = win == 16 ? (ring == 128   ? (const void *)lz4_decode_ring_kernel<128, 16>
+                                     : ring == 256 ? (const void *)lz4_decode_ring_kernel<256, 16>
+                                                   : (const void *)lz4_decode_ring_kernel<512, 16>)
+                                  : (ring == 128   ? (const void *)lz4_decode_ring_kernel<128, 32>
+                                     : ring == 256 ? (const void *)lz4_decode_ring_kernel<256, 32>
+                                                   : (const void *)lz4_decode_ring_kernel<512, 32>);
         const int32_t rbytes = ring == 128 ? 128 : ring == 256 ? 256 : 512;
         const size_t lds = 64 * (size_t)(rbytes + 48);
         static bool attr = false;
