@@ -300,3 +300,32 @@ def test_decode_lane_path_roundtrip(tc, dist):
     out, rv = tc.decompress_pages(comp, clen, plen)
     torch.cuda.synchronize()
     assert bool((rv == plen).all()) and torch.equal(out, pages)
+
+
+def test_decode_lane_path_corruptions(tc, oracle_mod):
+    """64K seeded corruptions (byte flips, truncations) through the lane-per-page decoder:
+    every return value is the restated LZ4_decompress_safe's (lz4.c:1251), and the
+    untouched pages decode bit-exactly."""
+    n, plen = 65536, 4096
+    pages = tc.pagegen(n, plen, seed=99, dist=0, device=DEV)
+    comp, clen = tc.compress_pages(pages)
+    torch.cuda.synchronize()
+    ch, lh = comp.cpu().numpy().copy(), clen.cpu().numpy().astype(np.int64).copy()
+    rng = np.random.default_rng(20170303)
+    kind = rng.integers(0, 4, n)          # 0 clean, 1 flip, 2 truncate, 3 flip + truncate
+    for i in np.nonzero(kind & 1)[0]:
+        for _ in range(int(rng.integers(1, 4))):
+            ch[i, rng.integers(0, lh[i])] ^= np.uint8(rng.integers(1, 256))
+    for i in np.nonzero(kind & 2)[0]:
+        lh[i] = int(rng.integers(0, lh[i]))
+    d_comp = torch.from_numpy(ch).to(DEV)
+    d_len = torch.from_numpy(lh.astype(np.int32)).to(DEV)
+    out, rv = tc.decompress_pages(d_comp, d_len, plen, max_comp_len=int(ch.shape[1]))
+    torch.cuda.synchronize()
+    rv, out = rv.cpu().numpy(), out.cpu().numpy()
+    host = pages.cpu().numpy()
+    for i in range(n):
+        r, dec = oracle_mod.lz4_decompress(ch[i, :lh[i]].tobytes(), plen)
+        assert rv[i] == r, (i, kind[i], rv[i], r)
+        if kind[i] == 0:
+            assert r == plen and out[i].tobytes() == host[i].tobytes(), i
