@@ -49,9 +49,26 @@ __device__ __forceinline__ u128 ld16(const uint8_t *p) {
     u32x4 v = *(const g_u32x4_ua *)(uintptr_t)p;
     return __builtin_bit_cast(u128, v);
 }
+// Cache-policy experiments (-DTYCHE_ABLATE, tools/time_decode.py over
+// libtyche_codec_ablN.so): 16 = non-temporal stream loads, 32 = non-temporal
+// line flushes.
+#ifndef TYCHE_ABLATE
+#define TYCHE_ABLATE 0
+#endif
+__device__ __forceinline__ u128 ld16s(const uint8_t *p) {
+    if (TYCHE_ABLATE & 16) return __builtin_bit_cast(u128, __builtin_nontemporal_load((const g_u32x4_ua *)(uintptr_t)p));
+    return ld16(p);
+}
 __device__ __forceinline__ uint64_t ld8(const uint8_t *p) { return *(const g_u64_ua *)(uintptr_t)p; }
 __device__ __forceinline__ void st16(uint8_t *p, u128 v) {
     *(g_u32x4_ua *)(uintptr_t)p = __builtin_bit_cast(u32x4, v);
+}
+__device__ __forceinline__ void st16f(uint8_t *p, u128 v) {
+    if (TYCHE_ABLATE & 32) {
+        __builtin_nontemporal_store(__builtin_bit_cast(u32x4, v), (g_u32x4_ua *)(uintptr_t)p);
+        return;
+    }
+    st16(p, v);
 }
 __device__ __forceinline__ uint32_t ld1(const uint8_t *p) { return *(const g_u8 *)(uintptr_t)p; }
 __device__ __forceinline__ void st1(uint8_t *p, uint32_t v) { *(g_u8 *)(uintptr_t)p = (uint8_t)v; }
@@ -243,7 +260,7 @@ template <int32_t kRing>
 __device__ __forceinline__ void ring_flush(uint8_t *rb, uint8_t *__restrict__ out, int32_t &fl, int32_t fin) {
     while (fin - fl >= kLine) {
 #pragma unroll
-        for (int32_t j = 0; j < kLine; j += 16) st16(out + fl + j, ring_rd<kRing>(rb, fl + j));
+        for (int32_t j = 0; j < kLine; j += 16) st16f(out + fl + j, ring_rd<kRing>(rb, fl + j));
         fl += kLine;
     }
 }
@@ -270,9 +287,9 @@ __device__ __forceinline__ Win windowN(const uint8_t *__restrict__ in, int32_t i
     Win w;
     w.hi = 0;
     if (ip + 16 <= L) {
-        w.lo = ld16(in + ip);
+        w.lo = ld16s(in + ip);
     } else if (L >= 16) {
-        w.lo = ld16(in + L - 16) >> (8 * (ip - (L - 16)));
+        w.lo = ld16s(in + L - 16) >> (8 * (ip - (L - 16)));
     } else {
         w.lo = 0;
         for (int32_t j = L - 1; j >= ip; j--) w.lo = (w.lo << 8) | ld1(in + j);
@@ -419,10 +436,13 @@ __global__ __launch_bounds__(64) void lz4_decode_lane_kernel(tyche_batch_t b, ui
 }  // namespace
 
 // Threshold and residency (env, for A/B timing): TYCHE_LZ4_LANE_MIN pages per
-// batch (default 65536) switch the batch to this kernel, TYCHE_LZ4_LANE_WAVES
-// resident waves per CU (default kLaneWaves).
+// batch (default kLaneMin) switch the batch to this kernel, TYCHE_LZ4_LANE_WAVES
+// caps the resident waves per CU.  Crossover (16 KiB pages, ms per 1M pages,
+// wave / lane kernel): 16K pages 130.6 / 170.2, 32K 114.4 / 91.6, 64K 108.0 /
+// 52.9, 128K 104.2 / 41.2 -- the lane kernel needs ~512 pages per CU in flight.
+constexpr long kLaneMin = 32768;
 bool lz4_lane_decode_wanted(size_t count) {
-    static const long min_pages = getenv("TYCHE_LZ4_LANE_MIN") ? atol(getenv("TYCHE_LZ4_LANE_MIN")) : 65536;
+    static const long min_pages = getenv("TYCHE_LZ4_LANE_MIN") ? atol(getenv("TYCHE_LZ4_LANE_MIN")) : kLaneMin;
     return min_pages >= 0 && count >= (size_t)min_pages;
 }
 
