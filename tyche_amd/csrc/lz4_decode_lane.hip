@@ -233,7 +233,7 @@ __device__ int32_t decode_lane(const uint8_t *__restrict__ in, int32_t L, uint8_
 // written once, and matches whose source lies in the ring (70 % of them on the
 // bench pages: offset <= kRing - 32) never touch HBM; the others read the
 // page's already-flushed bytes back from HBM.
-// kRing (power of two): ring bytes per lane; stride adds 16 B front slack and
+// kRing: ring bytes per lane (a multiple of 16); stride adds 16 B front slack and
 // 32 B tail slack; offsets up to kRing - 32 read the ring
 constexpr int32_t kLine = 64;
 
@@ -247,10 +247,10 @@ __device__ __forceinline__ void lds16(uint8_t *p, u128 v) {
 // 16 bytes of the ring at page position x (valid for any x: the 16 bytes past
 // the ring's end mirror its first 16)
 template <int32_t kRing>
-__device__ __forceinline__ u128 ring_rd(uint8_t *rb, int32_t x) { return lds16(rb + (x & (kRing - 1))); }
+__device__ __forceinline__ u128 ring_rd(uint8_t *rb, int32_t x) { return lds16(rb + ((int32_t)((uint32_t)x % (uint32_t)kRing))); }
 template <int32_t kRing>
 __device__ __forceinline__ void ring_wr(uint8_t *rb, int32_t x, u128 v) {
-    const int32_t q = x & (kRing - 1);
+    const int32_t q = (int32_t)((uint32_t)x % (uint32_t)kRing);
     lds16(rb + q, v);
     if (q + 16 > kRing) lds16(rb + q - kRing, v);   // wrapped part, to the ring's start
     if (q < 16) lds16(rb + q + kRing, v);           // mirror of the start, past the end
@@ -448,7 +448,8 @@ bool lz4_lane_decode_wanted(size_t count) {
 
 // ring-less kernel: resident waves per CU (1M x 16 KiB pages, ms: 4 waves 80.8, 8: 92.1, 2: 97.7)
 constexpr size_t kLaneWaves = 4;
-// ring bytes per lane (0: the ring-less kernel)
+// ring bytes per lane (0: the ring-less kernel; a 208-byte ring, 10 waves per
+// CU, ran 34.7 ms per 1M pages vs 34.5 at 256 bytes and 8 waves)
 constexpr int kDefaultRing = 256;
 // stream window bytes per sequence (16 or 32; 1M x 16 KiB pages at 256-byte rings: 34.2 / 37.8 ms)
 constexpr int kDefaultWin = 16;
