@@ -329,3 +329,21 @@ def test_decode_lane_path_corruptions(tc, oracle_mod):
         assert rv[i] == r, (i, kind[i], rv[i], r)
         if kind[i] == 0:
             assert r == plen and out[i].tobytes() == host[i].tobytes(), i
+
+
+@pytest.mark.parametrize("plen", [8192, 32768, 65535])
+def test_decode_lane_path_page_sizes(tc, oracle_mod, plen):
+    """32K-page batches (the lane decoder's threshold) of 8 KiB, 32 KiB and 65,535-byte
+    pages: round trip on the GPU, and a sample of the streams decodes identically with the
+    oracle restatement."""
+    n = 32768
+    gen = (plen + 4095) // 4096 * 4096          # pagegen sizes; 65,535 = the byU16 limit, cut from 64 KiB
+    pages = tc.pagegen(n, gen, seed=31, first=plen, dist=0, device=DEV)[:, :plen].contiguous()
+    comp, clen = tc.compress_pages(pages)
+    out, rv = tc.decompress_pages(comp, clen, plen)
+    torch.cuda.synchronize()
+    assert bool((rv == plen).all()) and torch.equal(out, pages)
+    ch, lh, host = comp[:64].cpu().numpy(), clen[:64].cpu().numpy(), pages[:64].cpu().numpy()
+    for i in range(64):
+        r, dec = oracle_mod.lz4_decompress(ch[i, :lh[i]].tobytes(), plen)
+        assert r == plen and dec == host[i].tobytes(), i
