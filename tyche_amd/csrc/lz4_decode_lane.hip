@@ -1,26 +1,31 @@
 // lz4_decode_lane.hip -- throughput LZ4 block decode for large batches: one
-// page per LANE (64 pages per wave), decoded straight from the compressed
-// stream in HBM into the page's destination in HBM.
+// page per LANE (64 pages per wave), read straight from the compressed stream
+// in HBM (reference path: buffer__decompress, src/buffer.c:248-253 ->
+// LZ4_decompress_safe, src/lz4/lz4.c:1251, generic decoder lz4.c:1089-1248).
 //
 // The wave-per-page decoder (lz4_decode.hip) spends ~40 k wave instructions per
 // 16 KiB page reconstructing LZ4's two serial chains (token chain, match
 // dependencies) in parallel.  A lane that simply runs the reference's
-// sequential loop (lz4.c:1089-1248, restated in decode_page_serial) issues ~50
-// instructions per sequence, and with 64 pages per wave that is under 1/20th
-// of the instruction stream; the cost moves to the vector memory pipe (every
-// load/store touches 64 different lines) and to latency, which the batch
-// hides: a 1M-page batch keeps every lane of every resident wave busy.
+// sequential loop (restated in decode_page_serial) issues ~50 instructions per
+// sequence, and with 64 pages per wave that is ~1/20th of the instruction
+// stream; the cost moves to memory latency, which a batch of >= 32K pages
+// hides (launch_lz4_decode switches at kLaneMin).
 //
-// Copies are 16 bytes per access (unaligned global_load/store_dwordx4) and may
-// run past the sequence end ("wild copies", as lz4.c's LZ4_wildCopy) but never
-// past the page's capacity C; the bytes past the decoded end are overwritten by
-// later sequences before anything reads them.  A lane's store followed by its
-// own load of the same address returns the stored value (vector memory
-// operations of one wave are performed in order), which the forward semantics
-// of overlapping copies rely on.  Self-overlapping matches with offset < 16
-// (runs: offset 1 = a repeated byte) are expanded in registers to a 16-byte
-// pattern of period `offset` and stored with a stride that is a multiple of
-// the offset -- no read-after-write through memory at all.
+// Two kernels:
+//  * lz4_decode_ring_kernel (default): the page is assembled in a per-lane LDS
+//    ring of its last kRing output bytes and leaves for HBM in aligned whole
+//    64-byte lines; near matches read the ring, far ones the page's flushed
+//    lines in HBM.  One 16-byte stream window per sequence, loaded before the
+//    current sequence's copies.
+//  * lz4_decode_lane_kernel (TYCHE_LZ4_LANE_RING=0, the A/B baseline): copies
+//    16 bytes per access straight between HBM buffers, "wild" past a
+//    sequence's end as lz4.c's LZ4_wildCopy but never past the capacity C.  A
+//    lane's store followed by its own load of the same address returns the
+//    stored value (one wave's vector memory operations are performed in order),
+//    which overlapping forward copies rely on.
+// Both expand self-overlapping matches with offset < 16 (offset 1 = a run) in
+// registers to a 16-byte pattern of period `offset`, stored with a stride that
+// is a multiple of the offset.
 //
 // Results are LZ4_decompress_safe's, checks in the reference's order: the
 // decoded size, or -(input bytes consumed)-1 for a malformed stream (the
@@ -73,10 +78,11 @@ __device__ __forceinline__ void st16f(uint8_t *p, u128 v) {
 __device__ __forceinline__ uint32_t ld1(const uint8_t *p) { return *(const g_u8 *)(uintptr_t)p; }
 __device__ __forceinline__ void st1(uint8_t *p, uint32_t v) { *(g_u8 *)(uintptr_t)p = (uint8_t)v; }
 
-// 32-byte stream window at ip, zero past L.  The parse of a sequence reads
-// its token, length bytes, short literals and offset from the window; the
-// next sequence's window is loaded before the current one's copies, so one
-// load latency per sequence sits on the serial chain.
+// 32-byte stream window at ip, zero past L (windowN<16> below is the default
+// 16-byte one).  The parse of a sequence reads its token, length bytes, short
+// literals and offset from the window; the next sequence's window is loaded
+// before the current one's copies, so one load latency per sequence sits on
+// the serial chain.
 struct Win {
     u128 lo, hi;
 };
