@@ -35,14 +35,15 @@ def _newer(target: str, deps: list[str]) -> bool:
 
 
 def build(force: bool = False, verbose: bool = False, profile: bool = False, ablate: int = 0,
-          eablate: int = 0) -> str:
+          eablate: int = 0, defines: tuple = ()) -> str:
     """profile=True builds the diagnostic variant (per-phase cycle stamps, -DTYCHE_PROFILE)
     as libtyche_codec_prof.so; it is never loaded by the product path."""
-    tag = ("_prof" if profile else "") + (f"_abl{ablate}" if ablate else "") + (f"_eabl{eablate}" if eablate else "")
+    tag = ("_prof" if profile else "") + (f"_abl{ablate}" if ablate else "") + (f"_eabl{eablate}" if eablate else "") + \
+        "".join("_" + d.replace("TYCHE_", "").replace("=", "").lower() for d in defines)   # A/B variant libraries
     build_dir = BUILD + tag
     lib_path = LIB.replace(".so", tag + ".so")
     flags = FLAGS + (["-DTYCHE_PROFILE"] if profile else []) + ([f"-DTYCHE_ABLATE={ablate}"] if ablate else []) + \
-        ([f"-DTYCHE_EABLATE={eablate}"] if eablate else [])
+        ([f"-DTYCHE_EABLATE={eablate}"] if eablate else []) + ["-D" + d for d in defines]
     os.makedirs(build_dir, exist_ok=True)
     headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
     headers.append(os.path.join(HERE, "..", "include", "tyche_codec.h"))
