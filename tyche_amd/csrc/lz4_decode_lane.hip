@@ -241,7 +241,14 @@ __device__ int32_t decode_lane(const uint8_t *__restrict__ in, int32_t L, uint8_
 // page's already-flushed bytes back from HBM.
 // kRing: ring bytes per lane (a multiple of 16); stride adds 16 B front slack and
 // 32 B tail slack; offsets up to kRing - 32 read the ring
-constexpr int32_t kLine = 64;
+#ifndef TYCHE_LANE_LINE
+#define TYCHE_LANE_LINE 64
+#endif
+// HBM flush granule (128-byte lines at the 256-byte ring: 34.04-34.08 vs
+// 34.14-34.65 ms per 1M pages with 64, within noise): the unflushed tail stays below kLine + 16 bytes, so far
+// reads (offset > kRing - 32) need kRing >= kLine + 64
+template <int32_t kRing>
+constexpr int32_t line_for() { return kRing >= TYCHE_LANE_LINE + 64 ? TYCHE_LANE_LINE : 64; }
 
 typedef __attribute__((address_space(3))) u32x4_ua l_u32x4_ua;
 __device__ __forceinline__ u128 lds16(const uint8_t *p) {
@@ -264,6 +271,8 @@ __device__ __forceinline__ void ring_wr(uint8_t *rb, int32_t x, u128 v) {
 // write out the whole lines of [fl, fin)
 template <int32_t kRing>
 __device__ __forceinline__ void ring_flush(uint8_t *rb, uint8_t *__restrict__ out, int32_t &fl, int32_t fin) {
+    constexpr int32_t kLine = line_for<kRing>();
+    static_assert(kRing >= kLine + 64, "ring too small for the flush granule");
     while (fin - fl >= kLine) {
 #pragma unroll
         for (int32_t j = 0; j < kLine; j += 16) st16f(out + fl + j, ring_rd<kRing>(rb, fl + j));
