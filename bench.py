@@ -11,12 +11,13 @@ value = uncompressed bytes of all ranks' pages x steps / max-over-ranks wall tim
 
 Prints ONE JSON line on rank 0 with `roofline` (dominant kernel, HIP events on
 the codec's stream) and `cpu_baseline` (the reference's vendored LZ4 1.7.5 from
-oracle/_ref when present, else the oracle port, on the host cores, bounded sample).
+oracle/_ref, timed by oracle/_ref/cpu_baseline: C pthreads on every core the
+process may use -- its affinity mask, capped by its cgroup CPU quota -- over a
+bounded sample of the same pages).
 """
 from __future__ import annotations
 
 import argparse
-import concurrent.futures as cf
 import glob
 import json
 import os
@@ -44,8 +45,8 @@ def parse():
     ap.add_argument("--page-len", type=int, default=16384)
     ap.add_argument("--dist", type=int, default=0, help="pagegen distribution (0 = pg mix)")
     ap.add_argument("--seed", type=int, default=20170303)
-    ap.add_argument("--cpu-pages", type=int, default=131072, help="CPU baseline sample (pages)")
-    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--cpu-pages", type=int, default=131072, help="CPU baseline sample (pages, at least 2048 per thread)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every core the process may use (affinity, cgroup quota)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--e2e-pages", type=int, default=32768, help="host-buffer (PCIe-inclusive) sample; 0 = skip")
     ap.add_argument("--no-extra", action="store_true", help="skip the secondary C3 (zstd) measurement")
@@ -54,119 +55,51 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(pages_dev: torch.Tensor, n: int, threads: int) -> dict:
-    """Vendored LZ4 1.7.5 (or the oracle port) on the host: one codec call per page, pthreads by page range."""
-    import numpy as np
-
-    from oracle import oracle as O
-
-    host = pages_dev[:n].cpu().numpy()
-    plen = host.shape[1]
-    use_ref = O.have_ref()
-    kind = "reference" if use_ref else "port"
-    cap = O.lz4_bound(plen)
-    comp = np.zeros((n, cap), dtype=np.uint8)
-    clen = np.zeros(n, dtype=np.int32)
-    out = np.zeros_like(host)
-    rv = np.zeros(n, dtype=np.int32)
-    chunks = [(i * n // threads, (i + 1) * n // threads) for i in range(threads)]
-
-    if use_ref:
-        import ctypes
-        lib = O._Lib.ref()
-        u8p = ctypes.POINTER(ctypes.c_uint8)
-        base_in, base_c, base_o = host.ctypes.data, comp.ctypes.data, out.ctypes.data
-
-        def comp_range(a, b):
-            for i in range(a, b):
-                clen[i] = lib.LZ4_compress_default(ctypes.cast(base_in + i * plen, u8p),
-                                                   ctypes.cast(base_c + i * cap, u8p), plen, cap)
-
-        def dec_range(a, b):
-            for i in range(a, b):
-                rv[i] = lib.LZ4_decompress_safe(ctypes.cast(base_c + i * cap, u8p),
-                                                ctypes.cast(base_o + i * plen, u8p), int(clen[i]), plen)
-    else:
-        def comp_range(a, b):
-            O.lz4_compress_pages(host, comp, clen, a, b - a)
-
-        def dec_range(a, b):
-            O.lz4_decompress_pages(comp, clen, out, rv, a, b - a)
-
-    best_c = best_d = float("inf")
-    with cf.ThreadPoolExecutor(max_workers=threads) as ex:
-        for _ in range(3):   # best of 3, like the survey's probe
-            t0 = time.perf_counter()
-            list(ex.map(lambda r: comp_range(*r), chunks))
-            t1 = time.perf_counter()
-            list(ex.map(lambda r: dec_range(*r), chunks))
-            t2 = time.perf_counter()
-            best_c, best_d = min(best_c, t1 - t0), min(best_d, t2 - t1)
-    assert (rv == plen).all() and np.array_equal(out, host), "CPU baseline round trip failed"
-    nbytes = n * plen
-    return {
-        "value": round(nbytes / (best_c + best_d) / GIB, 3),
-        "unit": "GiB/s",
-        "cores": threads,
-        "kind": kind,
-        "sample": f"first {n} of the same pages ({nbytes / GIB:.1f} GiB), "
-                  f"{'LZ4_compress_default/LZ4_decompress_safe from oracle/_ref (vendored LZ4 1.7.5)' if use_ref else 'oracle/lz4_oracle.c port'}"
-                  f", one call per page, {threads} threads by page range, best of 3",
-        "compress_gib_s": round(nbytes / best_c / GIB, 3),
-        "decompress_gib_s": round(nbytes / best_d / GIB, 3),
-        "ratio": round(nbytes / float(clen.sum()), 4),
-    }
+def host_cpu() -> tuple[int, str]:
+    """(cores this process can run on, CPU model name): the affinity mask, capped by the cgroup CPU
+    quota when one is set (the GPU box grants 16 CPUs of quota on a 256-CPU affinity mask; more
+    threads than the quota only time-slice the same 16 CPUs)."""
+    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            cores = max(1, min(cores, -(-int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return cores, model
 
 
-def zstd_cpu_baseline(pages_dev: torch.Tensor, n: int, threads: int) -> dict:
-    """The reference's vendored zstd 1.1.2 (oracle/_ref) at level 1 on the host, one call per page."""
-    import ctypes
+def cpu_baseline(codec: str, n: int, page_len: int, threads: int, seed: int, reps: int = 3) -> dict:
+    """The reference's vendored codec on the host: oracle/_ref/cpu_baseline (C, pthreads by page range,
+    one codec call per page, one thread per core of the affinity mask, best of `reps`), over the first n
+    pages of the same generator; None when the reference build is not present."""
+    import subprocess
 
-    import numpy as np
-
-    from oracle import oracle as O
-
-    if not O.have_ref():
+    exe = os.path.join(ROOT, "oracle", "_ref", "cpu_baseline")
+    if not os.path.exists(exe):
         return None
-    lib = O._Lib.ref()
-    host = pages_dev[:n].cpu().numpy()
-    plen = host.shape[1]
-    cap = int(lib.ZSTD_compressBound(plen))
-    comp = np.zeros((n, cap), dtype=np.uint8)
-    clen = np.zeros(n, dtype=np.int64)
-    out = np.zeros_like(host)
-    rv = np.zeros(n, dtype=np.int64)
-    u8p = ctypes.POINTER(ctypes.c_uint8)
-    base_in, base_c, base_o = host.ctypes.data, comp.ctypes.data, out.ctypes.data
-    chunks = [(i * n // threads, (i + 1) * n // threads) for i in range(threads)]
-
-    def comp_range(a, b):
-        for i in range(a, b):
-            clen[i] = lib.ZSTD_compress(ctypes.cast(base_c + i * cap, u8p), cap, ctypes.cast(base_in + i * plen, u8p),
-                                        plen, 1)
-
-    def dec_range(a, b):
-        for i in range(a, b):
-            rv[i] = lib.ZSTD_decompress(ctypes.cast(base_o + i * plen, u8p), plen, ctypes.cast(base_c + i * cap, u8p),
-                                        int(clen[i]))
-
-    best_c = best_d = float("inf")
-    with cf.ThreadPoolExecutor(max_workers=threads) as ex:
-        for _ in range(2):
-            t0 = time.perf_counter()
-            list(ex.map(lambda r: comp_range(*r), chunks))
-            t1 = time.perf_counter()
-            list(ex.map(lambda r: dec_range(*r), chunks))
-            t2 = time.perf_counter()
-            best_c, best_d = min(best_c, t1 - t0), min(best_d, t2 - t1)
-    assert (rv == plen).all() and np.array_equal(out, host), "zstd CPU baseline round trip failed"
-    nbytes = n * plen
-    return {"value": round(nbytes / (best_c + best_d) / GIB, 3), "unit": "GiB/s", "cores": threads,
-            "kind": "reference",
-            "sample": f"first {n} of the same pages ({nbytes / GIB:.2f} GiB), ZSTD_compress(level 1)/ZSTD_decompress "
-                      f"from oracle/_ref (vendored zstd 1.1.2), one call per page, {threads} threads, best of 2",
-            "compress_gib_s": round(nbytes / best_c / GIB, 3), "decompress_gib_s": round(nbytes / best_d / GIB, 3),
-            "ratio": round(nbytes / float(clen.sum()), 4)}
+    out = subprocess.run([exe, codec, str(n), str(page_len), str(threads), str(reps), str(seed)],
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=600)
+    if out.returncode != 0:
+        raise SystemExit(f"CPU baseline failed: {out.stdout.decode()} {out.stderr.decode()}")
+    r = json.loads(out.stdout.decode().strip().splitlines()[-1])
+    _, model = host_cpu()
+    calls = {"lz4": "LZ4_compress_default/LZ4_decompress_safe (vendored LZ4 1.7.5)",
+             "zstd": "ZSTD_compress(level 1)/ZSTD_decompress (vendored zstd 1.1.2)",
+             "zlib": "compress2(level 1)/uncompress (vendored zlib 1.2.8)"}[codec]
+    return {"value": r["combined_gib_s"], "unit": "GiB/s", "cores": r["threads"], "kind": "reference",
+            "sample": f"first {n} of the same pages ({n * page_len / GIB:.1f} GiB), {calls} from oracle/_ref, "
+                      f"one call per page, C pthreads by page range on {r['threads']} threads ({model}), "
+                      f"best of {reps}",
+            "compress_gib_s": r["compress_gib_s"], "decompress_gib_s": r["decompress_gib_s"], "ratio": r["ratio"]}
 
 
 def measure_codec(cid: int, name: str, n: int, plen: int, steps: int, warmup: int, dev, seed: int, first: int,
@@ -358,11 +291,12 @@ def main():
         "ratio": round(page_bytes / comp_bytes, 4),
     }
     if info.rank == 0 and info.world == 1:
-        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        threads = args.cpu_threads or host_cpu()[0]
         if args.e2e_pages > 0:
             result["e2e_host_path"] = e2e_host(pages, min(args.e2e_pages, n))
         if not args.no_cpu:
-            result["cpu_baseline"] = cpu_baseline(pages, min(args.cpu_pages, n), threads)
+            result["cpu_baseline"] = cpu_baseline("lz4", min(max(args.cpu_pages, threads * 2048), n), plen, threads,
+                                                  args.seed)
         if not args.no_extra:
             # C3 (configs[2]): zstd level-1 compress+decompress, 1M x 32 KiB pages, 1 GPU -- reported
             # beside the headline line, never as `value`
@@ -372,7 +306,8 @@ def main():
                                        args.dist)
             c3["workload"] = "C3: zstd level-1 compress+decompress, 1M x 32 KiB pages, 1 GPU, device-resident"
             if not args.no_cpu:
-                c3["cpu_baseline"] = zstd_cpu_baseline(zpages, min(16384, args.extra_pages), threads)
+                c3["cpu_baseline"] = cpu_baseline("zstd", min(max(32768, threads * 256), args.extra_pages), 32768,
+                                                  threads, args.seed, reps=2)
             result["configs"] = {"C3_zstd": c3}
             del zpages
             torch.cuda.empty_cache()

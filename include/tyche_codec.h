@@ -79,7 +79,9 @@ void buffer__destroy(Buffer *buf, const bool destroy_data);
 void buffer__lock(Buffer *buf);
 void buffer__unlock(Buffer *buf);
 void buffer__release_pin(Buffer *buf);
-/* replaces src/buffer.c:159-219: LZ4/zlib/zstd by compressor_id, on the GPU */
+/* replaces src/buffer.c:159-219: LZ4/zlib/zstd by compressor_id, on the GPU.
+ * On a codec or device failure (126 / TYCHE_E_DEVICE) *compressed_data is set
+ * to NULL (the reference leaves it at a leaked, unfilled block). */
 int buffer__compress(Buffer *buf, void **compressed_data, int compressor_id, int compressor_level);
 /* replaces src/buffer.c:227-281 */
 int buffer__decompress(Buffer *buf, int compressor_id);
@@ -98,10 +100,11 @@ int tyche_buffers_compress(Buffer **bufs, void **compressed, int *status, size_t
 int tyche_buffers_decompress(Buffer **bufs, int *status, size_t n, int compressor_id);
 
 /* ---- restore queue: coalesced per-hit restores (src/list.c:563-589) ------- */
-/* Starts a dispatcher thread (on the calling thread's device) that batches
- * concurrent tyche_buffer_restore calls: once a request arrives it waits up to
- * max_wait_us for up to max_batch requests, then runs one GPU decompress batch
- * per codec.  Idempotent. */
+/* Starts the dispatcher threads (TYCHE_RESTORE_DISPATCHERS, default two per
+ * active device; they inherit the calling thread's device choice) that batch
+ * concurrent tyche_buffer_restore calls: once a request arrives one dispatcher
+ * waits up to max_wait_us for up to max_batch requests, then runs one GPU
+ * decompress batch per codec while the next dispatcher collects.  Idempotent. */
 int tyche_restore_queue_start(int max_batch, int max_wait_us);
 /* Drains and stops the dispatcher. */
 void tyche_restore_queue_stop(void);
@@ -162,12 +165,34 @@ int tyche_decompress_host(int compressor_id, size_t n, const void *const *src, c
                           void *const *dst, const uint32_t *dst_capacities, int32_t *results);
 
 /* ---- runtime ------------------------------------------------------------- */
+/* The reference is one process whose compressor pool (src/list.c:142-168,
+ * opts.cpu_count threads, src/manager.c:85) and workers call the codec
+ * concurrently; it has no notion of devices.  By default the host entry points
+ * (Buffer API, host batches, restore queue) therefore use every visible gfx950
+ * device (the first TYCHE_DEVICES of them when that is set): a host batch of at
+ * least two parts' worth of input is cut into contiguous page ranges of about
+ * equal input bytes, one per device, run concurrently (tyche_plan_split); a
+ * smaller one goes whole to the device with the fewest batches in flight, so
+ * concurrent per-page callers spread over all devices.  tyche_set_device(d)
+ * pins the calling thread to device d instead; TYCHE_ALL_DEVICES undoes that.
+ * The device-resident batch API always runs on the caller's current device. */
+#define TYCHE_ALL_DEVICES (-1)
 int tyche_device_count(void);
-/* selects the device used by the calling thread (default 0) */
+/* pins the calling thread's host-path work to `device`, or TYCHE_ALL_DEVICES (default) */
 int tyche_set_device(int device);
+/* devices the calling thread's host-path work is spread over (1 when pinned) */
+int tyche_active_devices(void);
+/* The fan-out plan of a host batch (exported so it can be checked without a
+ * GPU): splits n pages into at most ndev contiguous ranges of about equal input
+ * bytes, each holding at least min_part_bytes of input (0 = no minimum).
+ * Writes cuts[0..k] (cuts[0] = 0, cuts[k] = n; cuts needs ndev + 1 entries)
+ * and returns the number of ranges k >= 1.  The engine uses
+ * min_part_bytes = TYCHE_FANOUT_MIN_BYTES (default 64 MiB, one staging chunk). */
+size_t tyche_plan_split(size_t n, const uint32_t *src_lengths, int ndev, uint64_t min_part_bytes, size_t *cuts);
 /* message for the last TYCHE_E_DEVICE on this thread */
 const char *tyche_last_error(void);
-/* 1 if the library's gfx950 code object is usable on the current device */
+/* 1 if the library's gfx950 code object is usable on the calling thread's
+ * (first) device */
 int tyche_device_ready(void);
 
 /* ---- synthetic input (bench/tests; same generator as the host copy) ------ */

@@ -1,0 +1,154 @@
+"""The host side of the engine as tyche's threads see it (include/tyche_codec.h).
+
+tyche is one process that calls the codec from opts.cpu_count compressor
+threads (src/list.c:142-168, 1051) and its workers (src/list.c:572) at once,
+with no notion of devices.  Covered here:
+
+* CPU: the multi-device fan-out plan (tyche_plan_split) for any injected
+  device count -- contiguous ranges, every page exactly once, balanced input
+  bytes, no part below the minimum.
+* GPU: 300 threads calling buffer__compress / buffer__decompress directly
+  (tools/stress.c: more callers than staging contexts, far more launches than
+  any fixed counter ring) with every page verified; the C5-shaped
+  sweep/restore cycle (tools/cycle.c: mixed 8/16/32 KiB pages, LZ4 + zlib
+  tags, a compressor pool of 250-victim batches, 64 biased restorer threads
+  through the restore queue) on the GPU, and again with the fan-out rehearsed
+  over four "devices" (TYCHE_DEVICE_IDS=0,0,0,0) and small fan-out parts; a
+  host batch that fails part-way leaves no chunk behind for the next call.
+"""
+import ctypes
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+from tyche_amd import _lib
+
+TOOLS = os.path.join(ROOT, "tools", "bin")
+
+
+def _plan(lens, ndev, min_bytes):
+    lib = _lib.load()
+    n = len(lens)
+    arr = (ctypes.c_uint32 * max(n, 1))(*lens)
+    cuts = (ctypes.c_size_t * (max(ndev, 1) + 1))()
+    k = lib.tyche_plan_split(n, arr, ndev, min_bytes, cuts)
+    return [cuts[i] for i in range(k + 1)]
+
+
+def test_plan_split_small_batches_stay_whole():
+    assert _plan([], 8, 64 << 20) == [0, 0]
+    assert _plan([16384] * 1000, 8, 64 << 20) == [0, 1000]          # 16 MiB < two parts' worth
+    assert _plan([16384] * 1000, 1, 0) == [0, 1000]
+
+
+@pytest.mark.parametrize("ndev", [2, 3, 4, 7, 8])
+def test_plan_split_even_pages(ndev):
+    n = 100_000
+    cuts = _plan([16384] * n, ndev, 64 << 20)
+    assert cuts[0] == 0 and cuts[-1] == n and len(cuts) == ndev + 1
+    sizes = np.diff(cuts)
+    assert (sizes > 0).all() and sizes.max() - sizes.min() <= 1
+
+
+def test_plan_split_ragged_balances_bytes():
+    rng = np.random.default_rng(7)
+    lens = rng.choice([8192, 16384, 32768], size=50_000).astype(np.uint32)
+    for ndev in (2, 5, 8):
+        cuts = _plan(lens.tolist(), ndev, 1 << 20)
+        assert len(cuts) == ndev + 1 and cuts[-1] == len(lens)
+        part = [int(lens[a:b].sum()) for a, b in zip(cuts[:-1], cuts[1:])]
+        assert sum(part) == int(lens.sum())
+        assert max(part) - min(part) <= 2 * 32768                     # within a page either side of the goal
+
+
+def test_plan_split_respects_minimum_part():
+    # 8 devices but only ~2.5 minimum parts of input: 2 parts
+    lens = [16384] * 10_000                                            # 156.25 MiB
+    cuts = _plan(lens, 8, 64 << 20)
+    assert len(cuts) == 3 and cuts[-1] == 10_000
+    assert all(b - a >= 4096 for a, b in zip(cuts[:-1], cuts[1:]))
+
+
+def _run_tool(args, env_extra=None, timeout=100):
+    exe = os.path.join(TOOLS, args[0])
+    if not os.path.exists(exe):
+        pytest.skip(f"{exe} not built")
+    env = dict(os.environ)
+    env.update(env_extra or {})
+    p = subprocess.run([exe] + [str(a) for a in args[1:]], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                       timeout=timeout, env=env)
+    out = p.stdout.decode()
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert p.returncode == 0 and lines, (p.returncode, out[-2000:], p.stderr.decode()[-2000:])
+    return json.loads(lines[-1])
+
+
+@pytest.mark.gpu
+def test_buffer_api_300_concurrent_threads():
+    r = _run_tool(["stress", 300, 6])
+    assert r["threads"] == 300 and r["round_trips"] == 300 * 6
+    assert r["mismatches"] == 0 and r["errors"] == 0
+
+
+@pytest.mark.gpu
+def test_c5_cycle_one_process():
+    r = _run_tool(["cycle", 12000, 64, 300, 16])
+    assert r["sweep_fails"] == 0 and r["mismatches"] == 0
+    assert r["restored"] > 0 and r["queue_batches"] < r["restored"]
+
+
+@pytest.mark.gpu
+def test_c5_cycle_fanout_rehearsal():
+    """Four entries in the device set (all device 0 on a one-GPU box) and 1 MiB fan-out parts:
+    sweep batches are split four ways and run concurrently, restores spread by load."""
+    r = _run_tool(["cycle", 8000, 64, 200, 8], {"TYCHE_DEVICE_IDS": "0,0,0,0", "TYCHE_FANOUT_MIN_BYTES": "1048576"})
+    assert r["devices"] == 4
+    assert r["sweep_fails"] == 0 and r["mismatches"] == 0 and r["restored"] > 0
+
+
+@pytest.mark.gpu
+def test_failed_host_batch_leaves_nothing_for_the_next_call(oracle_mod):
+    """A host batch whose second chunk cannot launch (a page capacity the decoders cannot stage)
+    fails with TYCHE_E_DEVICE after its first chunk is already in flight; the staging context goes
+    back to the pool drained, so the next call on the same thread gets exactly its own results."""
+    lib = _lib.load()
+    assert lib.tyche_set_device(0) == 0
+    try:
+        O = oracle_mod
+        plen = 16384
+        n = 12_000                                       # ~6 KB streams: two 64 MiB staging chunks
+        pages = O.pagegen(n, plen, seed=99, dist=0)
+        cap = O.lz4_bound(plen)
+        comp = np.zeros((n, cap), dtype=np.uint8)
+        clen = np.zeros(n, dtype=np.int32)
+        O.lz4_compress_pages(pages, comp, clen, 0, n)
+        bad_cap = 1 << 20                                # LDS for a 1 MiB page window: no decoder takes it
+        out = np.zeros((n + 1, plen), dtype=np.uint8)
+        big = np.zeros(bad_cap, dtype=np.uint8)
+        vp = ctypes.c_void_p * (n + 1)
+        src = vp(*([comp.ctypes.data + i * cap for i in range(n)] + [comp.ctypes.data]))
+        slen = (ctypes.c_uint32 * (n + 1))(*([int(x) for x in clen] + [int(clen[0])]))
+        dst = vp(*([out.ctypes.data + i * plen for i in range(n)] + [big.ctypes.data]))
+        dcap = (ctypes.c_uint32 * (n + 1))(*([plen] * n + [bad_cap]))
+        res = np.zeros(n + 1, dtype=np.int32)
+        i32p = ctypes.POINTER(ctypes.c_int32)
+        rc = lib.tyche_decompress_host(1, n + 1, src, slen, dst, dcap, res.ctypes.data_as(i32p))
+        assert rc == _lib.E_DEVICE, (rc, _lib.last_error())
+        # the next call: a small batch with arrays sized exactly for it
+        m = 100
+        out2 = np.zeros((m, plen), dtype=np.uint8)
+        res2 = np.full(m, -7, dtype=np.int32)
+        src2 = (ctypes.c_void_p * m)(*[comp.ctypes.data + i * cap for i in range(m)])
+        slen2 = (ctypes.c_uint32 * m)(*[int(x) for x in clen[:m]])
+        dst2 = (ctypes.c_void_p * m)(*[out2.ctypes.data + i * plen for i in range(m)])
+        dcap2 = (ctypes.c_uint32 * m)(*([plen] * m))
+        rc = lib.tyche_decompress_host(1, m, src2, slen2, dst2, dcap2, res2.ctypes.data_as(i32p))
+        assert rc == 0, _lib.last_error()
+        assert (res2 == plen).all()
+        assert np.array_equal(out2, pages[:m])
+    finally:
+        lib.tyche_set_device(_lib.ALL_DEVICES)

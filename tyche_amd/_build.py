@@ -14,7 +14,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 BUILD = os.path.join(HERE, "..", "build", "tyche_amd")
 LIB = os.path.join(HERE, "libtyche_codec.so")
-SOURCES = ["engine.hip", "lz4_decode.hip", "lz4_decode_lane.hip", "lz4_encode.hip", "zlib_inflate.hip", "zstd_decode.hip", "zstd_encode.hip", "zlib_deflate.hip", "pagegen.hip"]
+SOURCES = ["engine.hip", "lz4_decode.hip", "lz4_decode_lane.hip", "lz4_encode.hip", "zlib_inflate.hip", "zstd_decode.hip", "zstd_encode.hip", "zlib_deflate.hip", "pagegen.hip",
+           "errno_guard.hip"]   # errno_guard last: its constructor runs after the code-object registrations
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 FLAGS = ["--offload-arch=" + ARCH, "-O3", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-variable",
@@ -69,22 +70,26 @@ def build(force: bool = False, verbose: bool = False, profile: bool = False, abl
     return lib_path
 
 
-def build_tools(verbose: bool = False) -> str:
-    """tools/bin/cycle: the tyche-shaped C harness (tools/cycle.c) linked against the engine."""
+def build_tools(verbose: bool = False) -> list:
+    """tools/bin/{cycle,stress}: C harnesses over the C ABI (tools/cycle.c: the tyche-shaped
+    sweep/restore cycle; tools/stress.c: hundreds of concurrent Buffer API callers)."""
     root = os.path.abspath(os.path.join(HERE, ".."))
-    src = os.path.join(root, "tools", "cycle.c")
     out_dir = os.path.join(root, "tools", "bin")
-    out = os.path.join(out_dir, "cycle")
     os.makedirs(out_dir, exist_ok=True)
-    deps = [src, os.path.join(root, "include", "tyche_codec.h"), os.path.join(CSRC, "pagegen.h"), LIB]
-    if _newer(out, deps):
-        return out
-    cmd = ["gcc", "-O2", "-std=gnu99", "-Wall", "-o", out, src, "-I" + os.path.join(root, "include"),
-           "-L" + HERE, "-ltyche_codec", "-Wl,-rpath,$ORIGIN/../../tyche_amd", "-lpthread"]
-    if verbose:
-        print(" ".join(cmd))
-    subprocess.check_call(cmd)
-    return out
+    outs = []
+    for name in ("cycle", "stress"):
+        src = os.path.join(root, "tools", name + ".c")
+        out = os.path.join(out_dir, name)
+        outs.append(out)
+        deps = [src, os.path.join(root, "include", "tyche_codec.h"), os.path.join(CSRC, "pagegen.h"), LIB]
+        if _newer(out, deps):
+            continue
+        cmd = ["gcc", "-O2", "-g", "-rdynamic", "-std=gnu99", "-Wall", "-o", out, src, "-I" + os.path.join(root, "include"),
+               "-L" + HERE, "-ltyche_codec", "-Wl,-rpath,$ORIGIN/../../tyche_amd", "-lpthread"]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.check_call(cmd)
+    return outs
 
 
 if __name__ == "__main__":

@@ -31,6 +31,7 @@ E_BUFFER_COMPRESSION_PROBLEM = 126
 E_NO_MEMORY = 150
 E_BAD_ARGS = 190
 E_DEVICE = 199
+ALL_DEVICES = -1        # tyche_set_device: spread host work over the device set (TYCHE_ALL_DEVICES)
 
 RESULT_TOO_LARGE = -(2 ** 31)
 
@@ -115,6 +116,9 @@ SIGNATURES = {
     "tyche_restore_queue_stats": (None, [ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
     "tyche_device_count": (ctypes.c_int, []),
     "tyche_set_device": (ctypes.c_int, [ctypes.c_int]),
+    "tyche_active_devices": (ctypes.c_int, []),
+    "tyche_plan_split": (ctypes.c_size_t, [ctypes.c_size_t, _u32p, ctypes.c_int, ctypes.c_uint64,
+                                           ctypes.POINTER(ctypes.c_size_t)]),
     "tyche_last_error": (ctypes.c_char_p, []),
     "tyche_device_ready": (ctypes.c_int, []),
     "tyche_pagegen": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,

@@ -70,7 +70,7 @@ inline size_t waves_per_cu(const void *kernel, size_t lds) {
 }
 
 hipError_t launch_lz4_decode(const tyche_batch_t &b, uint32_t in_cap, uint32_t out_cap, hipStream_t s);
-bool lz4_lane_decode_wanted(size_t count);
+bool lz4_lane_decode_wanted(size_t count, uint32_t in_cap, uint32_t out_cap);
 hipError_t launch_lz4_decode_lane(const tyche_batch_t &b, uint32_t in_cap, uint32_t out_cap, hipStream_t s);
 hipError_t launch_lz4_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream_t s);
 hipError_t launch_zstd_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream_t s);
@@ -82,9 +82,29 @@ hipError_t launch_zstd_decode(const tyche_batch_t &b, uint32_t in_cap, uint32_t 
 // SIMDs, the waves sharing a SIMD run slower than the lone ones, and static
 // striding (page += gridDim.x) leaves the lone waves idle at the end.  Instead
 // each wave starts at blockIdx.x and then claims pages from a per-launch
-// counter.  work_counter() hands out a zeroed counter for a launch on stream s
-// (a ring of device counters, reset with an async memset on that stream).
-unsigned *work_counter(hipStream_t s);
+// counter.  A WorkCounter leases one zeroed device counter for one launch on
+// stream s: constructed just before the launch (an async memset on s), it is
+// returned to the device's pool when it goes out of scope, right after the
+// launch call, as an event recorded on s -- the counter is handed out again
+// only once that event has completed, i.e. once the kernel that claims pages
+// from it has finished, whatever stream or thread asks next.
+class WorkCounter {
+  public:
+    explicit WorkCounter(hipStream_t s);
+    ~WorkCounter();
+    WorkCounter(const WorkCounter &) = delete;
+    WorkCounter &operator=(const WorkCounter &) = delete;
+    unsigned *get() const { return p_; }   // nullptr if no counter could be allocated
+
+  private:
+    hipStream_t s_;
+    int dev_ = -1, idx_ = -1;
+    unsigned *p_ = nullptr;
+};
+// Per-device, thread-safe launch preparation: raises `kernel`'s dynamic-LDS
+// limit to the CU's 160 KiB once per (device, kernel) and returns the current
+// device's CU count.
+size_t prepare_launch(const void *kernel);
 __device__ __forceinline__ size_t claim_page(unsigned *counter, uint32_t lane) {
     unsigned v = 0;
     if (lane == 0) v = atomicAdd(counter, 1u);

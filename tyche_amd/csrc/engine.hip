@@ -23,6 +23,7 @@
 #include <condition_variable>
 #include <functional>
 #include <mutex>
+#include <set>
 #include <string>
 #include <thread>
 #include <vector>
@@ -31,24 +32,99 @@
 
 using namespace tyche;
 
-unsigned *tyche::work_counter(hipStream_t s) {
-    constexpr int kRing = 256;   // launches in flight at once stay far below this
+namespace {
+constexpr int kMaxDevices = 64;
+
+// ------------------------------------------------------------- work counters
+// One pool of device counters per device.  An entry is free, leased (between
+// WorkCounter's constructor and destructor), or released: an event recorded on
+// the launch stream after the kernel that claims pages from it.  A released
+// entry is handed out again only when its event has completed, so a counter is
+// never reset while a kernel on any stream still claims from it.
+struct CounterPool {
+    struct Entry {
+        unsigned *p;
+        hipEvent_t ev;
+        int state;   // 0 free, 1 leased, 2 released (event pending)
+    };
+    std::mutex mu;
+    std::vector<Entry> e;
+    size_t cursor = 0;
+};
+CounterPool g_counters[kMaxDevices];
+constexpr size_t kCounterBlock = 64;
+}  // namespace
+
+tyche::WorkCounter::WorkCounter(hipStream_t s) : s_(s) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return;
+    CounterPool &P = g_counters[dev];
+    std::lock_guard<std::mutex> g(P.mu);
+    const size_t n = P.e.size();
+    size_t take = n;
+    for (size_t k = 0; k < n; k++) {   // from the oldest release on: those are done first
+        const size_t i = (P.cursor + k) % n;
+        CounterPool::Entry &x = P.e[i];
+        if (x.state == 1) continue;
+        if (x.state == 2 && hipEventQuery(x.ev) != hipSuccess) continue;   // its kernel may still run
+        take = i;
+        break;
+    }
+    if (take == n) {   // all in use: one more block
+        unsigned *blk = nullptr;
+        if (hipMalloc((void **)&blk, kCounterBlock * sizeof(unsigned)) != hipSuccess) return;
+        for (size_t j = 0; j < kCounterBlock; j++) {
+            hipEvent_t ev;
+            if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) break;
+            P.e.push_back({blk + j, ev, 0});
+        }
+        if (P.e.size() == n) return;
+    }
+    CounterPool::Entry &x = P.e[take];
+    if (hipMemsetAsync(x.p, 0, sizeof(unsigned), s) != hipSuccess) return;
+    x.state = 1;
+    P.cursor = take + 1;
+    dev_ = dev;
+    idx_ = (int)take;
+    p_ = x.p;
+}
+
+tyche::WorkCounter::~WorkCounter() {
+    if (idx_ < 0) return;
+    CounterPool &P = g_counters[dev_];
+    std::lock_guard<std::mutex> g(P.mu);
+    CounterPool::Entry &x = P.e[(size_t)idx_];
+    if (hipEventRecord(x.ev, s_) == hipSuccess) {
+        x.state = 2;
+    } else {
+        (void)hipStreamSynchronize(s_);   // no event: wait for the launch instead
+        x.state = 0;
+    }
+}
+
+size_t tyche::prepare_launch(const void *kernel) {
     static std::mutex mu;
-    static unsigned *ring[64] = {nullptr};
-    static unsigned next_slot[64] = {0};
+    static std::set<std::pair<int, const void *>> raised;
+    static int cus[kMaxDevices] = {0};
     int dev = 0;
     (void)hipGetDevice(&dev);
-    if (dev < 0 || dev >= 64) return nullptr;
+    if (dev < 0 || dev >= kMaxDevices) return 256;
     std::lock_guard<std::mutex> g(mu);
-    if (!ring[dev] && hipMalloc((void **)&ring[dev], kRing * sizeof(unsigned)) != hipSuccess) return nullptr;
-    unsigned *c = ring[dev] + (next_slot[dev]++ % kRing);
-    if (hipMemsetAsync(c, 0, sizeof(unsigned), s) != hipSuccess) return nullptr;
-    return c;
+    if (cus[dev] == 0) {
+        int n = 0;
+        (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+        cus[dev] = n > 0 ? n : 256;
+    }
+    if (raised.insert({dev, kernel}).second)
+        (void)hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    return (size_t)cus[dev];
 }
 
 namespace {
 
-thread_local int t_device = 0;
+// -1: the host API spreads work over every usable device (the default);
+// >= 0: tyche_set_device pinned the calling thread to that device
+thread_local int t_device = -1;
 thread_local std::string t_error;
 
 int fail(const char *what, hipError_t e) {
@@ -72,14 +148,65 @@ bool device_is_gfx950(int dev) {
     return strncmp(prop.gcnArchName, "gfx950", 6) == 0;
 }
 
-int ensure_device() {
+// The devices the host API uses when the thread is not pinned: the visible
+// gfx950 devices, the first TYCHE_DEVICES of them when that is set.
+struct DeviceSet {
+    std::vector<int> ids;
+    std::string why;   // empty when ids is non-empty
+};
+const DeviceSet &device_set() {
+    static DeviceSet ds = [] {
+        DeviceSet d;
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
+            d.why = "no HIP device available (the codec runs only on the GPU)";
+            return d;
+        }
+        // TYCHE_DEVICE_IDS: an explicit list ("0,1,2"; repeats allowed, which lets
+        // one GPU rehearse the multi-device fan-out in tests)
+        if (const char *ids = getenv("TYCHE_DEVICE_IDS")) {
+            for (const char *p = ids; *p;) {
+                char *end = nullptr;
+                const long v = strtol(p, &end, 10);
+                if (end == p) break;
+                if (v >= 0 && v < n && v < kMaxDevices && device_is_gfx950((int)v)) d.ids.push_back((int)v);
+                p = *end == ',' ? end + 1 : end;
+            }
+        } else {
+            const char *env = getenv("TYCHE_DEVICES");
+            const int want = env ? atoi(env) : n;
+            for (int i = 0; i < n && (int)d.ids.size() < want && i < kMaxDevices; i++)
+                if (device_is_gfx950(i)) d.ids.push_back(i);
+        }
+        if (d.ids.empty()) d.why = "no gfx950 device; libtyche_codec.so carries gfx950 code only";
+        return d;
+    }();
+    return ds;
+}
+
+// makes `dev` current on this thread after checking it (cached per device)
+int ensure_device(int dev) {
+    static std::atomic<int> ok[kMaxDevices];   // 0 unknown, 1 gfx950, 2 unusable
     int n = 0;
     hipError_t e = hipGetDeviceCount(&n);
     if (e != hipSuccess || n == 0) return fail_msg("no HIP device available (the codec runs only on the GPU)");
-    if (t_device >= n) return fail_msg("selected device out of range");
-    e = hipSetDevice(t_device);
+    if (dev < 0 || dev >= n || dev >= kMaxDevices) return fail_msg("selected device out of range");
+    e = hipSetDevice(dev);
     if (e != hipSuccess) return fail("hipSetDevice", e);
-    if (!device_is_gfx950(t_device)) return fail_msg("device is not gfx950; libtyche_codec.so carries gfx950 code only");
+    if (ok[dev].load() == 0) ok[dev].store(device_is_gfx950(dev) ? 1 : 2);
+    if (ok[dev].load() != 1) return fail_msg("device is not gfx950; libtyche_codec.so carries gfx950 code only");
+    return TYCHE_E_OK;
+}
+
+// the device for a thread's device-side work: its pinned one, else the first of the set
+int current_device(int *dev) {
+    if (t_device >= 0) {
+        *dev = t_device;
+        return TYCHE_E_OK;
+    }
+    const DeviceSet &ds = device_set();
+    if (ds.ids.empty()) return fail_msg(ds.why);
+    *dev = ds.ids[0];
     return TYCHE_E_OK;
 }
 
@@ -126,57 +253,118 @@ inline uint32_t decode_in_cap(const tyche_batch_t &b, uint32_t fallback) {
 //
 // so chunk c's gather overlaps chunk c-1's copies and kernel and chunk c-2's
 // scatter; the two copy directions and the kernels of different slots run
-// concurrently.  One context per calling thread (tyche calls the codec from its
-// compressor pool and from worker threads concurrently, src/list.c:1051, 572).
+// concurrently.  tyche calls the codec from its compressor pool and its
+// worker threads at once (src/list.c:1051, 572; opts.cpu_count threads,
+// src/options.c:64): the staging contexts are therefore a small per-device pool
+// (TYCHE_HOST_CONTEXTS, default kContextsPerDevice) that a call borrows for its
+// duration, not one per calling thread, so streams and pinned arenas stay
+// bounded however many threads call in.
 struct Arena {
     void *p = nullptr;
     size_t cap = 0;
-    int grow(size_t need, bool host) {
+    bool host = false;
+    int grow(size_t need) {
         if (need <= cap) return TYCHE_E_OK;
         size_t n = std::max(need, cap * 2);
         n = (n + 4095) & ~size_t(4095);
-        if (p) {
-            if (host) (void)hipHostFree(p); else (void)hipFree(p);
-            p = nullptr;
-            cap = 0;
-        }
+        release();
         hipError_t e = host ? hipHostMalloc(&p, n, hipHostMallocDefault) : hipMalloc(&p, n);
-        if (e != hipSuccess) return fail(host ? "hipHostMalloc" : "hipMalloc", e);
+        if (e != hipSuccess) {
+            p = nullptr;
+            return fail(host ? "hipHostMalloc" : "hipMalloc", e);
+        }
         cap = n;
         return TYCHE_E_OK;
+    }
+    void release() {
+        if (p) {
+            if (host) (void)hipHostFree(p); else (void)hipFree(p);
+        }
+        p = nullptr;
+        cap = 0;
     }
 };
 
 constexpr int kSlots = 3;
 constexpr size_t kChunkBytes = size_t(64) << 20;
+constexpr int kContextsPerDevice = 8;
 
 struct Slot {
     hipStream_t stream = nullptr;
     Arena h_in, h_out, h_meta, d_in, d_out, d_meta;
     size_t first = 0, count = 0;   // pages of the chunk in flight
     bool busy = false;
+    Slot() { h_in.host = h_out.host = h_meta.host = true; }
 };
 
 struct HostCtx {
-    int device = -1;
     Slot slot[kSlots];
-    int init(int dev) {
-        if (device == dev && slot[0].stream) return TYCHE_E_OK;
-        device = dev;
-        for (Slot &s : slot) {
-            hipError_t e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
-            if (e != hipSuccess) return fail("hipStreamCreate", e);
-        }
-        return TYCHE_E_OK;
+    // waits for whatever the slots still hold and forgets it (error paths)
+    void abandon() {
+        for (Slot &s : slot)
+            if (s.busy) {
+                (void)hipStreamSynchronize(s.stream);
+                s.busy = false;
+            }
     }
 };
-thread_local HostCtx t_ctx[16];
+
+struct CtxPool {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<HostCtx *> all, idle;
+};
+CtxPool g_ctx[kMaxDevices];
+
+int context_cap() {
+    static const int cap = [] {
+        const char *env = getenv("TYCHE_HOST_CONTEXTS");
+        const int v = env ? atoi(env) : kContextsPerDevice;
+        return v > 0 ? v : kContextsPerDevice;
+    }();
+    return cap;
+}
+
+// borrows a staging context of device dev (current on this thread); waits while all are busy
+int acquire_ctx(int dev, HostCtx **out) {
+    CtxPool &P = g_ctx[dev];
+    std::unique_lock<std::mutex> g(P.mu);
+    P.cv.wait(g, [&] { return !P.idle.empty() || (int)P.all.size() < context_cap(); });
+    if (!P.idle.empty()) {
+        *out = P.idle.back();
+        P.idle.pop_back();
+        return TYCHE_E_OK;
+    }
+    HostCtx *c = new HostCtx;
+    for (Slot &s : c->slot) {
+        hipError_t e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
+        if (e != hipSuccess) {
+            for (Slot &t : c->slot)
+                if (t.stream) (void)hipStreamDestroy(t.stream);
+            delete c;
+            return fail("hipStreamCreate", e);
+        }
+    }
+    P.all.push_back(c);
+    *out = c;
+    return TYCHE_E_OK;
+}
+void release_ctx(int dev, HostCtx *c) {
+    CtxPool &P = g_ctx[dev];
+    {
+        std::lock_guard<std::mutex> g(P.mu);
+        P.idle.push_back(c);
+    }
+    P.cv.notify_one();
+}
 
 inline size_t up16(size_t x) { return (x + 15) & ~size_t(15); }
 
-// A small persistent worker pool for the host-side page copies (memcpy of
-// scattered malloc'd pages into and out of pinned staging).  One job at a
-// time; concurrent callers queue on the mutex.
+// A persistent worker pool for the host-side page copies (memcpy of scattered
+// malloc'd pages into and out of pinned staging).  Several callers (one per
+// device of a fanned-out batch, concurrent tyche threads) may run jobs at once:
+// each caller works on its own job and idle workers join whichever job still
+// has ranges left.
 class CopyPool {
   public:
     static CopyPool &get() {
@@ -191,27 +379,31 @@ class CopyPool {
             for (size_t i = 0; i < n; i++) f(i);
             return;
         }
-        std::lock_guard<std::mutex> job_lock(job_mu_);
         std::function<void(size_t, size_t)> body = [&f](size_t a, size_t b) {
             for (size_t i = a; i < b; i++) f(i);
         };
+        Job j;
+        j.body = &body;
+        j.n = n;
         {
             std::lock_guard<std::mutex> g(mu_);
-            body_ = &body;
-            n_ = n;
-            next_.store(0);
-            pending_ = workers_.size();
-            gen_++;
+            jobs_.push_back(&j);
         }
         cv_.notify_all();
-        work();
+        work(j);
         std::unique_lock<std::mutex> g(mu_);
-        done_cv_.wait(g, [this] { return pending_ == 0; });
-        body_ = nullptr;
+        jobs_.erase(std::find(jobs_.begin(), jobs_.end(), &j));   // no worker joins it from now on
+        done_cv_.wait(g, [&] { return j.active == 0; });
     }
 
   private:
     static constexpr size_t kGrain = 32;
+    struct Job {
+        const std::function<void(size_t, size_t)> *body = nullptr;
+        size_t n = 0;
+        std::atomic<size_t> next{0};
+        int active = 0;   // workers inside work(); guarded by mu_
+    };
     CopyPool() {
         unsigned t = std::thread::hardware_concurrency();
         const char *env = getenv("TYCHE_HOST_THREADS");
@@ -219,49 +411,69 @@ class CopyPool {
         for (unsigned i = 1; i < want; i++) workers_.emplace_back([this] { loop(); });
         for (auto &w : workers_) w.detach();
     }
-    void work() {
+    static void work(Job &j) {
         for (;;) {
-            const size_t a = next_.fetch_add(kGrain);
-            if (a >= n_) break;
-            (*body_)(a, std::min(n_, a + kGrain));
+            const size_t a = j.next.fetch_add(kGrain);
+            if (a >= j.n) break;
+            (*j.body)(a, std::min(j.n, a + kGrain));
         }
     }
+    Job *open_job() {   // under mu_
+        for (Job *j : jobs_)
+            if (j->next.load() < j->n) return j;
+        return nullptr;
+    }
     void loop() {
-        uint64_t seen = 0;
         for (;;) {
+            Job *j = nullptr;
             {
+                // j->next advances outside the lock (callers and workers claim ranges with
+                // fetch_add): pick the job once, in the predicate, and pin it there
                 std::unique_lock<std::mutex> g(mu_);
-                cv_.wait(g, [&] { return gen_ != seen; });
-                seen = gen_;
+                cv_.wait(g, [&] { return (j = open_job()) != nullptr; });
+                j->active++;
             }
-            work();
-            std::lock_guard<std::mutex> g(mu_);
-            if (--pending_ == 0) done_cv_.notify_all();
+            work(*j);
+            {
+                std::lock_guard<std::mutex> g(mu_);
+                j->active--;
+            }
+            done_cv_.notify_all();
         }
     }
     std::vector<std::thread> workers_;
-    std::mutex job_mu_, mu_;
+    std::mutex mu_;
     std::condition_variable cv_, done_cv_;
-    const std::function<void(size_t, size_t)> *body_ = nullptr;
-    size_t n_ = 0;
-    std::atomic<size_t> next_{0};
-    size_t pending_ = 0;
-    uint64_t gen_ = 0;
+    std::vector<Job *> jobs_;
 };
 
-// Moves n host pages through `launch` chunk by chunk (see above).  results[i]
-// gets the kernel's per-page result; for results in (0, dst_cap[i]] that many
-// output bytes land in dst[i].
+std::atomic<int> g_inflight[kMaxDevices];   // host batches running per device
+
+// Moves n host pages through `launch` on device dev, chunk by chunk (see
+// above).  results[i] gets the kernel's per-page result; for results in
+// (0, dst_cap[i]] that many output bytes land in dst[i].  On any failure the
+// context's slots are drained before it goes back to the pool, so a later call
+// never scatters a failed call's chunk.
 template <typename Launch>
-int run_host_batch(size_t n, const void *const *src, const uint32_t *src_len, void *const *dst,
+int run_host_batch(int dev, size_t n, const void *const *src, const uint32_t *src_len, void *const *dst,
                    const uint32_t *dst_cap, int32_t *results, Launch launch) {
-    int rc = ensure_device();
+    int rc = ensure_device(dev);
     if (rc) return rc;
-    if (t_device >= 16) return fail_msg("device index too large");
-    HostCtx &c = t_ctx[t_device];
-    if ((rc = c.init(t_device))) return rc;
+    struct Inflight {
+        int d;
+        explicit Inflight(int dd) : d(dd) { g_inflight[d]++; }
+        ~Inflight() { g_inflight[d]--; }
+    } inflight(dev);
+    HostCtx *cp = nullptr;
+    if ((rc = acquire_ctx(dev, &cp))) return rc;
+    HostCtx &c = *cp;
     CopyPool &pool = CopyPool::get();
     hipError_t e;
+    auto bail = [&](int r) {
+        c.abandon();
+        release_ctx(dev, cp);
+        return r;
+    };
 
     // completes the chunk held by slot s: wait for its stream, scatter its outputs
     auto finish = [&](Slot &S) -> int {
@@ -296,13 +508,13 @@ int run_host_batch(size_t n, const void *const *src, const uint32_t *src_len, vo
         }
         const size_t k = last - first;
         Slot &S = c.slot[si];
-        if ((rc = finish(S))) return rc;   // the slot's previous chunk
+        if ((rc = finish(S))) return bail(rc);   // the slot's previous chunk
         // meta layout: soff[k] u64, doff[k] u64, slen[k] u32, dcap[k] u32, res[k] i32
         const size_t meta_bytes = k * 28 + 64;
-        if ((rc = S.h_in.grow(in_bytes + 16, true)) || (rc = S.h_out.grow(out_bytes + 16, true)) ||
-            (rc = S.h_meta.grow(meta_bytes, true)) || (rc = S.d_in.grow(in_bytes + 16, false)) ||
-            (rc = S.d_out.grow(out_bytes + 16, false)) || (rc = S.d_meta.grow(meta_bytes, false)))
-            return rc;
+        if ((rc = S.h_in.grow(in_bytes + 16)) || (rc = S.h_out.grow(out_bytes + 16)) ||
+            (rc = S.h_meta.grow(meta_bytes)) || (rc = S.d_in.grow(in_bytes + 16)) ||
+            (rc = S.d_out.grow(out_bytes + 16)) || (rc = S.d_meta.grow(meta_bytes)))
+            return bail(rc);
         uint64_t *m_soff = (uint64_t *)S.h_meta.p;
         uint64_t *m_doff = m_soff + k;
         uint32_t *m_slen = (uint32_t *)(m_doff + k);
@@ -324,10 +536,13 @@ int run_host_batch(size_t n, const void *const *src, const uint32_t *src_len, vo
         // ---- H2D -> kernel -> D2H on the slot's stream
         uint8_t *dmeta = (uint8_t *)S.d_meta.p;
         const size_t head_bytes = (uint8_t *)m_res - (uint8_t *)m_soff;
+        S.first = first;
+        S.count = k;
+        S.busy = true;   // from the first enqueued copy on, the slot must be drained on failure
         if ((e = hipMemcpyAsync(dmeta, S.h_meta.p, head_bytes, hipMemcpyHostToDevice, S.stream)) != hipSuccess)
-            return fail("hipMemcpyAsync(meta)", e);
+            return bail(fail("hipMemcpyAsync(meta)", e));
         if (so && (e = hipMemcpyAsync(S.d_in.p, hin, so, hipMemcpyHostToDevice, S.stream)) != hipSuccess)
-            return fail("hipMemcpyAsync(in)", e);
+            return bail(fail("hipMemcpyAsync(in)", e));
         tyche_batch_t b{};
         b.count = k;
         b.src = S.d_in.p;
@@ -339,20 +554,73 @@ int run_host_batch(size_t n, const void *const *src, const uint32_t *src_len, vo
         b.dst_capacities = (const uint32_t *)(dmeta + ((uint8_t *)m_dcap - (uint8_t *)m_soff));
         b.dst_capacity = max_out;
         b.results = (int32_t *)(dmeta + head_bytes);
-        if ((e = launch(b, S.stream)) != hipSuccess) return fail("kernel launch", e);
+        if ((e = launch(b, S.stream)) != hipSuccess) return bail(fail("kernel launch", e));
         if ((e = hipMemcpyAsync(m_res, b.results, k * 4, hipMemcpyDeviceToHost, S.stream)) != hipSuccess)
-            return fail("hipMemcpyAsync(results)", e);
+            return bail(fail("hipMemcpyAsync(results)", e));
         if (dof && (e = hipMemcpyAsync(S.h_out.p, S.d_out.p, dof, hipMemcpyDeviceToHost, S.stream)) != hipSuccess)
-            return fail("hipMemcpyAsync(out)", e);
-        S.first = first;
-        S.count = k;
-        S.busy = true;
+            return bail(fail("hipMemcpyAsync(out)", e));
         first = last;
         si = (si + 1) % kSlots;
     }
     // drain in issue order
     for (int j = 0; j < kSlots; j++)
-        if ((rc = finish(c.slot[(si + j) % kSlots]))) return rc;
+        if ((rc = finish(c.slot[(si + j) % kSlots]))) return bail(rc);
+    release_ctx(dev, cp);
+    return TYCHE_E_OK;
+}
+
+// minimum input bytes per device before a host batch is split across devices
+uint64_t fanout_min_bytes() {
+    static const uint64_t v = [] {
+        const char *env = getenv("TYCHE_FANOUT_MIN_BYTES");
+        return env ? (uint64_t)strtoull(env, nullptr, 10) : (uint64_t)kChunkBytes;
+    }();
+    return v;
+}
+
+// the device with the fewest host batches in flight (ties rotate)
+int pick_device(const std::vector<int> &ids) {
+    static std::atomic<unsigned> rot{0};
+    const unsigned r = rot++;
+    int best = ids[r % ids.size()];
+    for (size_t k = 0; k < ids.size(); k++) {
+        const int d = ids[(r + k) % ids.size()];
+        if (g_inflight[d].load() < g_inflight[best].load()) best = d;
+    }
+    return best;
+}
+
+// Host batch over the calling thread's devices: its pinned device, or the
+// device set.  Batches of at least two parts' worth of input
+// (tyche_plan_split) are cut into contiguous page ranges of about equal input
+// bytes, one per device, run concurrently; smaller ones go whole to the least
+// busy device, so concurrent small calls (tyche's per-page compressor pool and
+// restores) spread over all devices.
+template <typename Launch>
+int run_host(size_t n, const void *const *src, const uint32_t *src_len, void *const *dst, const uint32_t *dst_cap,
+             int32_t *results, Launch launch) {
+    if (t_device >= 0) return run_host_batch(t_device, n, src, src_len, dst, dst_cap, results, launch);
+    const DeviceSet &ds = device_set();
+    if (ds.ids.empty()) return fail_msg(ds.why);
+    std::vector<size_t> cuts(ds.ids.size() + 1);
+    const size_t parts = tyche_plan_split(n, src_len, (int)ds.ids.size(), fanout_min_bytes(), cuts.data());
+    if (parts <= 1) return run_host_batch(pick_device(ds.ids), n, src, src_len, dst, dst_cap, results, launch);
+    std::vector<int> rcs(parts, TYCHE_E_OK);
+    std::vector<std::string> errs(parts);
+    std::vector<std::thread> th;
+    auto part = [&](size_t p) {
+        const size_t a = cuts[p], m = cuts[p + 1] - cuts[p];
+        rcs[p] = run_host_batch(ds.ids[p], m, src + a, src_len + a, dst + a, dst_cap + a, results + a, launch);
+        if (rcs[p]) errs[p] = t_error;
+    };
+    for (size_t p = 1; p < parts; p++) th.emplace_back(part, p);
+    part(0);
+    for (auto &t : th) t.join();
+    for (size_t p = 0; p < parts; p++)
+        if (rcs[p]) {
+            t_error = errs[p];
+            return rcs[p];
+        }
     return TYCHE_E_OK;
 }
 
@@ -368,14 +636,46 @@ int tyche_device_count(void) {
 }
 
 int tyche_set_device(int device) {
-    if (device < 0) return TYCHE_E_BAD_ARGS;
+    if (device < TYCHE_ALL_DEVICES) return TYCHE_E_BAD_ARGS;
     t_device = device;
     return TYCHE_E_OK;
 }
 
+int tyche_active_devices(void) {
+    if (t_device >= 0) return 1;
+    return (int)device_set().ids.size();
+}
+
+size_t tyche_plan_split(size_t n, const uint32_t *src_lengths, int ndev, uint64_t min_part_bytes, size_t *cuts) {
+    cuts[0] = 0;
+    uint64_t total = 0;
+    for (size_t i = 0; i < n; i++) total += src_lengths[i];
+    uint64_t parts = ndev > 0 ? (uint64_t)ndev : 1u;
+    if (min_part_bytes > 0) parts = std::min<uint64_t>(parts, total / min_part_bytes);
+    parts = std::min<uint64_t>(std::max<uint64_t>(parts, 1u), std::max<size_t>(n, 1u));
+    size_t i = 0;
+    uint64_t acc = 0;
+    for (uint64_t p = 1; p < parts; p++) {   // part p-1 ends where the input bytes pass p/parts of the total
+        const uint64_t goal = total / parts * p + (total % parts) * p / parts;
+        while (i < n && acc < goal) acc += src_lengths[i++];
+        cuts[p] = i;
+    }
+    cuts[parts] = n;
+    size_t k = 1;   // drop empty parts
+    for (uint64_t p = 1; p <= parts; p++)
+        if (cuts[p] > cuts[k - 1]) cuts[k++] = cuts[p];
+    if (k == 1) cuts[k++] = n;   // n == 0: one empty part
+    return k - 1;
+}
+
 const char *tyche_last_error(void) { return t_error.c_str(); }
 
-int tyche_device_ready(void) { return ensure_device() == TYCHE_E_OK ? 1 : 0; }
+int tyche_device_ready(void) {
+    int dev = 0;
+    int rc = current_device(&dev);
+    if (rc == TYCHE_E_OK) rc = ensure_device(dev);
+    return rc == TYCHE_E_OK ? 1 : 0;
+}
 
 uint32_t tyche_compress_bound(int compressor_id, uint32_t n) {
     if (compressor_id == TYCHE_LZ4_COMPRESSOR_ID) return lz4_bound(n);
@@ -430,7 +730,7 @@ int tyche_compress_host(int compressor_id, int compressor_level, size_t n, const
     if (n == 0) return TYCHE_E_OK;
     for (size_t i = 0; i < n; i++)
         if (src_lengths[i] > 65535u) { t_error = "pages above 64 KiB are not supported by the device encoders"; return TYCHE_E_BAD_ARGS; }
-    return run_host_batch(n, src, src_lengths, dst, dst_capacities, results,
+    return run_host(n, src, src_lengths, dst, dst_capacities, results,
                           [compressor_id](const tyche_batch_t &b, hipStream_t s) {
                               return launch_encode(compressor_id, b, std::max(b.max_src_length, 1u), s);
                           });
@@ -441,16 +741,16 @@ int tyche_decompress_host(int compressor_id, size_t n, const void *const *src, c
     if (!valid_decode_codec(compressor_id)) { t_error = codec_msg(compressor_id); return TYCHE_E_BAD_ARGS; }
     if (n == 0) return TYCHE_E_OK;
     if (compressor_id == TYCHE_ZLIB_COMPRESSOR_ID)
-        return run_host_batch(n, src, src_lengths, dst, dst_capacities, results,
+        return run_host(n, src, src_lengths, dst, dst_capacities, results,
                               [](const tyche_batch_t &b, hipStream_t s) {
                                   return launch_zlib_inflate(b, b.dst_capacity, s);
                               });
     if (compressor_id == TYCHE_ZSTD_COMPRESSOR_ID)
-        return run_host_batch(n, src, src_lengths, dst, dst_capacities, results,
+        return run_host(n, src, src_lengths, dst, dst_capacities, results,
                               [](const tyche_batch_t &b, hipStream_t s) {
                                   return launch_zstd_decode(b, b.max_src_length, b.dst_capacity, s);
                               });
-    return run_host_batch(n, src, src_lengths, dst, dst_capacities, results,
+    return run_host(n, src, src_lengths, dst, dst_capacities, results,
                           [](const tyche_batch_t &b, hipStream_t s) {
                               return launch_lz4_decode(b, b.max_src_length, b.dst_capacity, s);
                           });
@@ -569,7 +869,10 @@ int tyche_buffers_compress(Buffer **bufs, void **compressed, int *status, size_t
         dst[k] = malloc(dcap[k]);
         if (!dst[k]) {
             for (size_t j = 0; j < k; j++) free(dst[j]);
-            for (size_t j = 0; j < m; j++) status[idx[j]] = TYCHE_E_NO_MEMORY;
+            for (size_t j = 0; j < m; j++) {
+                status[idx[j]] = TYCHE_E_NO_MEMORY;
+                compressed[idx[j]] = NULL;
+            }
             return TYCHE_E_NO_MEMORY;
         }
     }
@@ -581,7 +884,12 @@ int tyche_buffers_compress(Buffer **bufs, void **compressed, int *status, size_t
         Buffer *b = bufs[idx[k]];
         size_t i = idx[k];
         if (rc != TYCHE_E_OK || res[k] < 1) {
-            free(dst[k]);   // the reference leaks here (buffer.c:185-186)
+            // The reference leaks its output block here (buffer.c:185-186) and leaves
+            // *compressed_data pointing at it; this frees it and sets NULL, so a caller
+            // that ignores the status (list.c:1050-1058 installs the pointer on any
+            // status but 124) never installs memory it does not own.
+            free(dst[k]);
+            compressed[i] = NULL;
             status[i] = rc != TYCHE_E_OK ? TYCHE_E_DEVICE : TYCHE_E_BUFFER_COMPRESSION_PROBLEM;
             continue;
         }
@@ -680,6 +988,10 @@ int buffer__decompress(Buffer *buf, int compressor_id) {
 // max_wait_us for company once the first request arrives), runs one
 // tyche_buffers_decompress per codec over the batch, and wakes each caller with
 // its buffer__decompress status.  Per-buffer semantics are unchanged.
+// Several dispatchers run (TYCHE_RESTORE_DISPATCHERS, default two per device):
+// one collects while the others' batches are on the GPUs, so a restore waits
+// for its own batch, not for the one before it; the host path sends each batch
+// to the least busy device.
 namespace {
 struct RestoreReq {
     Buffer *buf;
@@ -691,25 +1003,28 @@ struct RestoreQueue {
     std::mutex mu;
     std::condition_variable cv, done_cv;
     std::vector<RestoreReq *> q;
-    bool running = false, stop = false;
-    int max_batch = 1024, max_wait_us = 50, device = 0;
+    bool running = false, stop = false, collecting = false;
+    int max_batch = 1024, max_wait_us = 50, device = -1;
     uint64_t batches = 0, buffers = 0;
-    std::thread th;
+    std::vector<std::thread> th;
     void loop() {
         (void)tyche_set_device(device);
         std::vector<RestoreReq *> take;
         for (;;) {
             {
                 std::unique_lock<std::mutex> g(mu);
-                cv.wait(g, [&] { return stop || !q.empty(); });
-                if (stop && q.empty()) return;
+                cv.wait(g, [&] { return (stop && q.empty()) || (!q.empty() && !collecting); });
+                if (q.empty()) return;   // stopping
+                collecting = true;
                 if ((int)q.size() < max_batch && max_wait_us > 0)
                     cv.wait_for(g, std::chrono::microseconds(max_wait_us),
                                 [&] { return stop || (int)q.size() >= max_batch; });
                 const size_t k = std::min(q.size(), (size_t)max_batch);
                 take.assign(q.begin(), q.begin() + k);
                 q.erase(q.begin(), q.begin() + k);
+                collecting = false;
             }
+            cv.notify_all();   // the next dispatcher may collect
             // one batch per codec id present
             for (int codec = 0; codec <= 3; codec++) {
                 std::vector<Buffer *> bufs;
@@ -743,8 +1058,12 @@ int tyche_restore_queue_start(int max_batch, int max_wait_us) {
     g_rq.max_wait_us = max_wait_us >= 0 ? max_wait_us : 50;
     g_rq.device = t_device;
     g_rq.stop = false;
+    g_rq.collecting = false;
     g_rq.running = true;
-    g_rq.th = std::thread([] { g_rq.loop(); });
+    const char *env = getenv("TYCHE_RESTORE_DISPATCHERS");
+    int k = env ? atoi(env) : 2 * std::max(1, tyche_active_devices());
+    k = std::max(1, std::min(k, 64));
+    for (int i = 0; i < k; i++) g_rq.th.emplace_back([] { g_rq.loop(); });
     return TYCHE_E_OK;
 }
 
@@ -755,8 +1074,9 @@ void tyche_restore_queue_stop(void) {
         g_rq.stop = true;
     }
     g_rq.cv.notify_all();
-    g_rq.th.join();
+    for (auto &t : g_rq.th) t.join();
     std::lock_guard<std::mutex> g(g_rq.mu);
+    g_rq.th.clear();
     g_rq.running = false;
 }
 
@@ -770,7 +1090,7 @@ int tyche_buffer_restore(Buffer *buf, int compressor_id) {
         }
         g_rq.q.push_back(&r);
     }
-    g_rq.cv.notify_one();
+    g_rq.cv.notify_all();   // the collecting dispatcher, whichever it is
     std::unique_lock<std::mutex> g(g_rq.mu);
     g_rq.done_cv.wait(g, [&] { return r.done; });
     return r.status;
@@ -785,7 +1105,10 @@ void tyche_restore_queue_stats(uint64_t *batches, uint64_t *buffers) {
 // ---------------------------------------------------------- synthetic input
 int tyche_pagegen(void *dst, uint64_t stride, uint32_t page_len, uint64_t seed, uint64_t first, size_t count,
                   uint32_t dist, void *stream) {
-    int rc = ensure_device();
+    // device-resident like the batch API: runs on the caller's current device
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return fail_msg("no HIP device available (the codec runs only on the GPU)");
+    int rc = ensure_device(dev);
     if (rc) return rc;
     hipError_t e = launch_pagegen(dst, stride, page_len, seed, first, count, dist, (hipStream_t)stream);
     if (e != hipSuccess) return fail("pagegen launch", e);

@@ -567,7 +567,7 @@ __global__ __launch_bounds__(64) void lz4_decode_wave_kernel(tyche_batch_t b, ui
 hipError_t launch_lz4_decode(const tyche_batch_t &b, uint32_t in_cap, uint32_t out_cap, hipStream_t s) {
     if (b.count == 0) return hipSuccess;
     // large batches: one page per lane (lz4_decode_lane.hip)
-    if (lz4_lane_decode_wanted(b.count)) return launch_lz4_decode_lane(b, in_cap, out_cap, s);
+    if (lz4_lane_decode_wanted(b.count, in_cap, out_cap)) return launch_lz4_decode_lane(b, in_cap, out_cap, s);
     // page window (output; the parse's owner stamps, so at least in_cap bytes;
     // the token positions at its top, <= in_cap / 3 + 1 of them, which always
     // fit: W >= in_cap + 20), then the staged stream
@@ -580,39 +580,27 @@ hipError_t launch_lz4_decode(const tyche_batch_t &b, uint32_t in_cap, uint32_t o
         // large pages: sequential decoder, LDS = page window + stream only
         const size_t lds2 = ((out_cap + 15u) & ~15u) + ((in_cap + 16u + kPad + 15u) & ~15u);
         if (lds2 > 160 * 1024) return hipErrorInvalidValue;
-        static bool attr2 = false;
-        if (!attr2) {
-            (void)hipFuncSetAttribute((const void *)lz4_decode_serial_kernel,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            attr2 = true;
-        }
+        (void)prepare_launch((const void *)lz4_decode_serial_kernel);
         hipLaunchKernelGGL(lz4_decode_serial_kernel, dim3((unsigned)b.count), dim3(kWave), lds2, s, b, in_cap,
                            out_cap);
         return hipGetLastError();
     }
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    static int cus[64] = {0};
-    if (dev < 64 && cus[dev] == 0) {
-        (void)hipFuncSetAttribute((const void *)lz4_decode_wave_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  160 * 1024);
-        int n = 0;
-        (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-        cus[dev] = n > 0 ? n : 256;
-    }
-    const size_t ncu = dev < 64 ? cus[dev] : 256;
+    const size_t ncu = prepare_launch((const void *)lz4_decode_wave_kernel);
     // LDS is granted in 512-byte granules per workgroup
     auto lds_for = [&](uint32_t cap) -> size_t {
         return ((std::max(out_cap, cap + 4u) + 16u + 15u) & ~15u) + ((cap + 16u + kPad + 15u) & ~15u) + TYCHE_LDS_EXTRA;
     };
     auto granted = [](size_t l) -> size_t { return (l + 511u) & ~(size_t)511u; };
-    auto launch = [&](uint32_t cap, uint32_t lo, uint32_t hi, uint32_t chunk) {
+    auto launch = [&](uint32_t cap, uint32_t lo, uint32_t hi, uint32_t chunk) -> hipError_t {
         const size_t l = lds_for(cap);
         const uint32_t win = (std::max(out_cap, cap + 4u) + 16u + 15u) & ~15u;
         const size_t per_cu = waves_per_cu((const void *)lz4_decode_wave_kernel, l);
         const size_t grid = std::min<size_t>(b.count, ncu * per_cu);
+        WorkCounter ctr(s);
+        if (chunk && !ctr.get()) return hipErrorOutOfMemory;
         hipLaunchKernelGGL(lz4_decode_wave_kernel, dim3((unsigned)grid), dim3(kWave), l, s, b, cap, out_cap, win, lo, hi,
-                           chunk ? work_counter(s) : nullptr, chunk);
+                           chunk ? ctr.get() : nullptr, chunk);
+        return hipGetLastError();
     };
     // Size classes: the decoder is latency-bound and its residency is set by
     // the LDS per wave, i.e. by the longest stream of the batch.  When streams
@@ -637,13 +625,12 @@ hipError_t launch_lz4_decode(const tyche_batch_t &b, uint32_t in_cap, uint32_t o
         while (T > 16u && granted(lds_for(T)) > target) T -= 16u;
         if (granted(lds_for(T)) <= target && T >= in_cap / 2u && T < in_cap &&
             waves_per_cu((const void *)lz4_decode_wave_kernel, lds_for(T)) > waves) {
-            launch(T, 0u, T, 1u);
-            launch(in_cap, T + 1u, 0xFFFFFFFFu, kClassChunk);
-            return hipGetLastError();
+            hipError_t e = launch(T, 0u, T, 1u);
+            if (e != hipSuccess) return e;
+            return launch(in_cap, T + 1u, 0xFFFFFFFFu, kClassChunk);
         }
     }
-    launch(in_cap, 0u, 0xFFFFFFFFu, 1u);
-    return hipGetLastError();
+    return launch(in_cap, 0u, 0xFFFFFFFFu, 1u);
 }
 
 #ifdef TYCHE_PROFILE

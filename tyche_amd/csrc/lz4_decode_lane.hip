@@ -427,7 +427,7 @@ __global__ __launch_bounds__(64) void lz4_decode_ring_kernel(tyche_batch_t b, ui
 }
 
 // Pages are claimed per lane: lane g starts at page g, then takes the next
-// unclaimed one from the launch's counter (engine.h: work_counter).
+// unclaimed one from the launch's counter (engine.h: WorkCounter).
 __global__ __launch_bounds__(64) void lz4_decode_lane_kernel(tyche_batch_t b, uint32_t in_cap, uint32_t out_cap,
                                                               unsigned *ctr) {
     const size_t nthreads = (size_t)gridDim.x * blockDim.x;
@@ -456,9 +456,15 @@ __global__ __launch_bounds__(64) void lz4_decode_lane_kernel(tyche_batch_t b, ui
 // wave / lane kernel): 16K pages 130.6 / 170.2, 32K 114.4 / 91.6, 64K 108.0 /
 // 52.9, 128K 104.2 / 41.2 -- the lane kernel needs ~512 pages per CU in flight.
 constexpr long kLaneMin = 32768;
-bool lz4_lane_decode_wanted(size_t count) {
+// The lane kernels sum literal and match lengths in int32 without the
+// reference's pointer-overflow guards (lz4.c:1142, 1181: op+length < op): a run
+// of 0xFF length bytes adds 255 per byte, so streams are bounded to
+// kLaneMaxStream bytes (255 * 4 MiB < 2^31); larger ones take the wave/serial
+// decoders, whose LDS sizing rejects them.
+constexpr uint32_t kLaneMaxStream = 4u << 20;
+bool lz4_lane_decode_wanted(size_t count, uint32_t in_cap, uint32_t out_cap) {
     static const long min_pages = getenv("TYCHE_LZ4_LANE_MIN") ? atol(getenv("TYCHE_LZ4_LANE_MIN")) : kLaneMin;
-    return min_pages >= 0 && count >= (size_t)min_pages;
+    return min_pages >= 0 && count >= (size_t)min_pages && in_cap <= kLaneMaxStream && out_cap <= kLaneMaxStream;
 }
 
 // ring-less kernel: resident waves per CU (1M x 16 KiB pages, ms: 4 waves 80.8, 8: 92.1, 2: 97.7)
@@ -471,15 +477,6 @@ constexpr int kDefaultWin = 16;
 
 hipError_t launch_lz4_decode_lane(const tyche_batch_t &b, uint32_t in_cap, uint32_t out_cap, hipStream_t s) {
     if (b.count == 0) return hipSuccess;
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    static int cus[64] = {0};
-    if (dev < 64 && cus[dev] == 0) {
-        int n = 0;
-        (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-        cus[dev] = n > 0 ? n : 256;
-    }
-    const size_t ncu = dev < 64 ? cus[dev] : 256;
     static const long env_waves = getenv("TYCHE_LZ4_LANE_WAVES") ? atol(getenv("TYCHE_LZ4_LANE_WAVES")) : 0;
     static const int ring = getenv("TYCHE_LZ4_LANE_RING") ? atoi(getenv("TYCHE_LZ4_LANE_RING")) : kDefaultRing;
     if (ring) {
@@ -492,25 +489,24 @@ hipError_t launch_lz4_decode_lane(const tyche_batch_t &b, uint32_t in_cap, uint3
                                                    : (const void *)lz4_decode_ring_kernel<512, 32>);
         const int32_t rbytes = ring == 128 ? 128 : ring == 256 ? 256 : 512;
         const size_t lds = 64 * (size_t)(rbytes + 48);
-        static bool attr = false;
-        if (!attr) {
-            (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            attr = true;
-        }
+        const size_t ncu = prepare_launch(k);
         size_t waves = waves_per_cu(k, lds);
         if (env_waves > 0) waves = std::min<size_t>(waves, (size_t)env_waves);
         const size_t grid = std::min<size_t>((b.count + 63) / 64, ncu * waves);
-        void *args[] = {(void *)&b, &in_cap, &out_cap, nullptr};
-        unsigned *ctr = work_counter(s);
-        args[3] = &ctr;
+        WorkCounter ctr(s);
+        unsigned *cp = ctr.get();
+        if (!cp) return hipErrorOutOfMemory;
+        void *args[] = {(void *)&b, &in_cap, &out_cap, &cp};
         (void)hipLaunchKernel(k, dim3((unsigned)grid), dim3(64), args, lds, s);
         return hipGetLastError();
     }
+    const size_t ncu = prepare_launch((const void *)lz4_decode_lane_kernel);
     size_t waves = waves_per_cu((const void *)lz4_decode_lane_kernel, 0);
     waves = std::min<size_t>(waves, env_waves > 0 ? (size_t)env_waves : kLaneWaves);
     const size_t grid = std::min<size_t>((b.count + 63) / 64, ncu * waves);
-    hipLaunchKernelGGL(lz4_decode_lane_kernel, dim3((unsigned)grid), dim3(64), 0, s, b, in_cap, out_cap,
-                       work_counter(s));
+    WorkCounter ctr(s);
+    if (!ctr.get()) return hipErrorOutOfMemory;
+    hipLaunchKernelGGL(lz4_decode_lane_kernel, dim3((unsigned)grid), dim3(64), 0, s, b, in_cap, out_cap, ctr.get());
     return hipGetLastError();
 }
 

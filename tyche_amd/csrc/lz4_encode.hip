@@ -262,19 +262,12 @@ hipError_t launch_lz4_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream_
     if (in_cap > 65535u) return hipErrorInvalidValue;    // 16-bit positions (byU16 regime)
     const size_t lds = kHashSize * sizeof(uint16_t) + 4 * kWave + kWave * 8 + kWave * 16 +
                        ((in_cap + 16u + kPad + 15u) & ~15u);
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    static int cus[64] = {0};
-    if (dev < 64 && cus[dev] == 0) {
-        (void)hipFuncSetAttribute((const void *)lz4_encode_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  160 * 1024);
-        int n = 0;
-        (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-        cus[dev] = n > 0 ? n : 256;
-    }
+    const size_t ncu = prepare_launch((const void *)lz4_encode_kernel);
     const size_t per_cu = waves_per_cu((const void *)lz4_encode_kernel, lds);
-    const size_t grid = std::min<size_t>(b.count, (size_t)(dev < 64 ? cus[dev] : 256) * per_cu);
-    hipLaunchKernelGGL(lz4_encode_kernel, dim3((unsigned)grid), dim3(kWave), lds, s, b, in_cap, work_counter(s));
+    const size_t grid = std::min<size_t>(b.count, ncu * per_cu);
+    WorkCounter ctr(s);
+    if (!ctr.get()) return hipErrorOutOfMemory;
+    hipLaunchKernelGGL(lz4_encode_kernel, dim3((unsigned)grid), dim3(kWave), lds, s, b, in_cap, ctr.get());
     return hipGetLastError();
 }
 

@@ -542,20 +542,13 @@ hipError_t launch_zlib_inflate(const tyche_batch_t &b, uint32_t out_cap, hipStre
     const uint32_t off_lens = (out_cap + 64u + 15u) & ~15u;
     const size_t lds = off_lens + 320 + 2 * 320 + 2 * 32;
     if (lds > 160 * 1024) return hipErrorInvalidValue;
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    static int cus[64] = {0};
-    if (dev < 64 && cus[dev] == 0) {
-        (void)hipFuncSetAttribute((const void *)zlib_inflate_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  160 * 1024);
-        int n = 0;
-        (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-        cus[dev] = n > 0 ? n : 256;
-    }
+    const size_t ncu = prepare_launch((const void *)zlib_inflate_kernel);
     const size_t per_cu = waves_per_cu((const void *)zlib_inflate_kernel, lds);
-    const size_t grid = std::min<size_t>(b.count, (size_t)(dev < 64 ? cus[dev] : 256) * (size_t)per_cu);
+    const size_t grid = std::min<size_t>(b.count, ncu * per_cu);
+    WorkCounter ctr(s);
+    if (!ctr.get()) return hipErrorOutOfMemory;
     hipLaunchKernelGGL(zlib_inflate_kernel, dim3((unsigned)grid), dim3(kWave), lds, s, b, out_cap, off_lens,
-                       work_counter(s));
+                       ctr.get());
     return hipGetLastError();
 }
 

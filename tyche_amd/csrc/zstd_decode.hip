@@ -1209,20 +1209,13 @@ hipError_t launch_zstd_decode(const tyche_batch_t &b, uint32_t in_cap, uint32_t 
     if (b.count == 0) return hipSuccess;
     const Layout lay = make_layout(in_cap, out_cap);
     if (lay.total > 160u * 1024u) return hipErrorInvalidValue;
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    static int cus[64] = {0};
-    if (dev < 64 && cus[dev] == 0) {
-        (void)hipFuncSetAttribute((const void *)zstd_decode_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  160 * 1024);
-        int n = 0;
-        (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-        cus[dev] = n > 0 ? n : 256;
-    }
+    const size_t ncu = prepare_launch((const void *)zstd_decode_kernel);
     const size_t per_cu = waves_per_cu((const void *)zstd_decode_kernel, lay.total);
-    const size_t grid = std::min<size_t>(b.count, (size_t)(dev < 64 ? cus[dev] : 256) * per_cu);
+    const size_t grid = std::min<size_t>(b.count, ncu * per_cu);
+    WorkCounter ctr(s);
+    if (!ctr.get()) return hipErrorOutOfMemory;
     hipLaunchKernelGGL(zstd_decode_kernel, dim3((unsigned)grid), dim3(kWave), lay.total, s, b, in_cap, out_cap, lay,
-                       work_counter(s));
+                       ctr.get());
     return hipGetLastError();
 }
 

@@ -675,19 +675,12 @@ hipError_t launch_zstd_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream
     if (in_cap > 65535u) return hipErrorInvalidValue;    // 16-bit positions in the parse and sequence records
     const size_t lds = kHashSize * sizeof(uint16_t) + kWave + kWave * 8 + kSeqCap * 8 + kHtab * 4 + 256 +
                        ((in_cap + 16u + kPad + 15u) & ~15u);
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    static int cus[64] = {0};
-    if (dev < 64 && cus[dev] == 0) {
-        (void)hipFuncSetAttribute((const void *)zstd_encode_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  160 * 1024);
-        int n = 0;
-        (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-        cus[dev] = n > 0 ? n : 256;
-    }
+    const size_t ncu = prepare_launch((const void *)zstd_encode_kernel);
     const size_t per_cu = waves_per_cu((const void *)zstd_encode_kernel, lds);
-    const size_t grid = std::min<size_t>(b.count, (size_t)(dev < 64 ? cus[dev] : 256) * per_cu);
-    hipLaunchKernelGGL(zstd_encode_kernel, dim3((unsigned)grid), dim3(kWave), lds, s, b, in_cap, work_counter(s));
+    const size_t grid = std::min<size_t>(b.count, ncu * per_cu);
+    WorkCounter ctr(s);
+    if (!ctr.get()) return hipErrorOutOfMemory;
+    hipLaunchKernelGGL(zstd_encode_kernel, dim3((unsigned)grid), dim3(kWave), lds, s, b, in_cap, ctr.get());
     return hipGetLastError();
 }
 
