@@ -6,8 +6,11 @@ Metric: GiB/s device-resident LZ4 compress+decompress of 1M x 16 KiB pages
 compress pass + one decompress pass over the rank's 1,048,576 resident pages;
 value = uncompressed bytes of all ranks' pages x steps / max-over-ranks wall time.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2|C4]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+--config C4 measures BASELINE configs[3] instead: LZ4 decompress-only of 8M x 8 KiB
+pages, split over the ranks by contiguous page ranges (strong scaling).
 
 Prints ONE JSON line on rank 0 with `roofline` (dominant kernel, HIP events on
 the codec's stream) and `cpu_baseline` (the reference's vendored LZ4 1.7.5 from
@@ -52,6 +55,10 @@ def parse():
     ap.add_argument("--no-extra", action="store_true", help="skip the secondary C3 (zstd) measurement")
     ap.add_argument("--extra-pages", type=int, default=1 << 20, help="pages for the C3 zstd measurement")
     ap.add_argument("--extra-steps", type=int, default=2)
+    ap.add_argument("--config", default="C2", choices=["C2", "C4"],
+                    help="C2: the headline (LZ4 compress+decompress, 1M x 16 KiB per GPU); "
+                         "C4: BASELINE configs[3], LZ4 decompress-only of 8M x 8 KiB pages split over the ranks")
+    ap.add_argument("--c4-pages", type=int, default=8 << 20, help="C4 total pages over all ranks")
     return ap.parse_args()
 
 
@@ -202,9 +209,70 @@ def pmc_traffic(kernel: str, pages: int, page_len: int):
     return None
 
 
+def run_c4(args, info, dev):
+    """BASELINE configs[3]: LZ4 decompress-only (the restore path) of 8M x 8 KiB pages split across the ranks
+    by contiguous page ranges (sharding.page_range, strong scaling: the total is fixed).  Each rank compresses
+    its range once (untimed, every page round-trip checked), then times decode-only steps."""
+    from tyche_amd import sharding
+
+    plen = 8192
+    a, n = sharding.page_range(args.c4_pages, info.rank, info.world)
+    pages = codec.pagegen(n, plen, seed=args.seed, first=a, dist=args.dist, device=dev)
+    comp, clen = codec.compress_pages(pages)
+    torch.cuda.synchronize()
+    mx = int(clen.max().item())
+    out = torch.empty_like(pages)
+    rv = torch.empty((n,), dtype=torch.int32, device=dev)
+    for _ in range(max(args.warmup, 1)):
+        codec.decompress_pages(comp, clen, plen, out=out, rv=rv, max_comp_len=mx)
+    torch.cuda.synchronize()
+    if not (bool((rv == plen).all().item()) and torch.equal(out, pages)):
+        raise SystemExit("C4: round trip failed")
+    del pages
+    comp_bytes = int(clen.to(torch.int64).sum().item())
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(args.steps)]
+    runner.barrier(info)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        events[k][0].record()
+        codec.decompress_pages(comp, clen, plen, out=out, rv=rv, max_comp_len=mx)
+        events[k][1].record()
+    torch.cuda.synchronize()
+    runner.barrier(info)
+    elapsed = runner.max_over_ranks(info, time.perf_counter() - t0)
+    d_ms = sum(e[0].elapsed_time(e[1]) for e in events) / args.steps
+    total = runner.sum_over_ranks(info, float(n))
+    algo = n * plen + comp_bytes
+    achieved = algo / (d_ms * 1e-3) / 1e9
+    result = {
+        "metric": "GiB/s device-resident LZ4 decompress, 8M x 8 KiB pages split over the GPUs (BASELINE configs[3])",
+        "value": round(total * plen * args.steps / elapsed / GIB, 3), "unit": "GiB/s", "n_gpus": info.world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (pagegen.h PostgreSQL-like pages, seed 20170303)",
+        "config": {"workload": "C4: LZ4 decompress-only, 8M x 8 KiB pages, contiguous page ranges per rank",
+                   "total_pages": args.c4_pages, "pages_this_rank": n, "page_len": plen, "codec": "lz4",
+                   "parallelism": f"page-range x{info.world}"},
+        "roofline": {"bound": "hbm", "kernel": "lz4_decode", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "algorithmic_bytes_per_launch": algo},
+        "kernel_ms": {"lz4_decode": round(d_ms, 4)}, "ratio": round(n * plen / comp_bytes, 4),
+    }
+    if info.rank == 0:
+        print(json.dumps(result), flush=True)
+    runner.shutdown(info)
+
+
 def main():
     args = parse()
     info = runner.init_distributed()
+    if args.config == "C4":
+        dev = torch.device("cuda", info.local_rank)
+        torch.cuda.set_device(dev)
+        if _lib.load().tyche_device_ready() != 1:
+            raise SystemExit(f"device not ready: {_lib.last_error()}")
+        return run_c4(args, info, dev)
     dev = torch.device("cuda", info.local_rank)
     torch.cuda.set_device(dev)
     lib = _lib.load()

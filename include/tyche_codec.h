@@ -100,11 +100,12 @@ int tyche_buffers_compress(Buffer **bufs, void **compressed, int *status, size_t
 int tyche_buffers_decompress(Buffer **bufs, int *status, size_t n, int compressor_id);
 
 /* ---- restore queue: coalesced per-hit restores (src/list.c:563-589) ------- */
-/* Starts the dispatcher threads (TYCHE_RESTORE_DISPATCHERS, default two per
- * active device; they inherit the calling thread's device choice) that batch
- * concurrent tyche_buffer_restore calls: once a request arrives one dispatcher
- * waits up to max_wait_us for up to max_batch requests, then runs one GPU
- * decompress batch per codec while the next dispatcher collects.  Idempotent. */
+/* Starts the dispatcher threads (per codec, TYCHE_RESTORE_DISPATCHERS each,
+ * default one per active device; they inherit the calling thread's device
+ * choice) that batch concurrent tyche_buffer_restore calls: once a request
+ * arrives a dispatcher of its codec waits up to max_wait_us for up to max_batch
+ * requests of that codec, then runs one GPU decompress batch while the next
+ * dispatcher collects.  Idempotent. */
 int tyche_restore_queue_start(int max_batch, int max_wait_us);
 /* Drains and stops the dispatcher. */
 void tyche_restore_queue_stop(void);

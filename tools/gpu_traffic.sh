@@ -1,0 +1,16 @@
+#!/bin/bash
+# HBM traffic of the bench kernels at the bench's sizes (C2: LZ4 1M x 16 KiB; C3: zstd 1M x 32 KiB;
+# C4 shard: LZ4 1M x 8 KiB): FETCH_SIZE and WRITE_SIZE passes (separate rocprofv3 --pmc runs) over
+# tools/run_codec.py with REPS=1, reduced by tools/pmc_traffic.py.
+#   bash tools/gpu_traffic.sh <round-tag, e.g. r02>
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+T=${1:-r02}
+mkdir -p $R/gpurun_out/traffic_$T
+cd /tmp && export TMPDIR=/tmp REPS=1
+run() {   # tag codec plen pages
+  for c in FETCH_SIZE WRITE_SIZE; do
+    CODEC=$2 PLEN=$3 PAGES=$4 timeout -s KILL 120 rocprofv3 --pmc $c --output-format csv \
+      -d $R/gpurun_out/traffic_$T/$1_$c -o run -- python3 $R/tools/run_codec.py > $R/gpurun_out/traffic_$T/$1_$c.log 2>&1 || { echo "pass $1 $c failed"; return 1; }
+  done
+}
+run c2 lz4 16384 1048576 && run c3 zstd 32768 1048576 && run c4 lz4 8192 1048576 && echo done

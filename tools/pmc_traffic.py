@@ -3,9 +3,14 @@
     python tools/pmc_traffic.py profiles/r01_pmc_fetch_size.csv profiles/r01_pmc_write_size.csv \
         --pages 262144 --page-len 16384 -o profiles/r01_traffic.json
 
-Correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE and WRITE_SIZE are in
-KiB; on gfx950 FETCH_SIZE reports half the bytes of a 16-B/lane streaming read,
-so HBM bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.  Each kernel's figure is
+Correction: FETCH_SIZE and WRITE_SIZE are in KiB.  On gfx950 FETCH_SIZE reports
+half the bytes of a wide coalesced 16-B/lane streaming read (MI355X_MICROARCH.md,
+HBM section): the kernels that stage whole pages into LDS read that way, so
+their read bytes are 2 * FETCH_SIZE.  The lane-per-page LZ4 decoder reads
+scattered 16-byte pieces, one lane per page; for that pattern the calibration
+probe (tools/probes/fetch_calib.hip, profiles/r02_fetch_calib.json) shows
+FETCH_SIZE = 64 B per fabric read request = the bytes actually fetched, so its
+read bytes are 1 * FETCH_SIZE.  Each kernel's figure is
 its bytes per codec call divided by the pages of a call.  A call is one
 dispatch, except where --calls says how many calls the kernel's dispatches
 make up (the LZ4 decoder runs two size-class launches per call:
@@ -22,7 +27,12 @@ KERNELS = {"lz4_encode": "lz4_encode_kernel", "lz4_decode": "lz4_decode_",
            "zlib_encode": "zlib_deflate_kernel", "zlib_decode": "zlib_inflate_kernel"}
 
 
+# read-byte factor per FETCH_SIZE byte, by kernel symbol (see the module docstring)
+SCATTERED = ("lz4_decode_ring_kernel", "lz4_decode_lane_kernel")
+
+
 def per_dispatch(path, counter):
+    """kernel -> list of per-dispatch values; FETCH_SIZE already scaled to read bytes (KiB)."""
     acc = defaultdict(float)
     names = {}
     for r in csv.DictReader(open(path)):
@@ -32,6 +42,8 @@ def per_dispatch(path, counter):
         names[r["Dispatch_Id"]] = r["Kernel_Name"]
     out = defaultdict(list)
     for d, v in acc.items():
+        if counter == "FETCH_SIZE":
+            v *= 1.0 if any(sym in names[d] for sym in SCATTERED) else 2.0
         for k, sym in KERNELS.items():
             if sym in names[d]:
                 out[k].append(v)
@@ -51,13 +63,15 @@ def main():
     f = per_dispatch(a.fetch, "FETCH_SIZE")
     w = per_dispatch(a.write, "WRITE_SIZE")
     res = {"pages_per_call": a.pages, "page_len": a.page_len, "calls": calls,
-           "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024 / pages (gfx950 FETCH_SIZE half-count corrected)",
+           "formula": "(c*FETCH_SIZE + WRITE_SIZE) * 1024 / pages; c = 2 for the page-staging kernels (gfx950 "
+                      "half count of coalesced streaming reads), 1 for the scattered lane LZ4 decoder (calibrated, "
+                      "tools/probes/fetch_calib.hip)",
            "bytes_per_page": {}, "read_bytes_per_page": {}, "write_bytes_per_page": {}}
     for k in KERNELS:
         if not f.get(k) or not w.get(k):
             continue
         nf, nw = calls.get(k, len(f[k])), calls.get(k, len(w[k]))
-        rd = 2 * 1024 * sum(f[k]) / nf / a.pages
+        rd = 1024 * sum(f[k]) / nf / a.pages
         wr = 1024 * sum(w[k]) / nw / a.pages
         res["read_bytes_per_page"][k] = round(rd, 1)
         res["write_bytes_per_page"][k] = round(wr, 1)

@@ -986,63 +986,64 @@ int buffer__decompress(Buffer *buf, int compressor_id) {
 // share GPU launches: a caller enqueues its Buffer and blocks; a dispatcher
 // thread takes whatever is queued (up to max_batch, after waiting at most
 // max_wait_us for company once the first request arrives), runs one
-// tyche_buffers_decompress per codec over the batch, and wakes each caller with
-// its buffer__decompress status.  Per-buffer semantics are unchanged.
-// Several dispatchers run (TYCHE_RESTORE_DISPATCHERS, default two per device):
-// one collects while the others' batches are on the GPUs, so a restore waits
-// for its own batch, not for the one before it; the host path sends each batch
-// to the least busy device.
+// tyche_buffers_decompress over the batch, and wakes each caller with its
+// buffer__decompress status.  Per-buffer semantics are unchanged.
+//
+// Each codec has its own queue and dispatchers (TYCHE_RESTORE_DISPATCHERS per
+// codec, default one per device): a batch's latency is that of its slowest
+// page (one wave decodes one page: ~0.2 ms for a 16 KiB LZ4 page, ~1.4 ms for
+// zlib, tools/latency.c), so LZ4 restores never wait behind a zlib batch.  More
+// dispatchers per codec than that do not help: the process has 4 hardware
+// queues (GPU_MAX_HW_QUEUES), and batches on more streams than that run behind
+// each other anyway (profiles/r02_restore.json).
 namespace {
 struct RestoreReq {
     Buffer *buf;
-    int codec;
     int status;
     bool done;
 };
 struct RestoreQueue {
     std::mutex mu;
     std::condition_variable cv, done_cv;
-    std::vector<RestoreReq *> q;
-    bool running = false, stop = false, collecting = false;
+    std::vector<RestoreReq *> q[4];   // by codec id (NO is restored by the caller)
+    bool collecting[4] = {false, false, false, false};
+    bool running = false, stop = false;
     int max_batch = 1024, max_wait_us = 50, device = -1;
     uint64_t batches = 0, buffers = 0;
     std::vector<std::thread> th;
-    void loop() {
+    void loop(int codec) {
         (void)tyche_set_device(device);
         std::vector<RestoreReq *> take;
+        std::vector<Buffer *> bufs;
+        std::vector<int> st;
+        std::vector<RestoreReq *> &cq = q[codec];
         for (;;) {
             {
                 std::unique_lock<std::mutex> g(mu);
-                cv.wait(g, [&] { return (stop && q.empty()) || (!q.empty() && !collecting); });
-                if (q.empty()) return;   // stopping
-                collecting = true;
-                if ((int)q.size() < max_batch && max_wait_us > 0)
+                cv.wait(g, [&] { return (stop && cq.empty()) || (!cq.empty() && !collecting[codec]); });
+                if (cq.empty()) return;   // stopping
+                collecting[codec] = true;
+                if ((int)cq.size() < max_batch && max_wait_us > 0)
                     cv.wait_for(g, std::chrono::microseconds(max_wait_us),
-                                [&] { return stop || (int)q.size() >= max_batch; });
-                const size_t k = std::min(q.size(), (size_t)max_batch);
-                take.assign(q.begin(), q.begin() + k);
-                q.erase(q.begin(), q.begin() + k);
-                collecting = false;
+                                [&] { return stop || (int)cq.size() >= max_batch; });
+                const size_t k = std::min(cq.size(), (size_t)max_batch);
+                take.assign(cq.begin(), cq.begin() + k);
+                cq.erase(cq.begin(), cq.begin() + k);
+                collecting[codec] = false;
             }
-            cv.notify_all();   // the next dispatcher may collect
-            // one batch per codec id present
-            for (int codec = 0; codec <= 3; codec++) {
-                std::vector<Buffer *> bufs;
-                std::vector<RestoreReq *> reqs;
-                for (RestoreReq *r : take)
-                    if (r->codec == codec) { bufs.push_back(r->buf); reqs.push_back(r); }
-                if (bufs.empty()) continue;
-                std::vector<int> st(bufs.size());
-                tyche_buffers_decompress(bufs.data(), st.data(), bufs.size(), codec);
-                for (size_t i = 0; i < reqs.size(); i++) reqs[i]->status = st[i];
-            }
-            for (RestoreReq *r : take)
-                if (r->codec < 0 || r->codec > 3) r->status = buffer__decompress(r->buf, r->codec);
+            cv.notify_all();   // the next dispatcher of this codec may collect
+            bufs.resize(take.size());
+            st.resize(take.size());
+            for (size_t i = 0; i < take.size(); i++) bufs[i] = take[i]->buf;
+            tyche_buffers_decompress(bufs.data(), st.data(), bufs.size(), codec);
             {
                 std::lock_guard<std::mutex> g(mu);
                 batches++;
                 buffers += take.size();
-                for (RestoreReq *r : take) r->done = true;
+                for (size_t i = 0; i < take.size(); i++) {
+                    take[i]->status = st[i];
+                    take[i]->done = true;
+                }
             }
             done_cv.notify_all();
         }
@@ -1058,12 +1059,13 @@ int tyche_restore_queue_start(int max_batch, int max_wait_us) {
     g_rq.max_wait_us = max_wait_us >= 0 ? max_wait_us : 50;
     g_rq.device = t_device;
     g_rq.stop = false;
-    g_rq.collecting = false;
+    for (bool &c : g_rq.collecting) c = false;
     g_rq.running = true;
     const char *env = getenv("TYCHE_RESTORE_DISPATCHERS");
-    int k = env ? atoi(env) : 2 * std::max(1, tyche_active_devices());
+    int k = env ? atoi(env) : std::max(1, tyche_active_devices());
     k = std::max(1, std::min(k, 64));
-    for (int i = 0; i < k; i++) g_rq.th.emplace_back([] { g_rq.loop(); });
+    for (int codec = 1; codec <= 3; codec++)
+        for (int i = 0; i < k; i++) g_rq.th.emplace_back([codec] { g_rq.loop(codec); });
     return TYCHE_E_OK;
 }
 
@@ -1081,14 +1083,16 @@ void tyche_restore_queue_stop(void) {
 }
 
 int tyche_buffer_restore(Buffer *buf, int compressor_id) {
-    RestoreReq r{buf, compressor_id, TYCHE_E_OK, false};
+    // NO and unknown ids need no GPU batch: the direct path gives the reference's answer
+    if (compressor_id < 1 || compressor_id > 3) return buffer__decompress(buf, compressor_id);
+    RestoreReq r{buf, TYCHE_E_OK, false};
     {
         std::unique_lock<std::mutex> g(g_rq.mu);
         if (!g_rq.running || g_rq.stop) {
             g.unlock();
             return buffer__decompress(buf, compressor_id);   // no queue: the direct path
         }
-        g_rq.q.push_back(&r);
+        g_rq.q[compressor_id].push_back(&r);
     }
     g_rq.cv.notify_all();   // the collecting dispatcher, whichever it is
     std::unique_lock<std::mutex> g(g_rq.mu);

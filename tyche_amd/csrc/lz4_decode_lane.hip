@@ -373,7 +373,7 @@ __device__ int32_t decode_ring(const uint8_t *__restrict__ in, int32_t L, uint8_
         // the unflushed tail is < kLine + 16 bytes here and the ring holds every
         // position above op + 16 - kRing, so a source at offset > kRing - 32
         // (>= 96) is already in HBM and a nearer one is in the ring
-        const bool far = off > kRing - 32;
+        const bool far = (TYCHE_ABLATE & 64) ? false : off > kRing - 32;   // 64: timing only (far matches read the ring: wrong output)
         u128 m = far ? ld16(out + op - off) : ring_rd<kRing>(rb, op - off);
         ip += pos;
         w = windowN<kWin>(in, ip, L);

@@ -167,16 +167,119 @@ __device__ bool emit_records(const uint2 *rec, uint32_t n, uint32_t anchor, cons
     return true;
 }
 
+// ---- output staging (the default emission).
+//
+// emit_records above resolves every output byte's owner and field (a map
+// stamp, a max-scan, a select chain per byte): ~330 instructions per 256 output
+// bytes, 27 % of the encoder's wave cycles (tools/phase_prof.py, r02).  Here each
+// sequence's lane writes its own bytes -- token, literal-length bytes, literals,
+// offset, match-length bytes -- into a 1 KiB LDS ring with byte stores, and the
+// ring leaves for HBM in 256-byte steps, one dword store per lane.  The ring
+// reuses emit_records' field area, so the LDS budget (and 8 waves per CU) is
+// unchanged; a sink too large for the ring (long literal runs: the ring is
+// flushed first) still takes emit_records straight to HBM.
+constexpr uint32_t kOutRing = 1024;   // bytes; head is always a multiple of 256
+struct OutRing {
+    uint32_t head, pend;   // wave-uniform: ring position of the first unflushed byte, unflushed bytes
+};
+
+__device__ __forceinline__ void out_flush_steps(const uint8_t *ring, OutRing &r, uint8_t *dst, uint32_t &op,
+                                                uint32_t lane) {
+    while (r.pend >= 4 * kWave) {
+        const uint32_t w = *(const uint32_t *)(ring + ((r.head + 4 * lane) & (kOutRing - 1)));
+        store_u32_unaligned(dst + op + 4 * lane, w);
+        op += 4 * kWave;
+        r.head = (r.head + 4 * kWave) & (kOutRing - 1);
+        r.pend -= 4 * kWave;
+    }
+}
+
+__device__ __forceinline__ void out_flush_all(const uint8_t *ring, OutRing &r, uint8_t *dst, uint32_t &op,
+                                              uint32_t lane) {
+    out_flush_steps(ring, r, dst, op, lane);
+    const uint32_t j = 4 * lane;
+    if (j < r.pend) {
+        const uint32_t w = *(const uint32_t *)(ring + ((r.head + j) & (kOutRing - 1)));
+        if (j + 4 <= r.pend) {
+            store_u32_unaligned(dst + op + j, w);
+        } else {
+            for (uint32_t t = 0; j + t < r.pend; t++) dst[op + j + t] = (uint8_t)(w >> (8 * t));
+        }
+    }
+    op += r.pend;
+    r.head = 0;
+    r.pend = 0;
+    __builtin_amdgcn_wave_barrier();
+}
+
+// The sink of the default emission: n records (stream order) after the literal
+// run that starts at `anchor`; op counts the bytes already in dst.  Returns
+// false if the output would exceed cap.
+__device__ bool emit_staged(const uint2 *rec, uint32_t n, uint32_t anchor, const uint8_t *in, uint8_t *dst,
+                            uint32_t &op, uint32_t cap, uint8_t *ring, OutRing &r, uint8_t *map, uint32_t lane) {
+    const bool is_sel = lane < n;
+    const uint2 rc = rec[is_sel ? lane : 0];
+    const uint2 rp = rec[lane > 0 && is_sel ? lane - 1 : 0];
+    const uint32_t pos = rc.x & 0xFFFFu, cand = rc.x >> 16, len = rc.y & 0xFFFFu, back = rc.y >> 16;
+    const uint32_t prev_end = lane == 0 ? anchor : (rp.x & 0xFFFFu) + (rp.y & 0xFFFFu);
+    uint32_t lit = 0, lext = 0, lstart = 0, off = 0, mc = 0, mext = 0, token = 0, enc = 0;
+    if (is_sel) {
+        const uint32_t k = min(min(back, pos - prev_end), cand);   // catch-up (lz4.c:549)
+        lstart = prev_end;
+        lit = pos - k - prev_end;
+        lext = lit >= 15 ? (lit - 15) / 255 + 1 : 0;
+        off = pos - cand;
+        mc = len + k - kMinMatch;
+        mext = mc >= 15 ? (mc - 15) / 255 + 1 : 0;
+        token = (min(lit, 15u) << 4) | min(mc, 15u);
+        enc = 1 + lext + lit + 2 + mext;
+    }
+    const int32_t incl = wave_incl_sum((int32_t)enc);
+    const uint32_t eo = (uint32_t)incl - enc;
+    const uint32_t et = rdlane((uint32_t)incl, 63);
+    if (op + r.pend + et > cap) return false;
+    if (r.pend + et > kOutRing) {
+        out_flush_all(ring, r, dst, op, lane);
+        return emit_records(rec, n, anchor, in, dst, op, cap, map, (uint4 *)ring, lane);
+    }
+    if (is_sel) {
+        constexpr uint32_t m = kOutRing - 1;
+        uint32_t q = r.head + r.pend + eo;
+        ring[q & m] = (uint8_t)token;
+        q++;
+        for (uint32_t t = 0; t < lext; t++) ring[(q + t) & m] = (uint8_t)(t + 1 == lext ? (lit - 15) % 255 : 255);
+        q += lext;
+        for (uint32_t t = 0; t < lit; t++) ring[(q + t) & m] = in[lstart + t];
+        q += lit;
+        ring[q & m] = (uint8_t)off;
+        ring[(q + 1) & m] = (uint8_t)(off >> 8);
+        q += 2;
+        for (uint32_t t = 0; t < mext; t++) ring[(q + t) & m] = (uint8_t)(t + 1 == mext ? (mc - 15) % 255 : 255);
+    }
+    __builtin_amdgcn_wave_barrier();
+    r.pend += et;
+    out_flush_steps(ring, r, dst, op, lane);
+    __builtin_amdgcn_wave_barrier();
+    return true;
+}
+
 // Encodes one page held in LDS into dst (global, capacity cap).  Returns the
 // compressed size, or 0 if it does not fit in cap.
 __device__ int32_t encode_page(const uint8_t *in, uint32_t L, uint16_t *table, uint8_t *map, uint2 *rec,
                                uint4 *fld, uint8_t *dst, uint32_t cap, uint32_t lane) {
     uint32_t op = 0;
-    auto sink = [&](const uint2 *r, uint32_t n, uint32_t anchor) -> bool {
-        return emit_records(r, n, anchor, in, dst, op, cap, map, fld, lane);
+#ifndef TYCHE_LZ4_STAGED
+#define TYCHE_LZ4_STAGED 1
+#endif
+    OutRing r{0u, 0u};
+    uint8_t *ring = (uint8_t *)fld;
+    auto sink = [&](const uint2 *rr, uint32_t n, uint32_t anchor) -> bool {
+        if (TYCHE_LZ4_STAGED) return emit_staged(rr, n, anchor, in, dst, op, cap, ring, r, map, lane);
+        return emit_records(rr, n, anchor, in, dst, op, cap, map, fld, lane);
     };
     const uint32_t anchor = lzp::parse_page(in, L, table, rec, lane, sink);
     if (anchor == 0xFFFFFFFFu) return 0;
+    if (TYCHE_LZ4_STAGED) out_flush_all(ring, r, dst, op, lane);
     // ---- last literals: in[anchor, L)
     const uint32_t lit = L - anchor;
     const uint32_t lext = lit >= 15 ? (lit - 15) / 255 + 1 : 0;
