@@ -101,6 +101,23 @@ class WorkCounter {
     int dev_ = -1, idx_ = -1;
     unsigned *p_ = nullptr;
 };
+// A device scratch buffer of at least `bytes` for one launch on stream s,
+// returned to the device's pool when it goes out of scope (right after the
+// launch) as an event on s, and handed out again only once that event has
+// completed -- the WorkCounter scheme for kernels that need workspace.
+class ScratchLease {
+  public:
+    ScratchLease(hipStream_t s, size_t bytes);
+    ~ScratchLease();
+    ScratchLease(const ScratchLease &) = delete;
+    ScratchLease &operator=(const ScratchLease &) = delete;
+    void *get() const { return p_; }   // nullptr if no buffer could be allocated
+
+  private:
+    hipStream_t s_;
+    int dev_ = -1, idx_ = -1;
+    void *p_ = nullptr;
+};
 // Per-device, thread-safe launch preparation: raises `kernel`'s dynamic-LDS
 // limit to the CU's 160 KiB once per (device, kernel) and returns the current
 // device's CU count.

@@ -102,6 +102,61 @@ tyche::WorkCounter::~WorkCounter() {
     }
 }
 
+namespace {
+struct ScratchPool {
+    struct Entry {
+        void *p;
+        size_t bytes;
+        hipEvent_t ev;
+        int state;   // 0 free, 1 leased, 2 released (event pending)
+    };
+    std::mutex mu;
+    std::vector<Entry> e;
+};
+ScratchPool g_scratch[kMaxDevices];
+}  // namespace
+
+tyche::ScratchLease::ScratchLease(hipStream_t s, size_t bytes) : s_(s) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return;
+    ScratchPool &P = g_scratch[dev];
+    std::lock_guard<std::mutex> g(P.mu);
+    size_t take = P.e.size();
+    for (size_t i = 0; i < P.e.size(); i++) {
+        ScratchPool::Entry &x = P.e[i];
+        if (x.state == 1 || x.bytes < bytes) continue;
+        if (x.state == 2 && hipEventQuery(x.ev) != hipSuccess) continue;
+        take = i;
+        break;
+    }
+    if (take == P.e.size()) {
+        ScratchPool::Entry x{nullptr, (bytes + 0xFFFFF) & ~size_t(0xFFFFF), nullptr, 0};
+        if (hipMalloc(&x.p, x.bytes) != hipSuccess) return;
+        if (hipEventCreateWithFlags(&x.ev, hipEventDisableTiming) != hipSuccess) {
+            (void)hipFree(x.p);
+            return;
+        }
+        P.e.push_back(x);
+    }
+    P.e[take].state = 1;
+    dev_ = dev;
+    idx_ = (int)take;
+    p_ = P.e[take].p;
+}
+
+tyche::ScratchLease::~ScratchLease() {
+    if (idx_ < 0) return;
+    ScratchPool &P = g_scratch[dev_];
+    std::lock_guard<std::mutex> g(P.mu);
+    ScratchPool::Entry &x = P.e[(size_t)idx_];
+    if (hipEventRecord(x.ev, s_) == hipSuccess) {
+        x.state = 2;
+    } else {
+        (void)hipStreamSynchronize(s_);
+        x.state = 0;
+    }
+}
+
 size_t tyche::prepare_launch(const void *kernel) {
     static std::mutex mu;
     static std::set<std::pair<int, const void *>> raised;

@@ -165,18 +165,22 @@ __device__ __forceinline__ void decode_record(const uint2 *rec, uint32_t n, uint
 // 4-byte items that differ in one byte (page line pointers) are level 1's most
 // common 3-byte match (16 % of its matches on the bench pages).  A 3-byte
 // table of its own was tried: +0.3 % ratio for +8 % encode time.
+//
+// start (a multiple of 64, default 0): parse [start, L) only, with the table
+// holding earlier positions already (the split LZ4 encoder's second wave); the
+// first literal run starts at `start`.
 template <bool kRepCand = false, bool kMin3 = false, typename Sink>
 __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *table, uint2 *rec, uint32_t lane,
-                                      Sink &sink) {
-    uint32_t anchor = 0;
-    if (L < (uint32_t)(kMfLimit + 1)) return 0;
+                                      Sink &sink, uint32_t start = 0) {
+    uint32_t anchor = start;
+    if (L < (uint32_t)(kMfLimit + 1) || start > L - kMfLimit) return start;
     const uint32_t mflimit = L - kMfLimit;          // last position a match may start
     const uint32_t matchlimit = L - kLastLiterals;  // matches end at or before this
     const uint32_t ib = (uint32_t)(uintptr_t)in & 3u;               // in's offset from a dword boundary
     const uint32_t *A = (const uint32_t *)(in - ib);                // the page as aligned dwords
-    uint32_t cursor = 0;     // matches may start here (end of the last match)
+    uint32_t cursor = start; // matches may start here (end of the last match)
     uint32_t nacc = 0;       // records accumulated since the last hand-off
-    uint32_t blk = 0;        // current 64-position block
+    uint32_t blk = start;    // current 64-position block
     uint32_t R = 1, R2 = 4;  // repeat offsets 1 and 2 (kRepCand): zstd's initial {1, 4}
     bool done = false;
     PHASE_INIT();
