@@ -302,7 +302,7 @@ __device__ int32_t encode_page(const uint8_t *in, uint32_t L, uint16_t *table, u
 // buffers take 20 KiB of LDS, so a CU holds 8 of them (2 waves per SIMD), and
 // 8 KiB pages -- 13 waves per CU -- encode 25 % faster per byte.  Here two
 // waves share one staged page: wave A parses [0, H) and wave B [H, L), H = L/2
-// rounded to 64, each with its own table and buffers (24 KiB per page for both:
+// = 9/16 L rounded to 64 (B also seeds its table), each with its own table and buffers (24 KiB per page for both:
 // 6 workgroups = 12 waves per CU).  The halves join exactly:
 //   * A's matches end at or before H (its parse sees L' = H + LASTLITERALS) and
 //     it emits no trailing literal run: its output is complete sequences;
@@ -316,9 +316,13 @@ __device__ int32_t encode_page(const uint8_t *in, uint32_t L, uint16_t *table, u
 //     joint is the page's last literal run.
 // The LZ4 block rules hold on the joined stream (every match starts <= L-12 and
 // ends <= L-5; the last sequence is literals only); output never exceeds cap.
-// 16 KiB pages: 108.2 -> 98.9 ms per 1M pages (12 waves per CU instead of 8); 8 KiB pages stay on the
+// 16 KiB pages: 108.2 -> 93.3 ms per 1M pages (12 waves per CU instead of 8); 8 KiB pages stay on the
 // one-wave kernel (13 waves per CU already: 45.0 vs 57.6 ms split)
 constexpr uint32_t kSplitMin = 12288;
+#ifndef TYCHE_SPLIT_AT
+#define TYCHE_SPLIT_AT 36   // H = L * TYCHE_SPLIT_AT / 64, rounded down to 64 (ms per 1M x 16 KiB pages: 32: 98.7, 34: 94.3, 35: 93.2, 36: 93.3, 38: 95.4, 40: 99.1)
+#endif
+static_assert(TYCHE_SPLIT_AT >= 32 && TYCHE_SPLIT_AT < 64, "B's half must fit its scratch (sized for L / 2 + 64)");
 constexpr uint32_t kSplitPrefetch = 8;   // 16-byte vectors per thread prefetched for the next page
 struct SplitHdr {
     uint32_t next_lo, next_hi, next2_lo, next2_hi;
@@ -402,7 +406,7 @@ __global__ __launch_bounds__(128, 3) void lz4_encode_split_kernel(tyche_batch_t 
         const uint32_t L = p.src_len;
         const bool fits = L <= in_cap;
         const bool split = fits && L >= kSplitMin;
-        const uint32_t H = (L / 2u) & ~(kWave - 1u);
+        const uint32_t H = (L * TYCHE_SPLIT_AT / 64u) & ~(kWave - 1u);   // A takes a little more than half: B also seeds
         uint32_t opA = 0, cursorA = 0;
         bool okA = true;
         OutRing rA{0u, 0u};
