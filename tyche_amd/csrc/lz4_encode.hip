@@ -296,14 +296,15 @@ __device__ int32_t encode_page(const uint8_t *in, uint32_t L, uint16_t *table, u
     return (int32_t)(op + total);
 }
 
-// ---- split encoder (the default for batches of pages up to kSplitMin bytes and more).
+// ---- split encoder (the default when the batch's pages may reach kSplitMin bytes).
 //
 // The one-wave encoder is latency-bound: its page, hash table and sequence
 // buffers take 20 KiB of LDS, so a CU holds 8 of them (2 waves per SIMD), and
 // 8 KiB pages -- 13 waves per CU -- encode 25 % faster per byte.  Here two
-// waves share one staged page: wave A parses [0, H) and wave B [H, L), H = L/2
-// = 9/16 L rounded to 64 (B also seeds its table), each with its own table and buffers (24 KiB per page for both:
-// 6 workgroups = 12 waves per CU).  The halves join exactly:
+// waves share one staged page: wave A parses [0, H) and wave B [H, L), with
+// H = 9/16 L rounded down to 64 (B also seeds its table), each with its own
+// table and buffers (24 KiB per page for both: 6 workgroups = 12 waves per
+// CU).  The parts join exactly:
 //   * A's matches end at or before H (its parse sees L' = H + LASTLITERALS) and
 //     it emits no trailing literal run: its output is complete sequences;
 //   * B first inserts every position of [0, H) into its table, so its matches
