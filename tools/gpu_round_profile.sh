@@ -1,26 +1,23 @@
 #!/bin/bash
-# Round measurement on the GPU box: bench line, kernel-trace stats of the same
-# workload, and the HBM PMC passes (FETCH_SIZE / WRITE_SIZE kept apart) for the
-# C2 LZ4 kernels and the C3 zstd kernels.
-# Usage (via gpurun): bash tools/gpu_round_profile.sh r01
+# Round measurement on the GPU box: the bench line, the kernel-trace stats of the same workload,
+# the HBM PMC passes at the bench's sizes (tools/gpu_traffic.sh: FETCH_SIZE / WRITE_SIZE kept apart),
+# every codec's rates on resident pages (tools/time_codecs.py), the Buffer-API latency table
+# (tools/latency.c) and the sweep/restore cycle (tools/cycle.c).
+# Usage (via gpurun): bash tools/gpu_round_profile.sh r02
 set -e
-TAG=${1:-r01}
+TAG=${1:-r02}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out
 mkdir -p $OUT
 cd $R
-timeout -k 10 900 python bench.py > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err
-cat $OUT/bench_$TAG.json
+timeout -k 10 600 python bench.py > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err
+tail -c 300 $OUT/bench_$TAG.json
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o bench \
     -- python3 $R/bench.py --no-cpu --e2e-pages 0 > $OUT/prof_bench_$TAG.log 2>&1
-# reduce with tools/pmc_traffic.py (--calls lz4_decode=1: two size-class launches per call)
-for spec in lz4:16384 zstd:32768; do
-  c=${spec%%:*}; p=${spec##*:}
-  export CODEC=$c PLEN=$p PAGES=262144 REPS=1
-  timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_$TAG/${c}_fetch -o run \
-      -- python3 $R/tools/run_codec.py > $OUT/pmc_fetch_${c}_$TAG.log 2>&1
-  timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_$TAG/${c}_write -o run \
-      -- python3 $R/tools/run_codec.py > $OUT/pmc_write_${c}_$TAG.log 2>&1
-done
+cd $R
+bash tools/gpu_traffic.sh $TAG
+timeout -k 10 300 python tools/time_codecs.py > $OUT/time_codecs_$TAG.log 2>&1
+timeout -k 10 120 tools/bin/latency 30 > $OUT/latency_$TAG.jsonl
+timeout -k 10 200 tools/bin/cycle 65536 64 2000 16 > $OUT/cycle_$TAG.json
 echo DONE

@@ -22,7 +22,7 @@ import csv
 import json
 from collections import defaultdict
 
-KERNELS = {"lz4_encode": "lz4_encode_kernel", "lz4_decode": "lz4_decode_",
+KERNELS = {"lz4_encode": "lz4_encode_", "lz4_decode": "lz4_decode_",
            "zstd_encode": "zstd_encode_kernel", "zstd_decode": "zstd_decode_kernel",
            "zlib_encode": "zlib_deflate_kernel", "zlib_decode": "zlib_inflate_kernel"}
 
