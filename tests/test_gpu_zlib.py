@@ -398,3 +398,55 @@ def test_deflate_tight_capacity(tc, oracle_mod, slack):
             if oracle_mod.have_ref():
                 r2, dec2 = oracle_mod.ref_zlib_uncompress(s, plen)
                 assert r2 == plen and dec2 == host[i].tobytes()
+
+
+# ----------------------------------------------------------------- lane-parallel inflate
+def _bench_streams(tc, oracle_mod, plen, n):
+    """Device-encoded and host-zlib level-1 streams of bench pages (one dynamic block each)."""
+    pages = oracle_mod.pagegen(n, plen, seed=2024, first=plen, dist=0)
+    comp, clen = tc.compress_pages(torch.from_numpy(pages).to(DEV), compressor_id=ZLIB)
+    torch.cuda.synchronize()
+    ch, lh = comp.cpu().numpy(), clen.cpu().numpy()
+    streams = [ch[i, :lh[i]].tobytes() for i in range(n)] + [zlib.compress(pages[i].tobytes(), 1) for i in range(n)]
+    return [pages[i % n].tobytes() for i in range(2 * n)], streams
+
+
+@pytest.mark.parametrize("par", ["0", "1"])
+def test_inflate_serial_and_parallel_kernels(tc, oracle_mod, monkeypatch, par):
+    """Both inflate kernels (TYCHE_ZLIB_PAR=0: one symbol at a time; 1: lane-parallel symbol
+    decode with the serial decoder as its fallback) restore every page of every size exactly."""
+    monkeypatch.setenv("TYCHE_ZLIB_PAR", par)
+    for plen in (4096, 16384, 32768):
+        pages, streams = _bench_streams(tc, oracle_mod, plen, 24)
+        rv, outs = ragged_inflate(tc, streams, [plen] * len(streams), shift=plen % 7)
+        assert (rv == plen).all() and outs == pages, plen
+
+
+def test_inflate_parallel_corruptions(tc, oracle_mod):
+    """Seeded corruptions of bench streams (byte flips anywhere, flips inside the compressed data,
+    truncations, short capacities) through the lane-parallel kernel: the return value of every
+    stream and the bytes of every success equal the oracle's -- the parallel path hands every page
+    it cannot finish cleanly to the serial decoder, which gives the exact verdict."""
+    rng = np.random.default_rng(5150)
+    pages, streams = _bench_streams(tc, oracle_mod, 16384, 16)
+    cases, caps = [], []
+    for k in range(1500):
+        s = bytearray(streams[k % len(streams)])
+        kind = k % 5
+        if kind == 0:
+            s[int(rng.integers(0, len(s)))] ^= int(rng.integers(1, 256))
+        elif kind == 1:
+            for _ in range(int(rng.integers(1, 4))):
+                s[int(rng.integers(2, len(s) - 4))] ^= 1 << int(rng.integers(0, 8))
+        elif kind == 2:
+            s = s[:int(rng.integers(1, len(s)))]
+        elif kind == 3:
+            s[int(rng.integers(len(s) // 2, len(s)))] = int(rng.integers(0, 256))
+        cases.append(bytes(s))
+        caps.append(16384 if kind != 4 else int(rng.integers(1, 16384)))
+    rv, outs = ragged_inflate(tc, cases, caps)
+    for i, s in enumerate(cases):
+        orv, oout = oracle_mod.zlib_uncompress(s, caps[i])
+        assert rv[i] == orv, (i, i % 5, rv[i], orv)
+        if orv >= 0:
+            assert outs[i] == oout[:orv], i

@@ -69,6 +69,7 @@ __device__ __forceinline__ void st16(uint8_t *p, u128 v) {
     *(g_u32x4_ua *)(uintptr_t)p = __builtin_bit_cast(u32x4, v);
 }
 __device__ __forceinline__ void st16f(uint8_t *p, u128 v) {
+    if (TYCHE_ABLATE & (128 | 256)) return;   // 128: no line flushes, 256: parse only (timing; wrong output)
     if (TYCHE_ABLATE & 32) {
         __builtin_nontemporal_store(__builtin_bit_cast(u32x4, v), (g_u32x4_ua *)(uintptr_t)p);
         return;
@@ -263,6 +264,7 @@ template <int32_t kRing>
 __device__ __forceinline__ u128 ring_rd(uint8_t *rb, int32_t x) { return lds16(rb + ((int32_t)((uint32_t)x % (uint32_t)kRing))); }
 template <int32_t kRing>
 __device__ __forceinline__ void ring_wr(uint8_t *rb, int32_t x, u128 v) {
+    if (TYCHE_ABLATE & 256) return;
     const int32_t q = (int32_t)((uint32_t)x % (uint32_t)kRing);
     lds16(rb + q, v);
     if (q + 16 > kRing) lds16(rb + q - kRing, v);   // wrapped part, to the ring's start
@@ -373,15 +375,15 @@ __device__ int32_t decode_ring(const uint8_t *__restrict__ in, int32_t L, uint8_
         // the unflushed tail is < kLine + 16 bytes here and the ring holds every
         // position above op + 16 - kRing, so a source at offset > kRing - 32
         // (>= 96) is already in HBM and a nearer one is in the ring
-        const bool far = (TYCHE_ABLATE & 64) ? false : off > kRing - 32;   // 64: timing only (far matches read the ring: wrong output)
-        u128 m = far ? ld16(out + op - off) : ring_rd<kRing>(rb, op - off);
+        const bool far = (TYCHE_ABLATE & (64 | 256)) ? false : off > kRing - 32;   // 64: timing only (far matches read the ring: wrong output)
+        u128 m = far ? ld16(out + op - off) : (TYCHE_ABLATE & 256) ? (u128)0 : ring_rd<kRing>(rb, op - off);
         ip += pos;
         w = windowN<kWin>(in, ip, L);
         if (off >= 16) {
             ring_wr<kRing>(rb, op, m);
             for (int32_t k = 16; k < ml; k += 16) {
                 ring_flush<kRing>(rb, out, fl, op + k);
-                m = far ? ld16(out + op + k - off) : ring_rd<kRing>(rb, op + k - off);
+                m = far ? ld16(out + op + k - off) : (TYCHE_ABLATE & 256) ? (u128)0 : ring_rd<kRing>(rb, op + k - off);
                 ring_wr<kRing>(rb, op + k, m);
             }
         } else {

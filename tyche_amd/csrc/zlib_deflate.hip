@@ -419,14 +419,13 @@ __device__ int32_t encode_page(const uint8_t *in, uint32_t L, uint16_t *table, u
     const uint32_t extra = huf::wave_sum(xbits);
     // ---- code lengths (<= 15 bits), fixed-code cost of the same symbols
     uint32_t cll[5], lll[5], cd[1], ld[1];
-    uint32_t totl = 0, fixl = 0, usedl = 0;
+    uint32_t totl = 0, fixl = 0;
 #pragma unroll
     for (int j = 0; j < 5; j++) {
         const uint32_t sv = lane + 64u * (uint32_t)j;
         cll[j] = sv < kLL ? H[sv] : 0u;
         totl += cll[j];
         fixl += cll[j] * (sv < 144u ? 8u : sv < 256u ? 9u : sv < 280u ? 7u : 8u);
-        usedl += cll[j] ? 1u : 0u;
     }
     cd[0] = lane < kDist ? H[320u + lane] : 0u;
     totl = huf::wave_sum(totl);

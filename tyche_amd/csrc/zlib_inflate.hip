@@ -27,6 +27,7 @@
 // decoded length, or -3 (Z_DATA_ERROR) / -5 (Z_BUF_ERROR) at the same point of
 // the stream.
 #include <algorithm>
+#include <cstdlib>
 
 #include "engine.h"
 #include "lds_io.h"
@@ -86,7 +87,12 @@ struct Table {
 };
 
 __device__ __forceinline__ uint32_t lookup(const Table &t, uint32_t idx) {
-    return rdlane(t.root[idx >> 6], idx & 63u);
+    // index a register copy, not the struct: instcombine would turn rt[i] on a plain load back into
+    // an indexed load from the Table's stack slot, which SROA cannot split -- the table then lives
+    // in scratch memory
+    u32x16 rt = t.root;
+    asm volatile("" : "+v"(rt));
+    return rdlane(rt[idx >> 6], idx & 63u);
 }
 
 // Canonical decode of a code longer than the root (the bits are LSB-first in bb).
@@ -175,6 +181,8 @@ __device__ __forceinline__ bool build_table(const uint8_t *lens, uint32_t n, uin
         l_of[r] = l;
         sidx[r] = l <= 10 ? d + (v >> (10 - l)) : 0u;
     }
+    u32x16 rt;   // assembled as a value and stored whole: element stores into t.root get
+                 // merged into sub-vector stores that keep the table out of registers
 #pragma unroll
     for (uint32_t r = 0; r < 16; r++) {
         const uint32_t l = l_of[r];
@@ -182,13 +190,15 @@ __device__ __forceinline__ bool build_table(const uint8_t *lens, uint32_t n, uin
         if (l <= 10) e = sym_entry(table_kind, sorted[sidx[r]]) | l;
         else if (l <= 15) e = mk(kLong, 0, 0);
         else e = mk(kBad, 0, 0);
-        t.root[r] = e;
+        rt[r] = e;
     }
+    t.root = rt;
     return true;
 }
 
 // The fixed codes of RFC 1951 3.2.6, computed per entry.
 __device__ __forceinline__ void fixed_tables(Table &L, Table &D, uint32_t lane) {
+    u32x16 lr, dr;
 #pragma unroll
     for (uint32_t r = 0; r < 16; r++) {
         const uint32_t v = __builtin_bitreverse32(r * kWave + lane) >> 22;
@@ -197,9 +207,11 @@ __device__ __forceinline__ void fixed_tables(Table &L, Table &D, uint32_t lane) 
         else if ((v >> 2) < 192u) { sym = (v >> 2) - 48u; len = 8; }
         else if ((v >> 2) < 200u) { sym = 280u + (v >> 2) - 192u; len = 8; }
         else { sym = 144u + (v >> 1) - 400u; len = 9; }
-        L.root[r] = litlen_entry(sym) | len;
-        D.root[r] = dist_entry(v >> 5) | 5u;
+        lr[r] = litlen_entry(sym) | len;
+        dr[r] = dist_entry(v >> 5) | 5u;
     }
+    L.root = lr;
+    D.root = dr;
     L.lim = D.lim = 0xFFFFFFFFu;
     L.dlt = D.dlt = 0;
 }
@@ -336,10 +348,8 @@ __device__ __forceinline__ uint32_t cl_order(uint32_t i) {
     return (uint32_t)((i < 12 ? lo >> (5 * i) : hi >> (5 * (i - 12))) & 31u);
 }
 
-// Decodes one zlib stream into out (LDS, cap bytes).  Returns the decoded
-// length or kZData / kZBuf, as oracle_zlib_uncompress.
-__device__ __forceinline__ int32_t inflate_page(BitReader &r, const uint8_t *src, uint8_t *out, int32_t cap, uint8_t *lens,
-                                uint16_t *sortL, uint16_t *sortD, uint32_t lane) {
+// zlib header (RFC 1950: CMF/FLG, inflate.c HEAD); 0 or kZData
+__device__ __forceinline__ int32_t zlib_header(BitReader &r, uint32_t lane) {
     refill(r, lane);
     if (r.avail < 16) return kZData;
     const uint32_t cmf = take(r, 8), flg = take(r, 8);
@@ -347,6 +357,80 @@ __device__ __forceinline__ int32_t inflate_page(BitReader &r, const uint8_t *src
     if ((cmf & 15u) != 8u) return kZData;
     if ((cmf >> 4) + 8u > 15u) return kZData;
     if (flg & 0x20u) return kZData;
+    return 0;
+}
+
+// One block header (BFINAL, BTYPE; inflate.c TYPE/TABLE/LENLENS/CODELENS).
+// Returns 1 for a stored block (reader just past BTYPE), 0 when L and D hold
+// the block's fixed or dynamic codes, kZData on error.
+__device__ __forceinline__ int32_t block_head(BitReader &r, uint32_t &last, Table &L, Table &D, uint8_t *lens,
+                                              uint16_t *sortL, uint16_t *sortD, uint32_t lane) {
+    refill(r, lane);
+    if (r.avail < 3) return kZData;
+    last = take(r, 1);
+    const uint32_t type = take(r, 2);
+    if (type == 0) return 1;
+    if (type == 3) return kZData;
+    if (type == 1) {
+        fixed_tables(L, D, lane);
+        return 0;
+    }
+    refill(r, lane);
+    if (r.avail < 14) return kZData;
+    const uint32_t nlen = take(r, 5) + 257u, ndist = take(r, 5) + 1u, ncode = take(r, 4) + 4u;
+    if (nlen > 286u || ndist > 30u) return kZData;
+    if (r.avail < (int32_t)(3u * ncode)) return kZData;
+    uint32_t clv = 0;
+    for (uint32_t i = 0; i < ncode; i++) {
+        refill(r, lane);
+        clv = put_lane(clv, cl_order(i), take(r, 3), lane);
+    }
+    if (lane < 19u) lens[lane] = (uint8_t)clv;
+    if (!build_table(lens, 19, 0, L, sortL, lane)) return kZData;
+    const uint32_t total = nlen + ndist;
+    uint32_t n = 0, prev = 0;
+    while (n < total) {
+        refill(r, lane);
+        const uint32_t e = lookup(L, (uint32_t)r.bb & 1023u);
+        const uint32_t l = e_len(e);
+        if (e_kind(e) != kLit || (int32_t)l > r.avail) return kZData;
+        take(r, l);
+        const uint32_t sym = e_val(e);
+        if (sym < 16u) {
+            if (lane == 0) lens[n] = (uint8_t)sym;
+            prev = sym;
+            n++;
+            continue;
+        }
+        uint32_t rep, val = 0;
+        if (sym == 16u) {
+            if (n == 0) return kZData;
+            if (r.avail < 2) return kZData;
+            val = prev;
+            rep = 3u + take(r, 2);
+        } else if (sym == 17u) {
+            if (r.avail < 3) return kZData;
+            rep = 3u + take(r, 3);
+        } else {
+            if (r.avail < 7) return kZData;
+            rep = 11u + take(r, 7);
+        }
+        if (n + rep > total) return kZData;
+        for (uint32_t j = lane; j < rep; j += kWave) lens[n + j] = (uint8_t)val;
+        prev = val;
+        n += rep;
+    }
+    if (rfl(lens[256]) == 0) return kZData;
+    if (!build_table(lens, nlen, 1, L, sortL, lane)) return kZData;
+    if (!build_table(lens + nlen, ndist, 2, D, sortD, lane)) return kZData;
+    return 0;
+}
+
+// Decodes one zlib stream into out (LDS, cap bytes).  Returns the decoded
+// length or kZData / kZBuf, as oracle_zlib_uncompress.
+__device__ __forceinline__ int32_t inflate_page(BitReader &r, const uint8_t *src, uint8_t *out, int32_t cap, uint8_t *lens,
+                                uint16_t *sortL, uint16_t *sortD, uint32_t lane) {
+    if (zlib_header(r, lane)) return kZData;
     Table L, D;
     Pending q;
     q.lit = q.md = q.mx = 0;
@@ -354,11 +438,9 @@ __device__ __forceinline__ int32_t inflate_page(BitReader &r, const uint8_t *src
     int32_t op = 0;
     uint32_t last;
     do {
-        refill(r, lane);
-        if (r.avail < 3) return kZData;
-        last = take(r, 1);
-        const uint32_t type = take(r, 2);
-        if (type == 0) {
+        const int32_t hr = block_head(r, last, L, D, lens, sortL, sortD, lane);
+        if (hr < 0) return hr;
+        if (hr == 1) {
             // stored block (inflate.c STORED/COPY)
             take(r, r.bc & 7u);
             refill(r, lane);
@@ -374,59 +456,6 @@ __device__ __forceinline__ int32_t inflate_page(BitReader &r, const uint8_t *src
             r.avail -= (int32_t)(len * 8u);
             seek(r, P + len, lane);
             continue;
-        }
-        if (type == 3) return kZData;
-        if (type == 1) {
-            fixed_tables(L, D, lane);
-        } else {
-            refill(r, lane);
-            if (r.avail < 14) return kZData;
-            const uint32_t nlen = take(r, 5) + 257u, ndist = take(r, 5) + 1u, ncode = take(r, 4) + 4u;
-            if (nlen > 286u || ndist > 30u) return kZData;
-            if (r.avail < (int32_t)(3u * ncode)) return kZData;
-            uint32_t clv = 0;
-            for (uint32_t i = 0; i < ncode; i++) {
-                refill(r, lane);
-                clv = put_lane(clv, cl_order(i), take(r, 3), lane);
-            }
-            if (lane < 19u) lens[lane] = (uint8_t)clv;
-            if (!build_table(lens, 19, 0, L, sortL, lane)) return kZData;
-            const uint32_t total = nlen + ndist;
-            uint32_t n = 0, prev = 0;
-            while (n < total) {
-                refill(r, lane);
-                const uint32_t e = lookup(L, (uint32_t)r.bb & 1023u);
-                const uint32_t l = e_len(e);
-                if (e_kind(e) != kLit || (int32_t)l > r.avail) return kZData;
-                take(r, l);
-                const uint32_t sym = e_val(e);
-                if (sym < 16u) {
-                    if (lane == 0) lens[n] = (uint8_t)sym;
-                    prev = sym;
-                    n++;
-                    continue;
-                }
-                uint32_t rep, val = 0;
-                if (sym == 16u) {
-                    if (n == 0) return kZData;
-                    if (r.avail < 2) return kZData;
-                    val = prev;
-                    rep = 3u + take(r, 2);
-                } else if (sym == 17u) {
-                    if (r.avail < 3) return kZData;
-                    rep = 3u + take(r, 3);
-                } else {
-                    if (r.avail < 7) return kZData;
-                    rep = 11u + take(r, 7);
-                }
-                if (n + rep > total) return kZData;
-                for (uint32_t j = lane; j < rep; j += kWave) lens[n + j] = (uint8_t)val;
-                prev = val;
-                n += rep;
-            }
-            if (rfl(lens[256]) == 0) return kZData;
-            if (!build_table(lens, nlen, 1, L, sortL, lane)) return kZData;
-            if (!build_table(lens + nlen, ndist, 2, D, sortD, lane)) return kZData;
         }
         // ---- compressed data (inflate.c LEN/DIST; inffast.c)
         for (;;) {
@@ -474,6 +503,287 @@ __device__ __forceinline__ int32_t inflate_page(BitReader &r, const uint8_t *src
     const uint32_t want = __builtin_bswap32(take(r, 32));
     flush_literals(q, out, lane);
     flush_matches(q, out, lane);
+    if (lds_adler32(out, (uint32_t)op, lane) != want) return kZData;
+    return op;
+}
+
+// ------------------------------------------------- lane-parallel block decode
+// inflate_par: the latency path.  The serial decoder above spends ~1.3 ms of
+// one wave on a 16 KiB page (one Huffman symbol after another, every step a
+// chain of scalar/readlane dependencies); a restore that waits for its page
+// waits for that.  Here the 64 lanes decode the block's symbol stream
+// together, the way lz4_decode.hip splits LZ4's token chain:
+//   1. the stream is staged in LDS and its bits cut into 64 segments (32-bit
+//      aligned); lane k decodes compound symbols (a literal, or length +
+//      distance with their extra bits, or end-of-block) from the start of its
+//      segment to its end, setting the bit of every symbol start in a bitmap
+//      (V).  Only lane 0 starts at a true symbol boundary; a Huffman code
+//      resynchronises after a few symbols, so the others usually join the
+//      true chain quickly;
+//   2. from its exit each lane keeps decoding ("bridge") until it reaches a
+//      bit set by a later lane, end-of-block, an invalid code or the stream end;
+//   3. the true chain is lane 0's walk followed by the hand-offs (<= 64 steps of
+//      scalar code), which gives every on-chain lane its entry;
+//   4. on-chain lanes re-decode entry -> hand-off to count output bytes; a
+//      prefix sum places them; a third pass writes literals and leaves each
+//      match's (distance, length) in the first three bytes of its own output
+//      range, marking its start in a second bitmap (M);
+//   5. after the last block the matches are applied in order, 64 at a time,
+//      with the serial path's frontier-grouped copy (flush_matches).
+// Anything the happy path does not cover -- an invalid code or a stream that
+// ends early on the true chain, a distance beyond the output, output past the
+// capacity, stored blocks, a stream longer than the staging area -- returns
+// kFallback and the page is decoded again by inflate_page, so results and
+// error verdicts are exactly the serial decoder's.
+constexpr int32_t kFallback = INT32_MIN + 1;
+
+struct ParTabs {
+    const uint32_t *LT, *DT;          // 1024-entry root tables (LDS), entry format of Table
+    const uint16_t *sortL, *sortD;    // sorted symbols (slow path)
+    uint32_t limL[5], dltL[5], limD[5], dltD[5];   // lengths 11..15
+};
+
+__device__ __forceinline__ uint32_t peek32(const uint32_t *S32, uint32_t p) {
+    const uint32_t i = p >> 5;
+    return __builtin_amdgcn_alignbit(S32[i + 1], S32[i], p & 31u);
+}
+
+// per-lane canonical decode of a code longer than 10 bits (slow_entry's rule)
+__device__ __forceinline__ uint32_t slow_lane(const uint32_t *lim, const uint32_t *dlt, const uint16_t *sorted,
+                                              uint32_t table_kind, uint32_t w) {
+    const uint32_t v15 = __builtin_bitreverse32(w) >> 17;
+    if (v15 >= lim[4]) return mk(kBad, 0, 0);
+    const uint32_t i = (uint32_t)(v15 >= lim[0]) + (uint32_t)(v15 >= lim[1]) + (uint32_t)(v15 >= lim[2]) +
+                       (uint32_t)(v15 >= lim[3]);
+    const uint32_t l = 11u + i;
+    const uint32_t d = i == 0 ? dlt[0] : i == 1 ? dlt[1] : i == 2 ? dlt[2] : i == 3 ? dlt[3] : dlt[4];
+    return sym_entry(table_kind, sorted[d + (v15 >> (15u - l))]) | l;
+}
+
+enum : uint32_t { kSymLit = 0, kSymMatch = 1, kSymEob = 2, kSymBad = 3 };
+
+// one compound symbol at bit p: a literal (val = byte), a match (val =
+// length, dist), end-of-block, or an invalid code; advances p
+__device__ __forceinline__ uint32_t par_sym(const ParTabs &t, const uint32_t *S32, uint32_t &p, uint32_t &val,
+                                            uint32_t &dist) {
+    uint32_t w = peek32(S32, p);
+    uint32_t e = t.LT[w & 1023u];
+    if (e_kind(e) == kLong) e = slow_lane(t.limL, t.dltL, t.sortL, 1, w);
+    const uint32_t l = e_len(e), k = e_kind(e);
+    if (k == kLit) {
+        p += l;
+        val = e_val(e);
+        return kSymLit;
+    }
+    if (k == kEob) {
+        p += l;
+        return kSymEob;
+    }
+    if (k != kLen) return kSymBad;
+    const uint32_t x = e_extra(e);
+    val = e_val(e) + ((w >> l) & ((1u << x) - 1u));
+    p += l + x;
+    w = peek32(S32, p);
+    e = t.DT[w & 1023u];
+    if (e_kind(e) == kLong) e = slow_lane(t.limD, t.dltD, t.sortD, 2, w);
+    if (e_kind(e) != kLen) return kSymBad;
+    const uint32_t l2 = e_len(e), x2 = e_extra(e);
+    dist = e_val(e) + ((w >> l2) & ((1u << x2) - 1u));
+    p += l2 + x2;
+    return kSymMatch;
+}
+
+__device__ __forceinline__ void par_tables(ParTabs &t, const Table &L, const Table &D, uint32_t *LT, uint32_t *DT,
+                                           const uint16_t *sortL, const uint16_t *sortD, uint32_t lane) {
+#pragma unroll
+    for (uint32_t r = 0; r < 16; r++) {
+        LT[r * kWave + lane] = L.root[r];
+        DT[r * kWave + lane] = D.root[r];
+    }
+    t.LT = LT;
+    t.DT = DT;
+    t.sortL = sortL;
+    t.sortD = sortD;
+#pragma unroll
+    for (uint32_t i = 0; i < 5; i++) {
+        t.limL[i] = rdlane(L.lim, 11 + i);
+        t.dltL[i] = rdlane(L.dlt, 11 + i);
+        t.limD[i] = rdlane(D.lim, 11 + i);
+        t.dltD[i] = rdlane(D.dlt, 11 + i);
+    }
+}
+
+// Decodes one block's symbols [P0, end-of-block) of the staged stream (bit
+// positions in stage coordinates, E = stream end) into out at op.  Returns the
+// new output length and the bit position after end-of-block (yend), or
+// kFallback.  V: bitmap scratch inside the output window (out + vo, above op);
+// M: match-start bitmap.
+__device__ __forceinline__ int32_t par_block(const ParTabs &t, const uint32_t *S32, uint32_t P0, uint32_t E, uint8_t *out, int32_t op,
+                             int32_t cap, uint32_t W, uint32_t *M, uint32_t lane, uint32_t &yend) {
+    if (P0 >= E) return kFallback;
+    const uint32_t base = P0 & ~31u;
+    const uint32_t S = ((E - base + kWave - 1) / kWave + 31u) & ~31u;   // bits per segment
+    const uint32_t nv = (E - base + 31u) / 32u + 1u;                        // bitmap words
+    const uint32_t vo = ((uint32_t)op + 3u) & ~3u;
+    if (vo + 4u * nv > W) return kFallback;
+    uint32_t *V = (uint32_t *)(out + vo);
+    for (uint32_t w = lane; w < nv; w += kWave) V[w] = 0;
+    WAVE_SYNC();
+    // 1. walk the own segment
+    const uint32_t a = base + lane * S, b = min(a + S, E);
+    uint32_t y = lane == 0 ? P0 : a, stop = 0, val, dist;
+    if (a < E) {
+        while (y < b) {
+            atomicOr(&V[(y - base) >> 5], 1u << (y & 31u));
+            const uint32_t k = par_sym(t, S32, y, val, dist);
+            if (k >= kSymEob) {
+                stop = k;
+                break;
+            }
+        }
+    }
+    WAVE_SYNC();
+    // 2. bridge to a later lane's walk
+    uint32_t o = 0;   // owner lane + 1 of the hand-off position, 0 = chain ends here
+    if (a < E && stop == 0) {
+        while (y < E) {
+            if ((V[(y - base) >> 5] >> (y & 31u)) & 1u) {
+                o = (y - base) / S + 1u;
+                break;
+            }
+            const uint32_t k = par_sym(t, S32, y, val, dist);
+            if (k >= kSymEob) {
+                stop = k;
+                break;
+            }
+        }
+    }
+    // 3. follow the hand-offs from lane 0
+    uint32_t entry = 0xFFFFFFFFu;
+    uint32_t cur = 0, e = P0;
+    for (uint32_t it = 0; it < kWave; it++) {
+        if (lane == cur) entry = e;
+        e = rdlane(y, cur);
+        const uint32_t nx = rdlane(o, cur);
+        if (nx == 0) break;
+        cur = nx - 1;
+    }
+    if (rdlane(stop, cur) != kSymEob || e > E) return kFallback;
+    yend = e;
+    // 4. count, place, write
+    const bool on = entry != 0xFFFFFFFFu;
+    uint32_t nout = 0;
+    if (on) {
+        for (uint32_t q = entry; q < y;) {
+            const uint32_t k = par_sym(t, S32, q, val, dist);
+            if (k == kSymLit) nout++;
+            else if (k == kSymMatch) nout += val;
+            else break;
+        }
+    }
+    const int32_t incl = wave_incl_sum((int32_t)nout);
+    const int32_t total = op + (int32_t)rdlane((uint32_t)incl, kWave - 1);
+    if (total > cap) return kFallback;
+    WAVE_SYNC();   // V is dead from here on; the output overwrites it
+    bool bad = false;
+    if (on) {
+        uint32_t o2 = (uint32_t)(op + incl) - nout;
+        for (uint32_t q = entry; q < y;) {
+            const uint32_t k = par_sym(t, S32, q, val, dist);
+            if (k == kSymLit) {
+                out[o2++] = (uint8_t)val;
+            } else if (k == kSymMatch) {
+                if (dist > o2) bad = true;
+                out[o2] = (uint8_t)dist;
+                out[o2 + 1] = (uint8_t)(dist >> 8);
+                out[o2 + 2] = (uint8_t)(val - 3u);
+                atomicOr(&M[o2 >> 5], 1u << (o2 & 31u));
+                o2 += val;
+            } else {
+                break;
+            }
+        }
+    }
+    if (__ballot(bad)) return kFallback;
+    return total;
+}
+
+// Applies the matches recorded by par_block, in output order.  pos: scratch
+// for one chunk's match positions (<= 683 u16).
+__device__ __forceinline__ void par_matches(uint8_t *out, uint32_t total, const uint32_t *M, uint16_t *pos, uint32_t lane) {
+    const uint32_t nw = (total + 31u) >> 5;
+    Pending q;
+    q.lit = 0;
+    q.nlit = 0;
+    for (uint32_t w0 = 0; w0 < nw; w0 += kWave) {
+        uint32_t word = w0 + lane < nw ? M[w0 + lane] : 0u;
+        const uint32_t c = (uint32_t)__builtin_popcount(word);
+        const int32_t incl = wave_incl_sum((int32_t)c);
+        const uint32_t T = rdlane((uint32_t)incl, kWave - 1);
+        uint32_t at = (uint32_t)incl - c;
+        while (word) {
+            const uint32_t bit = (uint32_t)__builtin_ctz(word);
+            word &= word - 1u;
+            pos[at++] = (uint16_t)((w0 + lane) * 32u + bit);
+        }
+        WAVE_SYNC();
+        for (uint32_t i0 = 0; i0 < T; i0 += kWave) {
+            const uint32_t n = min(T - i0, kWave);
+            uint32_t d = 0, dist = 0, len = 0;
+            if (lane < n) {
+                d = pos[i0 + lane];
+                dist = (uint32_t)out[d] | ((uint32_t)out[d + 1] << 8);
+                len = (uint32_t)out[d + 2] + 3u;
+            }
+            q.md = d;
+            q.mx = dist | (len << 16);
+            q.nmat = n;
+            WAVE_SYNC();
+            flush_matches(q, out, lane);
+            WAVE_SYNC();
+        }
+    }
+}
+
+__device__ __forceinline__ void seek_bits(BitReader &r, uint32_t bitpos, uint32_t src_len, uint32_t lane) {
+    seek(r, bitpos >> 3, lane);
+    r.avail = (int32_t)(src_len * 8u - (bitpos & ~7u));
+    refill(r, lane);
+    take(r, bitpos & 7u);
+}
+
+// The page's stream is staged at stage + head (head = src & 15), zero-padded.
+// Returns the decoded length, kZData, or kFallback.
+__device__ __forceinline__ int32_t inflate_par(BitReader &r, const PageRef &p, const uint8_t *stage, uint32_t head, uint8_t *out,
+                               int32_t cap, uint32_t W, uint32_t *M, uint32_t *LT, uint32_t *DT, uint8_t *lens,
+                               uint16_t *sortL, uint16_t *sortD, uint32_t lane) {
+    if (zlib_header(r, lane)) return kFallback;
+    const uint32_t *S32 = (const uint32_t *)stage;
+    const uint32_t h8 = head * 8u, E = h8 + p.src_len * 8u;
+    for (uint32_t w = lane; w < ((uint32_t)cap + 31u) / 32u; w += kWave) M[w] = 0;
+    int32_t op = 0;
+    uint32_t last = 0, yend = 0;
+    Table L, D;
+    do {
+        const int32_t hr = block_head(r, last, L, D, lens, sortL, sortD, lane);
+        if (hr != 0) return kFallback;   // errors and stored blocks: the serial decoder
+        ParTabs t;
+        par_tables(t, L, D, LT, DT, sortL, sortD, lane);
+        WAVE_SYNC();
+        const uint32_t P0 = h8 + (uint32_t)p.src_len * 8u - (uint32_t)r.avail;
+        op = par_block(t, S32, P0, E, out, op, cap, W, M, lane, yend);
+        if (op < 0) return kFallback;
+        WAVE_SYNC();
+        if (!last) seek_bits(r, yend - h8, p.src_len, lane);
+    } while (!last);
+    // adler32 trailer: big-endian, byte aligned after the last block
+    const uint32_t tb = (yend - h8 + 7u) >> 3;
+    if (tb + 4u > p.src_len) return kFallback;
+    const uint8_t *tp = stage + head + tb;
+    const uint32_t want = ((uint32_t)tp[0] << 24) | ((uint32_t)tp[1] << 16) | ((uint32_t)tp[2] << 8) | tp[3];
+    WAVE_SYNC();
+    par_matches(out, (uint32_t)op, M, (uint16_t *)stage, lane);   // the stage is free now
+    WAVE_SYNC();
     if (lds_adler32(out, (uint32_t)op, lane) != want) return kZData;
     return op;
 }
@@ -535,11 +845,85 @@ __global__ __launch_bounds__(64) void zlib_inflate_kernel(tyche_batch_t b, uint3
     }
 }
 
+// The latency kernel: inflate_par per page (stream staged in LDS), the serial
+// decoder when it falls back.  LDS: output window | lens/sorted | LT | DT | M |
+// stage.
+__global__ __launch_bounds__(64) void zlib_inflate_par_kernel(tyche_batch_t b, uint32_t out_cap, uint32_t off_lens,
+                                                              uint32_t off_lt, uint32_t off_m, uint32_t off_stage,
+                                                              uint32_t stage_cap, unsigned *ctr) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint32_t lane = threadIdx.x;
+    uint8_t *out = smem;
+    uint8_t *lens = smem + off_lens;
+    uint16_t *sortL = (uint16_t *)(lens + 320);
+    uint16_t *sortD = sortL + 320;
+    uint32_t *LT = (uint32_t *)(smem + off_lt);
+    uint32_t *DT = LT + 1024;
+    uint32_t *M = (uint32_t *)(smem + off_m);
+    uint8_t *stage = smem + off_stage;
+    size_t page = blockIdx.x;
+    while (page < b.count) {
+        const PageRef p = batch_page(b, page);
+        int32_t rv;
+        if (p.dst_cap > out_cap || p.src_len > 0x0FFFFFFFu) {
+            rv = kResultTooLarge;
+        } else {
+            rv = kFallback;
+            const uint32_t head = (uint32_t)((uintptr_t)p.src & 15u);
+            if (head + p.src_len + 48u <= stage_cap) {
+                stage_in(p.src, p.src_len, stage, lane, kWave);
+                // zero the 32 bytes after the stream (symbol reads run past its end)
+                if (lane < 8u) lds_st32(stage + ((head + p.src_len + 15u) & ~15u) + 4u * lane, 0u);
+                WAVE_SYNC();
+                BitReader r;
+                reader_init(r, p, lane);
+                r.wa = load_win(r, 0, lane);
+                r.wb = load_win(r, 256, lane);
+                rv = inflate_par(r, p, stage, head, out, (int32_t)p.dst_cap, off_lens, M, LT, DT, lens, sortL, sortD,
+                                 lane);
+                WAVE_SYNC();
+            }
+            if (rv == kFallback) {
+                BitReader r;
+                reader_init(r, p, lane);
+                r.wa = load_win(r, 0, lane);
+                r.wb = load_win(r, 256, lane);
+                rv = inflate_page(r, p.src, out, (int32_t)p.dst_cap, lens, sortL, sortD, lane);
+                WAVE_SYNC();
+            }
+            if (rv > 0) stage_out(p.dst, out, (uint32_t)rv, lane, kWave);
+        }
+        if (lane == 0) b.results[page] = rv;
+        WAVE_SYNC();
+        page = claim_page(ctr, lane);
+    }
+}
+
 }  // namespace
 
+// TYCHE_ZLIB_PAR: 1 (default) the lane-parallel kernel, 0 the serial one (A/B timing)
 hipError_t launch_zlib_inflate(const tyche_batch_t &b, uint32_t out_cap, hipStream_t s) {
     if (b.count == 0) return hipSuccess;
+    const char *env = getenv("TYCHE_ZLIB_PAR");   // read per call: the parity tests switch it in-process
+    const int par = env ? atoi(env) : 1;
     const uint32_t off_lens = (out_cap + 64u + 15u) & ~15u;
+    if (par && out_cap <= 65535u) {
+        const uint32_t off_lt = (off_lens + 320u + 2u * 320u + 2u * 32u + 15u) & ~15u;
+        const uint32_t off_m = off_lt + 2u * 4096u;
+        const uint32_t off_stage = off_m + ((((out_cap + 31u) / 32u) * 4u + 15u) & ~15u);
+        const uint32_t stage_cap = (std::max(2048u, out_cap / 2u) + 63u) & ~15u;
+        const size_t lds = (size_t)off_stage + stage_cap;
+        if (lds <= 160 * 1024) {
+            const size_t ncu = prepare_launch((const void *)zlib_inflate_par_kernel);
+            const size_t per_cu = waves_per_cu((const void *)zlib_inflate_par_kernel, lds);
+            const size_t grid = std::min<size_t>(b.count, ncu * per_cu);
+            WorkCounter ctr(s);
+            if (!ctr.get()) return hipErrorOutOfMemory;
+            hipLaunchKernelGGL(zlib_inflate_par_kernel, dim3((unsigned)grid), dim3(kWave), lds, s, b, out_cap,
+                               off_lens, off_lt, off_m, off_stage, stage_cap, ctr.get());
+            return hipGetLastError();
+        }
+    }
     const size_t lds = off_lens + 320 + 2 * 320 + 2 * 32;
     if (lds > 160 * 1024) return hipErrorInvalidValue;
     const size_t ncu = prepare_launch((const void *)zlib_inflate_kernel);
