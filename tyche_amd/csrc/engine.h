@@ -88,9 +88,14 @@ hipError_t launch_zstd_decode(const tyche_batch_t &b, uint32_t in_cap, uint32_t 
 // launch call, as an event recorded on s -- the counter is handed out again
 // only once that event has completed, i.e. once the kernel that claims pages
 // from it has finished, whatever stream or thread asks next.
+//
+// claims = false: the launch's grid covers all its pages, so no wave ever claims
+// one (every claim returns >= gridDim.x >= count whatever the counter holds):
+// the counter is a shared scratch word, with no memset and no event -- two
+// fewer stream operations on the small-batch latency path.
 class WorkCounter {
   public:
-    explicit WorkCounter(hipStream_t s);
+    explicit WorkCounter(hipStream_t s, bool claims = true);
     ~WorkCounter();
     WorkCounter(const WorkCounter &) = delete;
     WorkCounter &operator=(const WorkCounter &) = delete;

@@ -50,16 +50,25 @@ struct CounterPool {
     std::mutex mu;
     std::vector<Entry> e;
     size_t cursor = 0;
+    unsigned *junk = nullptr;   // shared by launches whose grid covers all their pages
 };
 CounterPool g_counters[kMaxDevices];
 constexpr size_t kCounterBlock = 64;
 }  // namespace
 
-tyche::WorkCounter::WorkCounter(hipStream_t s) : s_(s) {
+tyche::WorkCounter::WorkCounter(hipStream_t s, bool claims) : s_(s) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return;
     CounterPool &P = g_counters[dev];
     std::lock_guard<std::mutex> g(P.mu);
+    if (!claims) {
+        // the grid covers every page: each claim returns >= gridDim.x >= count whatever the
+        // counter holds, so one shared, never-reset counter serves every such launch (no
+        // memset on the stream, no event)
+        if (!P.junk && hipMalloc((void **)&P.junk, sizeof(unsigned)) != hipSuccess) P.junk = nullptr;
+        p_ = P.junk;
+        return;
+    }
     const size_t n = P.e.size();
     size_t take = n;
     for (size_t k = 0; k < n; k++) {   // from the oldest release on: those are done first
@@ -316,6 +325,7 @@ inline uint32_t decode_in_cap(const tyche_batch_t &b, uint32_t fallback) {
 // bounded however many threads call in.
 struct Arena {
     void *p = nullptr;
+    void *dp = nullptr;   // host arenas: the device's address of the pinned buffer (zero-copy launches)
     size_t cap = 0;
     bool host = false;
     int grow(size_t need) {
@@ -328,6 +338,7 @@ struct Arena {
             p = nullptr;
             return fail(host ? "hipHostMalloc" : "hipMalloc", e);
         }
+        if (host && hipHostGetDevicePointer(&dp, p, 0) != hipSuccess) dp = nullptr;
         cap = n;
         return TYCHE_E_OK;
     }
@@ -335,7 +346,7 @@ struct Arena {
         if (p) {
             if (host) (void)hipHostFree(p); else (void)hipFree(p);
         }
-        p = nullptr;
+        p = dp = nullptr;
         cap = 0;
     }
 };
@@ -354,6 +365,7 @@ struct Slot {
 
 struct HostCtx {
     Slot slot[kSlots];
+    int group = 0;   // hardware-queue group of slot 0's stream (see acquire_ctx)
     // waits for whatever the slots still hold and forgets it (error paths)
     void abandon() {
         for (Slot &s : slot)
@@ -368,8 +380,27 @@ struct CtxPool {
     std::mutex mu;
     std::condition_variable cv;
     std::vector<HostCtx *> all, idle;
+    std::vector<int> busy;   // leased contexts per hardware-queue group
 };
 CtxPool g_ctx[kMaxDevices];
+
+// HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default), in
+// creation order; kernels of streams that share a queue run one after the
+// other (tools/probes/hwq.hip: with 24 streams, stream 0 overlaps streams
+// 1-6 but serializes with 7, 11, 15, ...).  Two restore batches (an LZ4 and a
+// zlib one, say) on contexts whose streams share a queue therefore wait for
+// each other.  So a device's contexts are created together, their streams in
+// an order that puts slot s of context i in group (i + s) mod Q -- the three
+// slots of one context on three queues, for the chunk pipeline -- and a call
+// borrows the idle context whose group has the fewest calls running.
+int hw_queues() {
+    static const int q = [] {
+        const char *env = getenv("GPU_MAX_HW_QUEUES");
+        const int v = env ? atoi(env) : 4;
+        return v > 0 ? v : 4;
+    }();
+    return q;
+}
 
 int context_cap() {
     static const int cap = [] {
@@ -380,34 +411,61 @@ int context_cap() {
     return cap;
 }
 
+// creates the device's contexts (under P.mu): stream k created goes to queue
+// group k mod Q, and is given to the (context, slot) pair of that group
+int create_contexts(CtxPool &P) {
+    const int n = context_cap(), Q = hw_queues();
+    std::vector<HostCtx *> cs;
+    for (int i = 0; i < n; i++) {
+        cs.push_back(new HostCtx);
+        cs.back()->group = i % Q;
+    }
+    std::vector<bool> made((size_t)n * kSlots, false);
+    for (int k = 0; k < n * kSlots; k++) {
+        int pick = -1;
+        for (int j = 0; j < n * kSlots && pick < 0; j++)
+            if (!made[j] && ((j / kSlots) + (j % kSlots)) % Q == k % Q) pick = j;
+        for (int j = 0; j < n * kSlots && pick < 0; j++)
+            if (!made[j]) pick = j;
+        made[pick] = true;
+        hipError_t e = hipStreamCreateWithFlags(&cs[pick / kSlots]->slot[pick % kSlots].stream, hipStreamNonBlocking);
+        if (e != hipSuccess) {
+            for (HostCtx *c : cs) {
+                for (Slot &t : c->slot)
+                    if (t.stream) (void)hipStreamDestroy(t.stream);
+                delete c;
+            }
+            return fail("hipStreamCreate", e);
+        }
+    }
+    P.all = cs;
+    P.idle = cs;
+    P.busy.assign((size_t)Q, 0);
+    return TYCHE_E_OK;
+}
+
 // borrows a staging context of device dev (current on this thread); waits while all are busy
 int acquire_ctx(int dev, HostCtx **out) {
     CtxPool &P = g_ctx[dev];
     std::unique_lock<std::mutex> g(P.mu);
-    P.cv.wait(g, [&] { return !P.idle.empty() || (int)P.all.size() < context_cap(); });
-    if (!P.idle.empty()) {
-        *out = P.idle.back();
-        P.idle.pop_back();
-        return TYCHE_E_OK;
+    if (P.all.empty()) {
+        const int rc = create_contexts(P);
+        if (rc) return rc;
     }
-    HostCtx *c = new HostCtx;
-    for (Slot &s : c->slot) {
-        hipError_t e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
-        if (e != hipSuccess) {
-            for (Slot &t : c->slot)
-                if (t.stream) (void)hipStreamDestroy(t.stream);
-            delete c;
-            return fail("hipStreamCreate", e);
-        }
-    }
-    P.all.push_back(c);
-    *out = c;
+    P.cv.wait(g, [&] { return !P.idle.empty(); });
+    size_t best = 0;
+    for (size_t k = 1; k < P.idle.size(); k++)
+        if (P.busy[(size_t)P.idle[k]->group] < P.busy[(size_t)P.idle[best]->group]) best = k;
+    *out = P.idle[best];
+    P.idle.erase(P.idle.begin() + (long)best);
+    P.busy[(size_t)(*out)->group]++;
     return TYCHE_E_OK;
 }
 void release_ctx(int dev, HostCtx *c) {
     CtxPool &P = g_ctx[dev];
     {
         std::lock_guard<std::mutex> g(P.mu);
+        P.busy[(size_t)c->group]--;
         P.idle.push_back(c);
     }
     P.cv.notify_one();
@@ -509,9 +567,25 @@ std::atomic<int> g_inflight[kMaxDevices];   // host batches running per device
 // (0, dst_cap[i]] that many output bytes land in dst[i].  On any failure the
 // context's slots are drained before it goes back to the pool, so a later call
 // never scatters a failed call's chunk.
+// Zero-copy limit: a decompress batch of at most this many bytes (input plus
+// output capacity) skips the device staging buffers -- the kernel reads the
+// gathered streams and the page table from the pinned host arenas and writes
+// results and pages straight back into them.  No H2D/D2H copies (two
+// hipMemcpyAsync calls and two copy kernels each way saved on the restore
+// path's small batches); the kernels stage their input in LDS with 16-byte
+// loads and write whole 16-byte vectors, which PCIe carries well.
+// TYCHE_ZERO_COPY_BYTES=0 turns it off.
+size_t zero_copy_bytes() {
+    static const size_t v = [] {
+        const char *env = getenv("TYCHE_ZERO_COPY_BYTES");
+        return env ? (size_t)strtoull(env, nullptr, 10) : (size_t)(4u << 20);
+    }();
+    return v;
+}
+
 template <typename Launch>
 int run_host_batch(int dev, size_t n, const void *const *src, const uint32_t *src_len, void *const *dst,
-                   const uint32_t *dst_cap, int32_t *results, Launch launch) {
+                   const uint32_t *dst_cap, int32_t *results, Launch launch, bool zc_ok = false) {
     int rc = ensure_device(dev);
     if (rc) return rc;
     struct Inflight {
@@ -547,6 +621,70 @@ int run_host_batch(int dev, size_t n, const void *const *src, const uint32_t *sr
         });
         return TYCHE_E_OK;
     };
+
+    if (zc_ok) {
+        size_t in_bytes = 0, out_bytes = 0;
+        uint32_t max_in = 0, max_out = 0;
+        for (size_t j = 0; j < n; j++) {
+            in_bytes += up16(src_len[j]);
+            out_bytes += up16(dst_cap[j]);
+            max_in = std::max(max_in, src_len[j]);
+            max_out = std::max(max_out, dst_cap[j]);
+        }
+        if (in_bytes + out_bytes <= zero_copy_bytes()) {
+            Slot &S = c.slot[0];
+            const size_t meta_bytes = n * 28 + 64;
+            if ((rc = S.h_in.grow(in_bytes + 16)) || (rc = S.h_out.grow(out_bytes + 16)) ||
+                (rc = S.h_meta.grow(meta_bytes)))
+                return bail(rc);
+            if (S.h_in.dp && S.h_out.dp && S.h_meta.dp) {
+                uint64_t *m_soff = (uint64_t *)S.h_meta.p;
+                uint64_t *m_doff = m_soff + n;
+                uint32_t *m_slen = (uint32_t *)(m_doff + n);
+                uint32_t *m_dcap = m_slen + n;
+                int32_t *m_res = (int32_t *)(m_dcap + n);
+                size_t so = 0, dof = 0;
+                for (size_t j = 0; j < n; j++) {
+                    m_soff[j] = so;
+                    m_doff[j] = dof;
+                    m_slen[j] = src_len[j];
+                    m_dcap[j] = dst_cap[j];
+                    so += up16(src_len[j]);
+                    dof += up16(dst_cap[j]);
+                }
+                uint8_t *hin = (uint8_t *)S.h_in.p;
+                pool.run(n, [&](size_t j) {
+                    if (m_slen[j]) memcpy(hin + m_soff[j], src[j], m_slen[j]);
+                });
+                uint8_t *dm = (uint8_t *)S.h_meta.dp;
+                tyche_batch_t b{};
+                b.count = n;
+                b.src = S.h_in.dp;
+                b.src_offsets = (const uint64_t *)dm;
+                b.src_lengths = (const uint32_t *)(dm + ((uint8_t *)m_slen - (uint8_t *)m_soff));
+                b.max_src_length = max_in;
+                b.dst = S.h_out.dp;
+                b.dst_offsets = (const uint64_t *)(dm + ((uint8_t *)m_doff - (uint8_t *)m_soff));
+                b.dst_capacities = (const uint32_t *)(dm + ((uint8_t *)m_dcap - (uint8_t *)m_soff));
+                b.dst_capacity = max_out;
+                b.results = (int32_t *)(dm + ((uint8_t *)m_res - (uint8_t *)m_soff));
+                S.first = 0;
+                S.count = n;
+                S.busy = true;
+                if ((e = launch(b, S.stream)) != hipSuccess) return bail(fail("kernel launch", e));
+                S.busy = false;
+                if ((e = hipStreamSynchronize(S.stream)) != hipSuccess) return bail(fail("hipStreamSynchronize", e));
+                const uint8_t *hout = (const uint8_t *)S.h_out.p;
+                pool.run(n, [&](size_t j) {
+                    const int32_t r = m_res[j];
+                    results[j] = r;
+                    if (r > 0 && (uint32_t)r <= dst_cap[j]) memcpy(dst[j], hout + m_doff[j], (size_t)r);
+                });
+                release_ctx(dev, cp);
+                return TYCHE_E_OK;
+            }
+        }
+    }
 
     size_t first = 0;
     int si = 0;
@@ -653,19 +791,20 @@ int pick_device(const std::vector<int> &ids) {
 // restores) spread over all devices.
 template <typename Launch>
 int run_host(size_t n, const void *const *src, const uint32_t *src_len, void *const *dst, const uint32_t *dst_cap,
-             int32_t *results, Launch launch) {
-    if (t_device >= 0) return run_host_batch(t_device, n, src, src_len, dst, dst_cap, results, launch);
+             int32_t *results, Launch launch, bool zc_ok = false) {
+    if (t_device >= 0) return run_host_batch(t_device, n, src, src_len, dst, dst_cap, results, launch, zc_ok);
     const DeviceSet &ds = device_set();
     if (ds.ids.empty()) return fail_msg(ds.why);
     std::vector<size_t> cuts(ds.ids.size() + 1);
     const size_t parts = tyche_plan_split(n, src_len, (int)ds.ids.size(), fanout_min_bytes(), cuts.data());
-    if (parts <= 1) return run_host_batch(pick_device(ds.ids), n, src, src_len, dst, dst_cap, results, launch);
+    if (parts <= 1)
+        return run_host_batch(pick_device(ds.ids), n, src, src_len, dst, dst_cap, results, launch, zc_ok);
     std::vector<int> rcs(parts, TYCHE_E_OK);
     std::vector<std::string> errs(parts);
     std::vector<std::thread> th;
     auto part = [&](size_t p) {
         const size_t a = cuts[p], m = cuts[p + 1] - cuts[p];
-        rcs[p] = run_host_batch(ds.ids[p], m, src + a, src_len + a, dst + a, dst_cap + a, results + a, launch);
+        rcs[p] = run_host_batch(ds.ids[p], m, src + a, src_len + a, dst + a, dst_cap + a, results + a, launch, zc_ok);
         if (rcs[p]) errs[p] = t_error;
     };
     for (size_t p = 1; p < parts; p++) th.emplace_back(part, p);
@@ -799,16 +938,16 @@ int tyche_decompress_host(int compressor_id, size_t n, const void *const *src, c
         return run_host(n, src, src_lengths, dst, dst_capacities, results,
                               [](const tyche_batch_t &b, hipStream_t s) {
                                   return launch_zlib_inflate(b, b.dst_capacity, s);
-                              });
+                              }, true);
     if (compressor_id == TYCHE_ZSTD_COMPRESSOR_ID)
         return run_host(n, src, src_lengths, dst, dst_capacities, results,
                               [](const tyche_batch_t &b, hipStream_t s) {
                                   return launch_zstd_decode(b, b.max_src_length, b.dst_capacity, s);
-                              });
+                              }, true);
     return run_host(n, src, src_lengths, dst, dst_capacities, results,
                           [](const tyche_batch_t &b, hipStream_t s) {
                               return launch_lz4_decode(b, b.max_src_length, b.dst_capacity, s);
-                          });
+                          }, true);
 }
 
 // ------------------------------------------------------- Buffer entry points

@@ -596,7 +596,7 @@ hipError_t launch_lz4_decode(const tyche_batch_t &b, uint32_t in_cap, uint32_t o
         const uint32_t win = (std::max(out_cap, cap + 4u) + 16u + 15u) & ~15u;
         const size_t per_cu = waves_per_cu((const void *)lz4_decode_wave_kernel, l);
         const size_t grid = std::min<size_t>(b.count, ncu * per_cu);
-        WorkCounter ctr(s);
+        WorkCounter ctr(s, grid < b.count);
         if (chunk && !ctr.get()) return hipErrorOutOfMemory;
         hipLaunchKernelGGL(lz4_decode_wave_kernel, dim3((unsigned)grid), dim3(kWave), l, s, b, cap, out_cap, win, lo, hi,
                            chunk ? ctr.get() : nullptr, chunk);

@@ -495,7 +495,7 @@ hipError_t launch_lz4_decode_lane(const tyche_batch_t &b, uint32_t in_cap, uint3
         size_t waves = waves_per_cu(k, lds);
         if (env_waves > 0) waves = std::min<size_t>(waves, (size_t)env_waves);
         const size_t grid = std::min<size_t>((b.count + 63) / 64, ncu * waves);
-        WorkCounter ctr(s);
+        WorkCounter ctr(s, grid * 64 < b.count);
         unsigned *cp = ctr.get();
         if (!cp) return hipErrorOutOfMemory;
         void *args[] = {(void *)&b, &in_cap, &out_cap, &cp};
@@ -506,7 +506,7 @@ hipError_t launch_lz4_decode_lane(const tyche_batch_t &b, uint32_t in_cap, uint3
     size_t waves = waves_per_cu((const void *)lz4_decode_lane_kernel, 0);
     waves = std::min<size_t>(waves, env_waves > 0 ? (size_t)env_waves : kLaneWaves);
     const size_t grid = std::min<size_t>((b.count + 63) / 64, ncu * waves);
-    WorkCounter ctr(s);
+    WorkCounter ctr(s, grid * 64 < b.count);
     if (!ctr.get()) return hipErrorOutOfMemory;
     hipLaunchKernelGGL(lz4_decode_lane_kernel, dim3((unsigned)grid), dim3(64), 0, s, b, in_cap, out_cap, ctr.get());
     return hipGetLastError();

@@ -600,7 +600,7 @@ hipError_t launch_lz4_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream_
         // B's scratch: its half's worst case (LZ4_compressBound of L - H < in_cap / 2 + 64), 256-byte aligned
         const uint32_t ws_stride = (lz4_bound(in_cap / 2u + kWave) + 64u + 255u) & ~255u;
         ScratchLease ws(s, grid * (size_t)ws_stride);
-        WorkCounter ctr(s);
+        WorkCounter ctr(s, grid < b.count);
         if (!ctr.get() || !ws.get()) return hipErrorOutOfMemory;
         hipLaunchKernelGGL(lz4_encode_split_kernel, dim3((unsigned)grid), dim3(2 * kWave), lds, s, b, in_cap,
                            ctr.get(), (uint8_t *)ws.get(), ws_stride);
@@ -611,7 +611,7 @@ hipError_t launch_lz4_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream_
     const size_t ncu = prepare_launch((const void *)lz4_encode_kernel);
     const size_t per_cu = waves_per_cu((const void *)lz4_encode_kernel, lds);
     const size_t grid = std::min<size_t>(b.count, ncu * per_cu);
-    WorkCounter ctr(s);
+    WorkCounter ctr(s, grid < b.count);
     if (!ctr.get()) return hipErrorOutOfMemory;
     hipLaunchKernelGGL(lz4_encode_kernel, dim3((unsigned)grid), dim3(kWave), lds, s, b, in_cap, ctr.get());
     return hipGetLastError();

@@ -39,6 +39,24 @@ constexpr uint32_t kWave = 64;
 constexpr int32_t kZData = -3;   // Z_DATA_ERROR
 constexpr int32_t kZBuf = -5;    // Z_BUF_ERROR (output full, input left: uncompr.c:47-53)
 
+// Optional phase profile of the lane-parallel path (diagnostic build only:
+// -DTYCHE_PROFILE, tools/zpar_pages.py): shader cycles per phase summed by lane 0.
+#ifdef TYCHE_PROFILE
+__device__ unsigned long long g_zprof[16];
+#define ZPROF_DECL unsigned long long _pt = clock64();
+#define ZPROF_MARK(slot)                                                       \
+    do {                                                                       \
+        unsigned long long _n = clock64();                                     \
+        if (lane == 0) atomicAdd(&g_zprof[slot], _n - _pt);                    \
+        _pt = _n;                                                              \
+    } while (0)
+#define ZPROF_ADD(slot, v) do { if (lane == 0) atomicAdd(&g_zprof[slot], (unsigned long long)(v)); } while (0)
+#else
+#define ZPROF_DECL
+#define ZPROF_MARK(slot) do { } while (0)
+#define ZPROF_ADD(slot, v) do { } while (0)
+#endif
+
 // ---------------------------------------------------------------- table entries
 // bits 0-3 code length, 4-6 kind, 8-11 extra bits, 16-31 value
 enum : uint32_t { kLit = 0, kLen = 1, kEob = 2, kLong = 3, kBad = 4 };
@@ -621,6 +639,7 @@ __device__ __forceinline__ void par_tables(ParTabs &t, const Table &L, const Tab
 __device__ __forceinline__ int32_t par_block(const ParTabs &t, const uint32_t *S32, uint32_t P0, uint32_t E, uint8_t *out, int32_t op,
                              int32_t cap, uint32_t W, uint32_t *M, uint32_t lane, uint32_t &yend) {
     if (P0 >= E) return kFallback;
+    ZPROF_DECL
     const uint32_t base = P0 & ~31u;
     const uint32_t S = ((E - base + kWave - 1) / kWave + 31u) & ~31u;   // bits per segment
     const uint32_t nv = (E - base + 31u) / 32u + 1u;                        // bitmap words
@@ -643,6 +662,7 @@ __device__ __forceinline__ int32_t par_block(const ParTabs &t, const uint32_t *S
         }
     }
     WAVE_SYNC();
+    ZPROF_MARK(2);
     // 2. bridge to a later lane's walk
     uint32_t o = 0;   // owner lane + 1 of the hand-off position, 0 = chain ends here
     if (a < E && stop == 0) {
@@ -668,6 +688,8 @@ __device__ __forceinline__ int32_t par_block(const ParTabs &t, const uint32_t *S
         if (nx == 0) break;
         cur = nx - 1;
     }
+    ZPROF_MARK(3);
+    ZPROF_ADD(10, cur);
     if (rdlane(stop, cur) != kSymEob || e > E) return kFallback;
     yend = e;
     // 4. count, place, write
@@ -681,6 +703,7 @@ __device__ __forceinline__ int32_t par_block(const ParTabs &t, const uint32_t *S
             else break;
         }
     }
+    ZPROF_MARK(4);
     const int32_t incl = wave_incl_sum((int32_t)nout);
     const int32_t total = op + (int32_t)rdlane((uint32_t)incl, kWave - 1);
     if (total > cap) return kFallback;
@@ -704,6 +727,7 @@ __device__ __forceinline__ int32_t par_block(const ParTabs &t, const uint32_t *S
             }
         }
     }
+    ZPROF_MARK(5);
     if (__ballot(bad)) return kFallback;
     return total;
 }
@@ -738,6 +762,8 @@ __device__ __forceinline__ void par_matches(uint8_t *out, uint32_t total, const 
             q.md = d;
             q.mx = dist | (len << 16);
             q.nmat = n;
+            ZPROF_ADD(12, 1);
+            ZPROF_ADD(13, n);
             WAVE_SYNC();
             flush_matches(q, out, lane);
             WAVE_SYNC();
@@ -757,6 +783,7 @@ __device__ __forceinline__ void seek_bits(BitReader &r, uint32_t bitpos, uint32_
 __device__ __forceinline__ int32_t inflate_par(BitReader &r, const PageRef &p, const uint8_t *stage, uint32_t head, uint8_t *out,
                                int32_t cap, uint32_t W, uint32_t *M, uint32_t *LT, uint32_t *DT, uint8_t *lens,
                                uint16_t *sortL, uint16_t *sortD, uint32_t lane) {
+    ZPROF_DECL
     if (zlib_header(r, lane)) return kFallback;
     const uint32_t *S32 = (const uint32_t *)stage;
     const uint32_t h8 = head * 8u, E = h8 + p.src_len * 8u;
@@ -770,6 +797,7 @@ __device__ __forceinline__ int32_t inflate_par(BitReader &r, const PageRef &p, c
         ParTabs t;
         par_tables(t, L, D, LT, DT, sortL, sortD, lane);
         WAVE_SYNC();
+        ZPROF_MARK(1);
         const uint32_t P0 = h8 + (uint32_t)p.src_len * 8u - (uint32_t)r.avail;
         op = par_block(t, S32, P0, E, out, op, cap, W, M, lane, yend);
         if (op < 0) return kFallback;
@@ -784,7 +812,10 @@ __device__ __forceinline__ int32_t inflate_par(BitReader &r, const PageRef &p, c
     WAVE_SYNC();
     par_matches(out, (uint32_t)op, M, (uint16_t *)stage, lane);   // the stage is free now
     WAVE_SYNC();
+    ZPROF_MARK(6);
     if (lds_adler32(out, (uint32_t)op, lane) != want) return kZData;
+    ZPROF_MARK(8);
+    ZPROF_ADD(0, 1);
     return op;
 }
 
@@ -850,7 +881,7 @@ __global__ __launch_bounds__(64) void zlib_inflate_kernel(tyche_batch_t b, uint3
 // stage.
 __global__ __launch_bounds__(64) void zlib_inflate_par_kernel(tyche_batch_t b, uint32_t out_cap, uint32_t off_lens,
                                                               uint32_t off_lt, uint32_t off_m, uint32_t off_stage,
-                                                              uint32_t stage_cap, unsigned *ctr) {
+                                                              uint32_t stage_cap, int32_t no_fallback, unsigned *ctr) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t lane = threadIdx.x;
     uint8_t *out = smem;
@@ -883,7 +914,7 @@ __global__ __launch_bounds__(64) void zlib_inflate_par_kernel(tyche_batch_t b, u
                                  lane);
                 WAVE_SYNC();
             }
-            if (rv == kFallback) {
+            if (rv == kFallback && !no_fallback) {
                 BitReader r;
                 reader_init(r, p, lane);
                 r.wa = load_win(r, 0, lane);
@@ -901,7 +932,18 @@ __global__ __launch_bounds__(64) void zlib_inflate_par_kernel(tyche_batch_t b, u
 
 }  // namespace
 
-// TYCHE_ZLIB_PAR: 1 (default) the lane-parallel kernel, 0 the serial one (A/B timing)
+#ifdef TYCHE_PROFILE
+extern "C" int tyche_debug_zlib_profile(unsigned long long *host16, int reset) {
+    if (reset) {
+        unsigned long long z[16] = {0};
+        return hipMemcpyToSymbol(HIP_SYMBOL(g_zprof), z, sizeof(z)) == hipSuccess ? 0 : 1;
+    }
+    return hipMemcpyFromSymbol(host16, HIP_SYMBOL(g_zprof), sizeof(unsigned long long) * 16) == hipSuccess ? 0 : 1;
+}
+#endif
+
+// TYCHE_ZLIB_PAR: 1 (default) the lane-parallel kernel, 0 the serial one (A/B timing), 2 the
+// parallel path without its fallback (diagnostics: such pages report INT32_MIN + 1)
 hipError_t launch_zlib_inflate(const tyche_batch_t &b, uint32_t out_cap, hipStream_t s) {
     if (b.count == 0) return hipSuccess;
     const char *env = getenv("TYCHE_ZLIB_PAR");   // read per call: the parity tests switch it in-process
@@ -917,10 +959,10 @@ hipError_t launch_zlib_inflate(const tyche_batch_t &b, uint32_t out_cap, hipStre
             const size_t ncu = prepare_launch((const void *)zlib_inflate_par_kernel);
             const size_t per_cu = waves_per_cu((const void *)zlib_inflate_par_kernel, lds);
             const size_t grid = std::min<size_t>(b.count, ncu * per_cu);
-            WorkCounter ctr(s);
+            WorkCounter ctr(s, grid < b.count);
             if (!ctr.get()) return hipErrorOutOfMemory;
             hipLaunchKernelGGL(zlib_inflate_par_kernel, dim3((unsigned)grid), dim3(kWave), lds, s, b, out_cap,
-                               off_lens, off_lt, off_m, off_stage, stage_cap, ctr.get());
+                               off_lens, off_lt, off_m, off_stage, stage_cap, (int32_t)(par == 2), ctr.get());
             return hipGetLastError();
         }
     }
@@ -929,7 +971,7 @@ hipError_t launch_zlib_inflate(const tyche_batch_t &b, uint32_t out_cap, hipStre
     const size_t ncu = prepare_launch((const void *)zlib_inflate_kernel);
     const size_t per_cu = waves_per_cu((const void *)zlib_inflate_kernel, lds);
     const size_t grid = std::min<size_t>(b.count, ncu * per_cu);
-    WorkCounter ctr(s);
+    WorkCounter ctr(s, grid < b.count);
     if (!ctr.get()) return hipErrorOutOfMemory;
     hipLaunchKernelGGL(zlib_inflate_kernel, dim3((unsigned)grid), dim3(kWave), lds, s, b, out_cap, off_lens,
                        ctr.get());

@@ -1212,7 +1212,7 @@ hipError_t launch_zstd_decode(const tyche_batch_t &b, uint32_t in_cap, uint32_t 
     const size_t ncu = prepare_launch((const void *)zstd_decode_kernel);
     const size_t per_cu = waves_per_cu((const void *)zstd_decode_kernel, lay.total);
     const size_t grid = std::min<size_t>(b.count, ncu * per_cu);
-    WorkCounter ctr(s);
+    WorkCounter ctr(s, grid < b.count);
     if (!ctr.get()) return hipErrorOutOfMemory;
     hipLaunchKernelGGL(zstd_decode_kernel, dim3((unsigned)grid), dim3(kWave), lay.total, s, b, in_cap, out_cap, lay,
                        ctr.get());

@@ -678,7 +678,7 @@ hipError_t launch_zstd_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream
     const size_t ncu = prepare_launch((const void *)zstd_encode_kernel);
     const size_t per_cu = waves_per_cu((const void *)zstd_encode_kernel, lds);
     const size_t grid = std::min<size_t>(b.count, ncu * per_cu);
-    WorkCounter ctr(s);
+    WorkCounter ctr(s, grid < b.count);
     if (!ctr.get()) return hipErrorOutOfMemory;
     hipLaunchKernelGGL(zstd_encode_kernel, dim3((unsigned)grid), dim3(kWave), lds, s, b, in_cap, ctr.get());
     return hipGetLastError();
