@@ -1,0 +1,15 @@
+#!/bin/bash
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out
+mkdir -p $OUT
+cd $R
+timeout -k 10 400 python -u -m pytest tests/test_gpu_zlib.py tests/test_gpu_lz4.py -x -q --timeout 120 --timeout-method thread > $OUT/p5_tests.log 2>&1 || { echo TESTS_FAILED; tail -30 $OUT/p5_tests.log; exit 1; }
+tail -1 $OUT/p5_tests.log
+TYCHE_LZ4_LANE_MIN=0 timeout -k 10 400 python -u -m pytest tests/test_gpu_lz4.py -x -q --timeout 120 --timeout-method thread > $OUT/p5_lane_tests.log 2>&1 || { echo LANE_TESTS_FAILED; tail -30 $OUT/p5_lane_tests.log; exit 1; }
+tail -1 $OUT/p5_lane_tests.log
+PAGES=1048576 timeout -k 10 200 python tools/time_variant.py 2>&1 | grep -v amdgpu.ids
+TYCHE_LZ4_FLAT=0 PAGES=1048576 timeout -k 10 200 python tools/time_variant.py 2>&1 | grep -v amdgpu.ids
+timeout -k 10 200 python tools/zpar_pages.py 2>&1 | grep -v amdgpu.ids
+CODEC=zlib PLEN=32768 PAGES=131072 timeout -k 10 200 python tools/time_variant.py 2>&1 | grep -v amdgpu.ids
+timeout -k 10 200 tools/bin/cycle 65536 64 2000 16
+echo DONE

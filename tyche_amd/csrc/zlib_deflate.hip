@@ -14,7 +14,8 @@
 // smaller than the stored form is written as stored blocks (BTYPE 00).
 //
 // Dynamic trees need the page's symbol statistics before the first bit: the
-// parse's records go to the tail of the output buffer (global scratch), the
+// parse's records go to a per-wave device scratch (or, without one, to the
+// tail of the output buffer), the
 // hash table's LDS holds the histograms and codes once the parse is done, and
 // the symbols are visited twice (count, then code).  When the records do not
 // fit below the stream the page is coded in one pass with the fixed codes.
@@ -350,14 +351,18 @@ __device__ __forceinline__ void two_symbol_code(uint32_t (&l)[R], uint32_t a, ui
 // Encodes in[0, L) (LDS, 64 zero bytes after).  Returns the stream size, or 0
 // if even the stored form does not fit in cap.
 __device__ int32_t encode_page(const uint8_t *in, uint32_t L, uint16_t *table, uint8_t *map, uint2 *rec,
-                               uint32_t *stage, uint8_t *dst, uint32_t cap, uint32_t lane) {
+                               uint32_t *stage, uint8_t *dst, uint32_t cap, uint8_t *ws, uint32_t ws_bytes,
+                               uint32_t lane) {
     const uint32_t adler = lds_adler32(in, L, lane);
     const uint32_t nblk = L ? (L + 65534u) / 65535u : 1u;
     const uint32_t stored = 2u + L + 5u * nblk + 4u;
     // ---- pass 1: parse; records (ls | ll << 16, ml | off << 16) go down from the
-    // 8-aligned end of the output buffer
-    const uintptr_t base = (uintptr_t)dst;
-    const uintptr_t top = (base + cap) & ~(uintptr_t)7;
+    // end of the wave's scratch (ws: room for L / 3 + 2 records, so every page's
+    // records fit and none takes the fixed-code fallback for lack of room), or
+    // without scratch from the 8-aligned end of the output buffer
+    const bool own = ws != nullptr;
+    const uintptr_t base = own ? (uintptr_t)ws : (uintptr_t)dst;
+    const uintptr_t top = own ? base + ws_bytes : (base + cap) & ~(uintptr_t)7;
     const uint32_t room = top > base + 8u ? (uint32_t)((top - base - 8u) / 8u) : 0u;   // records that fit above byte 8
     uint2 *recs = (uint2 *)top;        // record i at recs[-1 - i]
     uint32_t nrec = 0;
@@ -471,7 +476,7 @@ __device__ int32_t encode_page(const uint8_t *in, uint32_t L, uint16_t *table, u
     // ---- size checks: below the stored form, below the records still to be read
     const uint32_t bits = dyn ? dyn_bits : fixed_bits;
     const uint32_t size = 2u + (bits + 7u) / 8u + 4u;
-    const uint32_t rec_lo = (uint32_t)(top - base) - 8u * nrec;
+    const uint32_t rec_lo = own ? cap : (uint32_t)(top - base) - 8u * nrec;
     if (size >= stored || size > cap) return emit_stored(in, L, dst, cap, adler, lane);
     // (the stream may not reach records still to be read: checked as it grows, o.limit)
     // ---- codes (bit-reversed | length << 16) over the histograms
@@ -521,7 +526,7 @@ __device__ int32_t encode_page(const uint8_t *in, uint32_t L, uint16_t *table, u
     for (uint32_t r0 = 0; ok && r0 < nrec; r0 += kWave) {
         const uint32_t cnt = min(nrec - r0, kWave);
         const uint2 rv = lane < cnt ? recf[r0 + lane] : make_uint2(0, 1u << 16);
-        o.limit = min(cap, rec_lo + 8u * (r0 + cnt));   // this group's records are in registers now
+        o.limit = own ? cap : min(cap, rec_lo + 8u * (r0 + cnt));   // this group's records are in registers now
         ok = visit_runs(in, cnt, rv.x & 0xFFFFu, rv.x >> 16, rv.y & 0xFFFFu, rv.y >> 16, map, lane,
                         [&](bool valid, bool lit, uint32_t byte, uint32_t mlen, uint32_t dist) {
                             uint64_t v = 0;
@@ -563,7 +568,8 @@ __device__ int32_t encode_page(const uint8_t *in, uint32_t L, uint16_t *table, u
     return (int32_t)(o.op + 4u);
 }
 
-__global__ __launch_bounds__(64) void zlib_deflate_kernel(tyche_batch_t b, uint32_t in_cap, unsigned *ctr) {
+__global__ __launch_bounds__(64) void zlib_deflate_kernel(tyche_batch_t b, uint32_t in_cap, unsigned *ctr, uint8_t *ws,
+                                                          uint32_t ws_stride) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t lane = threadIdx.x;
     uint16_t *table = (uint16_t *)smem;
@@ -603,7 +609,8 @@ __global__ __launch_bounds__(64) void zlib_deflate_kernel(tyche_batch_t b, uint3
             uint8_t *in = stage + head;
             in[p.src_len + lane] = 0;
             WAVE_SYNC();
-            rv = encode_page(in, p.src_len, table, map, rec, stage_bits, p.dst, p.dst_cap, lane);
+            rv = encode_page(in, p.src_len, table, map, rec, stage_bits, p.dst, p.dst_cap,
+                             ws ? ws + (size_t)blockIdx.x * ws_stride : nullptr, ws_stride, lane);
         }
         if (lane == 0) b.results[page] = rv;
         if (next >= b.count) break;
@@ -636,7 +643,12 @@ hipError_t launch_zlib_deflate(const tyche_batch_t &b, uint32_t in_cap, hipStrea
     const size_t grid = std::min<size_t>(b.count, ncu * per_cu);
     WorkCounter ctr(s, grid < b.count);
     if (!ctr.get()) return hipErrorOutOfMemory;
-    hipLaunchKernelGGL(zlib_deflate_kernel, dim3((unsigned)grid), dim3(kWave), lds, s, b, in_cap, ctr.get());
+    // per-wave record scratch: L / 3 + 2 records of 8 bytes (each record but the
+    // last covers a match of >= 3 bytes)
+    const uint32_t ws_stride = ((in_cap / 3u + 3u) * 8u + 255u) & ~255u;
+    ScratchLease ws(s, grid * (size_t)ws_stride);
+    hipLaunchKernelGGL(zlib_deflate_kernel, dim3((unsigned)grid), dim3(kWave), lds, s, b, in_cap, ctr.get(),
+                       (uint8_t *)ws.get(), ws_stride);
     return hipGetLastError();
 }
 
