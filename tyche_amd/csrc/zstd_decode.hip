@@ -40,6 +40,24 @@
 namespace tyche {
 namespace {
 
+// Optional phase profile (diagnostic build only: -DTYCHE_PROFILE,
+// tools/zstd_prof.py): shader cycles per phase summed by lane 0.
+#ifdef TYCHE_PROFILE
+__device__ unsigned long long g_sdprof[16];
+#define SPROF_DECL unsigned long long _pt = clock64();
+#define SPROF_MARK(slot)                                                       \
+    do {                                                                       \
+        unsigned long long _n = clock64();                                     \
+        if (lane == 0) atomicAdd(&g_sdprof[slot], _n - _pt);                   \
+        _pt = _n;                                                              \
+    } while (0)
+#define SPROF_ADD(slot, v) do { if (lane == 0) atomicAdd(&g_sdprof[slot], (unsigned long long)(v)); } while (0)
+#else
+#define SPROF_DECL
+#define SPROF_MARK(slot) do { } while (0)
+#define SPROF_ADD(slot, v) do { } while (0)
+#endif
+
 constexpr uint32_t kWave = 64;
 #ifndef TYCHE_ZABLATE
 #define TYCHE_ZABLATE 0
@@ -865,6 +883,7 @@ __device__ int32_t seq_table(const Work &W, uint32_t *cells, uint32_t &log, uint
 __device__ int32_t decode_block(const Work &W, SeqTables &T, int32_t ip, int32_t n, int32_t op, int32_t cap,
                                 uint32_t lane) {
     const uint8_t *in = W.in;
+    SPROF_DECL
     ip = ru(ip);
     n = ru(n);
     op = ru(op);
@@ -946,6 +965,7 @@ __device__ int32_t decode_block(const Work &W, SeqTables &T, int32_t ip, int32_t
         }
     }
     __builtin_amdgcn_wave_barrier();
+    SPROF_MARK(2);
     // ---- sequences section (ZSTD_decodeSeqHeaders)
     int32_t sp = ip + lcons;
     const int32_t send = ip + n;
@@ -975,6 +995,7 @@ __device__ int32_t decode_block(const Work &W, SeqTables &T, int32_t ip, int32_t
         if (r < 0) return kErr;
         sp += r;
         __builtin_amdgcn_wave_barrier();
+        SPROF_MARK(3);
         // ---- sequence loop (ZSTD_decompressSequences)
         T.fse_entropy = true;
         BitD b;
@@ -1030,6 +1051,8 @@ __device__ int32_t decode_block(const Work &W, SeqTables &T, int32_t ip, int32_t
                     voff = offv;
                 }
             }
+            SPROF_MARK(4);
+            SPROF_ADD(9, k);
             if (k == 0) break;
 #if TYCHE_ZABLATE & 1
             // timing-only: skip execution (output wrong), keep the positions moving
@@ -1039,6 +1062,7 @@ __device__ int32_t decode_block(const Work &W, SeqTables &T, int32_t ip, int32_t
             if (!exec_batch(W.win, lit, lit_in_window, lit_win_base, k, vll, vml, voff, op, lp, lsize, cap, lane))
                 return kErr;
 #endif
+            SPROF_MARK(5);
         }
         if (nbseq) return kErr;
         T.rep0 = rep0;
@@ -1056,6 +1080,7 @@ __device__ int32_t decode_block(const Work &W, SeqTables &T, int32_t ip, int32_t
         __builtin_amdgcn_wave_barrier();
     }
     op += last;
+    SPROF_MARK(6);
     return op - op0;
 }
 
@@ -1195,7 +1220,10 @@ __global__ __launch_bounds__(64) void zstd_decode_kernel(tyche_batch_t b, uint32
             if (lane < kStreamPad / 4) lds_st32(in + p.src_len + lane * 4, 0u);
             WAVE_SYNC();
             W.in = in;
+            SPROF_DECL
             rv = decode_frame(W, (int32_t)p.src_len, (int32_t)p.dst_cap, lane);
+            SPROF_MARK(1);
+            SPROF_ADD(0, 1);
             WAVE_SYNC();
             if (rv > 0) stage_out(p.dst, W.win, (uint32_t)rv, lane, kWave);
         }
@@ -1204,6 +1232,16 @@ __global__ __launch_bounds__(64) void zstd_decode_kernel(tyche_batch_t b, uint32
 }
 
 }  // namespace
+
+#ifdef TYCHE_PROFILE
+extern "C" int tyche_debug_zstd_decode_profile(unsigned long long *host16, int reset) {
+    if (reset) {
+        unsigned long long z[16] = {0};
+        return hipMemcpyToSymbol(HIP_SYMBOL(g_sdprof), z, sizeof(z)) == hipSuccess ? 0 : 1;
+    }
+    return hipMemcpyFromSymbol(host16, HIP_SYMBOL(g_sdprof), sizeof(unsigned long long) * 16) == hipSuccess ? 0 : 1;
+}
+#endif
 
 hipError_t launch_zstd_decode(const tyche_batch_t &b, uint32_t in_cap, uint32_t out_cap, hipStream_t s) {
     if (b.count == 0) return hipSuccess;

@@ -42,6 +42,24 @@
 namespace tyche {
 namespace {
 
+// Optional phase profile (diagnostic build only: -DTYCHE_PROFILE,
+// tools/zstd_prof.py): shader cycles per phase summed by lane 0.
+#ifdef TYCHE_PROFILE
+__device__ unsigned long long g_seprof[16];
+#define SPROF_DECL unsigned long long _pt = clock64();
+#define SPROF_MARK(slot)                                                       \
+    do {                                                                       \
+        unsigned long long _n = clock64();                                     \
+        if (lane == 0) atomicAdd(&g_seprof[slot], _n - _pt);                  \
+        _pt = _n;                                                              \
+    } while (0)
+#define SPROF_ADD(slot, v) do { if (lane == 0) atomicAdd(&g_seprof[slot], (unsigned long long)(v)); } while (0)
+#else
+#define SPROF_DECL
+#define SPROF_MARK(slot) do { } while (0)
+#define SPROF_ADD(slot, v) do { } while (0)
+#endif
+
 using lzp::kHashSize;
 using lzp::kWave;
 constexpr uint32_t kPad = 64;
@@ -371,6 +389,7 @@ __device__ uint32_t huf_literals(Enc &e, uint32_t n, uint32_t trail, uint32_t li
 // Writes one block covering page bytes [s.bstart, bend) with the buffered
 // sequences; `last` sets Last_Block.  Returns false if it does not fit.
 __device__ __forceinline__ bool emit_block(Enc &e, uint32_t bend, bool last, uint32_t lane) {
+    SPROF_DECL
     const uint32_t n = e.nseq, blen = bend - e.bstart;
     // ---- per-sequence sizes (lane-parallel over 64-sequence groups)
     uint32_t lit_sum = 0, span = 0, xbits = 0;
@@ -408,6 +427,7 @@ __device__ __forceinline__ bool emit_block(Enc &e, uint32_t bend, bool last, uin
     if (e.op + 3u + comp_bound > e.cap) return false;
     uint32_t o = hdr + 3u;
     // ---- literals section: Huffman-compressed when it pays, else raw (ZSTD_noCompressLiterals)
+    SPROF_MARK(2);
     uint32_t lsec = lit_total >= kHufMinLit ? huf_literals(e, n, trail, lit_total, o, lane) : 0u;
     if (lsec == 0) {
         uint32_t h;
@@ -421,6 +441,7 @@ __device__ __forceinline__ bool emit_block(Enc &e, uint32_t bend, bool last, uin
         lsec = fl + lit_total;
     }
     o += lsec;
+    SPROF_MARK(3);
     // ---- sequences section header
     if (lane < nsh) {
         uint32_t h;
@@ -485,6 +506,8 @@ __device__ __forceinline__ bool emit_block(Enc &e, uint32_t bend, bool last, uin
             tml = huf::build_small_ct(nml, mml, 6, lane);
         }
         if (lane == 0) e.dst[mpos] = dyn ? (uint8_t)((2u << 6) | (2u << 4) | (2u << 2)) : 0u;
+        SPROF_MARK(4);
+        SPROF_ADD(9, n);
         // ---- FSE bitstream: groups of 64 sequences from the last, serial inside a group
         huf::BitW b;
         b.c = 0;
@@ -538,6 +561,7 @@ __device__ __forceinline__ bool emit_block(Enc &e, uint32_t bend, bool last, uin
         o = b.ptr + (b.pos > 0 ? 1u : 0u);
         if (b.pos > 0 && lane == 0) e.dst[b.ptr] = (uint8_t)b.c;
     }
+    SPROF_MARK(5);
     const uint32_t csize = o - (hdr + 3u);
     const uint32_t bh = (last ? 1u : 0u) | (2u << 1) | (csize << 3);
     if (lane < 3) e.dst[hdr + lane] = (uint8_t)(bh >> (8u * lane));
@@ -597,9 +621,12 @@ __device__ __forceinline__ int32_t encode_page(const uint8_t *in, uint32_t L, ui
         }
         return true;
     };
+    SPROF_DECL
     const uint32_t anchor = lzp::parse_page<true>(in, L, table, rec, lane, sink);
     if (anchor == 0xFFFFFFFFu) return 0;
     if (!emit_block(e, L, true, lane)) return 0;
+    SPROF_MARK(1);   // whole page (parse + every block)
+    SPROF_ADD(0, 1);
     return (int32_t)e.op;
 }
 
@@ -669,6 +696,16 @@ __global__ __launch_bounds__(64) void zstd_encode_kernel(tyche_batch_t b, uint32
 }
 
 }  // namespace
+
+#ifdef TYCHE_PROFILE
+extern "C" int tyche_debug_zstd_encode_profile(unsigned long long *host16, int reset) {
+    if (reset) {
+        unsigned long long z[16] = {0};
+        return hipMemcpyToSymbol(HIP_SYMBOL(g_seprof), z, sizeof(z)) == hipSuccess ? 0 : 1;
+    }
+    return hipMemcpyFromSymbol(host16, HIP_SYMBOL(g_seprof), sizeof(unsigned long long) * 16) == hipSuccess ? 0 : 1;
+}
+#endif
 
 hipError_t launch_zstd_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream_t s) {
     if (b.count == 0) return hipSuccess;
