@@ -314,9 +314,7 @@ def test_deflate_buffer_api(tc, oracle_mod):
 @pytest.mark.parametrize("plen", [8192, 16384, 32768])
 def test_deflate_dynamic_bench_pages(tc, oracle_mod, plen):
     """Bench-distribution pages are coded as one dynamic-Huffman block (BFINAL 1, BTYPE 10 in the
-    first stream bits), inflate everywhere, and compress well beyond the fixed-code ratio (~3.1).
-    A page whose match records (8 bytes each, kept in the output buffer's tail) do not fit next to
-    its stream takes the one-pass fixed-code form instead: allowed for a few pages."""
+    first stream bits), inflate everywhere, and compress near level 1's ratio (the fixed codes give ~3.1)."""
     n = 48
     pages = tc.pagegen(n, plen, seed=404, dist=0, device=DEV)
     comp, clen = tc.compress_pages(pages, compressor_id=ZLIB)
@@ -325,8 +323,9 @@ def test_deflate_dynamic_bench_pages(tc, oracle_mod, plen):
     assert torch.equal(out, pages) and bool((rv == plen).all())
     total = _check_zlib_streams(oracle_mod, comp, clen, pages.cpu().numpy())
     ch, lh = comp.cpu().numpy(), clen.cpu().numpy()
-    assert sum(ch[i, 2] & 7 == 5 for i in range(n)) >= n - n // 12
-    assert n * plen / total > 3.6
+    assert sum(ch[i, 2] & 7 == 5 for i in range(n)) == n       # records in device scratch: never the fixed codes
+    # 4-way buckets on a 3-byte hash (lz_parse.h kWays): level 1 gets 4.27 at 16 KiB on these pages
+    assert n * plen / total > {8192: 3.7, 16384: 4.0, 32768: 4.2}[plen]
 
 
 def _literal_heavy_page(rng, plen, draw):

@@ -169,9 +169,35 @@ __device__ __forceinline__ void decode_record(const uint2 *rec, uint32_t n, uint
 // start (a multiple of 64, default 0): parse [start, L) only, with the table
 // holding earlier positions already (the split LZ4 encoder's second wave); the
 // first literal run starts at `start`.
-template <bool kRepCand = false, bool kMin3 = false, typename Sink>
+//
+// kWays (deflate: 4): the table is 2 * kHashSize (TYCHE_WAYS_SCALE) 16-bit slots in buckets of
+// kWays positions, most recent first (table_slots<kWays>()); every position
+// verifies all of its bucket's candidates and keeps the longest match (the
+// most recent of equally long ones) -- deflate_fast's hash chain cut at 4
+// (max_chain 4 at level 1, deflate.c:134), with a bucket standing in for the
+// chain.  Lanes of one block that share a bucket insert in unspecified order
+// (one of them wins), as the single-slot table does.
+#ifndef TYCHE_HASH3
+#define TYCHE_HASH3 1   // kMin3 with buckets: hash 3 bytes (deflate's MIN_MATCH), not 4
+#endif
+#ifndef TYCHE_WAYS_SCALE
+#define TYCHE_WAYS_SCALE 2   // bucketed tables hold TYCHE_WAYS_SCALE * kHashSize slots
+#endif
+template <int kWays>
+__host__ __device__ constexpr uint32_t table_slots() { return kWays > 1 ? TYCHE_WAYS_SCALE * kHashSize : kHashSize; }
+
+template <int kWays>
+__device__ __forceinline__ uint32_t bucket_of(uint32_t v) {
+    constexpr uint32_t nb = table_slots<kWays>() / kWays;
+    constexpr uint32_t lg = nb >= 4096 ? 12 : nb >= 2048 ? 11 : nb >= 1024 ? 10 : 9;
+    static_assert((1u << lg) == nb, "bucket count is a power of two");
+    return (v * 2654435761u) >> (32 - lg);
+}
+
+template <bool kRepCand = false, bool kMin3 = false, int kWays = 1, typename Sink>
 __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *table, uint2 *rec, uint32_t lane,
                                       Sink &sink, uint32_t start = 0) {
+    static_assert(kWays == 1 || kWays == 2 || kWays == 4, "1, 2 or 4 ways");
     uint32_t anchor = start;
     if (L < (uint32_t)(kMfLimit + 1) || start > L - kMfLimit) return start;
     const uint32_t mflimit = L - kMfLimit;          // last position a match may start
@@ -195,13 +221,35 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
         const Window pw = lds_window(A, (live ? pos : mflimit) + ib);
         const uint32_t v = pw.w0;
         constexpr uint32_t vm = kMin3 ? 0xFFFFFFu : 0xFFFFFFFFu;   // the bytes a candidate must match
-        const uint32_t h = hash4(v);
-        uint32_t cand = table[h];
-        __builtin_amdgcn_wave_barrier();
-        table[h] = (uint16_t)pos;
+        uint32_t cands[kWays];
+        if (kWays == 1) {
+            const uint32_t h = hash4(v);
+            cands[0] = table[h];
+            __builtin_amdgcn_wave_barrier();
+            table[h] = (uint16_t)pos;
+        } else if (kWays == 2) {
+            uint32_t *T = (uint32_t *)table;
+            const uint32_t h = bucket_of<kWays>(kMin3 && TYCHE_HASH3 ? v & 0xFFFFFFu : v);
+            const uint32_t bk = T[h];
+            cands[0] = bk & 0xFFFFu;
+            cands[kWays > 1 ? 1 : 0] = bk >> 16;
+            __builtin_amdgcn_wave_barrier();
+            T[h] = pos | (bk << 16);
+        } else {
+            uint2 *T = (uint2 *)table;
+            const uint32_t h = bucket_of<kWays>(kMin3 && TYCHE_HASH3 ? v & 0xFFFFFFu : v);
+            const uint2 bk = T[h];
+            cands[0] = bk.x & 0xFFFFu;
+            cands[kWays > 1 ? 1 : 0] = bk.x >> 16;
+            cands[kWays > 2 ? 2 : 0] = bk.y & 0xFFFFu;
+            cands[kWays > 3 ? 3 : 0] = bk.y >> 16;
+            __builtin_amdgcn_wave_barrier();
+            T[h] = make_uint2(pos | (bk.x << 16), (bk.x >> 16) | (bk.y << 16));
+        }
         // ---- the candidate's window: 4-byte verify, forward probe (MINMATCH + up
         // to kProbe bytes) and backward probe (up to 4 bytes).  A candidate is a
         // position <= mflimit, so the window stays inside the page's zero pad.
+        uint32_t cand = cands[0];
         Window cw = lds_window(A, cand + ib);
         bool ok = live & (cand < pos) & (((cw.w0 ^ v) & vm) == 0u);
         uint32_t n = 4u + kProbe;
@@ -211,6 +259,26 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
             if (x) n = 4u + 4u * (uint32_t)k + ((uint32_t)__builtin_ctz(x) >> 3);
         }
         if (kMin3 && cw.w0 != v) n = 3u;
+#pragma unroll
+        for (int w = 1; w < kWays; w++) {
+            // older bucket entries: taken only when strictly longer
+            const uint32_t cw2 = cands[w];
+            const Window ww = lds_window(A, cw2 + ib);
+            const bool okw = live & (cw2 < pos) & (((ww.w0 ^ v) & vm) == 0u);
+            uint32_t nw = 4u + kProbe;
+#pragma unroll
+            for (int k = (int)kProbeWords - 1; k >= 0; k--) {
+                const uint32_t x = pw.fw[k] ^ ww.fw[k];
+                if (x) nw = 4u + 4u * (uint32_t)k + ((uint32_t)__builtin_ctz(x) >> 3);
+            }
+            if (kMin3 && ww.w0 != v) nw = 3u;
+            if (okw && (!ok || nw > n)) {
+                cand = cw2;
+                cw = ww;
+                n = nw;
+                ok = true;
+            }
+        }
         if (kMin3) {
             // distance 4 straight from this position's window (arrays of 4-byte
             // items differing in one byte), taken when at least as long

@@ -41,12 +41,17 @@
 #ifndef TYCHE_ZLIB_MIN3
 #define TYCHE_ZLIB_MIN3 1
 #endif
+#ifndef TYCHE_ZLIB_WAYS
+#define TYCHE_ZLIB_WAYS 4   // candidates per hash bucket (lz_parse.h kWays)
+#endif
 
 namespace tyche {
 namespace {
 
 using lzp::kHashSize;
 using lzp::kWave;
+constexpr int kWays = TYCHE_ZLIB_WAYS;
+constexpr uint32_t kTableSlots = lzp::table_slots<kWays>();
 constexpr uint32_t kPad = 64;
 constexpr uint32_t kStageWords = 128;
 constexpr uint32_t kPrefetchVec = 16;
@@ -261,7 +266,7 @@ __device__ int32_t emit_stored(const uint8_t *in, uint32_t L, uint8_t *dst, uint
 // stream size, or 0 if even the stored form does not fit in cap.
 __device__ int32_t encode_fixed1(const uint8_t *in, uint32_t L, uint32_t adler, uint16_t *table, uint8_t *map,
                                  uint2 *rec, uint32_t *stage, uint8_t *dst, uint32_t cap, uint32_t lane) {
-    for (uint32_t w = lane; w < kHashSize / 8; w += kWave) ((u32x4 *)table)[w] = u32x4{0, 0, 0, 0};
+    for (uint32_t w = lane; w < kTableSlots / 8; w += kWave) ((u32x4 *)table)[w] = u32x4{0, 0, 0, 0};
     WAVE_SYNC();
     const uint32_t nblk = L ? (L + 65534u) / 65535u : 1u;
     const uint32_t stored = 2u + L + 5u * nblk + 4u;
@@ -283,7 +288,7 @@ __device__ int32_t encode_fixed1(const uint8_t *in, uint32_t L, uint32_t adler, 
             if (off > 32768u) { ll += ml; ml = 0; }     // beyond the deflate window: literals
             return code_runs(o, in, n, ls, ll, ml, off, map, lane);
         };
-        anchor = lzp::parse_page<TYCHE_ZLIB_REP != 0, TYCHE_ZLIB_MIN3 != 0>(in, L, table, rec, lane, sink);
+        anchor = lzp::parse_page<TYCHE_ZLIB_REP != 0, TYCHE_ZLIB_MIN3 != 0, kWays>(in, L, table, rec, lane, sink);
         ok = anchor != 0xFFFFFFFFu;
     }
     if (ok) ok = code_runs(o, in, 1, anchor, L - anchor, 0, 1, map, lane);   // last literals
@@ -366,7 +371,7 @@ __device__ int32_t encode_page(const uint8_t *in, uint32_t L, uint16_t *table, u
     const uint32_t room = top > base + 8u ? (uint32_t)((top - base - 8u) / 8u) : 0u;   // records that fit above byte 8
     uint2 *recs = (uint2 *)top;        // record i at recs[-1 - i]
     uint32_t nrec = 0;
-    for (uint32_t w = lane; w < kHashSize / 8; w += kWave) ((u32x4 *)table)[w] = u32x4{0, 0, 0, 0};
+    for (uint32_t w = lane; w < kTableSlots / 8; w += kWave) ((u32x4 *)table)[w] = u32x4{0, 0, 0, 0};
     WAVE_SYNC();
     auto sink = [&](const uint2 *r, uint32_t n, uint32_t anc) -> bool {
         if (nrec + n > room) return false;
@@ -377,7 +382,7 @@ __device__ int32_t encode_page(const uint8_t *in, uint32_t L, uint16_t *table, u
         nrec += n;
         return true;
     };
-    const uint32_t anchor = lzp::parse_page<TYCHE_ZLIB_REP != 0, TYCHE_ZLIB_MIN3 != 0>(in, L, table, rec, lane, sink);
+    const uint32_t anchor = lzp::parse_page<TYCHE_ZLIB_REP != 0, TYCHE_ZLIB_MIN3 != 0, kWays>(in, L, table, rec, lane, sink);
     if (anchor == 0xFFFFFFFFu || nrec + 1u > room)
         return encode_fixed1(in, L, adler, table, map, rec, stage, dst, cap, lane);
     if (lane == 0) recs[-1 - (int32_t)nrec] = make_uint2(anchor | ((L - anchor) << 16), 1u << 16);   // last literals
@@ -573,7 +578,7 @@ __global__ __launch_bounds__(64) void zlib_deflate_kernel(tyche_batch_t b, uint3
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t lane = threadIdx.x;
     uint16_t *table = (uint16_t *)smem;
-    uint32_t *stage_bits = (uint32_t *)(smem + kHashSize * sizeof(uint16_t));
+    uint32_t *stage_bits = (uint32_t *)(smem + kTableSlots * sizeof(uint16_t));
     uint8_t *map = (uint8_t *)(stage_bits + kStageWords);
     uint2 *rec = (uint2 *)(map + kWave);
     uint8_t *stage = (uint8_t *)(rec + kWave);
@@ -636,7 +641,7 @@ __global__ __launch_bounds__(64) void zlib_deflate_kernel(tyche_batch_t b, uint3
 hipError_t launch_zlib_deflate(const tyche_batch_t &b, uint32_t in_cap, hipStream_t s) {
     if (b.count == 0) return hipSuccess;
     if (in_cap > 65535u) return hipErrorInvalidValue;    // 16-bit positions in the parse
-    const size_t lds = kHashSize * sizeof(uint16_t) + kStageWords * 4 + kWave + kWave * 8 +
+    const size_t lds = kTableSlots * sizeof(uint16_t) + kStageWords * 4 + kWave + kWave * 8 +
                        ((in_cap + 16u + kPad + 15u) & ~15u);
     const size_t ncu = prepare_launch((const void *)zlib_deflate_kernel);
     const size_t per_cu = waves_per_cu((const void *)zlib_deflate_kernel, lds);
