@@ -323,7 +323,7 @@ def test_deflate_dynamic_bench_pages(tc, oracle_mod, plen):
     assert torch.equal(out, pages) and bool((rv == plen).all())
     total = _check_zlib_streams(oracle_mod, comp, clen, pages.cpu().numpy())
     ch, lh = comp.cpu().numpy(), clen.cpu().numpy()
-    assert sum(ch[i, 2] & 7 == 5 for i in range(n)) == n       # records in device scratch: never the fixed codes
+    assert sum(ch[i, 2] & 7 == 5 for i in range(n)) >= n - n // 12   # fixed codes only where they are smaller
     # 4-way buckets on a 3-byte hash (lz_parse.h kWays): level 1 gets 4.27 at 16 KiB on these pages
     assert n * plen / total > {8192: 3.7, 16384: 4.0, 32768: 4.2}[plen]
 
