@@ -187,12 +187,19 @@ template <int kWays>
 __host__ __device__ constexpr uint32_t table_slots() { return kWays > 1 ? TYCHE_WAYS_SCALE * kHashSize : kHashSize; }
 
 template <int kWays>
-__device__ __forceinline__ uint32_t bucket_of(uint32_t v) {
+__device__ __forceinline__ uint32_t bucket_of(uint32_t v, uint32_t v2 = 0, uint32_t nbytes = 4) {
     constexpr uint32_t nb = table_slots<kWays>() / kWays;
     constexpr uint32_t lg = nb >= 4096 ? 12 : nb >= 2048 ? 11 : nb >= 1024 ? 10 : 9;
     static_assert((1u << lg) == nb, "bucket count is a power of two");
+    if (nbytes > 4) {   // 5 or 6 bytes: zstd's fast parse hashes searchLength bytes (ZSTD_hashPtr)
+        const uint64_t x = ((uint64_t)(v2 & (nbytes == 5 ? 0xFFu : 0xFFFFu)) << 32) | v;
+        return (uint32_t)((x * 0xCF1BBCDCB7A56463ull) >> (64 - lg));
+    }
     return (v * 2654435761u) >> (32 - lg);
 }
+#ifndef TYCHE_HASH_BYTES
+#define TYCHE_HASH_BYTES 5   // kRepCand (zstd): bytes hashed -- zstd level 1 hashes searchLength bytes
+#endif
 
 template <bool kRepCand = false, bool kMin3 = false, int kWays = 1, typename Sink>
 __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *table, uint2 *rec, uint32_t lane,
@@ -223,13 +230,17 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
         constexpr uint32_t vm = kMin3 ? 0xFFFFFFu : 0xFFFFFFFFu;   // the bytes a candidate must match
         uint32_t cands[kWays];
         if (kWays == 1) {
-            const uint32_t h = hash4(v);
+            const uint32_t h = kRepCand && TYCHE_HASH_BYTES > 4
+                                   ? (uint32_t)(((((uint64_t)(pw.fw[0] & (TYCHE_HASH_BYTES == 5 ? 0xFFu : 0xFFFFu)) << 32) | v) *
+                                                 0xCF1BBCDCB7A56463ull) >> (64 - kHashLog))
+                                   : hash4(v);
             cands[0] = table[h];
             __builtin_amdgcn_wave_barrier();
             table[h] = (uint16_t)pos;
         } else if (kWays == 2) {
             uint32_t *T = (uint32_t *)table;
-            const uint32_t h = bucket_of<kWays>(kMin3 && TYCHE_HASH3 ? v & 0xFFFFFFu : v);
+            const uint32_t h = kRepCand ? bucket_of<kWays>(v, pw.fw[0], TYCHE_HASH_BYTES)
+                                        : bucket_of<kWays>(kMin3 && TYCHE_HASH3 ? v & 0xFFFFFFu : v);
             const uint32_t bk = T[h];
             cands[0] = bk & 0xFFFFu;
             cands[kWays > 1 ? 1 : 0] = bk >> 16;
@@ -237,7 +248,8 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
             T[h] = pos | (bk << 16);
         } else {
             uint2 *T = (uint2 *)table;
-            const uint32_t h = bucket_of<kWays>(kMin3 && TYCHE_HASH3 ? v & 0xFFFFFFu : v);
+            const uint32_t h = kRepCand ? bucket_of<kWays>(v, pw.fw[0], TYCHE_HASH_BYTES)
+                                        : bucket_of<kWays>(kMin3 && TYCHE_HASH3 ? v & 0xFFFFFFu : v);
             const uint2 bk = T[h];
             cands[0] = bk.x & 0xFFFFu;
             cands[kWays > 1 ? 1 : 0] = bk.x >> 16;

@@ -61,6 +61,11 @@ __device__ unsigned long long g_seprof[16];
 #endif
 
 using lzp::kHashSize;
+#ifndef TYCHE_ZSTD_WAYS
+#define TYCHE_ZSTD_WAYS 2   // candidates per hash bucket (lz_parse.h kWays)
+#endif
+constexpr int kZWays = TYCHE_ZSTD_WAYS;
+constexpr uint32_t kTableSlots = lzp::table_slots<kZWays>();
 using lzp::kWave;
 constexpr uint32_t kPad = 64;
 constexpr uint32_t kSeqCap = 1024;       // sequences buffered per block
@@ -622,7 +627,7 @@ __device__ __forceinline__ int32_t encode_page(const uint8_t *in, uint32_t L, ui
         return true;
     };
     SPROF_DECL
-    const uint32_t anchor = lzp::parse_page<true>(in, L, table, rec, lane, sink);
+    const uint32_t anchor = lzp::parse_page<true, false, kZWays>(in, L, table, rec, lane, sink);
     if (anchor == 0xFFFFFFFFu) return 0;
     if (!emit_block(e, L, true, lane)) return 0;
     SPROF_MARK(1);   // whole page (parse + every block)
@@ -634,7 +639,7 @@ __global__ __launch_bounds__(64) void zstd_encode_kernel(tyche_batch_t b, uint32
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t lane = threadIdx.x;
     uint16_t *table = (uint16_t *)smem;
-    uint8_t *map = smem + kHashSize * sizeof(uint16_t);                 // 64-byte owner map
+    uint8_t *map = smem + kTableSlots * sizeof(uint16_t);               // 64-byte owner map
     uint2 *rec = (uint2 *)(map + kWave);                               // 64 parse records
     uint2 *seq = rec + kWave;                                          // kSeqCap block sequences
     uint32_t *htab = (uint32_t *)(seq + kSeqCap);                      // literal histogram / Huffman codes
@@ -670,7 +675,7 @@ __global__ __launch_bounds__(64) void zstd_encode_kernel(tyche_batch_t b, uint32
             rv = kResultTooLarge;
         } else {
             uint8_t *in = stage + head;
-            for (uint32_t w = lane; w < kHashSize / 8; w += kWave) ((u32x4 *)table)[w] = u32x4{0, 0, 0, 0};
+            for (uint32_t w = lane; w < kTableSlots / 8; w += kWave) ((u32x4 *)table)[w] = u32x4{0, 0, 0, 0};
             WAVE_SYNC();
             in[p.src_len + lane] = 0;
             WAVE_SYNC();
@@ -710,7 +715,7 @@ extern "C" int tyche_debug_zstd_encode_profile(unsigned long long *host16, int r
 hipError_t launch_zstd_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream_t s) {
     if (b.count == 0) return hipSuccess;
     if (in_cap > 65535u) return hipErrorInvalidValue;    // 16-bit positions in the parse and sequence records
-    const size_t lds = kHashSize * sizeof(uint16_t) + kWave + kWave * 8 + kSeqCap * 8 + kHtab * 4 + 256 +
+    const size_t lds = kTableSlots * sizeof(uint16_t) + kWave + kWave * 8 + kSeqCap * 8 + kHtab * 4 + 256 +
                        ((in_cap + 16u + kPad + 15u) & ~15u);
     const size_t ncu = prepare_launch((const void *)zstd_encode_kernel);
     const size_t per_cu = waves_per_cu((const void *)zstd_encode_kernel, lds);
