@@ -180,6 +180,10 @@ __device__ bool emit_records(const uint2 *rec, uint32_t n, uint32_t anchor, cons
 // unchanged; a sink too large for the ring (long literal runs: the ring is
 // flushed first) still takes emit_records straight to HBM.
 constexpr uint32_t kOutRing = 1024;   // bytes; head is always a multiple of 256
+#ifndef TYCHE_LIT_LANE
+#define TYCHE_LIT_LANE 8
+#endif
+constexpr uint32_t kLitLane = TYCHE_LIT_LANE;   // literal bytes a sequence's lane copies itself (emit_staged)
 struct OutRing {
     uint32_t head, pend;   // wave-uniform: ring position of the first unflushed byte, unflushed bytes
 };
@@ -243,19 +247,31 @@ __device__ bool emit_staged(const uint2 *rec, uint32_t n, uint32_t anchor, const
         out_flush_all(ring, r, dst, op, lane);
         return emit_records(rec, n, anchor, in, dst, op, cap, map, (uint4 *)ring, lane);
     }
+    constexpr uint32_t m = kOutRing - 1;
+    const uint32_t q_lit = r.head + r.pend + eo + 1 + lext;   // ring position of this sequence's literals
     if (is_sel) {
-        constexpr uint32_t m = kOutRing - 1;
         uint32_t q = r.head + r.pend + eo;
         ring[q & m] = (uint8_t)token;
         q++;
         for (uint32_t t = 0; t < lext; t++) ring[(q + t) & m] = (uint8_t)(t + 1 == lext ? (lit - 15) % 255 : 255);
-        q += lext;
-        for (uint32_t t = 0; t < lit; t++) ring[(q + t) & m] = in[lstart + t];
-        q += lit;
+        // literal runs: the first kLitLane bytes by the sequence's own lane, the
+        // rest of a long run by the whole wave below -- a byte loop as long as the
+        // batch's longest run kept every other lane idle (the sink was 56 % of
+        // the parse's cycles, tools/phase_prof.py)
+        const uint32_t ls = min(lit, kLitLane);
+        for (uint32_t t = 0; t < ls; t++) ring[(q_lit + t) & m] = in[lstart + t];
+        q = q_lit + lit;
         ring[q & m] = (uint8_t)off;
         ring[(q + 1) & m] = (uint8_t)(off >> 8);
         q += 2;
         for (uint32_t t = 0; t < mext; t++) ring[(q + t) & m] = (uint8_t)(t + 1 == mext ? (mc - 15) % 255 : 255);
+    }
+    uint64_t longm = __ballot(is_sel && lit > kLitLane);
+    while (longm) {
+        const uint32_t k = (uint32_t)__builtin_ctzll(longm);
+        longm &= longm - 1;
+        const uint32_t kl = rdlane(lit, k) - kLitLane, kq = rdlane(q_lit, k) + kLitLane, ks = rdlane(lstart, k) + kLitLane;
+        for (uint32_t i = lane; i < kl; i += kWave) ring[(kq + i) & m] = in[ks + i];
     }
     __builtin_amdgcn_wave_barrier();
     r.pend += et;
