@@ -497,3 +497,17 @@ def test_decode_huffman_tablelog12(tc, oracle_mod):
     torch.cuda.synchronize()
     assert bool((rv == 200).all())
     assert all(out[i].cpu().numpy().tobytes() == want for i in range(4))
+
+
+@pytest.mark.parametrize("mode", ["fused", "chunked"])
+def test_zstd_fused_kernel_and_chunked_split(tc, oracle_mod, monkeypatch, mode):
+    """The fused one-kernel decoder (TYCHE_ZSTD_SPLIT=0) and the two-pass decoder run through a
+    1 MiB pass-1 buffer (TYCHE_ZSTD_SCRATCH_MB=1: a handful of pages per chunk) give the verdicts
+    and bytes of the default path on the reference frames, the malformed set and the fuzz corpus."""
+    if mode == "fused":
+        monkeypatch.setenv("TYCHE_ZSTD_SPLIT", "0")
+    else:
+        monkeypatch.setenv("TYCHE_ZSTD_SCRATCH_MB", "1")
+    test_zstd_reference_frames(tc, 3)
+    test_zstd_malformed(tc, oracle_mod)
+    test_zstd_fuzz_vs_oracle(tc, oracle_mod)

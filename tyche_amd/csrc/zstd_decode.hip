@@ -91,31 +91,32 @@ __device__ __constant__ uint32_t c_of_base[29] = {0, 1, 1, 5, 0xD, 0x1D, 0x3D, 0
 // OF_base of zstd_decompress.c:864-879, zstd_internal.h:115-127), computed
 // instead of loaded so the serial sequence chain carries no memory waits.
 __device__ __forceinline__ uint32_t of_base(uint32_t c) { return c < 2u ? c : (1u << c) - 3u; }
+// The middle codes of both tables share one shape: k < 4 -> base step 2, 1 bit;
+// then pairs j = k - 4: base step (4 | 6) << (j / 2), 2 + j / 2 bits.  Written as
+// selects so the scalar chain has no branches.
+__device__ __forceinline__ void mid_code(uint32_t k, uint32_t &f, uint32_t &bits) {
+    const uint32_t j = k - 4u, h = j >> 1;
+    const uint32_t fj = ((j & 1u) ? 6u : 4u) << (h & 7u);
+    f = k < 4u ? k : fj;
+    bits = k < 4u ? 1u : 2u + h;
+}
 __device__ __forceinline__ void ll_code(uint32_t c, uint32_t &base, uint32_t &bits) {
-    if (c < 16u) { base = c; bits = 0; return; }
-    if (c < 24u) {
-        // codes 16..23: bases 16 18 20 22 24 28 32 40, bits 1 1 1 1 2 2 3 3
-        const uint32_t k = c - 16u;
-        bits = k < 4u ? 1u : (k < 6u ? 2u : 3u);
-        base = k < 4u ? 16u + 2u * k : (k < 6u ? 24u + 4u * (k - 4u) : 32u + 8u * (k - 6u));
-        return;
-    }
-    if (c == 24u) { base = 48u; bits = 4u; return; }
-    bits = c - 19u;
-    base = 1u << bits;
+    // 0..15: base c; 16..24: bases 16 18 20 22 24 28 32 40 48, bits 1 1 1 1 2 2 3 3 4;
+    // 25..35: bits c - 19, base 1 << bits
+    uint32_t f, mb;
+    mid_code(c - 16u, f, mb);
+    const uint32_t hb = c - 19u;
+    bits = c < 16u ? 0u : (c < 25u ? mb : hb);
+    base = c < 16u ? c : (c < 25u ? 16u + 2u * f : 1u << (hb & 31u));
 }
 __device__ __forceinline__ void ml_code(uint32_t c, uint32_t &base, uint32_t &bits) {
-    if (c < 32u) { base = c + 3u; bits = 0; return; }
-    if (c < 43u) {
-        // codes 32..42: bases 35 37 39 41 43 47 51 59 67 83 99, bits 1 1 1 1 2 2 3 3 4 4 5
-        const uint32_t k = c - 32u;
-        bits = k < 4u ? 1u : (k < 6u ? 2u : (k < 8u ? 3u : (k < 10u ? 4u : 5u)));
-        base = k < 4u ? 35u + 2u * k : (k < 6u ? 43u + 4u * (k - 4u) : (k < 8u ? 51u + 8u * (k - 6u)
-                                                                          : (k < 10u ? 67u + 16u * (k - 8u) : 99u)));
-        return;
-    }
-    bits = c - 36u;
-    base = (1u << bits) + 3u;
+    // 0..31: base c + 3; 32..42: bases 35 37 39 41 43 47 51 59 67 83 99,
+    // bits 1 1 1 1 2 2 3 3 4 4 5; 43..52: bits c - 36, base (1 << bits) + 3
+    uint32_t f, mb;
+    mid_code(c - 32u, f, mb);
+    const uint32_t hb = c - 36u;
+    bits = c < 32u ? 0u : (c < 43u ? mb : hb);
+    base = c < 32u ? c + 3u : (c < 43u ? 35u + 2u * f : (1u << (hb & 31u)) + 3u);
 }
 
 // The predefined decoding tables (ZSTD_buildSeqTable set_basic ->
@@ -646,6 +647,10 @@ __device__ int32_t huf_read_table(const Work &W, int32_t ip, int32_t n, uint32_t
 
 // Decodes the Huffman stream(s) of a literals section: 1 or 4 streams, lanes 0-3
 // each take one.  Literal k is written to out[k].  Returns false on error.
+// kGlobal: out is the pass-1 literal buffer in HBM; each stream's lane gathers
+// its symbols into 8-byte words and stores whole aligned words (bytes only at the
+// two ends of its segment).
+template <bool kGlobal>
 __device__ bool huf_decode(const Work &W, int32_t cs, int32_t n, bool single, uint32_t lsize, uint32_t tlog,
                            uint8_t *out, uint32_t lane) {
     const uint8_t *in = W.in;
@@ -679,6 +684,8 @@ __device__ bool huf_decode(const Work &W, int32_t cs, int32_t n, bool single, ui
     const uint32_t act_n = single ? 1u : 4u;
     const uint32_t mc = rdlane(cnt, 0);   // stream 1 holds the most symbols
     const uint32_t hsh = tlog == 12u ? 1u : 0u;   // the table is indexed by at most 11 bits
+    uint64_t acc = 0;
+    uint32_t lo = (uint32_t)((uintptr_t)(out + o0) & 7u);   // first valid byte of the current word
     for (uint32_t i = 0; i < mc; i++) {
         if (lane < act_n && i < cnt) {
             if (b.used > 52u) bitd_reload(b, in);
@@ -687,8 +694,24 @@ __device__ bool huf_decode(const Work &W, int32_t cs, int32_t n, bool single, ui
             // 12-bit code (tableLog 12), the mask keeps the other reads in bounds
             const uint32_t e0 = W.huf[v >> hsh], ep = W.hpair[v & 255u];
             const uint32_t e = (e0 >> 8) == 12u ? (ep | (12u << 8)) : e0;
-            out[o0 + i] = (uint8_t)e;
             b.used += e >> 8;
+            if (!kGlobal) {
+                out[o0 + i] = (uint8_t)e;
+            } else {
+                uint8_t *at = out + o0 + i;
+                const uint32_t k = (uint32_t)((uintptr_t)at & 7u);
+                acc |= (uint64_t)(e & 255u) << (8u * k);
+                if (k == 7u || i + 1u == cnt) {
+                    uint8_t *word = at - k;
+                    if (lo == 0u && k == 7u) {
+                        *(uint64_t *)word = acc;
+                    } else {
+                        for (uint32_t j = lo; j <= k; j++) word[j] = (uint8_t)(acc >> (8u * j));
+                    }
+                    acc = 0;
+                    lo = 0;
+                }
+            }
         }
     }
     // exact end of every stream (BIT_endOfDStream); a reload settles ptr/used
@@ -878,10 +901,74 @@ __device__ int32_t seq_table(const Work &W, uint32_t *cells, uint32_t &log, uint
     return hs;
 }
 
+// ------------------------------------------------------------ two-pass decode
+// The fused kernel holds window + staged frame + tables in LDS (~51 KiB for a
+// 32 KiB page: 3 waves per CU), and the serial FSE chain -- two thirds of its
+// time -- runs at that residency.  The split decode runs the same walk twice:
+//
+//   pass 1 (entropy, decode_frame<true>): frame and block structure, Huffman
+//     literals and the FSE sequence chain.  LDS = staged frame + tables, no
+//     window.  Output per page, in HBM: a stream of entries (three u32 planes)
+//     -- one command per block, each compressed block's command followed by its
+//     sequences (litLength, matchLength, offset after repeat resolution) -- and
+//     a literal buffer (raw blocks and literal sections, decoded).
+//   pass 2 (execution, exec_page): LDS = the window only.  Replays the entries:
+//     raw / RLE blocks, literal placement at the window tail, exec_batch.
+//
+// Every check the reference makes stays in one of the two passes; a page fails
+// when either does (callers compare success/failure, buffer.c only tests
+// ZSTD_isError).  Pass 1 also fails a page early where the reference would fail
+// later in any case: a block whose literals or whose output (literals + match
+// lengths) exceed the remaining capacity.  The entry and literal capacities
+// below are bounds no successful page reaches: every block has a 3-byte header,
+// every executed sequence writes >= 3 bytes, literals are part of the output.
+enum : uint32_t { kCmdRaw = 0, kCmdRle = 1, kCmdBlk = 2, kCmdEnd = 3 };
+
+struct Ent {
+    uint32_t *ll, *ml, *of;   // entry planes
+    uint8_t *lit;             // literal buffer
+    uint32_t ecap, lcap;      // entries, literal bytes
+};
+__host__ __device__ inline uint32_t ent_cap(uint32_t in_cap, uint32_t out_cap) {
+    return ((in_cap / 3u + out_cap / 3u + 72u) + 3u) & ~3u;   // multiple of 4: the literal buffer stays 16-aligned
+}
+__host__ __device__ inline uint32_t lit_cap(uint32_t out_cap) { return out_cap + 16u * (out_cap / 64u + 2u) + 64u; }
+__host__ __device__ inline size_t ent_page_bytes(uint32_t in_cap, uint32_t out_cap) {
+    return ((size_t)ent_cap(in_cap, out_cap) * 12u + lit_cap(out_cap) + 255u) & ~(size_t)255u;
+}
+__device__ inline Ent ent_of(uint8_t *base, uint32_t in_cap, uint32_t out_cap) {
+    Ent E;
+    E.ecap = ent_cap(in_cap, out_cap);
+    E.lcap = lit_cap(out_cap);
+    E.ll = (uint32_t *)base;
+    E.ml = E.ll + E.ecap;
+    E.of = E.ml + E.ecap;
+    E.lit = base + (size_t)E.ecap * 12u;
+    return E;
+}
+__device__ __forceinline__ void put_cmd(const Ent &E, uint32_t at, uint32_t a, uint32_t b, uint32_t c, uint32_t lane) {
+    if (lane == 0) {
+        E.ll[at] = a;
+        E.ml[at] = b;
+        E.of[at] = c;
+    }
+}
+// Literal-buffer position for n bytes that pass 2 copies to LDS offset `to`: runs
+// of 64+ bytes keep to's 16-byte phase, so the copy moves 16-byte vectors.
+__device__ __forceinline__ uint32_t lit_place(uint32_t litc, uint32_t to, uint32_t n) {
+    return n >= 64u ? litc + ((to - litc) & 15u) : litc;
+}
+// in[src, src+n) (LDS) -> the literal buffer at `at`
+__device__ __forceinline__ void lds_to_lit(uint8_t *dst, const uint8_t *in, int32_t src, int32_t n, uint32_t lane) {
+    for (int32_t i = (int32_t)lane; i < n; i += (int32_t)kWave) dst[i] = in[src + i];
+}
+
 // One compressed block at in[ip, ip+n); output from op (frame offset) up to cap.
-// Returns bytes written or < 0.
-__device__ int32_t decode_block(const Work &W, SeqTables &T, int32_t ip, int32_t n, int32_t op, int32_t cap,
-                                uint32_t lane) {
+// Returns bytes written or < 0.  kSplit: pass 1 (entries and literals to E;
+// ecur / litc are the page's entry and literal cursors).
+template <bool kSplit>
+__device__ int32_t decode_block(const Work &W, SeqTables &T, const Ent &E, uint32_t &ecur, uint32_t &litc,
+                                int32_t ip, int32_t n, int32_t op, int32_t cap, uint32_t lane) {
     const uint8_t *in = W.in;
     SPROF_DECL
     ip = ru(ip);
@@ -896,6 +983,7 @@ __device__ int32_t decode_block(const Work &W, SeqTables &T, int32_t ip, int32_t
     const uint8_t *lit;
     bool lit_in_window;
     int32_t lsize, lcons, lit_win_base = 0;
+    uint32_t lat = 0;   // kSplit: literal-buffer position of this block's literals
     if (ltype >= 2u) {
         if (ltype == 3u && !T.lit_entropy) return kErr;
         if (n < 5) return kErr;
@@ -911,17 +999,22 @@ __device__ int32_t decode_block(const Work &W, SeqTables &T, int32_t ip, int32_t
         // remaining capacity makes the reference fail later in any case
         if (op + lsize > cap) return kErrDst;
         uint8_t *dst = W.win + (cap - lsize);
+        if constexpr (kSplit) {
+            lat = lit_place(litc, (uint32_t)(cap - lsize), (uint32_t)lsize);
+            if (lat + (uint32_t)lsize > E.lcap) return kErr;
+            dst = E.lit + lat;
+        }
         const int32_t cs = ip + lh;
         bool ok;
         if (ltype == 3u) {
-            ok = huf_decode(W, cs, csize, single, (uint32_t)lsize, T.huf_log, dst, lane);
+            ok = huf_decode<kSplit>(W, cs, csize, single, (uint32_t)lsize, T.huf_log, dst, lane);
         } else if (single) {
             uint32_t tl;
             const int32_t hs = huf_read_table(W, cs, csize, tl, lane);
             ok = hs >= 0 && hs < csize;
             if (ok) {
                 T.huf_log = tl;
-                ok = huf_decode(W, cs + hs, csize - hs, true, (uint32_t)lsize, tl, dst, lane);
+                ok = huf_decode<kSplit>(W, cs + hs, csize - hs, true, (uint32_t)lsize, tl, dst, lane);
             }
         } else {
             ok = lsize != 0 && csize < lsize && csize > 1;
@@ -931,7 +1024,7 @@ __device__ int32_t decode_block(const Work &W, SeqTables &T, int32_t ip, int32_t
                 ok = hs >= 0 && hs < csize;
                 if (ok) {
                     T.huf_log = tl;
-                    ok = huf_decode(W, cs + hs, csize - hs, false, (uint32_t)lsize, tl, dst, lane);
+                    ok = huf_decode<kSplit>(W, cs + hs, csize - hs, false, (uint32_t)lsize, tl, dst, lane);
                 }
             }
         }
@@ -951,11 +1044,24 @@ __device__ int32_t decode_block(const Work &W, SeqTables &T, int32_t ip, int32_t
             lit = in + ip + lh;
             lit_in_window = false;
             lcons = lh + lsize;
+            if constexpr (kSplit) {
+                // pass 2 places every literal section at the window tail; a section
+                // that cannot fit makes the reference fail later in any case
+                if (op + lsize > cap) return kErrDst;
+                lat = lit_place(litc, (uint32_t)(cap - lsize), (uint32_t)lsize);
+                if (lat + (uint32_t)lsize > E.lcap) return kErr;
+                lds_to_lit(E.lit + lat, in, ip + lh, lsize, lane);
+            }
         } else {             // RLE
             if (lhl == 3u && n < 4) return kErr;
             if (lsize > (int32_t)kBlockMax) return kErr;
             if (op + lsize > cap) return kErrDst;
             uint8_t *dst = W.win + (cap - lsize);
+            if constexpr (kSplit) {
+                lat = lit_place(litc, (uint32_t)(cap - lsize), (uint32_t)lsize);
+                if (lat + (uint32_t)lsize > E.lcap) return kErr;
+                dst = E.lit + lat;
+            }
             const uint8_t v = in[ip + lh];
             for (int32_t i = (int32_t)lane; i < lsize; i += (int32_t)kWave) dst[i] = v;
             lit = dst;
@@ -972,6 +1078,13 @@ __device__ int32_t decode_block(const Work &W, SeqTables &T, int32_t ip, int32_t
     if (send - sp < 1) return kErr;
     int32_t nbseq = (int32_t)u8u(in, sp++);
     int32_t op0 = op, lp = 0;
+    uint32_t cmd_at = 0, nseq_all = 0;
+    int32_t mlsum = 0;   // kSplit: sum of match lengths (the block's output is lsize + mlsum)
+    if constexpr (kSplit) {
+        litc = lat + (uint32_t)lsize;
+        if (ecur >= E.ecap) return kErr;
+        cmd_at = ecur++;
+    }
     if (nbseq) {
         if (nbseq > 0x7F) {
             if (nbseq == 0xFF) {
@@ -984,6 +1097,7 @@ __device__ int32_t decode_block(const Work &W, SeqTables &T, int32_t ip, int32_t
             }
         }
         if (sp + 4 > send) return kErr;
+        nseq_all = (uint32_t)nbseq;
         const uint32_t modes = u8u(in, sp++);
         int32_t r = seq_table(W, W.ll, T.ll_log, modes >> 6, 35, 9, sp, send - sp, c_ll_def, 6, T.fse_entropy, lane);
         if (r < 0) return kErr;
@@ -1012,34 +1126,54 @@ __device__ int32_t decode_block(const Work &W, SeqTables &T, int32_t ip, int32_t
             // decode up to 64 sequences into lanes
             uint32_t vll = 0, vml = 0, voff = 0, k = 0;
             for (; k < kWave; k++) {
+                // the chain's state is wave-uniform: say so, or the compiler keeps the
+                // bit container in VGPRs and turns every branch on it into exec-mask
+                // code (v_lshlrev_b64 / s_and_saveexec per step)
+                b.c = (uint64_t)rfl((uint32_t)b.c) | ((uint64_t)rfl((uint32_t)(b.c >> 32)) << 32);
+                b.used = rfl(b.used);
+                b.ptr = ru(b.ptr);
+                b.start = ru(b.start);
+                sll = rfl(sll);
+                sml = rfl(sml);
+                sof = rfl(sof);
+                rep0 = rfl(rep0);
+                rep1 = rfl(rep1);
+                rep2 = rfl(rep2);
+                nbseq = ru(nbseq);
+                // the three cell reads go out before the container reload: both are
+                // LDS round trips and neither depends on the other
+                const uint32_t cl_v = W.ll[sll], cm_v = W.ml[sml], co_v = W.of[sof];
                 if (!((bitd_reload_u(b, in) <= kCompleted) && nbseq)) { more = false; break; }
                 nbseq--;
-                const uint32_t cl = rfl(W.ll[sll]), cm = rfl(W.ml[sml]), co = rfl(W.of[sof]);
+                const uint32_t cl = rfl(cl_v), cm = rfl(cm_v), co = rfl(co_v);
                 const uint32_t llc = cell_sym(cl), mlc = cell_sym(cm), ofc = cell_sym(co);
-                uint32_t offv;
-                if (!ofc) offv = 0;
-                else offv = of_base(ofc) + bitd_read_fast(b, ofc);
-                if (ofc <= 1u) {
-                    offv += llc == 0;
-                    if (offv) {
-                        uint32_t t = offv == 3u ? rep0 - 1u : (offv == 1u ? rep1 : rep2);
-                        t += t == 0;
-                        if (offv != 1u) rep2 = rep1;
-                        rep1 = rep0;
-                        rep0 = offv = t;
-                    } else {
-                        offv = rep0;
-                    }
-                } else {
-                    rep2 = rep1;
-                    rep1 = rep0;
-                    rep0 = offv;
+                // offset (ofCode 0 reads nothing; readBitsFast needs nb >= 1)
+                const uint32_t ofx = (uint32_t)bitd_look_fast(b, ofc);
+                b.used += ofc;
+                uint32_t offv = ofc ? of_base(ofc) + ofx : 0u;
+                {
+                    // repeat offsets (zstd_decompress.c:884-905) as selects
+                    const bool small = ofc <= 1u;
+                    const uint32_t adj = offv + (llc == 0u);
+                    uint32_t t = adj == 3u ? rep0 - 1u : (adj == 1u ? rep1 : rep2);
+                    t += t == 0u;
+                    const uint32_t n0 = small ? (adj ? t : rep0) : offv;
+                    const uint32_t n1 = small ? (adj ? rep0 : rep1) : rep0;
+                    const uint32_t n2 = small ? (adj ? (adj != 1u ? rep1 : rep2) : rep2) : rep1;
+                    offv = n0;
+                    rep0 = n0;
+                    rep1 = n1;
+                    rep2 = n2;
                 }
                 uint32_t mlbase, mlb, llbase, llb;
                 ml_code(mlc, mlbase, mlb);
                 ll_code(llc, llbase, llb);
-                const uint32_t mlv = mlbase + (mlc > 31u ? bitd_read_fast(b, mlb) : 0u);
-                const uint32_t llv = llbase + (llc > 15u ? bitd_read_fast(b, llb) : 0u);
+                const uint32_t mlx = (uint32_t)bitd_look_fast(b, mlb);
+                b.used += mlb;
+                const uint32_t mlv = mlbase + (mlb ? mlx : 0u);
+                const uint32_t llx = (uint32_t)bitd_look_fast(b, llb);
+                b.used += llb;
+                const uint32_t llv = llbase + (llb ? llx : 0u);
                 if (llb + mlb + ofc > 31u) bitd_reload_u(b, in);
                 sll = cell_state(cl) + bitd_read(b, cell_nb(cl));
                 sml = cell_state(cm) + bitd_read(b, cell_nb(cm));
@@ -1054,20 +1188,38 @@ __device__ int32_t decode_block(const Work &W, SeqTables &T, int32_t ip, int32_t
             SPROF_MARK(4);
             SPROF_ADD(9, k);
             if (k == 0) break;
+            if constexpr (kSplit) {
+                if (ecur + k > E.ecap) return kErr;
+                if (lane < k) {
+                    E.ll[ecur + lane] = vll;
+                    E.ml[ecur + lane] = vml;
+                    E.of[ecur + lane] = voff;
+                }
+                ecur += k;
+                // match lengths are < 2^18: a batch sums below 2^24
+                mlsum += (int32_t)rdlane((uint32_t)wave_incl_sum(lane < k ? (int32_t)vml : 0), kWave - 1);
+                if (mlsum > cap) return kErrDst;
+            } else {
 #if TYCHE_ZABLATE & 1
-            // timing-only: skip execution (output wrong), keep the positions moving
-            op += (int32_t)rdlane((uint32_t)wave_incl_sum(lane < k ? (int32_t)(vll + vml) : 0), kWave - 1);
-            lp += (int32_t)rdlane((uint32_t)wave_incl_sum(lane < k ? (int32_t)vll : 0), kWave - 1);
+                // timing-only: skip execution (output wrong), keep the positions moving
+                op += (int32_t)rdlane((uint32_t)wave_incl_sum(lane < k ? (int32_t)(vll + vml) : 0), kWave - 1);
+                lp += (int32_t)rdlane((uint32_t)wave_incl_sum(lane < k ? (int32_t)vll : 0), kWave - 1);
 #else
-            if (!exec_batch(W.win, lit, lit_in_window, lit_win_base, k, vll, vml, voff, op, lp, lsize, cap, lane))
-                return kErr;
+                if (!exec_batch(W.win, lit, lit_in_window, lit_win_base, k, vll, vml, voff, op, lp, lsize, cap, lane))
+                    return kErr;
 #endif
+            }
             SPROF_MARK(5);
         }
         if (nbseq) return kErr;
         T.rep0 = rep0;
         T.rep1 = rep1;
         T.rep2 = rep2;
+    }
+    if constexpr (kSplit) {
+        if (op + lsize + mlsum > cap) return kErrDst;
+        put_cmd(E, cmd_at, kCmdBlk | (lat << 2), (uint32_t)lsize, nseq_all, lane);
+        return lsize + mlsum;
     }
     // ---- last literals
     const int32_t last = lsize - lp;
@@ -1086,7 +1238,9 @@ __device__ int32_t decode_block(const Work &W, SeqTables &T, int32_t ip, int32_t
 
 // ZSTD_decompressFrame (zstd_decompress.c:1369-1436) for the frame staged at
 // W.in[0, L).  Returns the decoded size or < 0.
-__device__ int32_t decode_frame(const Work &W, int32_t L, int32_t cap, uint32_t lane) {
+// kSplit: pass 1 -- returns 0 or < 0 and leaves the page's entries in E.
+template <bool kSplit>
+__device__ int32_t decode_frame(const Work &W, const Ent &E, int32_t L, int32_t cap, uint32_t lane) {
     const uint8_t *in = W.in;
     if (L < 9) return kErr;
     const uint32_t magic = u32u(in, 0);
@@ -1132,6 +1286,7 @@ __device__ int32_t decode_frame(const Work &W, int32_t L, int32_t cap, uint32_t 
     T.rep1 = 4;
     T.rep2 = 8;
     int32_t ip = fh, remaining = L - fh, op = 0;
+    uint32_t ecur = 0, litc = 0;
     for (;;) {
         if (remaining < 3) return kErr;
         const uint32_t bh = u8u(in, ip) | (u8u(in, ip + 1) << 8) | (u8u(in, ip + 2) << 16);
@@ -1143,15 +1298,28 @@ __device__ int32_t decode_frame(const Work &W, int32_t L, int32_t cap, uint32_t 
         if (csize > remaining) return kErr;
         int32_t dec;
         if (btype == 2u) {
-            dec = decode_block(W, T, ip, csize, op, cap, lane);
+            dec = decode_block<kSplit>(W, T, E, ecur, litc, ip, csize, op, cap, lane);
         } else if (btype == 0u) {
             if (csize > cap - op) return kErrDst;
-            for (int32_t i = (int32_t)lane; i < csize; i += (int32_t)kWave) W.win[op + i] = in[ip + i];
+            if constexpr (kSplit) {
+                const uint32_t at = lit_place(litc, (uint32_t)op, (uint32_t)csize);
+                if (at + (uint32_t)csize > E.lcap || ecur >= E.ecap) return kErr;
+                lds_to_lit(E.lit + at, in, ip, csize, lane);
+                put_cmd(E, ecur++, kCmdRaw | (at << 2), (uint32_t)csize, 0u, lane);
+                litc = at + (uint32_t)csize;
+            } else {
+                for (int32_t i = (int32_t)lane; i < csize; i += (int32_t)kWave) W.win[op + i] = in[ip + i];
+            }
             dec = csize;
         } else {
             if ((int64_t)csize0 > (int64_t)(cap - op)) return kErrDst;
             const uint8_t v = in[ip];
-            for (int32_t i = (int32_t)lane; i < (int32_t)csize0; i += (int32_t)kWave) W.win[op + i] = v;
+            if constexpr (kSplit) {
+                if (ecur >= E.ecap) return kErr;
+                put_cmd(E, ecur++, kCmdRle, csize0, v, lane);
+            } else {
+                for (int32_t i = (int32_t)lane; i < (int32_t)csize0; i += (int32_t)kWave) W.win[op + i] = v;
+            }
             dec = (int32_t)csize0;
         }
         if (dec < 0) return dec;
@@ -1161,12 +1329,20 @@ __device__ int32_t decode_frame(const Work &W, int32_t L, int32_t cap, uint32_t 
         __builtin_amdgcn_wave_barrier();
         if (last) break;
     }
+    uint32_t sum = 0;
     if (checksum) {
         if (remaining < 4) return kErr;
-        if (lds_ld32(in + ip) != xxh64_lds(W.win, (uint32_t)op, lane)) return kErr;
+        sum = lds_ld32(in + ip);
+        if constexpr (!kSplit)
+            if (sum != xxh64_lds(W.win, (uint32_t)op, lane)) return kErr;
         remaining -= 4;
     }
     if (remaining) return kErr;
+    if constexpr (kSplit) {
+        if (ecur >= E.ecap) return kErr;
+        put_cmd(E, ecur, kCmdEnd | ((uint32_t)checksum << 2), 0u, sum, lane);
+        return 0;
+    }
     return op;
 }
 
@@ -1174,9 +1350,10 @@ struct Layout {
     uint32_t off_in, off_huf, off_ll, off_of, off_ml, off_wt, off_norm, off_next, off_w, off_hp, total;
 };
 
-__host__ __device__ inline Layout make_layout(uint32_t in_cap, uint32_t out_cap) {
+// with_window false: pass 1 (no window)
+__host__ __device__ inline Layout make_layout(uint32_t in_cap, uint32_t out_cap, bool with_window = true) {
     Layout l;
-    l.off_in = (out_cap + kWinPad + 15u) & ~15u;
+    l.off_in = with_window ? (out_cap + kWinPad + 15u) & ~15u : 0u;
     l.off_huf = l.off_in + ((in_cap + 16u + kStreamPad + 15u) & ~15u);
     l.off_ll = l.off_huf + 2048u * 2u;
     l.off_of = l.off_ll + 512u * 4u;
@@ -1221,13 +1398,171 @@ __global__ __launch_bounds__(64) void zstd_decode_kernel(tyche_batch_t b, uint32
             WAVE_SYNC();
             W.in = in;
             SPROF_DECL
-            rv = decode_frame(W, (int32_t)p.src_len, (int32_t)p.dst_cap, lane);
+            rv = decode_frame<false>(W, Ent{}, (int32_t)p.src_len, (int32_t)p.dst_cap, lane);
             SPROF_MARK(1);
             SPROF_ADD(0, 1);
             WAVE_SYNC();
             if (rv > 0) stage_out(p.dst, W.win, (uint32_t)rv, lane, kWave);
         }
         if (lane == 0) b.results[page] = rv;
+    }
+}
+
+// ---- pass 2
+
+// global src -> LDS dst, n bytes.  Equal 16-byte phases (pass 1 arranges that for
+// runs of 64+ bytes, lit_place) copy 16-byte vectors; anything else goes bytewise.
+__device__ __forceinline__ void lit_to_lds(uint8_t *dst, const uint8_t *src, int32_t n, uint32_t lane) {
+    int32_t i0 = 0;
+    if (n >= 64 && (((uintptr_t)dst ^ (uintptr_t)src) & 15u) == 0) {
+        const int32_t head = (int32_t)((16u - ((uint32_t)(uintptr_t)dst & 15u)) & 15u);
+        if ((int32_t)lane < head) dst[lane] = src[lane];
+        const int32_t nv = (n - head) >> 4;
+        const u32x4 *g = (const u32x4 *)(src + head);
+        u32x4 *l = (u32x4 *)(dst + head);
+        int32_t v = (int32_t)lane;
+        for (; v + 3 * (int32_t)kWave < nv; v += 4 * (int32_t)kWave) {
+            const u32x4 x0 = g[v], x1 = g[v + kWave], x2 = g[v + 2 * kWave], x3 = g[v + 3 * kWave];
+            l[v] = x0;
+            l[v + kWave] = x1;
+            l[v + 2 * kWave] = x2;
+            l[v + 3 * kWave] = x3;
+        }
+        for (; v < nv; v += (int32_t)kWave) l[v] = g[v];
+        i0 = head + (nv << 4);
+    }
+    for (int32_t i = i0 + (int32_t)lane; i < n; i += (int32_t)kWave) dst[i] = src[i];
+}
+
+// Replays a page's entries into the window.  Returns the decoded size or < 0.
+__device__ int32_t exec_page(uint8_t *win, const Ent &E, int32_t cap, uint32_t lane) {
+    uint32_t cur = 0;
+    int32_t op = 0;
+    for (;;) {
+        if (cur >= E.ecap) return kErr;
+        const uint32_t a = rfl(E.ll[cur]), bsz = rfl(E.ml[cur]), c = rfl(E.of[cur]);
+        cur++;
+        const uint32_t kind = a & 3u;
+        if (kind == kCmdEnd) {
+            if (((a >> 2) & 1u) && c != xxh64_lds(win, (uint32_t)op, lane)) return kErr;
+            return op;
+        }
+        const int32_t sz = (int32_t)bsz;
+        if (kind == kCmdRaw) {
+            if (sz > cap - op) return kErrDst;
+            lit_to_lds(win + op, E.lit + (a >> 2), sz, lane);
+            op += sz;
+        } else if (kind == kCmdRle) {
+            if (sz > cap - op) return kErrDst;
+            for (int32_t i = (int32_t)lane; i < sz; i += (int32_t)kWave) win[op + i] = (uint8_t)c;
+            op += sz;
+        } else {
+            const int32_t lsize = sz;
+            if (op + lsize > cap) return kErrDst;
+            uint8_t *lit = win + (cap - lsize);
+            lit_to_lds(lit, E.lit + (a >> 2), lsize, lane);
+            __builtin_amdgcn_wave_barrier();
+            int32_t lp = 0;
+            const uint32_t nseq = c;
+            if (nseq > E.ecap - cur) return kErr;
+            // the next batch's loads go out before this batch executes
+            uint32_t nll = 0, nml = 0, nof = 0;
+            if (lane < min(nseq, kWave)) {
+                nll = E.ll[cur + lane];
+                nml = E.ml[cur + lane];
+                nof = E.of[cur + lane];
+            }
+            for (uint32_t done = 0; done < nseq; done += kWave) {
+                const uint32_t k = min(nseq - done, kWave);
+                const uint32_t vll = nll, vml = nml, voff = nof;
+                const uint32_t nx = done + kWave;
+                if (nx < nseq && lane < min(nseq - nx, kWave)) {
+                    nll = E.ll[cur + nx + lane];
+                    nml = E.ml[cur + nx + lane];
+                    nof = E.of[cur + nx + lane];
+                }
+                if (!exec_batch(win, lit, true, cap - lsize, k, vll, vml, voff, op, lp, lsize, cap, lane)) return kErr;
+            }
+            cur += nseq;
+            const int32_t last = lsize - lp;
+            if (last > cap - op) return kErrDst;
+            for (int32_t c0 = 0; c0 < last; c0 += (int32_t)kWave) {
+                const int32_t i = c0 + (int32_t)lane;
+                const uint8_t v = i < last ? lit[lp + i] : 0;
+                __builtin_amdgcn_wave_barrier();
+                if (i < last) win[op + i] = v;
+                __builtin_amdgcn_wave_barrier();
+            }
+            op += last;
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// Pass 1 over pages [first, first + count) of b; page j's entries at ws + j * ws_page.
+__global__ __launch_bounds__(64) void zstd_entropy_kernel(tyche_batch_t b, size_t first, size_t count, uint32_t in_cap,
+                                                          uint32_t out_cap, Layout lay, uint8_t *ws, size_t ws_page,
+                                                          int32_t *st, unsigned *ctr) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint32_t lane = threadIdx.x;
+    Work W;
+    W.win = nullptr;
+    W.huf = (uint16_t *)(smem + lay.off_huf);
+    W.hpair = smem + lay.off_hp;
+    W.ll = (uint32_t *)(smem + lay.off_ll);
+    W.of = (uint32_t *)(smem + lay.off_of);
+    W.ml = (uint32_t *)(smem + lay.off_ml);
+    W.wt = (uint32_t *)(smem + lay.off_wt);
+    W.norm = (int16_t *)(smem + lay.off_norm);
+    W.next = (uint16_t *)(smem + lay.off_next);
+    W.w = smem + lay.off_w;
+    uint8_t *stage = smem + lay.off_in;
+    for (size_t j = blockIdx.x; j < count; j = ctr ? claim_page(ctr, lane) : j + gridDim.x) {
+        const PageRef p = batch_page(b, first + j);
+        int32_t rv;
+        if (p.src_len > in_cap || p.dst_cap > out_cap) {
+            rv = kResultTooLarge;
+        } else {
+            WAVE_SYNC();
+            const uint32_t head = stage_in(p.src, p.src_len, stage, lane, kWave);
+            uint8_t *in = stage + head;
+            WAVE_SYNC();
+            if (lane < kStreamPad / 4) lds_st32(in + p.src_len + lane * 4, 0u);
+            WAVE_SYNC();
+            W.in = in;
+            const Ent E = ent_of(ws + j * ws_page, in_cap, out_cap);
+            SPROF_DECL
+            rv = decode_frame<true>(W, E, (int32_t)p.src_len, (int32_t)p.dst_cap, lane);
+            SPROF_MARK(1);
+            SPROF_ADD(0, 1);
+        }
+        if (lane == 0) st[j] = rv;
+    }
+}
+
+// Pass 2: window in LDS, entries from pass 1.
+__global__ __launch_bounds__(64) void zstd_exec_kernel(tyche_batch_t b, size_t first, size_t count, uint32_t in_cap,
+                                                       uint32_t out_cap, const uint8_t *ws, size_t ws_page,
+                                                       const int32_t *st, unsigned *ctr) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint32_t lane = threadIdx.x;
+    for (size_t j = blockIdx.x; j < count; j = ctr ? claim_page(ctr, lane) : j + gridDim.x) {
+        const PageRef p = batch_page(b, first + j);
+        int32_t rv = st[j];
+        if (rv >= 0) {
+            const Ent E = ent_of(const_cast<uint8_t *>(ws) + j * ws_page, in_cap, out_cap);
+            WAVE_SYNC();
+#ifdef TYCHE_PROFILE
+            unsigned long long _pt = clock64();
+#endif
+            rv = exec_page(smem, E, (int32_t)p.dst_cap, lane);
+#ifdef TYCHE_PROFILE
+            if (lane == 0) atomicAdd(&g_sdprof[5], clock64() - _pt);
+#endif
+            WAVE_SYNC();
+            if (rv > 0) stage_out(p.dst, smem, (uint32_t)rv, lane, kWave);
+        }
+        if (lane == 0) b.results[first + j] = rv;
     }
 }
 
@@ -1243,8 +1578,9 @@ extern "C" int tyche_debug_zstd_decode_profile(unsigned long long *host16, int r
 }
 #endif
 
-hipError_t launch_zstd_decode(const tyche_batch_t &b, uint32_t in_cap, uint32_t out_cap, hipStream_t s) {
-    if (b.count == 0) return hipSuccess;
+// TYCHE_ZSTD_SPLIT: 1 (default) two-pass decode where it fits, 0 the fused kernel.
+// TYCHE_ZSTD_SCRATCH_MB bounds the pass-1 buffer; batches go through it in chunks.
+static hipError_t launch_fused(const tyche_batch_t &b, uint32_t in_cap, uint32_t out_cap, hipStream_t s) {
     const Layout lay = make_layout(in_cap, out_cap);
     if (lay.total > 160u * 1024u) return hipErrorInvalidValue;
     const size_t ncu = prepare_launch((const void *)zstd_decode_kernel);
@@ -1255,6 +1591,48 @@ hipError_t launch_zstd_decode(const tyche_batch_t &b, uint32_t in_cap, uint32_t 
     hipLaunchKernelGGL(zstd_decode_kernel, dim3((unsigned)grid), dim3(kWave), lay.total, s, b, in_cap, out_cap, lay,
                        ctr.get());
     return hipGetLastError();
+}
+
+hipError_t launch_zstd_decode(const tyche_batch_t &b, uint32_t in_cap, uint32_t out_cap, hipStream_t s) {
+    if (b.count == 0) return hipSuccess;
+    const char *env = getenv("TYCHE_ZSTD_SPLIT");
+    const bool split = !(env && env[0] == '0');
+    const Layout l1 = make_layout(in_cap, out_cap, false);
+    const uint32_t lds2 = (out_cap + kWinPad + 15u) & ~15u;
+    if (!split || l1.total > 160u * 1024u || lds2 > 160u * 1024u) return launch_fused(b, in_cap, out_cap, s);
+    const size_t page_bytes = ent_page_bytes(in_cap, out_cap);
+    const char *mb = getenv("TYCHE_ZSTD_SCRATCH_MB");
+    const size_t budget = (mb && atol(mb) > 0 ? (size_t)atol(mb) : (size_t)4096) << 20;
+    const size_t chunk = std::max<size_t>(1, std::min<size_t>(b.count, budget / page_bytes));
+    const size_t st_bytes = (chunk * 4u + 255u) & ~(size_t)255u;
+    ScratchLease ws(s, st_bytes + chunk * page_bytes);
+    if (!ws.get()) return launch_fused(b, in_cap, out_cap, s);
+    int32_t *st = (int32_t *)ws.get();
+    uint8_t *ent = (uint8_t *)ws.get() + st_bytes;
+    const size_t ncu = prepare_launch((const void *)zstd_entropy_kernel);
+    (void)prepare_launch((const void *)zstd_exec_kernel);
+    const size_t cu1 = waves_per_cu((const void *)zstd_entropy_kernel, l1.total);
+    const size_t cu2 = waves_per_cu((const void *)zstd_exec_kernel, lds2);
+    for (size_t first = 0; first < b.count; first += chunk) {
+        const size_t n = std::min(chunk, b.count - first);
+        const size_t g1 = std::min<size_t>(n, ncu * cu1);
+        {
+            WorkCounter ctr(s, g1 < n);
+            if (!ctr.get()) return hipErrorOutOfMemory;
+            hipLaunchKernelGGL(zstd_entropy_kernel, dim3((unsigned)g1), dim3(kWave), l1.total, s, b, first, n, in_cap,
+                               out_cap, l1, ent, page_bytes, st, ctr.get());
+        }
+        const size_t g2 = std::min<size_t>(n, ncu * cu2);
+        {
+            WorkCounter ctr(s, g2 < n);
+            if (!ctr.get()) return hipErrorOutOfMemory;
+            hipLaunchKernelGGL(zstd_exec_kernel, dim3((unsigned)g2), dim3(kWave), lds2, s, b, first, n, in_cap,
+                               out_cap, (const uint8_t *)ent, page_bytes, (const int32_t *)st, ctr.get());
+        }
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 }  // namespace tyche
