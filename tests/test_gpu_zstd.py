@@ -499,15 +499,18 @@ def test_decode_huffman_tablelog12(tc, oracle_mod):
     assert all(out[i].cpu().numpy().tobytes() == want for i in range(4))
 
 
-@pytest.mark.parametrize("mode", ["fused", "chunked"])
+@pytest.mark.parametrize("mode", ["fused", "chunked", "inline"])
 def test_zstd_fused_kernel_and_chunked_split(tc, oracle_mod, monkeypatch, mode):
-    """The fused one-kernel decoder (TYCHE_ZSTD_SPLIT=0) and the two-pass decoder run through a
-    1 MiB pass-1 buffer (TYCHE_ZSTD_SCRATCH_MB=1: a handful of pages per chunk) give the verdicts
-    and bytes of the default path on the reference frames, the malformed set and the fuzz corpus."""
+    """The fused one-kernel decoder (TYCHE_ZSTD_SPLIT=0), the split decoder run through a 1 MiB
+    pass-1 buffer (TYCHE_ZSTD_SCRATCH_MB=1: a handful of pages per chunk) and the split decoder
+    with the sequence chains inline in pass 1 (TYCHE_ZSTD_JOBS=0) give the verdicts and bytes of
+    the default path on the reference frames, the malformed set and the fuzz corpus."""
     if mode == "fused":
         monkeypatch.setenv("TYCHE_ZSTD_SPLIT", "0")
-    else:
+    elif mode == "chunked":
         monkeypatch.setenv("TYCHE_ZSTD_SCRATCH_MB", "1")
+    else:
+        monkeypatch.setenv("TYCHE_ZSTD_JOBS", "0")
     test_zstd_reference_frames(tc, 3)
     test_zstd_malformed(tc, oracle_mod)
     test_zstd_fuzz_vs_oracle(tc, oracle_mod)

@@ -872,6 +872,11 @@ struct SeqTables {
     bool fse_entropy, lit_entropy;
     uint32_t huf_log;
     uint32_t rep0, rep1, rep2;
+    // pass 1 with sequence jobs (the FSE chains run lane-per-page in zstd_seq_kernel):
+    // the tables in force (byte offsets into the page's table area; kTabDefault:
+    // none yet), jobs written, table bytes used
+    bool jobs;
+    uint32_t ll_off, of_off, ml_off, njobs, tb_used;
 };
 
 // ZSTD_buildSeqTable (zstd_decompress.c:693-724).  Returns bytes read or < 0.
@@ -928,16 +933,32 @@ struct Ent {
     uint32_t *ll, *ml, *of;   // entry planes
     uint8_t *lit;             // literal buffer
     uint32_t ecap, lcap;      // entries, literal bytes
+    uint32_t *jobs;           // [0] = job count, then kJobWords words per job
+    uint32_t *tabs;           // FSE cells of the tables the jobs use
 };
+// Sequence jobs: one per compressed block with sequences, decoded by
+// zstd_seq_kernel one page per lane -- the chain is serial within a page, so the
+// parallelism comes from the pages.  A page that needs more jobs or table space
+// than its area holds is redone with the chains inline (decode_frame, jobs off).
+constexpr uint32_t kJobWords = 8;   // start, length, nbSeq, first entry, ll/of/ml table, logs
+constexpr uint32_t kMaxJobs = 31;
+constexpr uint32_t kJobBytes = 4u * (4u + kMaxJobs * kJobWords);   // 1008
+constexpr uint32_t kTabBytes = 12u * 1024u;                       // two full LL+OF+ML sets and more
+constexpr uint32_t kAreaBytes = 13312u;                           // jobs + tables, 256-aligned
+constexpr uint32_t kTabDefault = 0xFFFFFFFFu;
+constexpr int32_t kRetryInline = -1000;
 __host__ __device__ inline uint32_t ent_cap(uint32_t in_cap, uint32_t out_cap) {
     return ((in_cap / 3u + out_cap / 3u + 72u) + 3u) & ~3u;   // multiple of 4: the literal buffer stays 16-aligned
 }
 __host__ __device__ inline uint32_t lit_cap(uint32_t out_cap) { return out_cap + 16u * (out_cap / 64u + 2u) + 64u; }
 __host__ __device__ inline size_t ent_page_bytes(uint32_t in_cap, uint32_t out_cap) {
-    return ((size_t)ent_cap(in_cap, out_cap) * 12u + lit_cap(out_cap) + 255u) & ~(size_t)255u;
+    return kAreaBytes + (((size_t)ent_cap(in_cap, out_cap) * 12u + lit_cap(out_cap) + 255u) & ~(size_t)255u);
 }
-__device__ inline Ent ent_of(uint8_t *base, uint32_t in_cap, uint32_t out_cap) {
+__device__ inline Ent ent_of(uint8_t *area, uint32_t in_cap, uint32_t out_cap) {
     Ent E;
+    E.jobs = (uint32_t *)area;
+    E.tabs = (uint32_t *)(area + kJobBytes);
+    uint8_t *base = area + kAreaBytes;
     E.ecap = ent_cap(in_cap, out_cap);
     E.lcap = lit_cap(out_cap);
     E.ll = (uint32_t *)base;
@@ -961,6 +982,22 @@ __device__ __forceinline__ uint32_t lit_place(uint32_t litc, uint32_t to, uint32
 // in[src, src+n) (LDS) -> the literal buffer at `at`
 __device__ __forceinline__ void lds_to_lit(uint8_t *dst, const uint8_t *in, int32_t src, int32_t n, uint32_t lane) {
     for (int32_t i = (int32_t)lane; i < n; i += (int32_t)kWave) dst[i] = in[src + i];
+}
+
+// Copies a table just built in LDS to the page's table area (jobs mode).  mode:
+// the block's compression mode for it (set_repeat keeps the one in force).
+// Returns false when the area is full.
+__device__ bool publish_table(const Ent &E, SeqTables &T, const uint32_t *cells, uint32_t mode, uint32_t log,
+                              uint32_t &off, uint32_t lane) {
+    if (mode == 3u) return true;
+    // set_basic: seq_table left the predefined cells in LDS like any other table
+    const uint32_t n = mode == 1u ? 1u : 1u << log;
+    if (T.tb_used + n * 4u > kTabBytes) return false;
+    uint32_t *g = E.tabs + T.tb_used / 4u;
+    for (uint32_t i = lane; i < n; i += kWave) g[i] = cells[i];
+    off = T.tb_used;
+    T.tb_used += n * 4u;
+    return true;
 }
 
 // One compressed block at in[ip, ip+n); output from op (frame offset) up to cap.
@@ -1110,6 +1147,33 @@ __device__ int32_t decode_block(const Work &W, SeqTables &T, const Ent &E, uint3
         sp += r;
         __builtin_amdgcn_wave_barrier();
         SPROF_MARK(3);
+        if constexpr (kSplit) {
+            if (T.jobs) {
+                // hand the chain to zstd_seq_kernel; the block's output size is
+                // checked in pass 2 (K1 only counts the literals toward op)
+                if (!publish_table(E, T, W.ll, modes >> 6, T.ll_log, T.ll_off, lane) ||
+                    !publish_table(E, T, W.of, (modes >> 4) & 3u, T.of_log, T.of_off, lane) ||
+                    !publish_table(E, T, W.ml, (modes >> 2) & 3u, T.ml_log, T.ml_off, lane) || T.njobs >= kMaxJobs)
+                    return kRetryInline;
+                if ((uint32_t)nbseq > E.ecap - ecur) return kErr;
+                if (lane == 0) {
+                    uint32_t *J = E.jobs + 4u + T.njobs * kJobWords;
+                    J[0] = (uint32_t)sp;
+                    J[1] = (uint32_t)(send - sp);
+                    J[2] = (uint32_t)nbseq;
+                    J[3] = ecur;
+                    J[4] = T.ll_off;
+                    J[5] = T.of_off;
+                    J[6] = T.ml_off;
+                    J[7] = T.ll_log | (T.of_log << 8) | (T.ml_log << 16);
+                }
+                T.njobs++;
+                ecur += (uint32_t)nbseq;
+                T.fse_entropy = true;
+                put_cmd(E, cmd_at, kCmdBlk | (lat << 2), (uint32_t)lsize, nseq_all, lane);
+                return lsize;
+            }
+        }
         // ---- sequence loop (ZSTD_decompressSequences)
         T.fse_entropy = true;
         BitD b;
@@ -1240,7 +1304,7 @@ __device__ int32_t decode_block(const Work &W, SeqTables &T, const Ent &E, uint3
 // W.in[0, L).  Returns the decoded size or < 0.
 // kSplit: pass 1 -- returns 0 or < 0 and leaves the page's entries in E.
 template <bool kSplit>
-__device__ int32_t decode_frame(const Work &W, const Ent &E, int32_t L, int32_t cap, uint32_t lane) {
+__device__ int32_t decode_frame(const Work &W, const Ent &E, int32_t L, int32_t cap, uint32_t lane, bool jobs = false) {
     const uint8_t *in = W.in;
     if (L < 9) return kErr;
     const uint32_t magic = u32u(in, 0);
@@ -1285,6 +1349,10 @@ __device__ int32_t decode_frame(const Work &W, const Ent &E, int32_t L, int32_t 
     T.rep0 = 1;
     T.rep1 = 4;
     T.rep2 = 8;
+    T.jobs = jobs;
+    T.ll_off = T.of_off = T.ml_off = kTabDefault;
+    T.njobs = 0;
+    T.tb_used = 0;
     int32_t ip = fh, remaining = L - fh, op = 0;
     uint32_t ecur = 0, litc = 0;
     for (;;) {
@@ -1341,6 +1409,7 @@ __device__ int32_t decode_frame(const Work &W, const Ent &E, int32_t L, int32_t 
     if constexpr (kSplit) {
         if (ecur >= E.ecap) return kErr;
         put_cmd(E, ecur, kCmdEnd | ((uint32_t)checksum << 2), 0u, sum, lane);
+        if (lane == 0) E.jobs[0] = T.njobs;
         return 0;
     }
     return op;
@@ -1405,6 +1474,196 @@ __global__ __launch_bounds__(64) void zstd_decode_kernel(tyche_batch_t b, uint32
             if (rv > 0) stage_out(p.dst, W.win, (uint32_t)rv, lane, kWave);
         }
         if (lane == 0) b.results[page] = rv;
+    }
+}
+
+// ---- sequence jobs: one page per lane
+
+// 8 bytes at any global address from aligned dwords that hold needed bytes only
+// (an aligned dword never crosses a page, so none of these reads can fault)
+__device__ __forceinline__ uint64_t ld64g(const uint8_t *p) {
+    const uint32_t s = (uint32_t)(uintptr_t)p & 3u;
+    const uint32_t *A = (const uint32_t *)(p - s);
+    const uint32_t d0 = A[0], d1 = A[1];
+    const uint32_t d2 = s ? A[2] : 0u;
+    return (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, s) | ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, s) << 32);
+}
+__device__ __forceinline__ uint32_t gld(const uint32_t *p) { return *(const __attribute__((address_space(1))) uint32_t *)(uintptr_t)p; }
+// A container reload in two halves: issue computes the reference's new ptr/used
+// and sends the load, finish takes the bytes.  Stores placed between the two do
+// not delay the wait for the load (in-order vmcnt).
+struct PendLoad {
+    uint32_t d0, d1, d2, s;
+    bool take;
+};
+__device__ __forceinline__ uint32_t gbitd_reload_issue(BitD &b, const uint8_t *in, PendLoad &L) {
+    uint32_t r = kUnfinished;
+    L.take = false;
+    if (b.used > 64u) {
+        r = kOverflow;
+    } else if (b.ptr >= b.start + 8) {
+        b.ptr -= (int32_t)(b.used >> 3);
+        b.used &= 7u;
+        L.take = true;
+    } else if (b.ptr == b.start) {
+        r = b.used < 64u ? kEndOfBuffer : kCompleted;
+    } else {
+        int32_t nbytes = (int32_t)(b.used >> 3);
+        if (b.ptr - nbytes < b.start) {
+            nbytes = b.ptr - b.start;
+            r = kEndOfBuffer;
+        }
+        b.ptr -= nbytes;
+        b.used -= (uint32_t)nbytes * 8u;
+        L.take = true;
+    }
+    // every lane loads (at ptr, always inside the stream); a dword past the needed
+    // bytes is never touched (index 1 again when the address is aligned)
+    const uint8_t *p = in + b.ptr;
+    L.s = (uint32_t)(uintptr_t)p & 3u;
+    const uint32_t *A = (const uint32_t *)(p - L.s);
+    L.d0 = gld(A);
+    L.d1 = gld(A + 1);
+    L.d2 = gld(A + (L.s ? 2 : 1));
+    return r;
+}
+__device__ __forceinline__ void gbitd_reload_finish(BitD &b, const PendLoad &L) {
+    if (L.take)
+        b.c = (uint64_t)__builtin_amdgcn_alignbyte(L.d1, L.d0, L.s) |
+              ((uint64_t)__builtin_amdgcn_alignbyte(L.d2, L.d1, L.s) << 32);
+}
+// BIT_initDStream / BIT_reloadDStream over global memory (the per-lane reader above, other loads)
+__device__ __forceinline__ bool gbitd_init(BitD &b, const uint8_t *in, int32_t start, int32_t n) {
+    b.start = start;
+    b.c = 0;
+    b.used = 0;
+    b.ptr = start;
+    if (n < 1) return false;
+    const uint32_t last = in[start + n - 1];
+    if (last == 0) return false;
+    const uint32_t mark = 8u - highbit(last);
+    if (n >= 8) {
+        b.ptr = start + n - 8;
+        b.c = ld64g(in + b.ptr);
+        b.used = mark;
+    } else {
+        uint64_t c = in[start];
+        for (int32_t k = 1; k < n; k++) c += (uint64_t)in[start + k] << (8u * (uint32_t)k);
+        b.c = c;
+        b.used = mark + (uint32_t)(8 - n) * 8u;
+    }
+    return true;
+}
+__device__ __forceinline__ uint32_t gbitd_reload(BitD &b, const uint8_t *in) {
+    if (b.used > 64u) return kOverflow;
+    if (b.ptr >= b.start + 8) {
+        b.ptr -= (int32_t)(b.used >> 3);
+        b.used &= 7u;
+        b.c = ld64g(in + b.ptr);
+        return kUnfinished;
+    }
+    if (b.ptr == b.start) return b.used < 64u ? kEndOfBuffer : kCompleted;
+    int32_t nbytes = (int32_t)(b.used >> 3);
+    uint32_t r = kUnfinished;
+    if (b.ptr - nbytes < b.start) {
+        nbytes = b.ptr - b.start;
+        r = kEndOfBuffer;
+    }
+    b.ptr -= nbytes;
+    b.used -= (uint32_t)nbytes * 8u;
+    b.c = ld64g(in + b.ptr);
+    return r;
+}
+
+// ZSTD_decompressSequences (zstd_decompress.c:1010-1060) for one job, this lane's
+// page.  Writes the decoded (litLength, matchLength, offset) triples as entries.
+__device__ bool seq_job(const Ent &E, const uint8_t *src, const uint32_t *J, uint32_t &rep0, uint32_t &rep1,
+                        uint32_t &rep2) {
+    const int32_t start = (int32_t)J[0], len = (int32_t)J[1];
+    const uint32_t nbseq = J[2], e0 = J[3];
+    const uint32_t *LL = E.tabs + J[4] / 4u, *OF = E.tabs + J[5] / 4u, *ML = E.tabs + J[6] / 4u;
+    const uint32_t lls = J[7] & 255u, ofs = (J[7] >> 8) & 255u, mls = (J[7] >> 16) & 255u;
+    BitD b;
+    if (!gbitd_init(b, src, start, len)) return false;
+    uint32_t sll = bitd_read(b, lls);
+    gbitd_reload(b, src);
+    uint32_t sof = bitd_read(b, ofs);
+    gbitd_reload(b, src);
+    uint32_t sml = bitd_read(b, mls);
+    gbitd_reload(b, src);
+    // loads and stores share vmcnt and complete in order: a step's loads go out
+    // before the previous step's stores, so waiting for them never waits for those
+    uint32_t pll = 0, pml = 0, pof = 0;
+    for (uint32_t i = 0; i < nbseq; i++) {
+        const uint32_t cl_v = gld(LL + sll), cm_v = gld(ML + sml), co_v = gld(OF + sof);
+        PendLoad pl;
+        const uint32_t rs = gbitd_reload_issue(b, src, pl);
+        if (i) {
+            E.ll[e0 + i - 1] = pll;
+            E.ml[e0 + i - 1] = pml;
+            E.of[e0 + i - 1] = pof;
+        }
+        if (rs > kCompleted) return false;
+        gbitd_reload_finish(b, pl);
+        const uint32_t cl = cl_v, cm = cm_v, co = co_v;
+        const uint32_t llc = cell_sym(cl), mlc = cell_sym(cm), ofc = cell_sym(co);
+        const uint32_t ofx = (uint32_t)bitd_look_fast(b, ofc);
+        b.used += ofc;
+        uint32_t offv = ofc ? of_base(ofc) + ofx : 0u;
+        {
+            const bool small = ofc <= 1u;
+            const uint32_t adj = offv + (llc == 0u);
+            uint32_t t = adj == 3u ? rep0 - 1u : (adj == 1u ? rep1 : rep2);
+            t += t == 0u;
+            const uint32_t n0 = small ? (adj ? t : rep0) : offv;
+            const uint32_t n1 = small ? (adj ? rep0 : rep1) : rep0;
+            const uint32_t n2 = small ? (adj ? (adj != 1u ? rep1 : rep2) : rep2) : rep1;
+            offv = n0;
+            rep0 = n0;
+            rep1 = n1;
+            rep2 = n2;
+        }
+        uint32_t mlbase, mlb, llbase, llb;
+        ml_code(mlc, mlbase, mlb);
+        ll_code(llc, llbase, llb);
+        const uint32_t mlx = (uint32_t)bitd_look_fast(b, mlb);
+        b.used += mlb;
+        const uint32_t mlv = mlbase + (mlb ? mlx : 0u);
+        const uint32_t llx = (uint32_t)bitd_look_fast(b, llb);
+        b.used += llb;
+        const uint32_t llv = llbase + (llb ? llx : 0u);
+        if (llb + mlb + ofc > 31u) gbitd_reload(b, src);
+        sll = cell_state(cl) + bitd_read(b, cell_nb(cl));
+        sml = cell_state(cm) + bitd_read(b, cell_nb(cm));
+        sof = cell_state(co) + bitd_read(b, cell_nb(co));
+        pll = llv;
+        pml = mlv;
+        pof = offv;
+    }
+    if (nbseq) {
+        E.ll[e0 + nbseq - 1] = pll;
+        E.ml[e0 + nbseq - 1] = pml;
+        E.of[e0 + nbseq - 1] = pof;
+    }
+    return true;
+}
+
+// One lane per page of the chunk: runs the page's jobs in order (repeat offsets
+// carry across blocks); a failed chain fails the page.
+__global__ __launch_bounds__(64) void zstd_seq_kernel(tyche_batch_t b, size_t first, size_t count, uint32_t in_cap,
+                                                      uint32_t out_cap, uint8_t *ws, size_t ws_page, int32_t *st) {
+    const size_t j = (size_t)blockIdx.x * kWave + threadIdx.x;
+    if (j >= count || st[j] < 0) return;
+    const Ent E = ent_of(ws + j * ws_page, in_cap, out_cap);
+    const uint32_t njobs = E.jobs[0];
+    if (njobs == 0) return;
+    const PageRef p = batch_page(b, first + j);
+    uint32_t rep0 = 1, rep1 = 4, rep2 = 8;
+    for (uint32_t q = 0; q < njobs; q++) {
+        if (!seq_job(E, p.src, E.jobs + 4u + q * kJobWords, rep0, rep1, rep2)) {
+            st[j] = kErr;
+            return;
+        }
     }
 }
 
@@ -1502,7 +1761,7 @@ __device__ int32_t exec_page(uint8_t *win, const Ent &E, int32_t cap, uint32_t l
 // Pass 1 over pages [first, first + count) of b; page j's entries at ws + j * ws_page.
 __global__ __launch_bounds__(64) void zstd_entropy_kernel(tyche_batch_t b, size_t first, size_t count, uint32_t in_cap,
                                                           uint32_t out_cap, Layout lay, uint8_t *ws, size_t ws_page,
-                                                          int32_t *st, unsigned *ctr) {
+                                                          int32_t *st, unsigned *ctr, bool use_jobs) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t lane = threadIdx.x;
     Work W;
@@ -1532,7 +1791,11 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(tyche_batch_t b, size_
             W.in = in;
             const Ent E = ent_of(ws + j * ws_page, in_cap, out_cap);
             SPROF_DECL
-            rv = decode_frame<true>(W, E, (int32_t)p.src_len, (int32_t)p.dst_cap, lane);
+            // jobs first; a page whose jobs do not fit is redone with the chains inline
+            for (bool jobs = use_jobs;; jobs = false) {
+                rv = decode_frame<true>(W, E, (int32_t)p.src_len, (int32_t)p.dst_cap, lane, jobs);
+                if (!(rv == kRetryInline && jobs)) break;
+            }
             SPROF_MARK(1);
             SPROF_ADD(0, 1);
         }
@@ -1579,6 +1842,7 @@ extern "C" int tyche_debug_zstd_decode_profile(unsigned long long *host16, int r
 #endif
 
 // TYCHE_ZSTD_SPLIT: 1 (default) two-pass decode where it fits, 0 the fused kernel.
+// TYCHE_ZSTD_JOBS: 1 (default) sequence chains lane-per-page (zstd_seq_kernel), 0 inline.
 // TYCHE_ZSTD_SCRATCH_MB bounds the pass-1 buffer; batches go through it in chunks.
 static hipError_t launch_fused(const tyche_batch_t &b, uint32_t in_cap, uint32_t out_cap, hipStream_t s) {
     const Layout lay = make_layout(in_cap, out_cap);
@@ -1598,11 +1862,19 @@ hipError_t launch_zstd_decode(const tyche_batch_t &b, uint32_t in_cap, uint32_t 
     const char *env = getenv("TYCHE_ZSTD_SPLIT");
     const bool split = !(env && env[0] == '0');
     const Layout l1 = make_layout(in_cap, out_cap, false);
+    const char *jenv = getenv("TYCHE_ZSTD_JOBS");   // 0: sequence chains inline in pass 1
+    const bool use_jobs = !(jenv && jenv[0] == '0');
     const uint32_t lds2 = (out_cap + kWinPad + 15u) & ~15u;
     if (!split || l1.total > 160u * 1024u || lds2 > 160u * 1024u) return launch_fused(b, in_cap, out_cap, s);
     const size_t page_bytes = ent_page_bytes(in_cap, out_cap);
+    // the sequence kernel's time per chunk is one page's chain (latency-bound, one
+    // lane per page), so chunks are made as large as memory allows: 16 GiB or a
+    // quarter of the free memory, whichever is less
     const char *mb = getenv("TYCHE_ZSTD_SCRATCH_MB");
-    const size_t budget = (mb && atol(mb) > 0 ? (size_t)atol(mb) : (size_t)4096) << 20;
+    size_t budget = (size_t)16 << 30;
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b / 4 < budget) budget = free_b / 4;
+    if (mb && atol(mb) > 0) budget = (size_t)atol(mb) << 20;
     const size_t chunk = std::max<size_t>(1, std::min<size_t>(b.count, budget / page_bytes));
     const size_t st_bytes = (chunk * 4u + 255u) & ~(size_t)255u;
     ScratchLease ws(s, st_bytes + chunk * page_bytes);
@@ -1620,8 +1892,10 @@ hipError_t launch_zstd_decode(const tyche_batch_t &b, uint32_t in_cap, uint32_t 
             WorkCounter ctr(s, g1 < n);
             if (!ctr.get()) return hipErrorOutOfMemory;
             hipLaunchKernelGGL(zstd_entropy_kernel, dim3((unsigned)g1), dim3(kWave), l1.total, s, b, first, n, in_cap,
-                               out_cap, l1, ent, page_bytes, st, ctr.get());
+                               out_cap, l1, ent, page_bytes, st, ctr.get(), use_jobs);
         }
+        hipLaunchKernelGGL(zstd_seq_kernel, dim3((unsigned)((n + kWave - 1) / kWave)), dim3(kWave), 0, s, b, first, n,
+                           in_cap, out_cap, ent, page_bytes, st);
         const size_t g2 = std::min<size_t>(n, ncu * cu2);
         {
             WorkCounter ctr(s, g2 < n);
