@@ -514,3 +514,20 @@ def test_zstd_fused_kernel_and_chunked_split(tc, oracle_mod, monkeypatch, mode):
     test_zstd_reference_frames(tc, 3)
     test_zstd_malformed(tc, oracle_mod)
     test_zstd_fuzz_vs_oracle(tc, oracle_mod)
+
+
+@pytest.mark.parametrize("mode", ["fused", "chunked"])
+def test_zstd_encode_fused_kernel_and_chunked_split(tc, oracle_mod, monkeypatch, mode):
+    """The one-kernel encoder (TYCHE_ZSTD_ENC_SPLIT=0) and the three-pass encoder run through a
+    1 MiB work area (TYCHE_ZSTD_SCRATCH_MB=1: a few pages per chunk) produce frames the reference
+    decodes: round trips over several distributions and sizes, multi-block and incompressible
+    pages, tight capacities."""
+    if mode == "fused":
+        monkeypatch.setenv("TYCHE_ZSTD_ENC_SPLIT", "0")
+    else:
+        monkeypatch.setenv("TYCHE_ZSTD_SCRATCH_MB", "1")
+    for dist in (0, 3):
+        for plen in (8192, 32768):
+            test_encode_roundtrip_reference_decoder(tc, oracle_mod, dist, plen)
+    test_encode_multiblock_and_incompressible(tc, oracle_mod)
+    test_encode_tight_capacity(tc, oracle_mod, 16)

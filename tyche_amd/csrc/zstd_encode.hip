@@ -141,7 +141,54 @@ struct Enc {
     uint32_t r0, r1, r2; // the decoder's repeat offsets after the blocks emitted so far (initial {1, 4, 8},
                          // zstd_internal.h:73); raw blocks leave them unchanged
     bool fail;
+    uint8_t *area;       // split encode: the page's work area (nullptr: the chain runs here)
+    uint32_t nblk, nrec; // blocks and sequence records written to the area
+    uint32_t rec_cap;
+    __device__ uint32_t nrec_cap() const { return rec_cap; }
 };
+
+// ------------------------------------------------------------ split encode
+// The FSE chain of a block is serial, and at one wave per page it ran as
+// wave-uniform code at the parse's residency (3 waves per CU for 32 KiB pages).
+// Split: pass A (zstd_encode_kernel with an area) writes each block with the FSE
+// bitstream's upper bound left open, plus the sequences' codes and the block's
+// three tables to the page's area; pass B (zstd_fse_kernel, one page per lane)
+// writes the bitstreams into the gaps; pass C (zstd_pack_kernel) closes the gaps
+// and patches the block headers.  Capacity decisions use the bounds, so a page
+// that pass A accepts always fits.
+constexpr uint32_t kMaxBlk = 24;                 // blocks per page (> 65535 / 4 / 960 + 1)
+constexpr uint32_t kBlkWords = 8;                // g_start, g_len, pre, fse (bound, then actual), n, rec, tab, flags
+// one table, packed for pass B's LDS copy: per symbol deltaNbBits | (deltaFindState + 64) << 19
+// (dnb < 2^19: log <= 6, every symbol's maxBitsOut >= 1; dfs in [-64, 63]), then the 64
+// stateTable bytes (values 64..127)
+constexpr uint32_t kCtWords = 64u + 16u;
+constexpr uint32_t kTabBytes = 3u * kCtWords * 4u;   // 960
+constexpr uint32_t kAreaHead = 16u + kMaxBlk * kBlkWords * 4u;
+__host__ __device__ inline size_t enc_area_bytes(uint32_t in_cap) {
+    return ((size_t)kAreaHead + (size_t)kMaxBlk * kTabBytes + ((size_t)in_cap / 4u + 64u) * 16u + 255u) & ~(size_t)255u;
+}
+__host__ __device__ inline uint32_t enc_rec_cap(uint32_t in_cap) { return in_cap / 4u + 64u; }
+__device__ __forceinline__ uint32_t *area_blk(uint8_t *a, uint32_t k) { return (uint32_t *)(a + 16u) + k * kBlkWords; }
+__device__ __forceinline__ uint32_t *area_tab(uint8_t *a, uint32_t k) {
+    return (uint32_t *)(a + kAreaHead + (size_t)k * kTabBytes);
+}
+__device__ __forceinline__ uint4 *area_rec(uint8_t *a) { return (uint4 *)(a + kAreaHead + (size_t)kMaxBlk * kTabBytes); }
+// a block record (lane 0)
+__device__ __forceinline__ void put_blk(Enc &e, uint32_t g_start, uint32_t g_len, uint32_t pre, uint32_t fse, uint32_t n,
+                                        uint32_t rec, uint32_t flags, uint32_t lane) {
+    if (lane == 0) {
+        uint32_t *B = area_blk(e.area, e.nblk);
+        B[0] = g_start;
+        B[1] = g_len;
+        B[2] = pre;
+        B[3] = fse;
+        B[4] = n;
+        B[5] = rec;
+        B[6] = e.nblk;
+        B[7] = flags;
+    }
+    e.nblk++;
+}
 
 // Codes of sequence i of the block, after resolve_repeats.
 __device__ __forceinline__ SeqCode seq_code_at(const Enc &e, uint32_t i) {
@@ -423,13 +470,16 @@ __device__ __forceinline__ bool emit_block(Enc &e, uint32_t bend, bool last, uin
     if (comp_bound >= blen) {
         // ---- raw block (Block_Type 0): header + the page bytes
         if (e.op + 3u + blen > e.cap) return false;
+        if (e.area && e.nblk >= kMaxBlk) return false;
         const uint32_t bh = (last ? 1u : 0u) | (0u << 1) | (blen << 3);
         if (lane < 3) e.dst[hdr + lane] = (uint8_t)(bh >> (8u * lane));
         for (uint32_t j = lane; j < blen; j += kWave) e.dst[hdr + 3u + j] = e.in[e.bstart + j];
+        if (e.area) put_blk(e, hdr, 3u + blen, blen, 0u, 0u, 0u, last ? 1u : 0u, lane);
         e.op += 3u + blen;
         return true;
     }
     if (e.op + 3u + comp_bound > e.cap) return false;
+    if (e.area && (e.nblk >= kMaxBlk || e.nrec + n > e.nrec_cap())) return false;
     uint32_t o = hdr + 3u;
     // ---- literals section: Huffman-compressed when it pays, else raw (ZSTD_noCompressLiterals)
     SPROF_MARK(2);
@@ -513,6 +563,37 @@ __device__ __forceinline__ bool emit_block(Enc &e, uint32_t bend, bool last, uin
         if (lane == 0) e.dst[mpos] = dyn ? (uint8_t)((2u << 6) | (2u << 4) | (2u << 2)) : 0u;
         SPROF_MARK(4);
         SPROF_ADD(9, n);
+        if (e.area) {
+            // pass A: the codes and tables go to the area, the bitstream's bound stays open
+            uint4 *R = area_rec(e.area) + e.nrec;
+            for (uint32_t g = 0; g < n; g += kWave) {
+                const uint32_t i = g + lane;
+                if (i < n) {
+                    const SeqCode c = seq_code_at(e, i);
+                    R[i] = make_uint4(c.llc | (c.mlc << 8) | (c.ofc << 16), c.llv | (c.llb << 24), c.mlv | (c.mlb << 24),
+                                      c.ofv);
+                }
+            }
+            uint32_t *T = area_tab(e.area, e.nblk);
+            const huf::SmallCT *ts[3] = {&tll, &tof, &tml};
+#pragma unroll
+            for (uint32_t t = 0; t < 3; t++) {
+                T[t * kCtWords + lane] = ts[t]->dnb | ((uint32_t)(ts[t]->dfs + 64) << 19);
+                ((uint8_t *)(T + t * kCtWords + 64u))[lane] = (uint8_t)ts[t]->state;
+            }
+            const uint32_t pre = o - (hdr + 3u);
+            const uint32_t glen = 3u + pre + fse_bound;
+            const uint32_t bh = (last ? 1u : 0u) | (2u << 1) | ((glen - 3u) << 3);
+            if (lane < 3) e.dst[hdr + lane] = (uint8_t)(bh >> (8u * lane));
+            put_blk(e, hdr, glen, pre, fse_bound, n, e.nrec, (last ? 1u : 0u) | 2u, lane);
+            e.nrec += n;
+            e.op = hdr + glen;
+            e.r0 = h0;
+            e.r1 = h1;
+            e.r2 = h2;
+            SPROF_MARK(5);
+            return true;
+        }
         // ---- FSE bitstream: groups of 64 sequences from the last, serial inside a group
         huf::BitW b;
         b.c = 0;
@@ -570,6 +651,7 @@ __device__ __forceinline__ bool emit_block(Enc &e, uint32_t bend, bool last, uin
     const uint32_t csize = o - (hdr + 3u);
     const uint32_t bh = (last ? 1u : 0u) | (2u << 1) | (csize << 3);
     if (lane < 3) e.dst[hdr + lane] = (uint8_t)(bh >> (8u * lane));
+    if (e.area) put_blk(e, hdr, 3u + csize, csize, 0u, 0u, 0u, last ? 1u : 0u, lane);
     e.op = o;
     e.r0 = h0;
     e.r1 = h1;
@@ -580,7 +662,8 @@ __device__ __forceinline__ bool emit_block(Enc &e, uint32_t bend, bool last, uin
 // Encodes one page held in LDS (in[0, L), 64 zero bytes after).  Returns the
 // frame size, or 0 if it does not fit in cap.
 __device__ __forceinline__ int32_t encode_page(const uint8_t *in, uint32_t L, uint16_t *table, uint8_t *map, uint2 *rec, uint2 *seq,
-                               uint32_t *htab, uint8_t *wts, uint8_t *dst, uint32_t cap, uint32_t lane) {
+                               uint32_t *htab, uint8_t *wts, uint8_t *dst, uint32_t cap, uint32_t lane,
+                               uint8_t *area = nullptr, uint32_t rec_cap = 0) {
     // ---- frame header: magic, single-segment descriptor with the content size
     const uint32_t fcs_id = L < 256u ? 0u : (L < 65536u + 256u ? 1u : 2u);
     const uint32_t fcs_len = fcs_id == 0u ? 1u : (fcs_id == 1u ? 2u : 4u);
@@ -611,6 +694,10 @@ __device__ __forceinline__ int32_t encode_page(const uint8_t *in, uint32_t L, ui
     e.wts = wts;
     e.stage = (uint32_t *)rec;
     e.fail = false;
+    e.area = area;
+    e.nblk = 0;
+    e.nrec = 0;
+    e.rec_cap = rec_cap;
     auto sink = [&](const uint2 *r, uint32_t n, uint32_t anchor) -> bool {
         uint32_t ls, ll, ml, off;
         lzp::decode_record(r, n, anchor, lane, ls, ll, ml, off);
@@ -632,10 +719,14 @@ __device__ __forceinline__ int32_t encode_page(const uint8_t *in, uint32_t L, ui
     if (!emit_block(e, L, true, lane)) return 0;
     SPROF_MARK(1);   // whole page (parse + every block)
     SPROF_ADD(0, 1);
+    if (area && lane == 0) ((uint32_t *)area)[0] = e.nblk;
     return (int32_t)e.op;
 }
 
-__global__ __launch_bounds__(64) void zstd_encode_kernel(tyche_batch_t b, uint32_t in_cap, unsigned *ctr) {
+// Pages [first, first + count) of b.  ws == nullptr: the whole encode (results to
+// b.results); else pass A of the split encode (results to st, areas in ws).
+__global__ __launch_bounds__(64) void zstd_encode_kernel(tyche_batch_t b, size_t first, size_t count, uint32_t in_cap,
+                                                         unsigned *ctr, uint8_t *ws, size_t ws_page, int32_t *st) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t lane = threadIdx.x;
     uint16_t *table = (uint16_t *)smem;
@@ -647,17 +738,17 @@ __global__ __launch_bounds__(64) void zstd_encode_kernel(tyche_batch_t b, uint32
     uint8_t *stage = wts + 256;
     const size_t stride = gridDim.x;
 
-    size_t page = blockIdx.x;
-    if (page >= b.count) return;
-    PageRef p = batch_page(b, page);
+    size_t page = blockIdx.x;   // chunk-local
+    if (page >= count) return;
+    PageRef p = batch_page(b, first + page);
     uint32_t head = stage_in(p.src, p.src_len <= in_cap ? p.src_len : 0, stage, lane, kWave);
     for (;;) {
         const size_t next = ctr ? claim_page(ctr, lane) : page + stride;   // dynamic assignment (engine.h)
         PageRef pn;
         u32x4 pf[kPrefetchVec];
         uint32_t nhead = 0, nvec = 0;
-        if (next < b.count) {
-            pn = batch_page(b, next);
+        if (next < count) {
+            pn = batch_page(b, first + next);
             if (pn.src_len <= in_cap && pn.src_len > 0) {
                 uintptr_t a = (uintptr_t)pn.src;
                 nhead = (uint32_t)(a & 15u);
@@ -679,10 +770,14 @@ __global__ __launch_bounds__(64) void zstd_encode_kernel(tyche_batch_t b, uint32
             WAVE_SYNC();
             in[p.src_len + lane] = 0;
             WAVE_SYNC();
-            rv = encode_page(in, p.src_len, table, map, rec, seq, htab, wts, p.dst, p.dst_cap, lane);
+            rv = encode_page(in, p.src_len, table, map, rec, seq, htab, wts, p.dst, p.dst_cap, lane,
+                             ws ? ws + page * ws_page : nullptr, enc_rec_cap(in_cap));
         }
-        if (lane == 0) b.results[page] = rv;
-        if (next >= b.count) break;
+        if (lane == 0) {
+            if (ws) st[page] = rv;
+            else b.results[first + page] = rv;
+        }
+        if (next >= count) break;
         WAVE_SYNC();
         page = next;
         p = pn;
@@ -700,6 +795,173 @@ __global__ __launch_bounds__(64) void zstd_encode_kernel(tyche_batch_t b, uint32
     }
 }
 
+// ---- pass B: the FSE bitstreams, one page per lane
+
+// Appends bytes to global memory in aligned 8-byte words (bytes only at the ends)
+struct ByteSink {
+    uintptr_t addr;   // next byte
+    uint64_t w;       // pending bytes of the word holding addr
+    uint32_t lo;      // first byte of that word that is ours
+};
+__device__ __forceinline__ void sink_word(uintptr_t a, uint64_t w, uint32_t lo, uint32_t hi) {
+    if (lo == 0 && hi == 8) {
+        *(uint64_t *)a = w;
+    } else {
+        for (uint32_t k = lo; k < hi; k++) ((uint8_t *)a)[k] = (uint8_t)(w >> (8u * k));
+    }
+}
+__device__ __forceinline__ void sink_put(ByteSink &s, uint64_t v, uint32_t nb) {   // nb <= 7 low bytes of v
+    if (nb == 0) return;
+    v &= (1ull << (8u * nb)) - 1ull;
+    const uint32_t k = (uint32_t)(s.addr & 7u);
+    s.w |= v << (8u * k);
+    if (k + nb >= 8u) {
+        sink_word(s.addr - k, s.w, s.lo, 8u);
+        s.w = v >> (8u * (8u - k));
+        s.lo = 0;
+    }
+    s.addr += nb;
+}
+__device__ __forceinline__ void sink_end(ByteSink &s) {
+    const uint32_t k = (uint32_t)(s.addr & 7u);
+    if (k > s.lo) sink_word(s.addr - k, s.w, s.lo, k);
+}
+
+struct LaneBits {
+    uint64_t c;
+    uint32_t pos;
+};
+__device__ __forceinline__ void lb_add(LaneBits &b, uint32_t v, uint32_t nb) {
+    b.c |= (uint64_t)(v & ((1u << nb) - 1u)) << b.pos;
+    b.pos += nb;
+}
+__device__ __forceinline__ void lb_flush(LaneBits &b, ByteSink &s) {   // BIT_flushBits
+    const uint32_t nbytes = b.pos >> 3;
+    sink_put(s, b.c, nbytes);
+    b.pos &= 7u;
+    b.c = nbytes >= 8u ? 0ull : b.c >> (8u * nbytes);
+}
+// FSE_initCState2 / FSE_encodeSymbol over a packed table (kCtWords) in LDS
+__device__ __forceinline__ uint32_t lct_init2(const uint32_t *T, uint32_t sym) {
+    const uint32_t pk = T[sym], dnb = pk & 0x7FFFFu;
+    const uint32_t nbo = (dnb + (1u << 15)) >> 16;
+    const uint32_t v = (nbo << 16) - dnb;
+    return ((const uint8_t *)(T + 64u))[(uint32_t)((int32_t)(v >> nbo) + (int32_t)(pk >> 19) - 64)];
+}
+__device__ __forceinline__ void lct_encode(LaneBits &b, uint32_t &st, const uint32_t *T, uint32_t sym) {
+    const uint32_t pk = T[sym];
+    const uint32_t nbo = (st + (pk & 0x7FFFFu)) >> 16;
+    lb_add(b, st, nbo);
+    st = ((const uint8_t *)(T + 64u))[(uint32_t)((int32_t)(st >> nbo) + (int32_t)(pk >> 19) - 64)];
+}
+
+// ZSTD_compressSequences' bitstream (zstd_compress.c:695-735) for n >= 1
+// sequences; the same steps as emit_block's wave-uniform loop.  Returns its size.
+__device__ uint32_t fse_lane(uint8_t *out, const uint4 *R, uint32_t n, const uint32_t *T) {
+    const uint32_t *tll = T, *tof = T + kCtWords, *tml = T + 2u * kCtWords;
+    ByteSink s;
+    s.addr = (uintptr_t)out;
+    s.w = 0;
+    s.lo = (uint32_t)(s.addr & 7u);
+    LaneBits b;
+    b.c = 0;
+    b.pos = 0;
+    uint32_t sll = 0, sml = 0, sof = 0;
+    uint4 nx = R[n - 1u];
+    for (uint32_t i = n; i-- > 0;) {
+        const uint4 r = nx;
+        if (i) nx = R[i - 1u];   // the next record is loaded a step ahead
+        const uint32_t llc = r.x & 0xFFu, mlc = (r.x >> 8) & 0xFFu, ofc = r.x >> 16;
+        const uint32_t llb = r.y >> 24, mlb = r.z >> 24;
+        if (i == n - 1u) {
+            sml = lct_init2(tml, mlc);
+            sof = lct_init2(tof, ofc);
+            sll = lct_init2(tll, llc);
+        } else {
+            lct_encode(b, sof, tof, ofc);
+            lct_encode(b, sml, tml, mlc);
+            lct_encode(b, sll, tll, llc);
+            if (ofc + mlb + llb >= 64u - 7u - (9u + 9u + 8u)) lb_flush(b, s);
+        }
+        lb_add(b, r.y & 0xFFFFFFu, llb);
+        lb_add(b, r.z & 0xFFFFFFu, mlb);
+        lb_add(b, r.w, ofc);
+        lb_flush(b, s);
+    }
+    lb_add(b, sml, 6u);
+    lb_flush(b, s);
+    lb_add(b, sof, 5u);
+    lb_flush(b, s);
+    lb_add(b, sll, 6u);
+    lb_flush(b, s);
+    lb_add(b, 1u, 1u);
+    lb_flush(b, s);
+    if (b.pos > 0) sink_put(s, b.c, 1u);
+    sink_end(s);
+    return (uint32_t)(s.addr - (uintptr_t)out);
+}
+
+// Each lane copies its block's three tables (960 bytes) into its own LDS slot.
+__global__ __launch_bounds__(64) void zstd_fse_kernel(tyche_batch_t b, size_t first, size_t count, uint8_t *ws,
+                                                      size_t ws_page, const int32_t *st) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const size_t j = (size_t)blockIdx.x * kWave + threadIdx.x;
+    if (j >= count || st[j] <= 0) return;
+    uint8_t *area = ws + j * ws_page;
+    const uint32_t nblk = ((const uint32_t *)area)[0];
+    uint8_t *dst = batch_page(b, first + j).dst;
+    uint32_t *lt = (uint32_t *)smem + threadIdx.x * (3u * kCtWords);
+    for (uint32_t k = 0; k < nblk; k++) {
+        uint32_t *B = area_blk(area, k);
+        if (!(B[7] & 2u)) continue;
+        const u32x4 *g = (const u32x4 *)area_tab(area, B[6]);
+#pragma unroll 4
+        for (uint32_t w = 0; w < 3u * kCtWords / 4u; w++) ((u32x4 *)lt)[w] = g[w];
+        B[3] = fse_lane(dst + B[0] + 3u + B[2], area_rec(area) + B[5], B[4], lt);
+    }
+}
+
+// ---- pass C: close the gaps, patch the compressed blocks' headers
+__global__ __launch_bounds__(64) void zstd_pack_kernel(tyche_batch_t b, size_t first, size_t count, uint8_t *ws,
+                                                       size_t ws_page, const int32_t *st, unsigned *ctr) {
+    const uint32_t lane = threadIdx.x;
+    for (size_t j = blockIdx.x; j < count; j = ctr ? claim_page(ctr, lane) : j + gridDim.x) {
+        int32_t rv = st[j];
+        if (rv > 0) {
+            const uint8_t *area = ws + j * ws_page;
+            const uint32_t nblk = __builtin_amdgcn_readfirstlane(((const uint32_t *)area)[0]);
+            uint8_t *dst = batch_page(b, first + j).dst;
+            uint32_t q = 0;
+            for (uint32_t k = 0; k < nblk; k++) {
+                const uint32_t *B = (const uint32_t *)(area + 16u) + k * kBlkWords;
+                const uint32_t g = __builtin_amdgcn_readfirstlane(B[0]), glen = __builtin_amdgcn_readfirstlane(B[1]);
+                const uint32_t pre = __builtin_amdgcn_readfirstlane(B[2]), fse = __builtin_amdgcn_readfirstlane(B[3]);
+                const uint32_t fl = __builtin_amdgcn_readfirstlane(B[7]);
+                if (k == 0) q = g;   // the frame header stays
+                const bool comp = (fl & 2u) != 0;
+                const uint32_t clen = comp ? 3u + pre + fse : glen;
+                const uint32_t bh = (fl & 1u) | (2u << 1) | ((pre + fse) << 3);
+                if (g == q) {
+                    if (comp && lane < 3) dst[q + lane] = (uint8_t)(bh >> (8u * lane));
+                } else {
+                    // left move in 64-byte steps: a step's reads precede its writes
+                    for (uint32_t c0 = 0; c0 < clen; c0 += kWave) {
+                        const uint32_t i = c0 + lane;
+                        uint8_t v = i < clen ? dst[g + i] : 0;
+                        if (comp && i < 3u) v = (uint8_t)(bh >> (8u * i));
+                        __builtin_amdgcn_wave_barrier();
+                        if (i < clen) dst[q + i] = v;
+                        __builtin_amdgcn_wave_barrier();
+                    }
+                }
+                q += clen;
+            }
+            rv = (int32_t)q;
+        }
+        if (lane == 0) b.results[first + j] = rv;
+    }
+}
+
 }  // namespace
 
 #ifdef TYCHE_PROFILE
@@ -712,6 +974,7 @@ extern "C" int tyche_debug_zstd_encode_profile(unsigned long long *host16, int r
 }
 #endif
 
+// TYCHE_ZSTD_ENC_SPLIT: 1 (default) three-pass encode (chains lane-per-page), 0 one kernel.
 hipError_t launch_zstd_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream_t s) {
     if (b.count == 0) return hipSuccess;
     if (in_cap > 65535u) return hipErrorInvalidValue;    // 16-bit positions in the parse and sequence records
@@ -719,11 +982,48 @@ hipError_t launch_zstd_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream
                        ((in_cap + 16u + kPad + 15u) & ~15u);
     const size_t ncu = prepare_launch((const void *)zstd_encode_kernel);
     const size_t per_cu = waves_per_cu((const void *)zstd_encode_kernel, lds);
-    const size_t grid = std::min<size_t>(b.count, ncu * per_cu);
-    WorkCounter ctr(s, grid < b.count);
-    if (!ctr.get()) return hipErrorOutOfMemory;
-    hipLaunchKernelGGL(zstd_encode_kernel, dim3((unsigned)grid), dim3(kWave), lds, s, b, in_cap, ctr.get());
-    return hipGetLastError();
+    const char *env = getenv("TYCHE_ZSTD_ENC_SPLIT");
+    const bool split = !(env && env[0] == '0');
+    const size_t page_bytes = enc_area_bytes(in_cap);
+    size_t chunk = b.count;
+    uint8_t *ws = nullptr;
+    int32_t *st = nullptr;
+    size_t budget = (size_t)8 << 30;
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b / 8 < budget) budget = free_b / 8;
+    const char *mb = getenv("TYCHE_ZSTD_SCRATCH_MB");
+    if (mb && atol(mb) > 0) budget = (size_t)atol(mb) << 20;
+    if (split) chunk = std::max<size_t>(1, std::min<size_t>(b.count, budget / page_bytes));
+    const size_t st_bytes = (chunk * 4u + 255u) & ~(size_t)255u;
+    ScratchLease lease(s, split ? st_bytes + chunk * page_bytes : 0);
+    if (split && lease.get()) {
+        st = (int32_t *)lease.get();
+        ws = (uint8_t *)lease.get() + st_bytes;
+    } else {
+        chunk = b.count;
+    }
+    for (size_t first = 0; first < b.count; first += chunk) {
+        const size_t n = std::min(chunk, b.count - first);
+        const size_t grid = std::min<size_t>(n, ncu * per_cu);
+        {
+            WorkCounter ctr(s, grid < n);
+            if (!ctr.get()) return hipErrorOutOfMemory;
+            hipLaunchKernelGGL(zstd_encode_kernel, dim3((unsigned)grid), dim3(kWave), lds, s, b, first, n, in_cap,
+                               ctr.get(), ws, page_bytes, st);
+        }
+        if (ws) {
+            hipLaunchKernelGGL(zstd_fse_kernel, dim3((unsigned)((n + kWave - 1) / kWave)), dim3(kWave),
+                               kWave * kTabBytes, s, b, first, n, ws, page_bytes, (const int32_t *)st);
+            const size_t g3 = std::min<size_t>(n, ncu * 8u);
+            WorkCounter ctr(s, g3 < n);
+            if (!ctr.get()) return hipErrorOutOfMemory;
+            hipLaunchKernelGGL(zstd_pack_kernel, dim3((unsigned)g3), dim3(kWave), 0, s, b, first, n, ws, page_bytes,
+                               (const int32_t *)st, ctr.get());
+        }
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 }  // namespace tyche
