@@ -183,8 +183,16 @@ __device__ __forceinline__ void decode_record(const uint2 *rec, uint32_t n, uint
 #ifndef TYCHE_WAYS_SCALE
 #define TYCHE_WAYS_SCALE 2   // bucketed tables hold TYCHE_WAYS_SCALE * kHashSize slots
 #endif
-template <int kWays>
-__host__ __device__ constexpr uint32_t table_slots() { return kWays > 1 ? TYCHE_WAYS_SCALE * kHashSize : kHashSize; }
+// kRepCand (zstd) with 2 ways: TYCHE_ZSTD_BUCKETS buckets, not a power of two --
+// 1856 buckets (7,424 bytes) keep a 32 KiB page's parse at 40,848 bytes of LDS,
+// 4 waves per CU (zstd_encode.hip); the bucket is the high product of the hash
+#ifndef TYCHE_ZSTD_BUCKETS
+#define TYCHE_ZSTD_BUCKETS 1856
+#endif
+template <int kWays, bool kRepCand = false>
+__host__ __device__ constexpr uint32_t table_slots() {
+    return kRepCand && kWays == 2 ? 2u * TYCHE_ZSTD_BUCKETS : kWays > 1 ? TYCHE_WAYS_SCALE * kHashSize : kHashSize;
+}
 
 template <int kWays>
 __device__ __forceinline__ uint32_t bucket_of(uint32_t v, uint32_t v2 = 0, uint32_t nbytes = 4) {
@@ -193,7 +201,9 @@ __device__ __forceinline__ uint32_t bucket_of(uint32_t v, uint32_t v2 = 0, uint3
     static_assert((1u << lg) == nb, "bucket count is a power of two");
     if (nbytes > 4) {   // 5 or 6 bytes: zstd's fast parse hashes searchLength bytes (ZSTD_hashPtr)
         const uint64_t x = ((uint64_t)(v2 & (nbytes == 5 ? 0xFFu : 0xFFFFu)) << 32) | v;
-        return (uint32_t)((x * 0xCF1BBCDCB7A56463ull) >> (64 - lg));
+        const uint64_t hx = x * 0xCF1BBCDCB7A56463ull;
+        if (kWays == 2) return (uint32_t)(((hx >> 32) * (uint64_t)TYCHE_ZSTD_BUCKETS) >> 32);
+        return (uint32_t)(hx >> (64 - lg));
     }
     return (v * 2654435761u) >> (32 - lg);
 }

@@ -65,7 +65,7 @@ using lzp::kHashSize;
 #define TYCHE_ZSTD_WAYS 2   // candidates per hash bucket (lz_parse.h kWays)
 #endif
 constexpr int kZWays = TYCHE_ZSTD_WAYS;
-constexpr uint32_t kTableSlots = lzp::table_slots<kZWays>();
+constexpr uint32_t kTableSlots = lzp::table_slots<kZWays, true>();
 using lzp::kWave;
 constexpr uint32_t kPad = 64;
 constexpr uint32_t kSeqCap = 1024;       // sequences buffered per block
@@ -150,12 +150,14 @@ struct Enc {
 // ------------------------------------------------------------ split encode
 // The FSE chain of a block is serial, and at one wave per page it ran as
 // wave-uniform code at the parse's residency (3 waves per CU for 32 KiB pages).
-// Split: pass A (zstd_encode_kernel with an area) writes each block with the FSE
-// bitstream's upper bound left open, plus the sequences' codes and the block's
-// three tables to the page's area; pass B (zstd_fse_kernel, one page per lane)
-// writes the bitstreams into the gaps; pass C (zstd_pack_kernel) closes the gaps
-// and patches the block headers.  Capacity decisions use the bounds, so a page
-// that pass A accepts always fits.
+// Split: pass A1 (zstd_parse_kernel) runs the parse alone -- LDS = page + hash
+// table, 4 waves per CU at 32 KiB -- and writes the sequences and the block
+// boundaries to the page's area; pass A2 (zstd_block_kernel, a few KiB of LDS)
+// emits each block with the FSE bitstream's upper bound left open, plus the
+// sequences' codes and the block's three tables; pass B (zstd_fse_kernel, one
+// page per lane) writes the bitstreams into the gaps; pass C (zstd_pack_kernel)
+// closes the gaps and patches the block headers.  Capacity decisions use the
+// bounds, so a page that pass A2 accepts always fits.
 constexpr uint32_t kMaxBlk = 24;                 // blocks per page (> 65535 / 4 / 960 + 1)
 constexpr uint32_t kBlkWords = 8;                // g_start, g_len, pre, fse (bound, then actual), n, rec, tab, flags
 // one table, packed for pass B's LDS copy: per symbol deltaNbBits | (deltaFindState + 64) << 19
@@ -163,16 +165,23 @@ constexpr uint32_t kBlkWords = 8;                // g_start, g_len, pre, fse (bo
 // stateTable bytes (values 64..127)
 constexpr uint32_t kCtWords = 64u + 16u;
 constexpr uint32_t kTabBytes = 3u * kCtWords * 4u;   // 960
-constexpr uint32_t kAreaHead = 16u + kMaxBlk * kBlkWords * 4u;
-__host__ __device__ inline size_t enc_area_bytes(uint32_t in_cap) {
-    return ((size_t)kAreaHead + (size_t)kMaxBlk * kTabBytes + ((size_t)in_cap / 4u + 64u) * 16u + 255u) & ~(size_t)255u;
-}
+constexpr uint32_t kPblkWords = 4;   // parse blocks: page start, page end, first sequence, sequences
+constexpr uint32_t kAreaHead = 16u + kMaxBlk * kBlkWords * 4u + kMaxBlk * kPblkWords * 4u;
+// area: [0] emitted blocks, [1] parse blocks | block records | parse blocks | tables |
+//       sequence codes (16 B, pass B) | the parse's sequences (8 B, pass A2)
 __host__ __device__ inline uint32_t enc_rec_cap(uint32_t in_cap) { return in_cap / 4u + 64u; }
+__host__ __device__ inline size_t enc_area_bytes(uint32_t in_cap) {
+    return ((size_t)kAreaHead + (size_t)kMaxBlk * kTabBytes + (size_t)enc_rec_cap(in_cap) * 24u + 255u) & ~(size_t)255u;
+}
 __device__ __forceinline__ uint32_t *area_blk(uint8_t *a, uint32_t k) { return (uint32_t *)(a + 16u) + k * kBlkWords; }
+__device__ __forceinline__ uint32_t *area_pblk(uint8_t *a, uint32_t k) {
+    return (uint32_t *)(a + 16u + kMaxBlk * kBlkWords * 4u) + k * kPblkWords;
+}
 __device__ __forceinline__ uint32_t *area_tab(uint8_t *a, uint32_t k) {
     return (uint32_t *)(a + kAreaHead + (size_t)k * kTabBytes);
 }
 __device__ __forceinline__ uint4 *area_rec(uint8_t *a) { return (uint4 *)(a + kAreaHead + (size_t)kMaxBlk * kTabBytes); }
+__device__ __forceinline__ uint2 *area_seq(uint8_t *a, uint32_t rec_cap) { return (uint2 *)(area_rec(a) + rec_cap); }
 // a block record (lane 0)
 __device__ __forceinline__ void put_blk(Enc &e, uint32_t g_start, uint32_t g_len, uint32_t pre, uint32_t fse, uint32_t n,
                                         uint32_t rec, uint32_t flags, uint32_t lane) {
@@ -662,8 +671,7 @@ __device__ __forceinline__ bool emit_block(Enc &e, uint32_t bend, bool last, uin
 // Encodes one page held in LDS (in[0, L), 64 zero bytes after).  Returns the
 // frame size, or 0 if it does not fit in cap.
 __device__ __forceinline__ int32_t encode_page(const uint8_t *in, uint32_t L, uint16_t *table, uint8_t *map, uint2 *rec, uint2 *seq,
-                               uint32_t *htab, uint8_t *wts, uint8_t *dst, uint32_t cap, uint32_t lane,
-                               uint8_t *area = nullptr, uint32_t rec_cap = 0) {
+                               uint32_t *htab, uint8_t *wts, uint8_t *dst, uint32_t cap, uint32_t lane) {
     // ---- frame header: magic, single-segment descriptor with the content size
     const uint32_t fcs_id = L < 256u ? 0u : (L < 65536u + 256u ? 1u : 2u);
     const uint32_t fcs_len = fcs_id == 0u ? 1u : (fcs_id == 1u ? 2u : 4u);
@@ -694,10 +702,10 @@ __device__ __forceinline__ int32_t encode_page(const uint8_t *in, uint32_t L, ui
     e.wts = wts;
     e.stage = (uint32_t *)rec;
     e.fail = false;
-    e.area = area;
+    e.area = nullptr;
     e.nblk = 0;
     e.nrec = 0;
-    e.rec_cap = rec_cap;
+    e.rec_cap = 0;
     auto sink = [&](const uint2 *r, uint32_t n, uint32_t anchor) -> bool {
         uint32_t ls, ll, ml, off;
         lzp::decode_record(r, n, anchor, lane, ls, ll, ml, off);
@@ -719,12 +727,102 @@ __device__ __forceinline__ int32_t encode_page(const uint8_t *in, uint32_t L, ui
     if (!emit_block(e, L, true, lane)) return 0;
     SPROF_MARK(1);   // whole page (parse + every block)
     SPROF_ADD(0, 1);
-    if (area && lane == 0) ((uint32_t *)area)[0] = e.nblk;
     return (int32_t)e.op;
 }
 
-// Pages [first, first + count) of b.  ws == nullptr: the whole encode (results to
-// b.results); else pass A of the split encode (results to st, areas in ws).
+// Pass A1: the parse of one page (LDS, 64 zero bytes after) into the area: the
+// sequences, and blocks cut where encode_page's sink cuts them.  Returns 1, or
+// 0 when a bound is exceeded (the page is then stored uncompressed by the caller).
+__device__ __forceinline__ int32_t parse_to_area(const uint8_t *in, uint32_t L, uint16_t *table, uint2 *rec,
+                                                 uint8_t *area, uint32_t rec_cap, uint32_t lane) {
+    uint2 *S = area_seq(area, rec_cap);
+    uint32_t nseq = 0, bseq = 0, bstart = 0, cursor = 0, npb = 0;
+    auto put_pblk = [&](uint32_t bend) {
+        if (lane == 0) {
+            uint32_t *P = area_pblk(area, npb);
+            P[0] = bstart;
+            P[1] = bend;
+            P[2] = bseq;
+            P[3] = nseq - bseq;
+        }
+        npb++;
+    };
+    auto sink = [&](const uint2 *r, uint32_t n, uint32_t anchor) -> bool {
+        uint32_t ls, ll, ml, off;
+        lzp::decode_record(r, n, anchor, lane, ls, ll, ml, off);
+        if (nseq + n > rec_cap) return false;
+        if (lane < n) S[nseq + lane] = make_uint2(ll | (off << 16), ml);
+        nseq += n;
+        const uint2 lastr = r[n - 1];
+        cursor = (lastr.x & 0xFFFFu) + (lastr.y & 0xFFFFu);
+        __builtin_amdgcn_wave_barrier();
+        if (nseq - bseq > kSeqCap - kWave) {
+            if (npb + 1u >= kMaxBlk) return false;
+            put_pblk(cursor);
+            bstart = cursor;
+            bseq = nseq;
+        }
+        return true;
+    };
+    const uint32_t anchor = lzp::parse_page<true, false, kZWays>(in, L, table, rec, lane, sink);
+    if (anchor == 0xFFFFFFFFu) return 0;
+    put_pblk(L);
+    if (lane == 0) ((uint32_t *)area)[1] = npb;
+    return 1;
+}
+
+// Pass A2: frame header and every block of the page from the area (the page
+// itself is read from global memory).  Returns the gapped frame size or 0.
+__device__ __forceinline__ int32_t emit_page(const uint8_t *src, uint32_t L, uint8_t *area, uint32_t rec_cap,
+                                             uint8_t *map, uint2 *stage, uint32_t *htab, uint8_t *wts, uint8_t *dst,
+                                             uint32_t cap, uint32_t lane) {
+    const uint32_t fcs_id = L < 256u ? 0u : (L < 65536u + 256u ? 1u : 2u);
+    const uint32_t fcs_len = fcs_id == 0u ? 1u : (fcs_id == 1u ? 2u : 4u);
+    const uint32_t fh = 5u + fcs_len;
+    if (fh + 3u > cap) return 0;
+    {
+        const uint32_t fcs = fcs_id == 1u ? L - 256u : L;
+        uint32_t v = 0;
+        if (lane < 4) v = 0xFD2FB528u >> (8u * lane);
+        else if (lane == 4) v = 0x20u | (fcs_id << 6);
+        else if (lane < 5u + fcs_len) v = fcs >> (8u * (lane - 5u));
+        if (lane < fh) dst[lane] = (uint8_t)v;
+    }
+    Enc e;
+    e.in = src;
+    e.dst = dst;
+    e.cap = cap;
+    e.op = fh;
+    e.map = map;
+    e.r0 = 1u;
+    e.r1 = 4u;
+    e.r2 = 8u;
+    e.htab = htab;
+    e.wts = wts;
+    e.stage = (uint32_t *)stage;
+    e.fail = false;
+    e.area = area;
+    e.nblk = 0;
+    e.nrec = 0;
+    e.rec_cap = rec_cap;
+    e.cursor = 0;
+    const uint32_t npb = __builtin_amdgcn_readfirstlane(((const uint32_t *)area)[1]);
+    uint2 *S = area_seq(area, rec_cap);
+    for (uint32_t k = 0; k < npb; k++) {
+        const uint32_t *P = area_pblk(area, k);
+        e.bstart = __builtin_amdgcn_readfirstlane(P[0]);
+        const uint32_t bend = __builtin_amdgcn_readfirstlane(P[1]);
+        e.seq = S + __builtin_amdgcn_readfirstlane(P[2]);
+        e.nseq = __builtin_amdgcn_readfirstlane(P[3]);
+        if (!emit_block(e, bend, k + 1u == npb, lane)) return 0;
+    }
+    if (lane == 0) ((uint32_t *)area)[0] = e.nblk;
+    return (int32_t)e.op;
+}
+
+// The one-kernel encode of pages [first, first + count) of b (TYCHE_ZSTD_ENC_SPLIT=0).
+// kParse: pass A1 of the split encode instead (the parse only, into ws; status to st).
+template <bool kParse>
 __global__ __launch_bounds__(64) void zstd_encode_kernel(tyche_batch_t b, size_t first, size_t count, uint32_t in_cap,
                                                          unsigned *ctr, uint8_t *ws, size_t ws_page, int32_t *st) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -735,7 +833,7 @@ __global__ __launch_bounds__(64) void zstd_encode_kernel(tyche_batch_t b, size_t
     uint2 *seq = rec + kWave;                                          // kSeqCap block sequences
     uint32_t *htab = (uint32_t *)(seq + kSeqCap);                      // literal histogram / Huffman codes
     uint8_t *wts = (uint8_t *)(htab + kHtab);                          // Huffman weights
-    uint8_t *stage = wts + 256;
+    uint8_t *stage = kParse ? (uint8_t *)seq : wts + 256;               // A1: no block buffers
     const size_t stride = gridDim.x;
 
     size_t page = blockIdx.x;   // chunk-local
@@ -770,11 +868,11 @@ __global__ __launch_bounds__(64) void zstd_encode_kernel(tyche_batch_t b, size_t
             WAVE_SYNC();
             in[p.src_len + lane] = 0;
             WAVE_SYNC();
-            rv = encode_page(in, p.src_len, table, map, rec, seq, htab, wts, p.dst, p.dst_cap, lane,
-                             ws ? ws + page * ws_page : nullptr, enc_rec_cap(in_cap));
+            if (kParse) rv = parse_to_area(in, p.src_len, table, rec, ws + page * ws_page, enc_rec_cap(in_cap), lane);
+            else rv = encode_page(in, p.src_len, table, map, rec, seq, htab, wts, p.dst, p.dst_cap, lane);
         }
         if (lane == 0) {
-            if (ws) st[page] = rv;
+            if (kParse) st[page] = rv;
             else b.results[first + page] = rv;
         }
         if (next >= count) break;
@@ -792,6 +890,27 @@ __global__ __launch_bounds__(64) void zstd_encode_kernel(tyche_batch_t b, size_t
             const u32x4 *g = (const u32x4 *)((uintptr_t)p.src - nhead);
             for (uint32_t v = lane + kPrefetchVec * kWave; v < nvec; v += kWave) l[v] = gload_nt(g + v);
         }
+    }
+}
+
+// ---- pass A2
+constexpr uint32_t kA2Lds = kWave + kWave * 8u + kHtab * 4u + 256u;   // map, stage, htab, weights
+__global__ __launch_bounds__(64) void zstd_block_kernel(tyche_batch_t b, size_t first, size_t count, uint32_t in_cap,
+                                                        uint8_t *ws, size_t ws_page, int32_t *st, unsigned *ctr) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint32_t lane = threadIdx.x;
+    uint8_t *map = smem;
+    uint2 *stage = (uint2 *)(smem + kWave);
+    uint32_t *htab = (uint32_t *)(stage + kWave);
+    uint8_t *wts = (uint8_t *)(htab + kHtab);
+    for (size_t j = blockIdx.x; j < count; j = ctr ? claim_page(ctr, lane) : j + gridDim.x) {
+        const int32_t s0 = st[j];
+        if (s0 != 1) continue;   // 0: does not fit; kResultTooLarge passes through
+        const PageRef p = batch_page(b, first + j);
+        WAVE_SYNC();
+        const int32_t rv = emit_page(p.src, p.src_len, ws + j * ws_page, enc_rec_cap(in_cap), map, stage, htab, wts,
+                                     p.dst, p.dst_cap, lane);
+        if (lane == 0) st[j] = rv;
     }
 }
 
@@ -974,50 +1093,65 @@ extern "C" int tyche_debug_zstd_encode_profile(unsigned long long *host16, int r
 }
 #endif
 
-// TYCHE_ZSTD_ENC_SPLIT: 1 (default) three-pass encode (chains lane-per-page), 0 one kernel.
+// TYCHE_ZSTD_ENC_SPLIT: 1 (default) four-pass encode, 0 one kernel.
 hipError_t launch_zstd_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream_t s) {
     if (b.count == 0) return hipSuccess;
     if (in_cap > 65535u) return hipErrorInvalidValue;    // 16-bit positions in the parse and sequence records
-    const size_t lds = kTableSlots * sizeof(uint16_t) + kWave + kWave * 8 + kSeqCap * 8 + kHtab * 4 + 256 +
-                       ((in_cap + 16u + kPad + 15u) & ~15u);
-    const size_t ncu = prepare_launch((const void *)zstd_encode_kernel);
-    const size_t per_cu = waves_per_cu((const void *)zstd_encode_kernel, lds);
+    const size_t page_lds = (in_cap + 16u + kPad + 15u) & ~15u;
+    const size_t lds = kTableSlots * sizeof(uint16_t) + kWave + kWave * 8 + kSeqCap * 8 + kHtab * 4 + 256 + page_lds;
+    const size_t lds1 = kTableSlots * sizeof(uint16_t) + kWave + kWave * 8 + page_lds;   // pass A1
     const char *env = getenv("TYCHE_ZSTD_ENC_SPLIT");
     const bool split = !(env && env[0] == '0');
     const size_t page_bytes = enc_area_bytes(in_cap);
-    size_t chunk = b.count;
-    uint8_t *ws = nullptr;
-    int32_t *st = nullptr;
     size_t budget = (size_t)8 << 30;
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b / 8 < budget) budget = free_b / 8;
     const char *mb = getenv("TYCHE_ZSTD_SCRATCH_MB");
     if (mb && atol(mb) > 0) budget = (size_t)atol(mb) << 20;
-    if (split) chunk = std::max<size_t>(1, std::min<size_t>(b.count, budget / page_bytes));
+    const size_t chunk = split ? std::max<size_t>(1, std::min<size_t>(b.count, budget / page_bytes)) : b.count;
     const size_t st_bytes = (chunk * 4u + 255u) & ~(size_t)255u;
     ScratchLease lease(s, split ? st_bytes + chunk * page_bytes : 0);
-    if (split && lease.get()) {
-        st = (int32_t *)lease.get();
-        ws = (uint8_t *)lease.get() + st_bytes;
-    } else {
-        chunk = b.count;
+    if (!split || !lease.get()) {
+        const void *k = (const void *)zstd_encode_kernel<false>;
+        const size_t ncu = prepare_launch(k);
+        const size_t grid = std::min<size_t>(b.count, ncu * waves_per_cu(k, lds));
+        WorkCounter ctr(s, grid < b.count);
+        if (!ctr.get()) return hipErrorOutOfMemory;
+        hipLaunchKernelGGL(zstd_encode_kernel<false>, dim3((unsigned)grid), dim3(kWave), lds, s, b, (size_t)0, b.count,
+                           in_cap, ctr.get(), (uint8_t *)nullptr, (size_t)0, (int32_t *)nullptr);
+        return hipGetLastError();
     }
+    int32_t *st = (int32_t *)lease.get();
+    uint8_t *ws = (uint8_t *)lease.get() + st_bytes;
+    const void *k1 = (const void *)zstd_encode_kernel<true>;
+    const size_t ncu = prepare_launch(k1);
+    (void)prepare_launch((const void *)zstd_block_kernel);
+    (void)prepare_launch((const void *)zstd_fse_kernel);
+    (void)prepare_launch((const void *)zstd_pack_kernel);
+    const size_t cu1 = waves_per_cu(k1, lds1), cu2 = waves_per_cu((const void *)zstd_block_kernel, kA2Lds);
     for (size_t first = 0; first < b.count; first += chunk) {
         const size_t n = std::min(chunk, b.count - first);
-        const size_t grid = std::min<size_t>(n, ncu * per_cu);
         {
-            WorkCounter ctr(s, grid < n);
+            const size_t g = std::min<size_t>(n, ncu * cu1);
+            WorkCounter ctr(s, g < n);
             if (!ctr.get()) return hipErrorOutOfMemory;
-            hipLaunchKernelGGL(zstd_encode_kernel, dim3((unsigned)grid), dim3(kWave), lds, s, b, first, n, in_cap,
+            hipLaunchKernelGGL(zstd_encode_kernel<true>, dim3((unsigned)g), dim3(kWave), lds1, s, b, first, n, in_cap,
                                ctr.get(), ws, page_bytes, st);
         }
-        if (ws) {
-            hipLaunchKernelGGL(zstd_fse_kernel, dim3((unsigned)((n + kWave - 1) / kWave)), dim3(kWave),
-                               kWave * kTabBytes, s, b, first, n, ws, page_bytes, (const int32_t *)st);
-            const size_t g3 = std::min<size_t>(n, ncu * 8u);
-            WorkCounter ctr(s, g3 < n);
+        {
+            const size_t g = std::min<size_t>(n, ncu * cu2);
+            WorkCounter ctr(s, g < n);
             if (!ctr.get()) return hipErrorOutOfMemory;
-            hipLaunchKernelGGL(zstd_pack_kernel, dim3((unsigned)g3), dim3(kWave), 0, s, b, first, n, ws, page_bytes,
+            hipLaunchKernelGGL(zstd_block_kernel, dim3((unsigned)g), dim3(kWave), kA2Lds, s, b, first, n, in_cap, ws,
+                               page_bytes, st, ctr.get());
+        }
+        hipLaunchKernelGGL(zstd_fse_kernel, dim3((unsigned)((n + kWave - 1) / kWave)), dim3(kWave), kWave * kTabBytes, s,
+                           b, first, n, ws, page_bytes, (const int32_t *)st);
+        {
+            const size_t g = std::min<size_t>(n, ncu * 8u);
+            WorkCounter ctr(s, g < n);
+            if (!ctr.get()) return hipErrorOutOfMemory;
+            hipLaunchKernelGGL(zstd_pack_kernel, dim3((unsigned)g), dim3(kWave), 0, s, b, first, n, ws, page_bytes,
                                (const int32_t *)st, ctr.get());
         }
         hipError_t e = hipGetLastError();
