@@ -14,7 +14,8 @@ read bytes are 1 * FETCH_SIZE.  Each kernel's figure is
 its bytes per codec call divided by the pages of a call.  A call is one
 dispatch, except where --calls says how many calls the kernel's dispatches
 make up (the LZ4 decoder runs two size-class launches per call:
---calls lz4_decode=1 for tools/run_codec.py with REPS=1).
+--calls lz4_decode=1 for tools/run_codec.py with REPS=1; the split zstd codec
+runs 3-4 kernels per chunk of pages: --calls zstd_encode=2 --calls zstd_decode=1).
 bench.py scales the per-page figure to its own launch for `roofline.traffic`.
 """
 import argparse
@@ -22,9 +23,12 @@ import csv
 import json
 from collections import defaultdict
 
-KERNELS = {"lz4_encode": "lz4_encode_", "lz4_decode": "lz4_decode_",
-           "zstd_encode": "zstd_encode_kernel", "zstd_decode": "zstd_decode_kernel",
-           "zlib_encode": "zlib_deflate_kernel", "zlib_decode": "zlib_inflate_kernel"}
+# codec call -> the kernel symbols its dispatches carry (the split zstd codec runs several
+# kernels per chunk of pages and several chunks per call: give --calls for it)
+KERNELS = {"lz4_encode": ("lz4_encode_",), "lz4_decode": ("lz4_decode_",),
+           "zstd_encode": ("zstd_encode_kernel", "zstd_block_kernel", "zstd_fse_kernel", "zstd_pack_kernel"),
+           "zstd_decode": ("zstd_decode_kernel", "zstd_entropy_kernel", "zstd_seq_kernel", "zstd_exec_kernel"),
+           "zlib_encode": ("zlib_deflate_kernel",), "zlib_decode": ("zlib_inflate_kernel",)}
 
 
 # read-byte factor per FETCH_SIZE byte, by kernel symbol (see the module docstring)
@@ -44,8 +48,8 @@ def per_dispatch(path, counter):
     for d, v in acc.items():
         if counter == "FETCH_SIZE":
             v *= 1.0 if any(sym in names[d] for sym in SCATTERED) else 2.0
-        for k, sym in KERNELS.items():
-            if sym in names[d]:
+        for k, syms in KERNELS.items():
+            if any(sym in names[d] for sym in syms):
                 out[k].append(v)
     return out
 
