@@ -948,7 +948,7 @@ constexpr uint32_t kAreaBytes = 13312u;                           // jobs + tabl
 constexpr uint32_t kTabDefault = 0xFFFFFFFFu;
 constexpr int32_t kRetryInline = -1000;
 __host__ __device__ inline uint32_t ent_cap(uint32_t in_cap, uint32_t out_cap) {
-    return ((in_cap / 3u + out_cap / 3u + 72u) + 3u) & ~3u;   // multiple of 4: the literal buffer stays 16-aligned
+    return ((in_cap / 3u + out_cap / 3u + 72u) + 15u) & ~15u;   // multiple of 16: planes and literals 64-aligned
 }
 __host__ __device__ inline uint32_t lit_cap(uint32_t out_cap) { return out_cap + 16u * (out_cap / 64u + 2u) + 64u; }
 __host__ __device__ inline size_t ent_page_bytes(uint32_t in_cap, uint32_t out_cap) {
@@ -1577,12 +1577,36 @@ __device__ __forceinline__ uint32_t gbitd_reload(BitD &b, const uint8_t *in) {
 
 // ZSTD_decompressSequences (zstd_decompress.c:1010-1060) for one job, this lane's
 // page.  Writes the decoded (litLength, matchLength, offset) triples as entries.
+//
+// kSmall (table logs <= 6/5/6, every level-1 frame of this encoder and the
+// predefined tables): the lane's three tables are copied into its LDS slot as
+// 16-bit cells (newState | symbol << 6 | nbBits << 12) and its entries are
+// staged there 16 at a time, so each plane gets whole 64-byte lines; otherwise
+// cells are gathered from the table area and entries stored one by one.
+constexpr uint32_t kSlotCells = 64u + 32u + 64u;   // LL, OF, ML
+constexpr uint32_t kSeqLds = kWave * (kSlotCells * 2u + 3u * 16u * 4u);
+__device__ __forceinline__ uint32_t cell16(uint32_t c) { return (c & 63u) | (((c >> 6) & 63u) << 16) | ((c >> 12) << 24); }
+template <bool kSmall>
 __device__ bool seq_job(const Ent &E, const uint8_t *src, const uint32_t *J, uint32_t &rep0, uint32_t &rep1,
-                        uint32_t &rep2) {
+                        uint32_t &rep2, uint16_t *lt, uint32_t *sg) {
     const int32_t start = (int32_t)J[0], len = (int32_t)J[1];
     const uint32_t nbseq = J[2], e0 = J[3];
     const uint32_t *LL = E.tabs + J[4] / 4u, *OF = E.tabs + J[5] / 4u, *ML = E.tabs + J[6] / 4u;
     const uint32_t lls = J[7] & 255u, ofs = (J[7] >> 8) & 255u, mls = (J[7] >> 16) & 255u;
+    if (kSmall) {
+        for (uint32_t u = 0; u < (1u << lls); u++) {
+            const uint32_t c = gld(LL + u);
+            lt[u] = (uint16_t)((c & 0xFFFFu) | (((c >> 16) & 0xFFu) << 6) | ((c >> 24) << 12));
+        }
+        for (uint32_t u = 0; u < (1u << ofs); u++) {
+            const uint32_t c = gld(OF + u);
+            lt[64u + u] = (uint16_t)((c & 0xFFFFu) | (((c >> 16) & 0xFFu) << 6) | ((c >> 24) << 12));
+        }
+        for (uint32_t u = 0; u < (1u << mls); u++) {
+            const uint32_t c = gld(ML + u);
+            lt[96u + u] = (uint16_t)((c & 0xFFFFu) | (((c >> 16) & 0xFFu) << 6) | ((c >> 24) << 12));
+        }
+    }
     BitD b;
     if (!gbitd_init(b, src, start, len)) return false;
     uint32_t sll = bitd_read(b, lls);
@@ -1595,10 +1619,19 @@ __device__ bool seq_job(const Ent &E, const uint8_t *src, const uint32_t *J, uin
     // before the previous step's stores, so waiting for them never waits for those
     uint32_t pll = 0, pml = 0, pof = 0;
     for (uint32_t i = 0; i < nbseq; i++) {
-        const uint32_t cl_v = gld(LL + sll), cm_v = gld(ML + sml), co_v = gld(OF + sof);
+        uint32_t cl_v, cm_v, co_v;
+        if (kSmall) {
+            cl_v = cell16(lt[sll]);
+            cm_v = cell16(lt[96u + sml]);
+            co_v = cell16(lt[64u + sof]);
+        } else {
+            cl_v = gld(LL + sll);
+            cm_v = gld(ML + sml);
+            co_v = gld(OF + sof);
+        }
         PendLoad pl;
         const uint32_t rs = gbitd_reload_issue(b, src, pl);
-        if (i) {
+        if (!kSmall && i) {
             E.ll[e0 + i - 1] = pll;
             E.ml[e0 + i - 1] = pml;
             E.of[e0 + i - 1] = pof;
@@ -1636,11 +1669,36 @@ __device__ bool seq_job(const Ent &E, const uint8_t *src, const uint32_t *J, uin
         sll = cell_state(cl) + bitd_read(b, cell_nb(cl));
         sml = cell_state(cm) + bitd_read(b, cell_nb(cm));
         sof = cell_state(co) + bitd_read(b, cell_nb(co));
-        pll = llv;
-        pml = mlv;
-        pof = offv;
+        if (kSmall) {
+            // stage; a full 16-entry line (or the job's last entry) goes out
+            const uint32_t e = e0 + i, k = e & 15u;
+            sg[k] = llv;
+            sg[16u + k] = mlv;
+            sg[32u + k] = offv;
+            if (k == 15u || i + 1u == nbseq) {
+                const uint32_t lo = e - k < e0 ? e0 & 15u : 0u, base = e - k;
+                if (lo == 0u && k == 15u) {
+#pragma unroll
+                    for (uint32_t q = 0; q < 4u; q++) {
+                        ((u32x4 *)(E.ll + base))[q] = ((const u32x4 *)sg)[q];
+                        ((u32x4 *)(E.ml + base))[q] = ((const u32x4 *)(sg + 16u))[q];
+                        ((u32x4 *)(E.of + base))[q] = ((const u32x4 *)(sg + 32u))[q];
+                    }
+                } else {
+                    for (uint32_t q = lo; q <= k; q++) {
+                        E.ll[base + q] = sg[q];
+                        E.ml[base + q] = sg[16u + q];
+                        E.of[base + q] = sg[32u + q];
+                    }
+                }
+            }
+        } else {
+            pll = llv;
+            pml = mlv;
+            pof = offv;
+        }
     }
-    if (nbseq) {
+    if (!kSmall && nbseq) {
         E.ll[e0 + nbseq - 1] = pll;
         E.ml[e0 + nbseq - 1] = pml;
         E.of[e0 + nbseq - 1] = pof;
@@ -1658,9 +1716,17 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(tyche_batch_t b, size_t fi
     const uint32_t njobs = E.jobs[0];
     if (njobs == 0) return;
     const PageRef p = batch_page(b, first + j);
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint16_t *lt = (uint16_t *)smem + threadIdx.x * kSlotCells;
+    uint32_t *sg = (uint32_t *)(smem + kWave * kSlotCells * 2u) + threadIdx.x * 48u;
     uint32_t rep0 = 1, rep1 = 4, rep2 = 8;
     for (uint32_t q = 0; q < njobs; q++) {
-        if (!seq_job(E, p.src, E.jobs + 4u + q * kJobWords, rep0, rep1, rep2)) {
+        const uint32_t *J = E.jobs + 4u + q * kJobWords;
+        const uint32_t logs = J[7];
+        const bool small = (logs & 255u) <= 6u && ((logs >> 8) & 255u) <= 5u && ((logs >> 16) & 255u) <= 6u;
+        const bool ok = small ? seq_job<true>(E, p.src, J, rep0, rep1, rep2, lt, sg)
+                              : seq_job<false>(E, p.src, J, rep0, rep1, rep2, lt, sg);
+        if (!ok) {
             st[j] = kErr;
             return;
         }
@@ -1894,8 +1960,8 @@ hipError_t launch_zstd_decode(const tyche_batch_t &b, uint32_t in_cap, uint32_t 
             hipLaunchKernelGGL(zstd_entropy_kernel, dim3((unsigned)g1), dim3(kWave), l1.total, s, b, first, n, in_cap,
                                out_cap, l1, ent, page_bytes, st, ctr.get(), use_jobs);
         }
-        hipLaunchKernelGGL(zstd_seq_kernel, dim3((unsigned)((n + kWave - 1) / kWave)), dim3(kWave), 0, s, b, first, n,
-                           in_cap, out_cap, ent, page_bytes, st);
+        hipLaunchKernelGGL(zstd_seq_kernel, dim3((unsigned)((n + kWave - 1) / kWave)), dim3(kWave), kSeqLds, s, b, first,
+                           n, in_cap, out_cap, ent, page_bytes, st);
         const size_t g2 = std::min<size_t>(n, ncu * cu2);
         {
             WorkCounter ctr(s, g2 < n);
