@@ -30,6 +30,13 @@ from conftest import load_golden, unpack
 
 pytestmark = pytest.mark.gpu
 
+
+@pytest.fixture(autouse=True)
+def _split_for_every_batch(monkeypatch):
+    """Batches below TYCHE_ZSTD_SPLIT_MIN (4096 pages) take the one-launch kernels; the tests
+    here run the multi-pass codec on every batch size (the fused kernels get their own tests)."""
+    monkeypatch.setenv("TYCHE_ZSTD_SPLIT_MIN", "1")
+
 DEV = torch.device("cuda:0")
 ZSTD = 3
 
@@ -501,16 +508,19 @@ def test_decode_huffman_tablelog12(tc, oracle_mod):
 
 @pytest.mark.parametrize("mode", ["fused", "chunked", "inline"])
 def test_zstd_fused_kernel_and_chunked_split(tc, oracle_mod, monkeypatch, mode):
-    """The fused one-kernel decoder (TYCHE_ZSTD_SPLIT=0), the split decoder run through a 1 MiB
-    pass-1 buffer (TYCHE_ZSTD_SCRATCH_MB=1: a handful of pages per chunk) and the split decoder
-    with the sequence chains inline in pass 1 (TYCHE_ZSTD_JOBS=0) give the verdicts and bytes of
-    the default path on the reference frames, the malformed set and the fuzz corpus."""
+    """The fused one-kernel decoder (TYCHE_ZSTD_SPLIT=0), the split decoder on every batch size
+    (TYCHE_ZSTD_SPLIT_MIN=1) run through a 1 MiB pass-1 buffer (TYCHE_ZSTD_SCRATCH_MB=1: a handful of
+    pages per chunk) and the split decoder with the sequence chains inline in pass 1
+    (TYCHE_ZSTD_JOBS=0) give the verdicts and bytes of the default path on the reference frames,
+    the malformed set and the fuzz corpus."""
     if mode == "fused":
         monkeypatch.setenv("TYCHE_ZSTD_SPLIT", "0")
     elif mode == "chunked":
         monkeypatch.setenv("TYCHE_ZSTD_SCRATCH_MB", "1")
+        monkeypatch.setenv("TYCHE_ZSTD_SPLIT_MIN", "1")   # every batch, however small, through the split
     else:
         monkeypatch.setenv("TYCHE_ZSTD_JOBS", "0")
+        monkeypatch.setenv("TYCHE_ZSTD_SPLIT_MIN", "1")
     test_zstd_reference_frames(tc, 3)
     test_zstd_malformed(tc, oracle_mod)
     test_zstd_fuzz_vs_oracle(tc, oracle_mod)
@@ -526,6 +536,7 @@ def test_zstd_encode_fused_kernel_and_chunked_split(tc, oracle_mod, monkeypatch,
         monkeypatch.setenv("TYCHE_ZSTD_ENC_SPLIT", "0")
     else:
         monkeypatch.setenv("TYCHE_ZSTD_SCRATCH_MB", "1")
+        monkeypatch.setenv("TYCHE_ZSTD_SPLIT_MIN", "1")
     for dist in (0, 3):
         for plen in (8192, 32768):
             test_encode_roundtrip_reference_decoder(tc, oracle_mod, dist, plen)

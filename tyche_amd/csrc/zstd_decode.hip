@@ -119,6 +119,35 @@ __device__ __forceinline__ void ml_code(uint32_t c, uint32_t &base, uint32_t &bi
     base = c < 32u ? c + 3u : (c < 43u ? 35u + 2u * f : (1u << (hb & 31u)) + 3u);
 }
 
+// The same as branches: the wave-uniform chain below runs faster on SALU
+// branches than on selects (2,087 vs 2,294 ms per 1M C3 pages, fused kernel)
+__device__ __forceinline__ void ll_code_s(uint32_t c, uint32_t &base, uint32_t &bits) {
+    if (c < 16u) { base = c; bits = 0; return; }
+    if (c < 24u) {
+        // codes 16..23: bases 16 18 20 22 24 28 32 40, bits 1 1 1 1 2 2 3 3
+        const uint32_t k = c - 16u;
+        bits = k < 4u ? 1u : (k < 6u ? 2u : 3u);
+        base = k < 4u ? 16u + 2u * k : (k < 6u ? 24u + 4u * (k - 4u) : 32u + 8u * (k - 6u));
+        return;
+    }
+    if (c == 24u) { base = 48u; bits = 4u; return; }
+    bits = c - 19u;
+    base = 1u << bits;
+}
+__device__ __forceinline__ void ml_code_s(uint32_t c, uint32_t &base, uint32_t &bits) {
+    if (c < 32u) { base = c + 3u; bits = 0; return; }
+    if (c < 43u) {
+        // codes 32..42: bases 35 37 39 41 43 47 51 59 67 83 99, bits 1 1 1 1 2 2 3 3 4 4 5
+        const uint32_t k = c - 32u;
+        bits = k < 4u ? 1u : (k < 6u ? 2u : (k < 8u ? 3u : (k < 10u ? 4u : 5u)));
+        base = k < 4u ? 35u + 2u * k : (k < 6u ? 43u + 4u * (k - 4u) : (k < 8u ? 51u + 8u * (k - 6u)
+                                                                          : (k < 10u ? 67u + 16u * (k - 8u) : 99u)));
+        return;
+    }
+    bits = c - 36u;
+    base = (1u << bits) + 3u;
+}
+
 // The predefined decoding tables (ZSTD_buildSeqTable set_basic ->
 // LL/OF/ML_defaultDTable, zstd_decompress.c:517-687) are FSE_buildDTable over
 // the default distributions; built here at compile time.
@@ -1190,54 +1219,34 @@ __device__ int32_t decode_block(const Work &W, SeqTables &T, const Ent &E, uint3
             // decode up to 64 sequences into lanes
             uint32_t vll = 0, vml = 0, voff = 0, k = 0;
             for (; k < kWave; k++) {
-                // the chain's state is wave-uniform: say so, or the compiler keeps the
-                // bit container in VGPRs and turns every branch on it into exec-mask
-                // code (v_lshlrev_b64 / s_and_saveexec per step)
-                b.c = (uint64_t)rfl((uint32_t)b.c) | ((uint64_t)rfl((uint32_t)(b.c >> 32)) << 32);
-                b.used = rfl(b.used);
-                b.ptr = ru(b.ptr);
-                b.start = ru(b.start);
-                sll = rfl(sll);
-                sml = rfl(sml);
-                sof = rfl(sof);
-                rep0 = rfl(rep0);
-                rep1 = rfl(rep1);
-                rep2 = rfl(rep2);
-                nbseq = ru(nbseq);
-                // the three cell reads go out before the container reload: both are
-                // LDS round trips and neither depends on the other
-                const uint32_t cl_v = W.ll[sll], cm_v = W.ml[sml], co_v = W.of[sof];
                 if (!((bitd_reload_u(b, in) <= kCompleted) && nbseq)) { more = false; break; }
                 nbseq--;
-                const uint32_t cl = rfl(cl_v), cm = rfl(cm_v), co = rfl(co_v);
+                const uint32_t cl = rfl(W.ll[sll]), cm = rfl(W.ml[sml]), co = rfl(W.of[sof]);
                 const uint32_t llc = cell_sym(cl), mlc = cell_sym(cm), ofc = cell_sym(co);
-                // offset (ofCode 0 reads nothing; readBitsFast needs nb >= 1)
-                const uint32_t ofx = (uint32_t)bitd_look_fast(b, ofc);
-                b.used += ofc;
-                uint32_t offv = ofc ? of_base(ofc) + ofx : 0u;
-                {
-                    // repeat offsets (zstd_decompress.c:884-905) as selects
-                    const bool small = ofc <= 1u;
-                    const uint32_t adj = offv + (llc == 0u);
-                    uint32_t t = adj == 3u ? rep0 - 1u : (adj == 1u ? rep1 : rep2);
-                    t += t == 0u;
-                    const uint32_t n0 = small ? (adj ? t : rep0) : offv;
-                    const uint32_t n1 = small ? (adj ? rep0 : rep1) : rep0;
-                    const uint32_t n2 = small ? (adj ? (adj != 1u ? rep1 : rep2) : rep2) : rep1;
-                    offv = n0;
-                    rep0 = n0;
-                    rep1 = n1;
-                    rep2 = n2;
+                uint32_t offv;
+                if (!ofc) offv = 0;
+                else offv = of_base(ofc) + bitd_read_fast(b, ofc);
+                if (ofc <= 1u) {
+                    offv += llc == 0;
+                    if (offv) {
+                        uint32_t t = offv == 3u ? rep0 - 1u : (offv == 1u ? rep1 : rep2);
+                        t += t == 0;
+                        if (offv != 1u) rep2 = rep1;
+                        rep1 = rep0;
+                        rep0 = offv = t;
+                    } else {
+                        offv = rep0;
+                    }
+                } else {
+                    rep2 = rep1;
+                    rep1 = rep0;
+                    rep0 = offv;
                 }
                 uint32_t mlbase, mlb, llbase, llb;
-                ml_code(mlc, mlbase, mlb);
-                ll_code(llc, llbase, llb);
-                const uint32_t mlx = (uint32_t)bitd_look_fast(b, mlb);
-                b.used += mlb;
-                const uint32_t mlv = mlbase + (mlb ? mlx : 0u);
-                const uint32_t llx = (uint32_t)bitd_look_fast(b, llb);
-                b.used += llb;
-                const uint32_t llv = llbase + (llb ? llx : 0u);
+                ml_code_s(mlc, mlbase, mlb);
+                ll_code_s(llc, llbase, llb);
+                const uint32_t mlv = mlbase + (mlc > 31u ? bitd_read_fast(b, mlb) : 0u);
+                const uint32_t llv = llbase + (llc > 15u ? bitd_read_fast(b, llb) : 0u);
                 if (llb + mlb + ofc > 31u) bitd_reload_u(b, in);
                 sll = cell_state(cl) + bitd_read(b, cell_nb(cl));
                 sml = cell_state(cm) + bitd_read(b, cell_nb(cm));
@@ -1907,7 +1916,8 @@ extern "C" int tyche_debug_zstd_decode_profile(unsigned long long *host16, int r
 }
 #endif
 
-// TYCHE_ZSTD_SPLIT: 1 (default) two-pass decode where it fits, 0 the fused kernel.
+// TYCHE_ZSTD_SPLIT: 1 (default) two-pass decode where it fits and the batch has at
+// least TYCHE_ZSTD_SPLIT_MIN (4096) pages, 0 the fused kernel.
 // TYCHE_ZSTD_JOBS: 1 (default) sequence chains lane-per-page (zstd_seq_kernel), 0 inline.
 // TYCHE_ZSTD_SCRATCH_MB bounds the pass-1 buffer; batches go through it in chunks.
 static hipError_t launch_fused(const tyche_batch_t &b, uint32_t in_cap, uint32_t out_cap, hipStream_t s) {
@@ -1925,8 +1935,12 @@ static hipError_t launch_fused(const tyche_batch_t &b, uint32_t in_cap, uint32_t
 
 hipError_t launch_zstd_decode(const tyche_batch_t &b, uint32_t in_cap, uint32_t out_cap, hipStream_t s) {
     if (b.count == 0) return hipSuccess;
+    // small batches (restores) take the one-launch kernel: the split's extra
+    // launches cost more latency than its throughput gains on a few pages
     const char *env = getenv("TYCHE_ZSTD_SPLIT");
-    const bool split = !(env && env[0] == '0');
+    const char *mn = getenv("TYCHE_ZSTD_SPLIT_MIN");
+    const size_t split_min = mn && atol(mn) > 0 ? (size_t)atol(mn) : 4096;
+    const bool split = !(env && env[0] == '0') && b.count >= split_min;
     const Layout l1 = make_layout(in_cap, out_cap, false);
     const char *jenv = getenv("TYCHE_ZSTD_JOBS");   // 0: sequence chains inline in pass 1
     const bool use_jobs = !(jenv && jenv[0] == '0');
@@ -1939,7 +1953,9 @@ hipError_t launch_zstd_decode(const tyche_batch_t &b, uint32_t in_cap, uint32_t 
     const char *mb = getenv("TYCHE_ZSTD_SCRATCH_MB");
     size_t budget = (size_t)16 << 30;
     size_t free_b = 0, total_b = 0;
-    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b / 4 < budget) budget = free_b / 4;
+    if (b.count * page_bytes > ((size_t)1 << 30) && hipMemGetInfo(&free_b, &total_b) == hipSuccess &&
+        free_b / 4 < budget)
+        budget = free_b / 4;
     if (mb && atol(mb) > 0) budget = (size_t)atol(mb) << 20;
     const size_t chunk = std::max<size_t>(1, std::min<size_t>(b.count, budget / page_bytes));
     const size_t st_bytes = (chunk * 4u + 255u) & ~(size_t)255u;
