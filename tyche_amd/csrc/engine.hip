@@ -453,8 +453,11 @@ int acquire_ctx(int dev, HostCtx **out) {
         if (rc) return rc;
     }
     P.cv.wait(g, [&] { return !P.idle.empty(); });
-    size_t best = 0;
-    for (size_t k = 1; k < P.idle.size(); k++)
+    // least-busy group; among equals the most recently released context (its
+    // pinned and device arenas are already grown -- a fresh context pays
+    // hipHostMalloc/hipMalloc for its staging slots on first use)
+    size_t best = P.idle.size() - 1;
+    for (size_t k = best; k-- > 0;)
         if (P.busy[(size_t)P.idle[k]->group] < P.busy[(size_t)P.idle[best]->group]) best = k;
     *out = P.idle[best];
     P.idle.erase(P.idle.begin() + (long)best);
