@@ -264,10 +264,12 @@ def test_decode_size_classes(tc):
     assert bool((rv == plen).all()) and torch.equal(out, pages)
 
 
-def test_decode_lane_path_fixtures(tc):
-    """Batches of >= 65,536 pages take the lane-per-page decoder (lz4_decode_lane.hip):
-    the reference-generated, sample and malformed fixtures, repeated to 64K pages, give
-    the reference's return values and bytes there too."""
+@pytest.mark.parametrize("target", [1, 8192, 65536])
+def test_decode_lane_path_fixtures(tc, target):
+    """The decoder is picked by batch size: below 4,096 pages the jump decoder (workgroup per
+    page, pointer-jumping match resolution), below 32,768 the wave decoder, from there the
+    lane-per-page decoder (lz4_decode_lane.hip).  The reference-generated, sample and malformed
+    fixtures, repeated to each size, give the reference's return values and bytes on all three."""
     gm, gg, gs = load_golden("lz4_malformed.npz"), load_golden("lz4_generated.npz"), load_golden("lz4_sample.npz")
     streams, caps, want_rv, want_dig = [], [], [], []
     for i in range(len(gm["cap"])):
@@ -282,7 +284,7 @@ def test_decode_lane_path_fixtures(tc):
             caps.append(capf(i))
             want_rv.append(caps[-1])
             want_dig.append(g["digest"][i].tobytes())
-    k = -(-65536 // len(streams))
+    k = -(-target // len(streams))
     rv, outs = ragged_decode(tc, streams * k, caps * k)
     for j in range(len(streams) * k):
         i = j % len(streams)
@@ -302,11 +304,12 @@ def test_decode_lane_path_roundtrip(tc, dist):
     assert bool((rv == plen).all()) and torch.equal(out, pages)
 
 
-def test_decode_lane_path_corruptions(tc, oracle_mod):
-    """64K seeded corruptions (byte flips, truncations) through the lane-per-page decoder:
-    every return value is the restated LZ4_decompress_safe's (lz4.c:1251), and the
-    untouched pages decode bit-exactly."""
-    n, plen = 65536, 4096
+@pytest.mark.parametrize("n", [3000, 8192, 65536])
+def test_decode_lane_path_corruptions(tc, oracle_mod, n):
+    """Seeded corruptions (byte flips, truncations) through the jump (3,000 pages), wave
+    (8,192) and lane-per-page (64K) decoders: every return value is the restated
+    LZ4_decompress_safe's (lz4.c:1251), and the untouched pages decode bit-exactly."""
+    plen = 4096
     pages = tc.pagegen(n, plen, seed=99, dist=0, device=DEV)
     comp, clen = tc.compress_pages(pages)
     torch.cuda.synchronize()
@@ -345,5 +348,46 @@ def test_decode_lane_path_page_sizes(tc, oracle_mod, plen):
     assert bool((rv == plen).all()) and torch.equal(out, pages)
     ch, lh, host = comp[:64].cpu().numpy(), clen[:64].cpu().numpy(), pages[:64].cpu().numpy()
     for i in range(64):
+        r, dec = oracle_mod.lz4_decompress(ch[i, :lh[i]].tobytes(), plen)
+        assert r == plen and dec == host[i].tobytes(), i
+
+
+@pytest.mark.parametrize("plen", [8192, 16384, 32768])
+@pytest.mark.parametrize("n", [1, 7, 300])
+def test_decode_jump_path_page_kinds(tc, oracle_mod, plen, n):
+    """Small batches (the jump decoder) of every pagegen distribution plus pages built for its
+    corner cases: incompressible (literal runs longer than a lane fills), all-zero and
+    short-period pages (long self-overlapping matches, the workgroup's run list), and pages whose
+    matches copy earlier matches hundreds of times (deep pointer chains).  Round trip on the GPU;
+    a sample decodes identically with the oracle restatement."""
+    g = torch.Generator(device="cpu").manual_seed(plen + n)
+    pages = tc.pagegen(n, plen, seed=plen * 3 + n, first=n, dist=0, device=DEV)
+    for i in range(n):
+        kind = i % 6
+        if kind == 1:
+            pages[i] = torch.randint(0, 256, (plen,), dtype=torch.uint8, generator=g).to(DEV)
+        elif kind == 2:
+            pages[i] = 0
+        elif kind == 3:
+            per = int(torch.randint(1, 40, (1,), generator=g))
+            pat = torch.randint(0, 256, (per,), dtype=torch.uint8, generator=g)
+            pages[i] = pat.repeat(plen // per + 1)[:plen].to(DEV)
+        elif kind == 4:
+            src = tc.pagegen(1, plen, seed=i, first=i, dist=i % 6, device=DEV)
+            pages[i] = src[0]
+        elif kind == 5:
+            rec = torch.randint(0, 256, (24,), dtype=torch.uint8, generator=g)
+            page = rec.repeat(plen // 24 + 1)[:plen].clone()
+            noise = torch.randint(0, plen, (plen // 97,), generator=g)
+            page[noise] = torch.randint(0, 256, (noise.numel(),), dtype=torch.uint8, generator=g)
+            pages[i] = page.to(DEV)
+    comp, clen = tc.compress_pages(pages)
+    mx = int(clen.max())
+    out, rv = tc.decompress_pages(comp, clen, plen, max_comp_len=mx)
+    torch.cuda.synchronize()
+    assert bool((rv == plen).all()), rv
+    assert torch.equal(out, pages)
+    ch, lh, host = comp[:12].cpu().numpy(), clen[:12].cpu().numpy(), pages[:12].cpu().numpy()
+    for i in range(min(n, 12)):
         r, dec = oracle_mod.lz4_decompress(ch[i, :lh[i]].tobytes(), plen)
         assert r == plen and dec == host[i].tobytes(), i

@@ -1,0 +1,49 @@
+"""Diagnostic: LZ4 decode time of the jump decoder vs the wave decoder per batch size.
+
+    python tools/time_jump.py            # prints one JSON line per (decoder, page_len, batch)
+Each decoder runs in a child process (TYCHE_LZ4_JUMP_MAX is read once per process):
+jump = every batch below the lane threshold on lz4_decode_jump_kernel, wave = none.
+Times are HIP events around the decompress call on device-resident pages (median of reps).
+"""
+import json
+import os
+import subprocess
+import sys
+
+CHILD = r'''
+import json, os, sys, torch
+sys.path.insert(0, os.getcwd())
+from tyche_amd import codec
+mode = os.environ["MODE"]
+for plen in (16384, 32768):
+    big = codec.pagegen(16384, plen, dist=0)
+    comp_all, clen_all = codec.compress_pages(big)
+    torch.cuda.synchronize()
+    for n in (1, 8, 64, 512, 4096, 16384):
+        comp, clen, pages = comp_all[:n].contiguous(), clen_all[:n].contiguous(), big[:n]
+        mx = int(clen.max())
+        out, rv = codec.decompress_pages(comp, clen, plen, max_comp_len=mx)
+        torch.cuda.synchronize()
+        ok = bool((rv == plen).all()) and torch.equal(out, pages)
+        ts = []
+        reps = 20 if n < 4096 else 5
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(); codec.decompress_pages(comp, clen, plen, out=out, rv=rv, max_comp_len=mx); e1.record()
+            torch.cuda.synchronize(); ts.append(e0.elapsed_time(e1))
+        ts.sort()
+        t = ts[len(ts) // 2]
+        print(json.dumps({"decoder": mode, "page_len": plen, "batch": n, "us": round(t * 1000, 1),
+                          "GiBps": round(n * plen / (t / 1000) / 2**30, 2), "correct": ok}), flush=True)
+'''
+
+
+def main():
+    for mode, jmax in (("jump", "32767"), ("wave", "0")):
+        env = dict(os.environ, MODE=mode, TYCHE_LZ4_JUMP_MAX=jmax)
+        r = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=600)
+        print(r.stdout.strip() or r.stderr.strip()[-1500:], flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -100,6 +100,81 @@ __device__ __forceinline__ uint32_t next_token(const uint8_t *in, int32_t L, uin
     return (uint32_t)q;
 }
 
+struct SeqIn {
+    int32_t lit, ls, off, ml, q2;
+    bool in_term, ml_err;
+    bool lit_win;     // lit <= 16 and its bytes are in lb[]
+    uint32_t lb[4];   // literal bytes 0..15 (lit_win)
+};
+// Input side of the sequence whose token is at p (the reads of lz4.c:1134-1143,
+// 1165, 1172-1182).  One round trip of 6 aligned dwords covers the token, up to
+// 14 literals and the offset (stream positions p .. p+19), so the common
+// sequence costs one LDS latency; length-extension bytes are read one by one.
+// (Byte-addressed reads cost a dependent LDS trip each, and an unaligned dword
+// read a replay.)
+__device__ __forceinline__ SeqIn decode_seq_in(const uint8_t *in, int32_t L, int32_t p) {
+    SeqIn s;
+    const uint32_t ib = (uint32_t)(uintptr_t)in & 3u;
+    const uint32_t *A = (const uint32_t *)(in - ib);
+    const uint32_t qa = (uint32_t)p + ib, sh = qa & 3u;
+    uint32_t w[6];
+#pragma unroll
+    for (int j = 0; j < 6; j++) w[j] = A[(qa >> 2) + j];
+    uint32_t x[5];   // bytes p .. p+19
+#pragma unroll
+    for (int j = 0; j < 5; j++) x[j] = __builtin_amdgcn_alignbyte(w[j + 1], w[j], sh);
+    const uint32_t t = x[0] & 0xFFu;
+    int32_t q = p + 1;
+    s.lit = (int32_t)(t >> 4);
+    s.lit_win = s.lit < kRunMask;
+#pragma unroll
+    for (int j = 0; j < 4; j++) s.lb[j] = __builtin_amdgcn_alignbyte(x[j + 1], x[j], 1u);
+    if (s.lit == kRunMask) {
+        uint32_t b;
+        do {
+            b = in[q];
+            q++;
+            s.lit += (int32_t)b;
+        } while (q < L - kRunMask && b == 255);
+    }
+    s.ls = q;
+    s.in_term = q + s.lit > L - 8;
+    s.off = 0;
+    s.ml = 0;
+    s.q2 = 0;
+    s.ml_err = false;
+    if (!s.in_term) {
+        if (s.lit_win) {
+            // offset = bytes 1+lit, 2+lit of the window (lit <= 14)
+            const uint32_t k = 1u + (uint32_t)s.lit, kd = k >> 2;
+            const uint32_t lo = kd == 0 ? x[0] : kd == 1 ? x[1] : kd == 2 ? x[2] : x[3];
+            const uint32_t hi = kd == 0 ? x[1] : kd == 1 ? x[2] : kd == 2 ? x[3] : x[4];
+            s.off = (int32_t)(__builtin_amdgcn_alignbyte(hi, lo, k & 3u) & 0xFFFFu);
+        } else {
+            s.off = (int32_t)lds_ld16(in + q + s.lit);
+        }
+        int32_t q2 = q + s.lit + 2;
+        int32_t ml = (int32_t)(t & 15);
+        if (ml == 15) {
+            uint32_t b;
+            do {
+                b = in[q2];
+                q2++;
+                if (q2 > L - kLastLiterals) { s.ml_err = true; break; }
+                ml += (int32_t)b;
+            } while (b == 255);
+        }
+        s.ml = ml + kMinMatch;
+        s.q2 = q2;
+    }
+    return s;
+}
+// next_token through the window decoder (same positions, same kEnd cases)
+__device__ __forceinline__ uint32_t next_token_w(const uint8_t *in, int32_t L, uint32_t p) {
+    const SeqIn s = decode_seq_in(in, L, (int32_t)p);
+    return s.in_term || s.ml_err ? kEnd : (uint32_t)s.q2;
+}
+
 // Parallel token-chain parse.  Writes the ordered token positions to the top
 // of the page window (seqpos = the last `total` u16 slots below win_end) and
 // returns their number.  owner: L bytes of scratch at the window's start
@@ -115,6 +190,60 @@ __device__ __forceinline__ uint32_t next_token(const uint8_t *in, int32_t L, uin
 //     code) gives every on-chain lane its entry point;
 //  4. each on-chain lane re-walks entry -> hand-off position to count and then
 //     write its positions.
+// Steps 1-3 of parse_chain: this lane's part of the true chain is [entry, y)
+// (entry = kEnd: the lane holds none of it).
+__device__ __forceinline__ void chain_entries(const uint8_t *in, int32_t L, uint8_t *owner, uint32_t lane,
+                                              uint32_t &entry_out, uint32_t &y_out) {
+    PROF_DECL
+    const uint32_t S = ((uint32_t)L + kWave - 1) / kWave;
+    const uint32_t seg0 = lane * S;
+    const uint32_t seg1 = min(seg0 + S, (uint32_t)L);
+    for (uint32_t w = lane; w < ((uint32_t)L + 3) / 4; w += kWave) ((uint32_t *)owner)[w] = 0;
+    WAVE_SYNC();
+    uint32_t p = seg0;
+    while (p < seg1) {
+        owner[p] = (uint8_t)(lane + 1);
+        p = next_token_w(in, L, p);
+    }
+    WAVE_SYNC();
+    PROF_MARK(2);
+    // Bridges in rounds of kBridgeSteps tokens, each followed by the hand-off
+    // walk as far as the finished bridges reach: only the lanes still ahead on
+    // the true chain keep walking.  (A lane whose speculative walk never meets
+    // a later lane's stamps can bridge for hundreds of tokens; one bridge loop
+    // for all lanes waited for the longest of them.)
+    constexpr uint32_t kBridgeSteps = 4;
+    uint32_t y = p, o = 0;
+    bool done = seg0 >= seg1 || y >= (uint32_t)L;
+    uint32_t entry = kEnd, cur = 0, e = 0;
+    for (bool fin = false; !fin;) {
+        for (uint32_t it = 0; it < kBridgeSteps; it++) {
+            if (!done) {
+                const uint32_t ow = owner[y];
+                if (ow > lane + 1) {
+                    o = ow;
+                    done = true;
+                } else {
+                    y = next_token_w(in, L, y);
+                    done = y >= (uint32_t)L;
+                }
+            }
+        }
+        for (;;) {
+            if (lane == cur) entry = e;
+            if (!rdlane((uint32_t)done, cur)) break;   // cur's hand-off not found yet
+            e = rdlane(y, cur);
+            const uint32_t nx = rdlane(o, cur);
+            if (nx == 0) { fin = true; break; }
+            cur = nx - 1;
+        }
+        if (lane < cur) done = true;                    // behind the resolved part of the chain
+    }
+    PROF_MARK(3);
+    entry_out = entry;
+    y_out = y;
+}
+
 __device__ uint32_t parse_chain(const uint8_t *in, int32_t L, uint8_t *owner, uint16_t *win_end, uint16_t *&seqpos,
                                 uint32_t lane) {
     PROF_DECL
@@ -562,12 +691,410 @@ __global__ __launch_bounds__(64) void lz4_decode_wave_kernel(tyche_batch_t b, ui
     }
 }
 
+// ---------------------------------------------------------------------------
+// Small-batch decoder (restore latency): one workgroup of kJumpThreads per page,
+// matches resolved by pointer jumping instead of dependency rounds.
+//
+// The page is rebuilt as 16-bit cells in LDS, one per output byte: a literal
+// byte is final (0x8000 | byte); a match byte holds the position it copies
+// (d - off + j, or d - off + j mod off for a self-overlapping match, so a cell
+// always points below its own match).  Every pointer leads down a chain that
+// ends at a literal, so "cell = cells[cell]" over all unresolved cells, repeated
+// until none is left, yields the forward byte-copy result of lz4.c:1209-1236 in
+// log2(chain depth) rounds (8 on the bench pages) -- the wave decoder needs ~294
+// dependent frontier rounds per 16 KiB page for the same copies.  Cells are
+// independent of fill order, so all runs are written in parallel.
+//
+// Wave 0 parses the token chain (chain_entries, as parse_chain) and walks its
+// lane's part of it twice: output lengths (prefix sum across lanes), then the
+// reference's acceptance checks in order (lz4.c:1147-1168, 1176, 1225) and the
+// cell fills; runs longer than kJumpLong go to a list that the whole workgroup
+// fills.  The first failing sequence in stream order gives the exact
+// -(consumed)-1 return.  Then all waves jump, pack cells to bytes and store.
+constexpr uint32_t kJumpThreads = 512;
+constexpr int32_t kJumpLong = 16;
+
+constexpr uint32_t kLitFlag = 0x8000u;
+// LDS bytes before the cells: the workgroup's shared words (8) and jump_scan's
+// chunk keys (one per 64 cells, pages <= 32 KiB)
+constexpr uint32_t kJumpHdr = 32 + 4 * 512;
+
+// cells [o + i0, o + n) step `step` of a literal run read from in[ls..]
+__device__ __forceinline__ void fill_lit(uint16_t *cells, const uint8_t *in, int32_t o, int32_t ls, int32_t n,
+                                         int32_t i0, int32_t step) {
+    for (int32_t i = i0; i < n; i += step) cells[o + i] = (uint16_t)(kLitFlag | in[ls + i]);
+}
+// cells of a match of ml bytes at d from offset off
+__device__ __forceinline__ void fill_match(uint16_t *cells, int32_t d, int32_t off, int32_t ml, int32_t i0,
+                                           int32_t step) {
+    const int32_t src = d - off;
+    if (off == 0) {
+        // the reference copies bytes it never wrote: only its return value is a parity target
+        for (int32_t i = i0; i < ml; i += step) cells[d + i] = (uint16_t)kLitFlag;
+    } else if (off >= ml) {
+        for (int32_t i = i0; i < ml; i += step) cells[d + i] = (uint16_t)(src + i);
+    } else {
+        for (int32_t i = i0; i < ml; i += step) cells[d + i] = (uint16_t)(src + (int32_t)mod_small((uint32_t)i, (uint32_t)off));
+    }
+}
+// a long run for the workgroup: x = dst | len << 16, y = ls | 1 << 31 (literals) or off (match)
+__device__ __forceinline__ void fill_item(uint16_t *cells, const uint8_t *in, uint2 it, int32_t i0, int32_t step) {
+    const int32_t dst = (int32_t)(it.x & 0xFFFFu), n = (int32_t)(it.x >> 16);
+    if (it.y >> 31) fill_lit(cells, in, dst, (int32_t)(it.y & 0x7FFFFFFFu), n, i0, step);
+    else fill_match(cells, dst, (int32_t)it.y, n, i0, step);
+}
+
+// Wave 0: parse, checks and fills of one page (in: L bytes + kPad zeros, cells:
+// >= max(C, (L + 4) / 2) cells).  Returns LZ4_decompress_safe's value.
+__device__ int32_t jump_front(const uint8_t *in, int32_t L, uint16_t *cells, int32_t C, uint32_t lane, uint2 *list,
+                              uint32_t list_cap, uint32_t *nlist, uint2 *lits, uint32_t lits_cap, uint32_t *nseq) {
+    if (C == 0) return (L == 1 && in[0] == 0) ? 0 : -1;
+    if (L <= 0) return -1;
+    uint32_t entry, y;
+    chain_entries(in, L, (uint8_t *)cells, lane, entry, y);   // owner stamps in the cells (dead after this)
+    PROF_DECL
+    {
+        // empty cells (0) are match bytes after their run's start marker (jump_scan)
+        const uint32_t nv = (((uint32_t)C + 63u) & ~63u) / 8u;
+        u32x4 *c4 = (u32x4 *)cells;
+        const u32x4 z = {0u, 0u, 0u, 0u};
+        for (uint32_t v = lane; v < nv; v += kWave) c4[v] = z;
+    }
+    // pass 1: output bytes of this lane's part of the chain
+    int32_t olen = 0, cnt = 0;
+    for (uint32_t q = entry; q < (uint32_t)L && q != y;) {
+        const SeqIn s = decode_seq_in(in, L, (int32_t)q);
+        cnt++;
+        if (s.in_term) { olen += s.lit; break; }
+        if (s.ml_err) break;
+        olen += s.lit + s.ml;
+        q = (uint32_t)s.q2;
+    }
+    WAVE_SYNC();
+    PROF_MARK(4);
+    const int32_t incl = wave_incl_sum(olen);
+    int32_t o = incl - olen;
+    const int32_t cincl = wave_incl_sum(cnt);
+    uint32_t k = (uint32_t)(cincl - cnt);   // this lane's first sequence number
+    if (lane == kWave - 1) *nseq = (uint32_t)cincl;
+    // pass 2: checks in the reference's order, then the fills
+    int32_t status = 0, rv = 0;   // 1 terminal success, 2 error
+    for (uint32_t q = entry; q < (uint32_t)L && q != y;) {
+        const SeqIn s = decode_seq_in(in, L, (int32_t)q);
+        const int32_t d = o + s.lit;
+        if (o + s.lit > C - kMfLimit || s.in_term) {
+            if (s.ls + s.lit != L || o + s.lit > C) { status = 2; rv = -s.ls - 1; }
+            else { status = 1; rv = o + s.lit; }
+        } else if (s.off > d) {
+            status = 2; rv = -(s.ls + s.lit + 2) - 1;
+        } else if (s.ml_err) {
+            status = 2; rv = -s.q2 - 1;
+        } else if (d + s.ml > C - kLastLiterals) {
+            status = 2; rv = -s.q2 - 1;
+        }
+        if (status == 2) break;
+        // literal runs: short ones as this sequence's item for the workgroup (lits[k]), long
+        // ones on the run list; per lane only when lits[] is full
+        const bool short_lit = s.lit <= kJumpLong;
+        if (k < lits_cap)
+            lits[k] = short_lit ? make_uint2((uint32_t)o | ((uint32_t)s.lit << 16), (uint32_t)s.ls) : make_uint2(0u, 0u);
+        if (!short_lit) {
+            const uint32_t kl = atomicAdd(nlist, 1u);
+            const uint2 it = make_uint2((uint32_t)o | ((uint32_t)s.lit << 16), (uint32_t)s.ls | 0x80000000u);
+            if (kl < list_cap) list[kl] = it;
+            else fill_item(cells, in, it, 0, 1);
+        } else if (s.lit > 0 && k >= lits_cap) {
+            // literal bytes straight from the decode window (or, for 15-16 of them, aligned dwords)
+            uint32_t w[4];
+            if (s.lit_win) {
+#pragma unroll
+                for (int32_t j = 0; j < 4; j++) w[j] = s.lb[j];
+            } else {
+                const uint32_t ib = (uint32_t)(uintptr_t)in & 3u, qa = (uint32_t)s.ls + ib;
+                const uint32_t *A = (const uint32_t *)(in - ib);
+                uint32_t a[5];
+#pragma unroll
+                for (int32_t j = 0; j < 5; j++) a[j] = A[(qa >> 2) + j];
+#pragma unroll
+                for (int32_t j = 0; j < 4; j++) w[j] = __builtin_amdgcn_alignbyte(a[j + 1], a[j], qa & 3u);
+            }
+#pragma unroll
+            for (int32_t i = 0; i < 16; i++)
+                if (i < s.lit) cells[o + i] = (uint16_t)(kLitFlag | ((w[i >> 2] >> (8 * (i & 3))) & 0xFFu));
+        }
+        if (status == 1) break;
+        if (s.off != 0) {
+            cells[d] = (uint16_t)s.off;   // the run's start marker (off <= d < 2^15); jump_scan fills the rest
+        } else if (s.ml > kJumpLong) {
+            const uint32_t k = atomicAdd(nlist, 1u);
+            const uint2 it = make_uint2((uint32_t)d | ((uint32_t)s.ml << 16), 0u);
+            if (k < list_cap) list[k] = it;
+            else fill_item(cells, in, it, 0, 1);
+        } else {
+            fill_match(cells, d, 0, s.ml, 0, 1);
+        }
+        o = d + s.ml;
+        q = (uint32_t)s.q2;
+        k++;
+    }
+    WAVE_SYNC();
+    PROF_MARK(5);
+    const uint64_t stop = __ballot(status != 0);
+    if (stop == 0) return -1;   // unreachable: the chain always ends in a terminal or failing sequence
+    return (int32_t)rdlane((uint32_t)rv, (uint32_t)__builtin_ctzll(stop));
+}
+
+// Match cells from their start markers: a cell is a literal (0x8000 | byte), a
+// run start (its offset, 1..0x7FFF) or empty (0: a later byte of the run that
+// started at the nearest marker to its left).  Chunks of 64 cells: (A) each
+// chunk's last marker as key = position << 16 | offset, (B) an inclusive
+// max-scan of the keys (positions grow, so the max is the nearest marker to the
+// left), (C) each chunk rewrites its cells with the carried-in run: byte d + j of
+// a run with offset off points at d - off + (j mod off).
+__device__ __forceinline__ void jump_scan(uint16_t *cells, uint32_t n64, uint32_t *keys, uint32_t tid) {
+    u32x4 *c4 = (u32x4 *)cells;
+    const uint32_t nch = n64 / 64u;
+    for (uint32_t c = tid; c < nch; c += kJumpThreads) {
+        uint32_t key = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < 8; j++) {
+            const u32x4 v = c4[8u * c + j];
+#pragma unroll
+            for (uint32_t h = 0; h < 8; h++) {
+                const uint32_t x = (v[h >> 1] >> (16u * (h & 1u))) & 0xFFFFu;
+                if (x != 0 && !(x & kLitFlag)) key = ((64u * c + 8u * j + h) << 16) | x;
+            }
+        }
+        keys[c] = key;
+    }
+    __syncthreads();
+    if (tid < kWave) {
+        int32_t carry = 0;
+        for (uint32_t base = 0; base < nch; base += kWave) {
+            const uint32_t c = base + tid;
+            int32_t m = wave_incl_max(c < nch ? (int32_t)keys[c] : 0);
+            m = max(m, carry);
+            if (c < nch) keys[c] = (uint32_t)m;
+            carry = (int32_t)rdlane((uint32_t)m, kWave - 1);
+        }
+    }
+    __syncthreads();
+    for (uint32_t c = tid; c < nch; c += kJumpThreads) {
+        const uint32_t key = c ? keys[c - 1] : 0u;
+        uint32_t d = key >> 16, off = key & 0xFFFFu;
+        uint32_t k = off ? mod_small(64u * c - d, off) : 0u;
+        for (uint32_t j = 0; j < 8; j++) {
+            u32x4 v = c4[8u * c + j];
+#pragma unroll
+            for (uint32_t h = 0; h < 8; h++) {
+                const uint32_t b = 64u * c + 8u * j + h;
+                const uint32_t sh = 16u * (h & 1u);
+                const uint32_t x = (v[h >> 1] >> sh) & 0xFFFFu;
+                const bool lit = (x & kLitFlag) != 0, start = !lit && x != 0;
+                if (start) {
+                    d = b;
+                    off = x;
+                    k = 0;
+                }
+                const uint32_t y = lit ? x : d - off + k;
+                if (!lit) {
+                    k++;
+                    if (k == off) k = 0;
+                }
+                v[h >> 1] = (v[h >> 1] & ~(0xFFFFu << sh)) | (y << sh);
+            }
+            c4[8u * c + j] = v;
+        }
+    }
+}
+
+// one round's update of 2 cells packed in a dword; `open` gathers the cells still unresolved afterwards
+__device__ __forceinline__ uint32_t jump_pair(const uint16_t *cells, uint32_t w, uint32_t &open) {
+    uint32_t lo = w & 0xFFFFu, hi = w >> 16;
+    if (!(lo & kLitFlag)) lo = cells[lo];
+    if (!(hi & kLitFlag)) hi = cells[hi];
+    open |= ~(lo & hi) & kLitFlag;
+    return lo | (hi << 16);
+}
+
+__global__ __launch_bounds__(kJumpThreads) void lz4_decode_jump_kernel(tyche_batch_t b, uint32_t in_cap,
+                                                                       uint32_t out_cap, uint32_t cells_bytes,
+                                                                       uint32_t list_cap, uint32_t lits_cap,
+                                                                       unsigned *ctr) {
+    // no static __shared__: prepare_launch raises the dynamic limit to the whole 160 KiB
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
+    uint32_t *shared_words = (uint32_t *)smem;   // [0] rv, [1] long-run count, [2] claimed page, [3..5] round flags, [6] sequences, [8..] chunk keys
+    int32_t &s_rv = *(int32_t *)&shared_words[0];
+    uint32_t &s_nlist = shared_words[1];
+    uint32_t &s_page = shared_words[2];
+    uint16_t *cells = (uint16_t *)(smem + kJumpHdr);
+    uint2 *list = (uint2 *)(smem + kJumpHdr + cells_bytes);
+    uint2 *lits = list + list_cap;
+    uint8_t *stage = smem + kJumpHdr + cells_bytes + 8u * (list_cap + lits_cap);
+    size_t page = blockIdx.x;
+    while (page < b.count) {
+        PROF_DECL
+        PROF_ADD(0, 1);
+        const PageRef p = batch_page(b, page);
+        const bool fits = p.src_len <= in_cap && p.dst_cap <= out_cap;
+        const uint32_t head = stage_in(p.src, fits ? p.src_len : 0u, stage, tid, kJumpThreads);
+        if (tid == 0) {
+            s_nlist = 0;
+            shared_words[3] = 0;   // round 0's flag
+        }
+        __syncthreads();
+        uint8_t *in = stage + head;
+        if (fits && tid < kPad) in[p.src_len + tid] = 0;   // kPad zero bytes past the end
+        __syncthreads();
+        PROF_MARK(1);
+        if (wave == 0) {
+            const int32_t r = fits ? jump_front(in, (int32_t)p.src_len, cells, (int32_t)p.dst_cap, lane, list,
+                                                list_cap, &s_nlist, lits, lits_cap, &shared_words[6])
+                                   : kResultTooLarge;
+            if (lane == 0) s_rv = r;
+        }
+        __syncthreads();
+        const int32_t rv = s_rv;
+        if (rv > 0) {
+            // long runs, then the tail of the last 16-cell group marked final
+            const uint32_t nl = min(s_nlist, list_cap);
+            for (uint32_t k = 0; k < nl; k++) fill_item(cells, in, list[k], (int32_t)tid, (int32_t)kJumpThreads);
+            // short literal runs, one sequence per thread
+            const uint32_t ns = min(shared_words[6], lits_cap);
+            const uint32_t ib = (uint32_t)(uintptr_t)in & 3u;
+            const uint32_t *A = (const uint32_t *)(in - ib);
+            for (uint32_t k = tid; k < ns; k += kJumpThreads) {
+                const uint2 it = lits[k];
+                const uint32_t n = it.x >> 16, o = it.x & 0xFFFFu, qa = it.y + ib;
+                if (n == 0) continue;
+                uint32_t a[5];
+#pragma unroll
+                for (int32_t j = 0; j < 5; j++) a[j] = A[(qa >> 2) + j];
+#pragma unroll
+                for (uint32_t i = 0; i < 16; i++)
+                    if (i < n)
+                        cells[o + i] = (uint16_t)(kLitFlag | ((__builtin_amdgcn_alignbyte(a[(i >> 2) + 1], a[i >> 2], qa & 3u) >>
+                                                               (8u * (i & 3u))) & 0xFFu));
+            }
+            const uint32_t n64 = ((uint32_t)rv + 63u) & ~63u;
+            if (tid < n64 - (uint32_t)rv) cells[(uint32_t)rv + tid] = (uint16_t)kLitFlag;
+            __syncthreads();
+            PROF_ADD(10, nl);
+            PROF_MARK(6);
+            jump_scan(cells, n64, shared_words + 8, tid);
+            __syncthreads();
+            PROF_MARK(7);
+            // pointer jumping, 8 cells per group
+            u32x4 *c4 = (u32x4 *)cells;
+            const uint32_t ng = n64 / 8u;
+            // round r's verdict: OR of every thread's open cells in flag[r % 3], which thread 0
+            // clears one round ahead (its last readers passed a barrier since)
+            uint32_t *flag = shared_words + 3;
+            for (uint32_t r = 0;; r++) {
+                if (tid == 0) flag[(r + 1) % 3] = 0;
+                uint32_t open = 0;
+                // two groups per step: 16 independent gathers in flight
+                for (uint32_t g = tid; g < ng; g += 2 * kJumpThreads) {
+                    const uint32_t g2 = g + kJumpThreads;
+                    const u32x4 fin = {0x80008000u, 0x80008000u, 0x80008000u, 0x80008000u};
+                    u32x4 v = c4[g], u = g2 < ng ? c4[g2] : fin;
+                    const bool dv = ((v.x & v.y & v.z & v.w) & 0x80008000u) != 0x80008000u;
+                    const bool du = ((u.x & u.y & u.z & u.w) & 0x80008000u) != 0x80008000u;
+                    if (dv) {
+                        v.x = jump_pair(cells, v.x, open);
+                        v.y = jump_pair(cells, v.y, open);
+                        v.z = jump_pair(cells, v.z, open);
+                        v.w = jump_pair(cells, v.w, open);
+                    }
+                    if (du) {
+                        u.x = jump_pair(cells, u.x, open);
+                        u.y = jump_pair(cells, u.y, open);
+                        u.z = jump_pair(cells, u.z, open);
+                        u.w = jump_pair(cells, u.w, open);
+                    }
+                    if (dv) c4[g] = v;
+                    if (du) c4[g2] = u;
+                }
+                if (open) atomicOr(&flag[r % 3], 1u);
+                __syncthreads();
+                PROF_ADD(9, 1);
+                if (flag[r % 3] == 0) break;
+            }
+            PROF_MARK(8);
+            // cells -> bytes, 16 per thread
+            uint8_t *dst = p.dst;
+            const bool al = ((uintptr_t)dst & 15u) == 0;
+            for (uint32_t g = tid; g < n64 / 16u; g += kJumpThreads) {
+                const u32x4 a = c4[2 * g], c = c4[2 * g + 1];
+                u32x4 o;
+                o.x = __builtin_amdgcn_perm(a.y, a.x, 0x06040200u);
+                o.y = __builtin_amdgcn_perm(a.w, a.z, 0x06040200u);
+                o.z = __builtin_amdgcn_perm(c.y, c.x, 0x06040200u);
+                o.w = __builtin_amdgcn_perm(c.w, c.z, 0x06040200u);
+                const uint32_t base = 16u * g;
+                if (al && base + 16u <= (uint32_t)rv) {
+                    __builtin_nontemporal_store(o, (u32x4 *)(dst + base));
+                } else {
+                    const uint32_t n = min(16u, (uint32_t)rv - base);
+                    for (uint32_t j = 0; j < n; j++) dst[base + j] = (uint8_t)(o[j >> 2] >> (8u * (j & 3u)));
+                }
+            }
+        }
+        PROF_MARK(12);
+        if (tid == 0) b.results[page] = rv;
+        if (ctr) {
+            if (tid == 0) s_page = atomicAdd(ctr, 1u) + gridDim.x;
+            __syncthreads();
+            page = s_page;
+        } else {
+            page += gridDim.x;
+        }
+        __syncthreads();
+    }
+}
+
 }  // namespace
+
+// Batches below this many pages (TYCHE_LZ4_JUMP_MAX) take the jump decoder when
+// the page fits its layout (16-bit cells: pages <= 32 KiB).
+constexpr long kJumpMax = 1024;
+static hipError_t launch_lz4_decode_jump(const tyche_batch_t &b, uint32_t in_cap, uint32_t out_cap, hipStream_t s,
+                                         bool &launched) {
+    launched = false;
+    static const long jmax = getenv("TYCHE_LZ4_JUMP_MAX") ? atol(getenv("TYCHE_LZ4_JUMP_MAX")) : kJumpMax;
+    if ((long)b.count >= jmax || out_cap > 32768u) return hipSuccess;
+    const uint32_t cells_bytes = std::max(2u * ((out_cap + 63u) & ~63u), (in_cap + 4u + 15u) & ~15u);
+    const uint32_t list_cap = out_cap / (uint32_t)(kJumpLong + 1) + 2u;
+    // one short-literal item per sequence (1,166 per bench page; pages with more fill per lane)
+    const uint32_t lits_cap = std::min(out_cap / 8u + 64u, 4096u);
+    const size_t lds = kJumpHdr + (size_t)cells_bytes + 8u * (list_cap + lits_cap) + ((in_cap + 16u + kPad + 15u) & ~15u);
+    if (lds > 150 * 1024) return hipSuccess;
+    const void *k = (const void *)lz4_decode_jump_kernel;
+    const size_t ncu = prepare_launch(k);
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kJumpThreads, lds) != hipSuccess || per_cu < 1)
+        per_cu = 1;
+    const size_t grid = std::min<size_t>(b.count, ncu * (size_t)per_cu);
+    WorkCounter ctr(s, grid < b.count);
+    if (grid < b.count && !ctr.get()) return hipErrorOutOfMemory;
+    unsigned *cp = grid < b.count ? ctr.get() : nullptr;
+    hipLaunchKernelGGL(lz4_decode_jump_kernel, dim3((unsigned)grid), dim3(kJumpThreads), lds, s, b, in_cap, out_cap,
+                       cells_bytes, list_cap, lits_cap, cp);
+    launched = true;
+    return hipGetLastError();
+}
 
 hipError_t launch_lz4_decode(const tyche_batch_t &b, uint32_t in_cap, uint32_t out_cap, hipStream_t s) {
     if (b.count == 0) return hipSuccess;
     // large batches: one page per lane (lz4_decode_lane.hip)
     if (lz4_lane_decode_wanted(b.count, in_cap, out_cap)) return launch_lz4_decode_lane(b, in_cap, out_cap, s);
+    // small batches: workgroup per page, pointer-jumping match resolution
+    {
+        bool launched = false;
+        const hipError_t e = launch_lz4_decode_jump(b, in_cap, out_cap, s, launched);
+        if (launched || e != hipSuccess) return e;
+    }
     // page window (output; the parse's owner stamps, so at least in_cap bytes;
     // the token positions at its top, <= in_cap / 3 + 1 of them, which always
     // fit: W >= in_cap + 20), then the staged stream
