@@ -38,7 +38,40 @@ for plen in (16384, 32768):
 '''
 
 
+ZCHILD = r'''
+import json, os, sys, torch
+sys.path.insert(0, os.getcwd())
+from tyche_amd import codec
+for plen in (16384, 32768):
+    big = codec.pagegen(2048, plen, dist=0)
+    comp_all, clen_all = codec.compress_pages(big, compressor_id=2)
+    torch.cuda.synchronize()
+    for n in (1, 8, 64, 512):
+        comp, clen, pages = comp_all[:n].contiguous(), clen_all[:n].contiguous(), big[:n]
+        mx = int(clen.max())
+        for mode, jmax in (("zlib-jump", "1024"), ("zlib-frontier", "0")):
+            os.environ["TYCHE_ZLIB_JUMP_MAX"] = jmax
+            out, rv = codec.decompress_pages(comp, clen, plen, compressor_id=2, max_comp_len=mx)
+            torch.cuda.synchronize()
+            ok = bool((rv == plen).all()) and torch.equal(out, pages)
+            ts = []
+            for _ in range(10):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(); codec.decompress_pages(comp, clen, plen, compressor_id=2, out=out, rv=rv, max_comp_len=mx); e1.record()
+                torch.cuda.synchronize(); ts.append(e0.elapsed_time(e1))
+            ts.sort()
+            t = ts[len(ts) // 2]
+            print(json.dumps({"decoder": mode, "page_len": plen, "batch": n, "us": round(t * 1000, 1),
+                              "GiBps": round(n * plen / (t / 1000) / 2**30, 2), "correct": ok}), flush=True)
+'''
+
+
 def main():
+    if os.environ.get("ZLIB", "1") != "0":
+        r = subprocess.run([sys.executable, "-c", ZCHILD], capture_output=True, text=True, timeout=600)
+        print(r.stdout.strip() or r.stderr.strip()[-1500:], flush=True)
+    if os.environ.get("LZ4", "1") == "0":
+        return
     for mode, jmax in (("jump", "32767"), ("wave", "0")):
         env = dict(os.environ, MODE=mode, TYCHE_LZ4_JUMP_MAX=jmax)
         r = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=600)

@@ -771,6 +771,109 @@ __device__ __forceinline__ void par_matches(uint8_t *out, uint32_t total, const 
     }
 }
 
+// The same matches resolved by pointer jumping (small batches, pages <= 32 KiB;
+// lz4_decode.hip's jump decoder describes the cells).  One 16-bit cell per
+// output byte: a literal is final (0x8000 | byte), a match byte holds the
+// position it copies, d - dist + (j mod dist), which always lies below its own
+// match; cell = cells[cell] until every cell is a literal gives inflate's
+// forward byte copies (inffast.c:263-307) in log2(chain depth) rounds.  Each
+// lane classifies a contiguous span of bytes, carrying in the last match start
+// before it (a max-scan over the lanes' last starts in M).  The frontier copy
+// above needs ~1,000 dependent rounds on a 16 KiB page of deflate's short
+// matches; the byte-level variant tried before it (one byte per step, 9 full
+// passes) was slower than the frontier.
+__device__ void par_matches_jump(uint8_t *out, uint32_t total, const uint32_t *M, uint16_t *cells, uint32_t lane) {
+    ZPROF_DECL
+    const uint32_t n8 = (total + 7u) & ~7u;
+    const uint32_t span = (((n8 + 63u) / 64u + kWave - 1u) / kWave) * 64u;   // bytes per lane, a multiple of 64
+    const uint32_t x0 = min(lane * span, n8), x1 = min(x0 + span, n8);
+    uint32_t last = 0;   // match starts are >= 1 (dist <= position)
+    for (uint32_t w = x0 >> 5; w < (x1 + 31u) >> 5; w++) {
+        const uint32_t m = M[w];
+        if (m) last = 32u * w + 31u - (uint32_t)__builtin_clz(m);
+    }
+    const int32_t incl = wave_incl_max((int32_t)last);
+    const int32_t before = __shfl_up(incl, 1);
+    const uint32_t carry = lane ? (uint32_t)before : 0u;
+    uint32_t d = 0, dist = 1, end = 0, k = 0;
+    if (carry) {
+        const uint32_t r = lds_ld32(out + carry);
+        d = carry;
+        dist = r & 0xFFFFu;
+        end = d + ((r >> 16) & 0xFFu) + 3u;
+        k = x0 < end ? mod_small(x0 - d, dist) : 0u;
+    }
+    for (uint32_t x = x0; x < x1; x += 8u) {
+        const uint32_t o0 = *(const uint32_t *)(out + x), o1 = *(const uint32_t *)(out + x + 4u);
+        const uint32_t mb = (M[x >> 5] >> (x & 31u)) & 0xFFu;
+        uint32_t c[4];
+#pragma unroll
+        for (uint32_t h = 0; h < 8; h++) {
+            const uint32_t xb = x + h;
+            if ((mb >> h) & 1u) {
+                const uint32_t r = lds_ld32(out + xb);   // the match's record: dist, len - 3
+                d = xb;
+                dist = r & 0xFFFFu;
+                end = xb + ((r >> 16) & 0xFFu) + 3u;
+                k = 0;
+            }
+            const uint32_t byte = ((h < 4 ? o0 : o1) >> (8u * (h & 3u))) & 0xFFu;
+            const bool in_match = xb < end;
+            const uint32_t v = in_match ? d - dist + k : (0x8000u | byte);
+            if (in_match) {
+                k++;
+                if (k == dist) k = 0;
+            }
+            if (h & 1u) c[h >> 1] |= v << 16;
+            else c[h >> 1] = v;
+        }
+        *(u32x4 *)(cells + x) = u32x4{c[0], c[1], c[2], c[3]};
+    }
+    WAVE_SYNC();
+    ZPROF_MARK(14);
+    u32x4 *c4 = (u32x4 *)cells;
+    const uint32_t ng = n8 / 8u;
+    for (;;) {
+        uint32_t open = 0;
+        for (uint32_t g = lane; g < ng; g += 2u * kWave) {
+            const uint32_t g2 = g + kWave;
+            const u32x4 fin = {0x80008000u, 0x80008000u, 0x80008000u, 0x80008000u};
+            u32x4 v = c4[g], u = g2 < ng ? c4[g2] : fin;
+            const bool dv = ((v.x & v.y & v.z & v.w) & 0x80008000u) != 0x80008000u;
+            const bool du = ((u.x & u.y & u.z & u.w) & 0x80008000u) != 0x80008000u;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                if (dv) {
+                    uint32_t lo = v[j] & 0xFFFFu, hi = v[j] >> 16;
+                    if (!(lo & 0x8000u)) lo = cells[lo];
+                    if (!(hi & 0x8000u)) hi = cells[hi];
+                    open |= ~(lo & hi) & 0x8000u;
+                    v[j] = lo | (hi << 16);
+                }
+                if (du) {
+                    uint32_t lo = u[j] & 0xFFFFu, hi = u[j] >> 16;
+                    if (!(lo & 0x8000u)) lo = cells[lo];
+                    if (!(hi & 0x8000u)) hi = cells[hi];
+                    open |= ~(lo & hi) & 0x8000u;
+                    u[j] = lo | (hi << 16);
+                }
+            }
+            if (dv) c4[g] = v;
+            if (du) c4[g2] = u;
+        }
+        ZPROF_ADD(15, 1);
+        if (!__ballot(open != 0)) break;
+        WAVE_SYNC();
+    }
+    WAVE_SYNC();
+    for (uint32_t g = lane; g < ng; g += kWave) {
+        const u32x4 a = c4[g];
+        uint32_t *o = (uint32_t *)(out + 8u * g);
+        o[0] = __builtin_amdgcn_perm(a.y, a.x, 0x06040200u);
+        o[1] = __builtin_amdgcn_perm(a.w, a.z, 0x06040200u);
+    }
+}
+
 __device__ __forceinline__ void seek_bits(BitReader &r, uint32_t bitpos, uint32_t src_len, uint32_t lane) {
     seek(r, bitpos >> 3, lane);
     r.avail = (int32_t)(src_len * 8u - (bitpos & ~7u));
@@ -782,7 +885,7 @@ __device__ __forceinline__ void seek_bits(BitReader &r, uint32_t bitpos, uint32_
 // Returns the decoded length, kZData, or kFallback.
 __device__ __forceinline__ int32_t inflate_par(BitReader &r, const PageRef &p, const uint8_t *stage, uint32_t head, uint8_t *out,
                                int32_t cap, uint32_t W, uint32_t *M, uint32_t *LT, uint32_t *DT, uint8_t *lens,
-                               uint16_t *sortL, uint16_t *sortD, uint32_t lane) {
+                               uint16_t *sortL, uint16_t *sortD, uint16_t *cells, uint32_t lane) {
     ZPROF_DECL
     if (zlib_header(r, lane)) return kFallback;
     const uint32_t *S32 = (const uint32_t *)stage;
@@ -810,7 +913,8 @@ __device__ __forceinline__ int32_t inflate_par(BitReader &r, const PageRef &p, c
     const uint8_t *tp = stage + head + tb;
     const uint32_t want = ((uint32_t)tp[0] << 24) | ((uint32_t)tp[1] << 16) | ((uint32_t)tp[2] << 8) | tp[3];
     WAVE_SYNC();
-    par_matches(out, (uint32_t)op, M, (uint16_t *)stage, lane);   // the stage is free now
+    if (cells) par_matches_jump(out, (uint32_t)op, M, cells, lane);
+    else par_matches(out, (uint32_t)op, M, (uint16_t *)stage, lane);   // the stage is free now
     WAVE_SYNC();
     ZPROF_MARK(6);
     if (lds_adler32(out, (uint32_t)op, lane) != want) return kZData;
@@ -881,7 +985,8 @@ __global__ __launch_bounds__(64) void zlib_inflate_kernel(tyche_batch_t b, uint3
 // stage.
 __global__ __launch_bounds__(64) void zlib_inflate_par_kernel(tyche_batch_t b, uint32_t out_cap, uint32_t off_lens,
                                                               uint32_t off_lt, uint32_t off_m, uint32_t off_stage,
-                                                              uint32_t stage_cap, int32_t no_fallback, unsigned *ctr) {
+                                                              uint32_t stage_cap, int32_t no_fallback, uint32_t off_cells,
+                                                              unsigned *ctr) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t lane = threadIdx.x;
     uint8_t *out = smem;
@@ -892,6 +997,7 @@ __global__ __launch_bounds__(64) void zlib_inflate_par_kernel(tyche_batch_t b, u
     uint32_t *DT = LT + 1024;
     uint32_t *M = (uint32_t *)(smem + off_m);
     uint8_t *stage = smem + off_stage;
+    uint16_t *cells = off_cells ? (uint16_t *)(smem + off_cells) : nullptr;
     size_t page = blockIdx.x;
     while (page < b.count) {
         const PageRef p = batch_page(b, page);
@@ -911,7 +1017,7 @@ __global__ __launch_bounds__(64) void zlib_inflate_par_kernel(tyche_batch_t b, u
                 r.wa = load_win(r, 0, lane);
                 r.wb = load_win(r, 256, lane);
                 rv = inflate_par(r, p, stage, head, out, (int32_t)p.dst_cap, off_lens, M, LT, DT, lens, sortL, sortD,
-                                 lane);
+                                 cells, lane);
                 WAVE_SYNC();
             }
             if (rv == kFallback && !no_fallback) {
@@ -954,7 +1060,13 @@ hipError_t launch_zlib_inflate(const tyche_batch_t &b, uint32_t out_cap, hipStre
         const uint32_t off_m = off_lt + 2u * 4096u;
         const uint32_t off_stage = off_m + ((((out_cap + 31u) / 32u) * 4u + 15u) & ~15u);
         const uint32_t stage_cap = (std::max(2048u, out_cap / 2u) + 63u) & ~15u;
-        const size_t lds = (size_t)off_stage + stage_cap;
+        // small batches (restores) resolve matches by pointer jumping: 2 bytes of LDS per
+        // output byte more (below TYCHE_ZLIB_JUMP_MAX pages, default 512: at 512 x 32 KiB the smaller residency
+        // already costs more than the frontier copies; 0 = never)
+        const char *jenv = getenv("TYCHE_ZLIB_JUMP_MAX");
+        const long jmax = jenv ? atol(jenv) : 512;
+        const uint32_t off_cells = (long)b.count < jmax && out_cap <= 32768u ? off_stage + stage_cap : 0u;
+        const size_t lds = (size_t)off_stage + stage_cap + (off_cells ? 2u * ((out_cap + 7u) & ~7u) : 0u);
         if (lds <= 160 * 1024) {
             const size_t ncu = prepare_launch((const void *)zlib_inflate_par_kernel);
             const size_t per_cu = waves_per_cu((const void *)zlib_inflate_par_kernel, lds);
@@ -962,7 +1074,7 @@ hipError_t launch_zlib_inflate(const tyche_batch_t &b, uint32_t out_cap, hipStre
             WorkCounter ctr(s, grid < b.count);
             if (!ctr.get()) return hipErrorOutOfMemory;
             hipLaunchKernelGGL(zlib_inflate_par_kernel, dim3((unsigned)grid), dim3(kWave), lds, s, b, out_cap,
-                               off_lens, off_lt, off_m, off_stage, stage_cap, (int32_t)(par == 2), ctr.get());
+                               off_lens, off_lt, off_m, off_stage, stage_cap, (int32_t)(par == 2), off_cells, ctr.get());
             return hipGetLastError();
         }
     }
