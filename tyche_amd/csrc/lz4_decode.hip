@@ -247,46 +247,15 @@ __device__ __forceinline__ void chain_entries(const uint8_t *in, int32_t L, uint
 __device__ uint32_t parse_chain(const uint8_t *in, int32_t L, uint8_t *owner, uint16_t *win_end, uint16_t *&seqpos,
                                 uint32_t lane) {
     PROF_DECL
-    const uint32_t S = ((uint32_t)L + kWave - 1) / kWave;
-    const uint32_t seg0 = lane * S;
-    const uint32_t seg1 = min(seg0 + S, (uint32_t)L);
-    for (uint32_t w = lane; w < ((uint32_t)L + 3) / 4; w += kWave) ((uint32_t *)owner)[w] = 0;
-    WAVE_SYNC();
-    uint32_t p = seg0;
-    while (p < seg1) {
-        owner[p] = (uint8_t)(lane + 1);
-        p = next_token(in, L, p);
-    }
-    WAVE_SYNC();
-    PROF_MARK(2);
-    uint32_t y = p, o = 0;                        // hand-off position and its stamp (0 = chain ends)
-    if (seg0 < seg1) {
-        while (y < (uint32_t)L) {
-            const uint32_t ow = owner[y];
-            if (ow > lane + 1) { o = ow; break; }
-            y = next_token(in, L, y);
-        }
-    }
-    uint32_t entry = kEnd;
-    {
-        uint32_t cur = 0, e = 0;
-        for (uint32_t it = 0; it < kWave; it++) {
-            if (lane == cur) entry = e;
-            e = rdlane(y, cur);
-            const uint32_t nx = rdlane(o, cur);
-            PROF_ADD(4, 1);
-            if (nx == 0) break;
-            cur = nx - 1;
-        }
-    }
-    PROF_MARK(3);
+    uint32_t entry, y;
+    chain_entries(in, L, owner, lane, entry, y);
     uint32_t cnt = 0;
-    for (uint32_t q = entry; q < (uint32_t)L && q != y; q = next_token(in, L, q)) cnt++;
+    for (uint32_t q = entry; q < (uint32_t)L && q != y; q = next_token_w(in, L, q)) cnt++;
     const int32_t incl = wave_incl_sum((int32_t)cnt);
     uint32_t base = (uint32_t)incl - cnt;
     const uint32_t total = rdlane((uint32_t)incl, kWave - 1);
     seqpos = win_end - total;
-    for (uint32_t q = entry; q < (uint32_t)L && q != y; q = next_token(in, L, q)) seqpos[base++] = (uint16_t)q;
+    for (uint32_t q = entry; q < (uint32_t)L && q != y; q = next_token_w(in, L, q)) seqpos[base++] = (uint16_t)q;
     WAVE_SYNC();
     PROF_MARK(5);
     PROF_ADD(11, total);
@@ -1058,7 +1027,7 @@ __global__ __launch_bounds__(kJumpThreads) void lz4_decode_jump_kernel(tyche_bat
 
 // Batches below this many pages (TYCHE_LZ4_JUMP_MAX) take the jump decoder when
 // the page fits its layout (16-bit cells: pages <= 32 KiB).
-constexpr long kJumpMax = 1024;
+constexpr long kJumpMax = 512;
 static hipError_t launch_lz4_decode_jump(const tyche_batch_t &b, uint32_t in_cap, uint32_t out_cap, hipStream_t s,
                                          bool &launched) {
     launched = false;

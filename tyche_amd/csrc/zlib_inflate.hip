@@ -663,30 +663,38 @@ __device__ __forceinline__ int32_t par_block(const ParTabs &t, const uint32_t *S
     }
     WAVE_SYNC();
     ZPROF_MARK(2);
-    // 2. bridge to a later lane's walk
+    // 2. bridge to a later lane's walk, and 3. follow the hand-offs from lane 0.
+    // Bridges advance in rounds of kBridgeSteps symbols, each followed by the
+    // hand-off walk as far as the finished bridges reach; lanes behind it stop
+    // (a lane off the true chain may bridge for a long way before it meets a
+    // later lane's walk, and one loop for all lanes waited for the longest).
+    constexpr uint32_t kBridgeSteps = 4;
     uint32_t o = 0;   // owner lane + 1 of the hand-off position, 0 = chain ends here
-    if (a < E && stop == 0) {
-        while (y < E) {
-            if ((V[(y - base) >> 5] >> (y & 31u)) & 1u) {
-                o = (y - base) / S + 1u;
-                break;
-            }
-            const uint32_t k = par_sym(t, S32, y, val, dist);
-            if (k >= kSymEob) {
-                stop = k;
-                break;
-            }
-        }
-    }
-    // 3. follow the hand-offs from lane 0
+    bool done = !(a < E && stop == 0) || y >= E;
     uint32_t entry = 0xFFFFFFFFu;
     uint32_t cur = 0, e = P0;
-    for (uint32_t it = 0; it < kWave; it++) {
-        if (lane == cur) entry = e;
-        e = rdlane(y, cur);
-        const uint32_t nx = rdlane(o, cur);
-        if (nx == 0) break;
-        cur = nx - 1;
+    for (bool fin = false; !fin;) {
+        for (uint32_t it = 0; it < kBridgeSteps; it++) {
+            if (!done) {
+                if ((V[(y - base) >> 5] >> (y & 31u)) & 1u) {
+                    o = (y - base) / S + 1u;
+                    done = true;
+                } else {
+                    const uint32_t k = par_sym(t, S32, y, val, dist);
+                    if (k >= kSymEob) stop = k;
+                    done = k >= kSymEob || y >= E;
+                }
+            }
+        }
+        for (;;) {
+            if (lane == cur) entry = e;
+            if (!rdlane((uint32_t)done, cur)) break;   // cur's hand-off not found yet
+            e = rdlane(y, cur);
+            const uint32_t nx = rdlane(o, cur);
+            if (nx == 0) { fin = true; break; }
+            cur = nx - 1;
+        }
+        if (lane < cur) done = true;
     }
     ZPROF_MARK(3);
     ZPROF_ADD(10, cur);
