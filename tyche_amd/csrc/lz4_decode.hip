@@ -71,35 +71,6 @@ __device__ unsigned long long g_prof[16];
 
 
 
-// Position of the token after the sequence whose token is at p, or kEnd when
-// that sequence ends the chain on the input side (terminal literal run, or an
-// overrun while reading match-length bytes).  Mirrors the input-side reads of
-// lz4.c:1134-1143, 1147, 1165, 1172-1182.
-__device__ __forceinline__ uint32_t next_token(const uint8_t *in, int32_t L, uint32_t p) {
-    uint32_t t = in[p];
-    int32_t q = (int32_t)p + 1;
-    int32_t lit = (int32_t)(t >> 4);
-    if (lit == kRunMask) {
-        uint32_t s;
-        do {
-            s = in[q];
-            q++;
-            lit += (int32_t)s;
-        } while (q < L - kRunMask && s == 255);
-    }
-    if (q + lit > L - 8) return kEnd;
-    q += lit + 2;
-    if ((t & 15) == 15) {
-        uint32_t s;
-        do {
-            s = in[q];
-            q++;
-            if (q > L - kLastLiterals) return kEnd;
-        } while (s == 255);
-    }
-    return (uint32_t)q;
-}
-
 struct SeqIn {
     int32_t lit, ls, off, ml, q2;
     bool in_term, ml_err;
@@ -169,7 +140,10 @@ __device__ __forceinline__ SeqIn decode_seq_in(const uint8_t *in, int32_t L, int
     }
     return s;
 }
-// next_token through the window decoder (same positions, same kEnd cases)
+// Position of the token after the sequence whose token is at p, or kEnd when
+// that sequence ends the chain on the input side (terminal literal run, or an
+// overrun while reading match-length bytes): the input-side reads of
+// lz4.c:1134-1143, 1147, 1165, 1172-1182.
 __device__ __forceinline__ uint32_t next_token_w(const uint8_t *in, int32_t L, uint32_t p) {
     const SeqIn s = decode_seq_in(in, L, (int32_t)p);
     return s.in_term || s.ml_err ? kEnd : (uint32_t)s.q2;
