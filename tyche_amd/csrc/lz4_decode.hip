@@ -660,7 +660,7 @@ constexpr int32_t kJumpLong = 16;
 constexpr uint32_t kLitFlag = 0x8000u;
 // LDS bytes before the cells: the workgroup's shared words (8) and jump_scan's
 // chunk keys (one per 64 cells, pages <= 32 KiB)
-constexpr uint32_t kJumpHdr = 32 + 4 * 512;
+constexpr uint32_t kJumpHdr = 32 + 4 * 512 + 4 * 3 * 64;   // + JumpLanes
 
 // cells [o + i0, o + n) step `step` of a literal run read from in[ls..]
 __device__ __forceinline__ void fill_lit(uint16_t *cells, const uint8_t *in, int32_t o, int32_t ls, int32_t n,
@@ -719,7 +719,7 @@ __device__ int32_t jump_front(const uint8_t *in, int32_t L, uint16_t *cells, int
     int32_t o = incl - olen;
     const int32_t cincl = wave_incl_sum(cnt);
     uint32_t k = (uint32_t)(cincl - cnt);   // this lane's first sequence number
-    if (lane == kWave - 1) *nseq = (uint32_t)cincl;
+    if (nseq && lane == kWave - 1) *nseq = (uint32_t)cincl;
     // pass 2: checks in the reference's order, then the fills
     int32_t status = 0, rv = 0;   // 1 terminal success, 2 error
     for (uint32_t q = entry; q < (uint32_t)L && q != y;) {
@@ -739,7 +739,7 @@ __device__ int32_t jump_front(const uint8_t *in, int32_t L, uint16_t *cells, int
         // literal runs: short ones as this sequence's item for the workgroup (lits[k]), long
         // ones on the run list; per lane only when lits[] is full
         const bool short_lit = s.lit <= kJumpLong;
-        if (k < lits_cap)
+        if (lits && k < lits_cap)
             lits[k] = short_lit ? make_uint2((uint32_t)o | ((uint32_t)s.lit << 16), (uint32_t)s.ls) : make_uint2(0u, 0u);
         if (!short_lit) {
             const uint32_t kl = atomicAdd(nlist, 1u);
@@ -785,6 +785,135 @@ __device__ int32_t jump_front(const uint8_t *in, int32_t L, uint16_t *cells, int
     const uint64_t stop = __ballot(status != 0);
     if (stop == 0) return -1;   // unreachable: the chain always ends in a terminal or failing sequence
     return (int32_t)rdlane((uint32_t)rv, (uint32_t)__builtin_ctzll(stop));
+}
+
+// Literal run of sequence s at output o: short ones from the decode window (or
+// aligned dwords), long ones onto the workgroup's run list.
+__device__ __forceinline__ void put_literals(uint16_t *cells, const uint8_t *in, const SeqIn &s, int32_t o, uint2 *list,
+                                             uint32_t list_cap, uint32_t *nlist) {
+    if (s.lit > kJumpLong) {
+        const uint32_t kl = atomicAdd(nlist, 1u);
+        const uint2 it = make_uint2((uint32_t)o | ((uint32_t)s.lit << 16), (uint32_t)s.ls | 0x80000000u);
+        if (kl < list_cap) list[kl] = it;
+        else fill_item(cells, in, it, 0, 1);
+        return;
+    }
+    if (s.lit <= 0) return;
+    uint32_t w[4];
+    if (s.lit_win) {
+#pragma unroll
+        for (int32_t j = 0; j < 4; j++) w[j] = s.lb[j];
+    } else {
+        const uint32_t ib = (uint32_t)(uintptr_t)in & 3u, qa = (uint32_t)s.ls + ib;
+        const uint32_t *A = (const uint32_t *)(in - ib);
+        uint32_t a[5];
+#pragma unroll
+        for (int32_t j = 0; j < 5; j++) a[j] = A[(qa >> 2) + j];
+#pragma unroll
+        for (int32_t j = 0; j < 4; j++) w[j] = __builtin_amdgcn_alignbyte(a[j + 1], a[j], qa & 3u);
+    }
+#pragma unroll
+    for (int32_t i = 0; i < 16; i++)
+        if (i < s.lit) cells[o + i] = (uint16_t)(kLitFlag | ((w[i >> 2] >> (8 * (i & 3))) & 0xFFu));
+}
+
+// The workgroup's view of wave 0's walk: items[i * 64 + l] = token position of
+// lane l's i-th sequence | its output offset within the lane's part << 16, and
+// per lane the sequence count, the output base and the first sequence number.
+struct JumpLanes {
+    uint32_t cnt[kWave], base_o[kWave], base_k[kWave];
+};
+constexpr int32_t kJumpPending = INT32_MIN + 2;   // rv decided by the workgroup's checks
+constexpr uint32_t kJumpOvf = 512;                // overflow items (sequences past a lane's rows)
+
+// Wave 0: chain entries, zeroed cells, one walk per lane recording its
+// sequences (items, rows per lane), the lanes' prefix sums.  Returns
+// kJumpPending, or the final value when no check is left to run (empty page),
+// or jump_front's value when a lane's part does not fit the items (> rows
+// sequences or > 64 KiB of output): the two-walk path below.
+__device__ int32_t jump_walk(const uint8_t *in, int32_t L, uint16_t *cells, int32_t C, uint32_t lane, uint32_t *items,
+                             uint32_t rows, uint2 *ovf, uint32_t ovf_cap, uint32_t *novf, JumpLanes *lanes, uint2 *list,
+                             uint32_t list_cap, uint32_t *nlist) {
+    if (C == 0) return (L == 1 && in[0] == 0) ? 0 : -1;
+    if (L <= 0) return -1;
+    uint32_t entry, y;
+    chain_entries(in, L, (uint8_t *)cells, lane, entry, y);
+    PROF_DECL
+    {
+        const uint32_t nv = (((uint32_t)C + 63u) & ~63u) / 8u;
+        u32x4 *c4 = (u32x4 *)cells;
+        const u32x4 z = {0u, 0u, 0u, 0u};
+        for (uint32_t v = lane; v < nv; v += kWave) c4[v] = z;
+    }
+    uint32_t olen = 0, cnt = 0, q_over = 0, o_over = 0;
+    bool over = false;
+    for (uint32_t q = entry; q < (uint32_t)L && q != y;) {
+        const SeqIn s = decode_seq_in(in, L, (int32_t)q);
+        over |= olen >= 0x10000u;
+        if (cnt < rows) items[cnt * kWave + lane] = q | (olen << 16);
+        if (cnt == rows) { q_over = q; o_over = olen; }
+        cnt++;
+        if (s.in_term) { olen += (uint32_t)s.lit; break; }
+        if (s.ml_err) break;
+        olen += (uint32_t)(s.lit + s.ml);
+        q = (uint32_t)s.q2;
+    }
+    WAVE_SYNC();
+    PROF_MARK(4);
+    // a lane's part can span several segments (the walks after it had not met
+    // the true chain): its sequences past `rows` go to the overflow items
+    const uint32_t extra = cnt > rows ? cnt - rows : 0u;
+    const uint32_t xi = (uint32_t)wave_incl_sum((int32_t)extra);
+    const uint32_t nx = rdlane(xi, kWave - 1);
+    if (__ballot(over) || nx > ovf_cap)
+        return jump_front(in, L, cells, C, lane, list, list_cap, nlist, nullptr, 0u, nullptr);
+    if (lane == 0) *novf = nx;
+    if (extra) {
+        uint32_t at = xi - extra, q = q_over, o = o_over;
+        for (uint32_t i = rows; i < cnt; i++) {
+            const SeqIn s = decode_seq_in(in, L, (int32_t)q);
+            ovf[at++] = make_uint2(q | (o << 16), lane | (i << 8));
+            o += (uint32_t)(s.in_term ? s.lit : s.lit + s.ml);
+            q = (uint32_t)s.q2;
+        }
+    }
+    const int32_t oi = wave_incl_sum((int32_t)olen), ci = wave_incl_sum((int32_t)cnt);
+    lanes->cnt[lane] = cnt;
+    lanes->base_o[lane] = (uint32_t)oi - olen;
+    lanes->base_k[lane] = (uint32_t)ci - cnt;
+    return kJumpPending;
+}
+
+// Item j of the workgroup's loops: lane l's i-th sequence (column items first, then the overflow)
+__device__ __forceinline__ bool jump_item(const uint32_t *items, const uint2 *ovf, uint32_t rows, uint32_t j,
+                                          const JumpLanes *lanes, uint32_t &l, uint32_t &i, uint32_t &it) {
+    if (j < rows * kWave) {
+        l = j & (kWave - 1);
+        i = j / kWave;
+        if (i >= min(lanes->cnt[l], rows)) return false;
+        it = items[j];
+        return true;
+    }
+    const uint2 x = ovf[j - rows * kWave];
+    l = x.y & 0xFFu;
+    i = x.y >> 8;
+    it = x.x;
+    return true;
+}
+
+// The reference's acceptance checks for one sequence at output position o
+// (lz4.c:1147-1168, 1176, 1225): 0 ok, 1 terminal success, 2 error; rv the value.
+__device__ __forceinline__ int32_t seq_check(const SeqIn &s, int32_t o, int32_t L, int32_t C, int32_t &rv) {
+    const int32_t d = o + s.lit;
+    if (o + s.lit > C - kMfLimit || s.in_term) {
+        if (s.ls + s.lit != L || o + s.lit > C) { rv = -s.ls - 1; return 2; }
+        rv = o + s.lit;
+        return 1;
+    }
+    if (s.off > d) { rv = -(s.ls + s.lit + 2) - 1; return 2; }
+    if (s.ml_err) { rv = -s.q2 - 1; return 2; }
+    if (d + s.ml > C - kLastLiterals) { rv = -s.q2 - 1; return 2; }
+    return 0;
 }
 
 // Match cells from their start markers: a cell is a literal (0x8000 | byte), a
@@ -862,19 +991,21 @@ __device__ __forceinline__ uint32_t jump_pair(const uint16_t *cells, uint32_t w,
 
 __global__ __launch_bounds__(kJumpThreads) void lz4_decode_jump_kernel(tyche_batch_t b, uint32_t in_cap,
                                                                        uint32_t out_cap, uint32_t cells_bytes,
-                                                                       uint32_t list_cap, uint32_t lits_cap,
+                                                                       uint32_t list_cap, uint32_t rows,
                                                                        unsigned *ctr) {
     // no static __shared__: prepare_launch raises the dynamic limit to the whole 160 KiB
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
-    uint32_t *shared_words = (uint32_t *)smem;   // [0] rv, [1] long-run count, [2] claimed page, [3..5] round flags, [6] sequences, [8..] chunk keys
+    uint32_t *shared_words = (uint32_t *)smem;   // [0] rv, [1] long-run count, [2] claimed page, [3..5] round flags, [6] overflow items, [7] first failing sequence, [8..519] chunk keys, then JumpLanes
     int32_t &s_rv = *(int32_t *)&shared_words[0];
     uint32_t &s_nlist = shared_words[1];
     uint32_t &s_page = shared_words[2];
     uint16_t *cells = (uint16_t *)(smem + kJumpHdr);
     uint2 *list = (uint2 *)(smem + kJumpHdr + cells_bytes);
-    uint2 *lits = list + list_cap;
-    uint8_t *stage = smem + kJumpHdr + cells_bytes + 8u * (list_cap + lits_cap);
+    uint32_t *items = (uint32_t *)(list + list_cap);
+    uint2 *ovf = (uint2 *)(items + kWave * rows);
+    uint8_t *stage = smem + kJumpHdr + cells_bytes + 8u * list_cap + 4u * kWave * rows + 8u * kJumpOvf;
+    JumpLanes *lanes = (JumpLanes *)(shared_words + 8 + 512);
     size_t page = blockIdx.x;
     while (page < b.count) {
         PROF_DECL
@@ -891,35 +1022,63 @@ __global__ __launch_bounds__(kJumpThreads) void lz4_decode_jump_kernel(tyche_bat
         if (fits && tid < kPad) in[p.src_len + tid] = 0;   // kPad zero bytes past the end
         __syncthreads();
         PROF_MARK(1);
+        const int32_t L = (int32_t)p.src_len, C = (int32_t)p.dst_cap;
         if (wave == 0) {
-            const int32_t r = fits ? jump_front(in, (int32_t)p.src_len, cells, (int32_t)p.dst_cap, lane, list,
-                                                list_cap, &s_nlist, lits, lits_cap, &shared_words[6])
+            const int32_t r = fits ? jump_walk(in, L, cells, C, lane, items, rows, ovf, kJumpOvf, &shared_words[6], lanes,
+                                               list, list_cap, &s_nlist)
                                    : kResultTooLarge;
-            if (lane == 0) s_rv = r;
+            if (lane == 0) {
+                s_rv = r;
+                shared_words[7] = 0xFFFFFFFFu;   // first failing sequence
+            }
         }
         __syncthreads();
+        PROF_MARK(5);
+        if (s_rv == kJumpPending) {
+            // every sequence checked at once; the first failing one in stream order decides
+            const uint32_t nitems = rows * kWave + shared_words[6];
+            for (uint32_t j = tid; j < nitems; j += kJumpThreads) {
+                uint32_t l, i, it;
+                if (!jump_item(items, ovf, rows, j, lanes, l, i, it)) continue;
+                const SeqIn sq = decode_seq_in(in, L, (int32_t)(it & 0xFFFFu));
+                int32_t r;
+                if (seq_check(sq, (int32_t)(lanes->base_o[l] + (it >> 16)), L, C, r))
+                    atomicMin(&shared_words[7], lanes->base_k[l] + i);
+            }
+            __syncthreads();
+            const uint32_t first = shared_words[7];
+            if (first == 0xFFFFFFFFu && tid == 0) s_rv = -1;   // unreachable: the chain ends in a stop
+            // fills of every sequence up to it (and its verdict)
+            for (uint32_t j = tid; j < nitems; j += kJumpThreads) {
+                uint32_t l, i, it;
+                if (!jump_item(items, ovf, rows, j, lanes, l, i, it) || lanes->base_k[l] + i > first) continue;
+                const SeqIn sq = decode_seq_in(in, L, (int32_t)(it & 0xFFFFu));
+                const int32_t o = (int32_t)(lanes->base_o[l] + (it >> 16));
+                int32_t r;
+                const int32_t st = seq_check(sq, o, L, C, r);
+                if (lanes->base_k[l] + i == first) s_rv = r;
+                if (st == 2) continue;
+                put_literals(cells, in, sq, o, list, list_cap, &s_nlist);
+                if (st == 1) continue;
+                const int32_t d = o + sq.lit;
+                if (sq.off != 0) {
+                    cells[d] = (uint16_t)sq.off;   // the run's start marker; jump_scan fills the rest
+                } else if (sq.ml > kJumpLong) {
+                    const uint32_t kl = atomicAdd(&s_nlist, 1u);
+                    const uint2 li = make_uint2((uint32_t)d | ((uint32_t)sq.ml << 16), 0u);
+                    if (kl < list_cap) list[kl] = li;
+                    else fill_item(cells, in, li, 0, 1);
+                } else {
+                    fill_match(cells, d, 0, sq.ml, 0, 1);
+                }
+            }
+            __syncthreads();
+        }
         const int32_t rv = s_rv;
         if (rv > 0) {
-            // long runs, then the tail of the last 16-cell group marked final
+            // long runs, then the tail of the last 64-cell chunk marked final
             const uint32_t nl = min(s_nlist, list_cap);
             for (uint32_t k = 0; k < nl; k++) fill_item(cells, in, list[k], (int32_t)tid, (int32_t)kJumpThreads);
-            // short literal runs, one sequence per thread
-            const uint32_t ns = min(shared_words[6], lits_cap);
-            const uint32_t ib = (uint32_t)(uintptr_t)in & 3u;
-            const uint32_t *A = (const uint32_t *)(in - ib);
-            for (uint32_t k = tid; k < ns; k += kJumpThreads) {
-                const uint2 it = lits[k];
-                const uint32_t n = it.x >> 16, o = it.x & 0xFFFFu, qa = it.y + ib;
-                if (n == 0) continue;
-                uint32_t a[5];
-#pragma unroll
-                for (int32_t j = 0; j < 5; j++) a[j] = A[(qa >> 2) + j];
-#pragma unroll
-                for (uint32_t i = 0; i < 16; i++)
-                    if (i < n)
-                        cells[o + i] = (uint16_t)(kLitFlag | ((__builtin_amdgcn_alignbyte(a[(i >> 2) + 1], a[i >> 2], qa & 3u) >>
-                                                               (8u * (i & 3u))) & 0xFFu));
-            }
             const uint32_t n64 = ((uint32_t)rv + 63u) & ~63u;
             if (tid < n64 - (uint32_t)rv) cells[(uint32_t)rv + tid] = (uint16_t)kLitFlag;
             __syncthreads();
@@ -1001,7 +1160,7 @@ __global__ __launch_bounds__(kJumpThreads) void lz4_decode_jump_kernel(tyche_bat
 
 // Batches below this many pages (TYCHE_LZ4_JUMP_MAX) take the jump decoder when
 // the page fits its layout (16-bit cells: pages <= 32 KiB).
-constexpr long kJumpMax = 512;
+constexpr long kJumpMax = 1024;
 static hipError_t launch_lz4_decode_jump(const tyche_batch_t &b, uint32_t in_cap, uint32_t out_cap, hipStream_t s,
                                          bool &launched) {
     launched = false;
@@ -1009,9 +1168,12 @@ static hipError_t launch_lz4_decode_jump(const tyche_batch_t &b, uint32_t in_cap
     if ((long)b.count >= jmax || out_cap > 32768u) return hipSuccess;
     const uint32_t cells_bytes = std::max(2u * ((out_cap + 63u) & ~63u), (in_cap + 4u + 15u) & ~15u);
     const uint32_t list_cap = out_cap / (uint32_t)(kJumpLong + 1) + 2u;
-    // one short-literal item per sequence (1,166 per bench page; pages with more fill per lane)
-    const uint32_t lits_cap = std::min(out_cap / 8u + 64u, 4096u);
-    const size_t lds = kJumpHdr + (size_t)cells_bytes + 8u * (list_cap + lits_cap) + ((in_cap + 16u + kPad + 15u) & ~15u);
+    // items: rows sequences per lane (the bench pages' segments hold <= 44 tokens at 16 KiB,
+    // <= 85 at 32 KiB), the rest of a longer lane part in kJumpOvf overflow items; a page
+    // with more takes jump_front's two walks
+    const uint32_t rows = std::min(std::max(out_cap / 512u, 24u), 64u);
+    const size_t lds = kJumpHdr + (size_t)cells_bytes + 8u * list_cap + 4u * 64u * rows + 8u * kJumpOvf +
+                       ((in_cap + 16u + kPad + 15u) & ~15u);
     if (lds > 150 * 1024) return hipSuccess;
     const void *k = (const void *)lz4_decode_jump_kernel;
     const size_t ncu = prepare_launch(k);
@@ -1023,7 +1185,7 @@ static hipError_t launch_lz4_decode_jump(const tyche_batch_t &b, uint32_t in_cap
     if (grid < b.count && !ctr.get()) return hipErrorOutOfMemory;
     unsigned *cp = grid < b.count ? ctr.get() : nullptr;
     hipLaunchKernelGGL(lz4_decode_jump_kernel, dim3((unsigned)grid), dim3(kJumpThreads), lds, s, b, in_cap, out_cap,
-                       cells_bytes, list_cap, lits_cap, cp);
+                       cells_bytes, list_cap, rows, cp);
     launched = true;
     return hipGetLastError();
 }
