@@ -14,8 +14,8 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from tyche_amd import _lib, codec  # noqa: E402
 
-WG = {0: "pages", 1: "stage_in", 6: "front+long_fill", 7: "scan_fill", 8: "jump_rounds", 12: "pack_store", 9: "rounds", 10: "long_runs"}
-W0 = {2: "chain_walk", 3: "chain_bridge", 4: "pass1_lengths", 5: "pass2_checks_fill"}
+WG = {0: "pages", 1: "stage_in", 5: "front_total", 6: "checks_fills+long_runs", 7: "scan_fill", 8: "jump_rounds", 12: "pack_store", 9: "rounds", 10: "long_runs"}
+W0 = {2: "chain_walk", 3: "chain_bridge", 4: "walk_items"}
 
 
 def main():
