@@ -1187,14 +1187,14 @@ int buffer__decompress(Buffer *buf, int compressor_id) {
 // buffer__decompress status.  Per-buffer semantics are unchanged.
 //
 // Each codec has its own queue and dispatchers (TYCHE_RESTORE_DISPATCHERS per
-// codec, default two per device): a batch's latency is that of its slowest
-// page (~0.1 ms for a 16 KiB LZ4 page on the jump decoder, ~0.3 ms for zlib,
-// tools/latency.c), so LZ4 restores never wait behind a zlib batch, and while
-// one batch of a codec runs the next one collects.  With two codecs active
-// that is 4 batches in flight, one per hardware queue (GPU_MAX_HW_QUEUES):
-// tools/cycle.c restores 1.32 / 1.70 / 0.85 / 0.70 GiB/s at 1 / 2 / 3 / 4
-// dispatchers per codec -- beyond the hardware queues batches only get smaller
-// and run behind each other (profiles/r02_restore_dispatch.jsonl).
+// codec, default one per device): a batch's latency is that of its slowest
+// page (~0.09 ms for a 16 KiB LZ4 page on the jump decoder, ~0.3 ms for zlib,
+// tools/latency.c), so LZ4 restores never wait behind a zlib batch.  A second
+// dispatcher per codec (4 batches in flight with two codecs, one per hardware
+// queue, GPU_MAX_HW_QUEUES) measured 1.70 vs 1.32 GiB/s of tools/cycle.c
+// restores on one box and 1.12-1.24 vs 1.32-1.36 on another; 3-4 per codec
+// oversubscribe the queues (0.85 / 0.70), batches only get smaller and run
+// behind each other (profiles/r02_restore_dispatch.jsonl).
 namespace {
 struct RestoreReq {
     Buffer *buf;
@@ -1261,7 +1261,7 @@ int tyche_restore_queue_start(int max_batch, int max_wait_us) {
     for (bool &c : g_rq.collecting) c = false;
     g_rq.running = true;
     const char *env = getenv("TYCHE_RESTORE_DISPATCHERS");
-    int k = env ? atoi(env) : 2 * std::max(1, tyche_active_devices());
+    int k = env ? atoi(env) : std::max(1, tyche_active_devices());
     k = std::max(1, std::min(k, 64));
     for (int codec = 1; codec <= 3; codec++)
         for (int i = 0; i < k; i++) g_rq.th.emplace_back([codec] { g_rq.loop(codec); });
