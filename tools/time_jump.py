@@ -49,8 +49,9 @@ for plen in (16384, 32768):
     for n in (1, 8, 64, 512):
         comp, clen, pages = comp_all[:n].contiguous(), clen_all[:n].contiguous(), big[:n]
         mx = int(clen.max())
-        for mode, jmax in (("zlib-jump", "1024"), ("zlib-frontier", "0")):
+        for mode, jmax, wg in (("zlib-jump-wg", "1024", "1"), ("zlib-jump-wave", "1024", "0"), ("zlib-frontier", "0", "1")):
             os.environ["TYCHE_ZLIB_JUMP_MAX"] = jmax
+            os.environ["TYCHE_ZLIB_JUMP_WG"] = wg
             out, rv = codec.decompress_pages(comp, clen, plen, compressor_id=2, max_comp_len=mx)
             torch.cuda.synchronize()
             ok = bool((rv == plen).all()) and torch.equal(out, pages)

@@ -893,7 +893,8 @@ __device__ __forceinline__ void seek_bits(BitReader &r, uint32_t bitpos, uint32_
 // Returns the decoded length, kZData, or kFallback.
 __device__ __forceinline__ int32_t inflate_par(BitReader &r, const PageRef &p, const uint8_t *stage, uint32_t head, uint8_t *out,
                                int32_t cap, uint32_t W, uint32_t *M, uint32_t *LT, uint32_t *DT, uint8_t *lens,
-                               uint16_t *sortL, uint16_t *sortD, uint16_t *cells, uint32_t lane) {
+                               uint16_t *sortL, uint16_t *sortD, uint16_t *cells, uint32_t lane,
+                               uint32_t *want_out = nullptr) {
     ZPROF_DECL
     if (zlib_header(r, lane)) return kFallback;
     const uint32_t *S32 = (const uint32_t *)stage;
@@ -920,6 +921,11 @@ __device__ __forceinline__ int32_t inflate_par(BitReader &r, const PageRef &p, c
     if (tb + 4u > p.src_len) return kFallback;
     const uint8_t *tp = stage + head + tb;
     const uint32_t want = ((uint32_t)tp[0] << 24) | ((uint32_t)tp[1] << 16) | ((uint32_t)tp[2] << 8) | tp[3];
+    if (want_out) {
+        // the workgroup kernel applies the matches and checks the trailer itself
+        if (lane == 0) *want_out = want;
+        return op;
+    }
     WAVE_SYNC();
     if (cells) par_matches_jump(out, (uint32_t)op, M, cells, lane);
     else par_matches(out, (uint32_t)op, M, (uint16_t *)stage, lane);   // the stage is free now
@@ -1044,6 +1050,184 @@ __global__ __launch_bounds__(64) void zlib_inflate_par_kernel(tyche_batch_t b, u
     }
 }
 
+// ------------------------------------------------------------ small batches
+// The restore path's zlib kernel: a workgroup of kZThreads per page.  Wave 0
+// decodes the page exactly as zlib_inflate_par_kernel (inflate_par up to the
+// match records); then every wave resolves the matches by pointer jumping
+// (par_matches_jump's cells, spread over the workgroup: the one-wave version
+// spent ~250 k cycles of a 16 KiB page there); wave 0 checks the adler32
+// trailer and takes the serial decoder on any fallback; all waves store the page.
+constexpr uint32_t kZThreads = 256;
+
+// wg: 16 scratch words (round flags [0..2], wave maxima [4..7])
+__device__ void par_matches_jump_wg(uint8_t *out, uint32_t total, const uint32_t *M, uint16_t *cells, uint32_t *wg,
+                                    uint32_t tid) {
+    const uint32_t lane = tid & (kWave - 1), wave = tid / kWave;
+    const uint32_t n8 = (total + 7u) & ~7u;
+    const uint32_t span = (((n8 + 63u) / 64u + kZThreads - 1u) / kZThreads) * 64u;
+    const uint32_t x0 = min(tid * span, n8), x1 = min(x0 + span, n8);
+    uint32_t last = 0;
+    for (uint32_t w = x0 >> 5; w < (x1 + 31u) >> 5; w++) {
+        const uint32_t m = M[w];
+        if (m) last = 32u * w + 31u - (uint32_t)__builtin_clz(m);
+    }
+    const int32_t incl = wave_incl_max((int32_t)last);
+    if (lane == kWave - 1) wg[4 + wave] = (uint32_t)incl;
+    if (tid == 0) wg[0] = 0;
+    __syncthreads();
+    uint32_t carry = 0;
+    for (uint32_t w = 0; w < wave; w++) carry = max(carry, wg[4 + w]);
+    const int32_t before = __shfl_up(incl, 1);
+    if (lane) carry = max(carry, (uint32_t)before);
+    uint32_t d = 0, dist = 1, end = 0, k = 0;
+    if (carry) {
+        const uint32_t r = lds_ld32(out + carry);
+        d = carry;
+        dist = r & 0xFFFFu;
+        end = d + ((r >> 16) & 0xFFu) + 3u;
+        k = x0 < end ? mod_small(x0 - d, dist) : 0u;
+    }
+    for (uint32_t x = x0; x < x1; x += 8u) {
+        const uint32_t o0 = *(const uint32_t *)(out + x), o1 = *(const uint32_t *)(out + x + 4u);
+        const uint32_t mb = (M[x >> 5] >> (x & 31u)) & 0xFFu;
+        uint32_t c[4];
+#pragma unroll
+        for (uint32_t h = 0; h < 8; h++) {
+            const uint32_t xb = x + h;
+            if ((mb >> h) & 1u) {
+                const uint32_t r = lds_ld32(out + xb);
+                d = xb;
+                dist = r & 0xFFFFu;
+                end = xb + ((r >> 16) & 0xFFu) + 3u;
+                k = 0;
+            }
+            const uint32_t byte = ((h < 4 ? o0 : o1) >> (8u * (h & 3u))) & 0xFFu;
+            const bool in_match = xb < end;
+            const uint32_t v = in_match ? d - dist + k : (0x8000u | byte);
+            if (in_match) {
+                k++;
+                if (k == dist) k = 0;
+            }
+            if (h & 1u) c[h >> 1] |= v << 16;
+            else c[h >> 1] = v;
+        }
+        *(u32x4 *)(cells + x) = u32x4{c[0], c[1], c[2], c[3]};
+    }
+    __syncthreads();
+    u32x4 *c4 = (u32x4 *)cells;
+    const uint32_t ng = n8 / 8u;
+    for (uint32_t rd = 0;; rd++) {
+        if (tid == 0) wg[(rd + 1) % 3] = 0;   // cleared one round ahead (its readers passed a barrier since)
+        uint32_t open = 0;
+        for (uint32_t g = tid; g < ng; g += 2u * kZThreads) {
+            const uint32_t g2 = g + kZThreads;
+            const u32x4 fin = {0x80008000u, 0x80008000u, 0x80008000u, 0x80008000u};
+            u32x4 v = c4[g], u = g2 < ng ? c4[g2] : fin;
+            const bool dv = ((v.x & v.y & v.z & v.w) & 0x80008000u) != 0x80008000u;
+            const bool du = ((u.x & u.y & u.z & u.w) & 0x80008000u) != 0x80008000u;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                if (dv) {
+                    uint32_t lo = v[j] & 0xFFFFu, hi = v[j] >> 16;
+                    if (!(lo & 0x8000u)) lo = cells[lo];
+                    if (!(hi & 0x8000u)) hi = cells[hi];
+                    open |= ~(lo & hi) & 0x8000u;
+                    v[j] = lo | (hi << 16);
+                }
+                if (du) {
+                    uint32_t lo = u[j] & 0xFFFFu, hi = u[j] >> 16;
+                    if (!(lo & 0x8000u)) lo = cells[lo];
+                    if (!(hi & 0x8000u)) hi = cells[hi];
+                    open |= ~(lo & hi) & 0x8000u;
+                    u[j] = lo | (hi << 16);
+                }
+            }
+            if (dv) c4[g] = v;
+            if (du) c4[g2] = u;
+        }
+        if (open) atomicOr(&wg[rd % 3], 1u);
+        __syncthreads();
+        if (wg[rd % 3] == 0) break;
+    }
+    for (uint32_t g = tid; g < ng; g += kZThreads) {
+        const u32x4 a = c4[g];
+        uint32_t *o = (uint32_t *)(out + 8u * g);
+        o[0] = __builtin_amdgcn_perm(a.y, a.x, 0x06040200u);
+        o[1] = __builtin_amdgcn_perm(a.w, a.z, 0x06040200u);
+    }
+    __syncthreads();
+}
+
+// LDS: output window | lens/sorted | LT | DT | M | stage | cells | wg (16 words)
+__global__ __launch_bounds__(kZThreads) void zlib_inflate_jump_kernel(tyche_batch_t b, uint32_t out_cap,
+                                                                       uint32_t off_lens, uint32_t off_lt,
+                                                                       uint32_t off_m, uint32_t off_stage,
+                                                                       uint32_t stage_cap, uint32_t off_cells,
+                                                                       uint32_t off_wg, unsigned *ctr) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
+    uint8_t *out = smem;
+    uint8_t *lens = smem + off_lens;
+    uint16_t *sortL = (uint16_t *)(lens + 320);
+    uint16_t *sortD = sortL + 320;
+    uint32_t *LT = (uint32_t *)(smem + off_lt);
+    uint32_t *DT = LT + 1024;
+    uint32_t *M = (uint32_t *)(smem + off_m);
+    uint8_t *stage = smem + off_stage;
+    uint16_t *cells = (uint16_t *)(smem + off_cells);
+    uint32_t *wg = (uint32_t *)(smem + off_wg);   // [0..2] flags, [4..7] wave maxima, [8] rv, [9] want, [10] page
+    size_t page = blockIdx.x;
+    while (page < b.count) {
+        const PageRef p = batch_page(b, page);
+        const bool fits = p.dst_cap <= out_cap && p.src_len <= 0x0FFFFFFFu;
+        const uint32_t head = (uint32_t)((uintptr_t)p.src & 15u);
+        const bool staged = fits && head + p.src_len + 48u <= stage_cap;
+        if (staged) stage_in(p.src, p.src_len, stage, tid, kZThreads);
+        __syncthreads();
+        if (wave == 0) {
+            int32_t rv = fits ? kFallback : kResultTooLarge;
+            if (staged) {
+                if (lane < 8u) lds_st32(stage + ((head + p.src_len + 15u) & ~15u) + 4u * lane, 0u);
+                WAVE_SYNC();
+                BitReader r;
+                reader_init(r, p, lane);
+                r.wa = load_win(r, 0, lane);
+                r.wb = load_win(r, 256, lane);
+                rv = inflate_par(r, p, stage, head, out, (int32_t)p.dst_cap, off_lens, M, LT, DT, lens, sortL, sortD,
+                                 cells, lane, &wg[9]);
+            }
+            if (lane == 0) wg[8] = (uint32_t)rv;
+        }
+        __syncthreads();
+        int32_t rv = (int32_t)wg[8];
+        if (rv > 0) par_matches_jump_wg(out, (uint32_t)rv, M, cells, wg, tid);
+        if (wave == 0) {
+            if (rv >= 0 && lds_adler32(out, (uint32_t)rv, lane) != wg[9]) rv = kZData;
+            if (rv == kFallback) {
+                BitReader r;
+                reader_init(r, p, lane);
+                r.wa = load_win(r, 0, lane);
+                r.wb = load_win(r, 256, lane);
+                rv = inflate_page(r, p.src, out, (int32_t)p.dst_cap, lens, sortL, sortD, lane);
+            }
+            WAVE_SYNC();
+            if (lane == 0) wg[8] = (uint32_t)rv;
+        }
+        __syncthreads();
+        rv = (int32_t)wg[8];
+        if (rv > 0) stage_out(p.dst, out, (uint32_t)rv, tid, kZThreads);
+        if (tid == 0) b.results[page] = rv;
+        if (ctr) {
+            if (tid == 0) wg[10] = (uint32_t)claim_page(ctr, 0);
+            __syncthreads();
+            page = wg[10];
+        } else {
+            page += gridDim.x;
+        }
+        __syncthreads();
+    }
+}
+
 }  // namespace
 
 #ifdef TYCHE_PROFILE
@@ -1075,6 +1259,23 @@ hipError_t launch_zlib_inflate(const tyche_batch_t &b, uint32_t out_cap, hipStre
         const long jmax = jenv ? atol(jenv) : 512;
         const uint32_t off_cells = (long)b.count < jmax && out_cap <= 32768u ? off_stage + stage_cap : 0u;
         const size_t lds = (size_t)off_stage + stage_cap + (off_cells ? 2u * ((out_cap + 7u) & ~7u) : 0u);
+        // the jump path on a workgroup of kZThreads per page (TYCHE_ZLIB_JUMP_WG=0: one wave)
+        const char *wenv = getenv("TYCHE_ZLIB_JUMP_WG");
+        if (off_cells && par == 1 && (!wenv || atoi(wenv)) && lds + 64u <= 160 * 1024) {
+            const void *k = (const void *)zlib_inflate_jump_kernel;
+            const size_t ncu = prepare_launch(k);
+            int per_cu = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kZThreads, lds + 64u) != hipSuccess ||
+                per_cu < 1)
+                per_cu = 1;
+            const size_t grid = std::min<size_t>(b.count, ncu * (size_t)per_cu);
+            WorkCounter ctr(s, grid < b.count);
+            if (grid < b.count && !ctr.get()) return hipErrorOutOfMemory;
+            unsigned *cp = grid < b.count ? ctr.get() : nullptr;
+            hipLaunchKernelGGL(zlib_inflate_jump_kernel, dim3((unsigned)grid), dim3(kZThreads), lds + 64u, s, b,
+                               out_cap, off_lens, off_lt, off_m, off_stage, stage_cap, off_cells, (uint32_t)lds, cp);
+            return hipGetLastError();
+        }
         if (lds <= 160 * 1024) {
             const size_t ncu = prepare_launch((const void *)zlib_inflate_par_kernel);
             const size_t per_cu = waves_per_cu((const void *)zlib_inflate_par_kernel, lds);
