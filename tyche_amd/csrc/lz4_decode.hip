@@ -36,6 +36,10 @@
 #include <algorithm>
 #include <cstdlib>
 
+#ifndef TYCHE_BRIDGE_STEPS
+#define TYCHE_BRIDGE_STEPS 4   // token-chain bridge steps per hand-off round (A/B builds)
+#endif
+
 namespace tyche {
 
 namespace {
@@ -186,7 +190,7 @@ __device__ __forceinline__ void chain_entries(const uint8_t *in, int32_t L, uint
     // the true chain keep walking.  (A lane whose speculative walk never meets
     // a later lane's stamps can bridge for hundreds of tokens; one bridge loop
     // for all lanes waited for the longest of them.)
-    constexpr uint32_t kBridgeSteps = 4;
+    constexpr uint32_t kBridgeSteps = TYCHE_BRIDGE_STEPS;
     uint32_t y = p, o = 0;
     bool done = seg0 >= seg1 || y >= (uint32_t)L;
     uint32_t entry = kEnd, cur = 0, e = 0;

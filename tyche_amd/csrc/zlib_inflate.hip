@@ -32,6 +32,10 @@
 #include "engine.h"
 #include "lds_io.h"
 
+#ifndef TYCHE_BRIDGE_STEPS
+#define TYCHE_BRIDGE_STEPS 4   // token-chain bridge steps per hand-off round (A/B builds)
+#endif
+
 namespace tyche {
 namespace {
 
@@ -668,7 +672,7 @@ __device__ __forceinline__ int32_t par_block(const ParTabs &t, const uint32_t *S
     // hand-off walk as far as the finished bridges reach; lanes behind it stop
     // (a lane off the true chain may bridge for a long way before it meets a
     // later lane's walk, and one loop for all lanes waited for the longest).
-    constexpr uint32_t kBridgeSteps = 4;
+    constexpr uint32_t kBridgeSteps = TYCHE_BRIDGE_STEPS;
     uint32_t o = 0;   // owner lane + 1 of the hand-off position, 0 = chain ends here
     bool done = !(a < E && stop == 0) || y >= E;
     uint32_t entry = 0xFFFFFFFFu;
