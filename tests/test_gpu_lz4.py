@@ -391,3 +391,21 @@ def test_decode_jump_path_page_kinds(tc, oracle_mod, plen, n):
     for i in range(min(n, 12)):
         r, dec = oracle_mod.lz4_decompress(ch[i, :lh[i]].tobytes(), plen)
         assert r == plen and dec == host[i].tobytes(), i
+
+
+def test_c2_full_size_round_trip(tc):
+    """BASELINE configs[1] at its full size on one GPU: 1,048,576 x 16 KiB synthetic pages
+    (16 GiB) LZ4-compressed and decompressed through the lane decoder, every page bit-exact,
+    every result the page length, and the ratio of the bench pages (the bench checks the same
+    round trip; this keeps it in the parity suite)."""
+    n, plen = 1 << 20, 16384
+    pages = tc.pagegen(n, plen, dist=0, device=DEV)
+    comp, clen = tc.compress_pages(pages)
+    out, rv = tc.decompress_pages(comp, clen, plen)
+    torch.cuda.synchronize()
+    assert bool((rv == plen).all())
+    assert torch.equal(out, pages)
+    ratio = n * plen / float(clen.to(torch.int64).sum())
+    assert 2.55 < ratio < 2.7, ratio
+    del pages, comp, out
+    torch.cuda.empty_cache()

@@ -542,3 +542,20 @@ def test_zstd_encode_fused_kernel_and_chunked_split(tc, oracle_mod, monkeypatch,
             test_encode_roundtrip_reference_decoder(tc, oracle_mod, dist, plen)
     test_encode_multiblock_and_incompressible(tc, oracle_mod)
     test_encode_tight_capacity(tc, oracle_mod, 16)
+
+
+def test_c3_full_size_round_trip(tc):
+    """BASELINE configs[2] at its full size on one GPU: 1,048,576 x 32 KiB synthetic pages
+    (32 GiB) through the device zstd encoder and decoder (the split kernels), every page
+    bit-exact, and the level-1 ratio of the bench pages."""
+    n, plen = 1 << 20, 32768
+    pages = tc.pagegen(n, plen, dist=0, device=DEV)
+    comp, clen = tc.compress_pages(pages, compressor_id=ZSTD)
+    out, rv = tc.decompress_pages(comp, clen, plen, compressor_id=ZSTD, max_comp_len=int(clen.max()))
+    torch.cuda.synchronize()
+    assert bool((rv == plen).all())
+    assert torch.equal(out, pages)
+    ratio = n * plen / float(clen.to(torch.int64).sum())
+    assert ratio > 4.8, ratio
+    del pages, comp, out
+    torch.cuda.empty_cache()
