@@ -653,11 +653,17 @@ __global__ __launch_bounds__(64) void lz4_decode_wave_kernel(tyche_batch_t b, ui
 // independent of fill order, so all runs are written in parallel.
 //
 // Wave 0 parses the token chain (chain_entries, as parse_chain) and walks its
-// lane's part of it twice: output lengths (prefix sum across lanes), then the
-// reference's acceptance checks in order (lz4.c:1147-1168, 1176, 1225) and the
-// cell fills; runs longer than kJumpLong go to a list that the whole workgroup
-// fills.  The first failing sequence in stream order gives the exact
-// -(consumed)-1 return.  Then all waves jump, pack cells to bytes and store.
+// lane's part of it once, recording every sequence as an item (token position,
+// output offset within the lane's part; jump_walk).  Then every thread takes
+// sequences of its own: decodes it again, runs the reference's acceptance
+// checks (lz4.c:1147-1168, 1176, 1225) at its absolute position and
+// atomicMin's the number of a failing one; the first failing sequence in
+// stream order gives the exact -(consumed)-1 return, and the sequences before
+// it write their literals and match start markers (a marker run is filled by
+// jump_scan; runs longer than kJumpLong go to a list the whole workgroup
+// fills).  Then all waves jump, pack cells to bytes and store.  Pages whose
+// lane parts overflow the items take jump_front: the same checks and fills as
+// a second per-lane walk.
 constexpr uint32_t kJumpThreads = 512;
 constexpr int32_t kJumpLong = 16;
 
@@ -691,8 +697,9 @@ __device__ __forceinline__ void fill_item(uint16_t *cells, const uint8_t *in, ui
     else fill_match(cells, dst, (int32_t)it.y, n, i0, step);
 }
 
-// Wave 0: parse, checks and fills of one page (in: L bytes + kPad zeros, cells:
-// >= max(C, (L + 4) / 2) cells).  Returns LZ4_decompress_safe's value.
+// Wave 0 alone: parse, checks and fills of one page (in: L bytes + kPad zeros,
+// cells: >= max(C, (L + 4) / 2) cells) -- jump_walk's fallback for pages whose
+// lane parts do not fit its items.  Returns LZ4_decompress_safe's value.
 __device__ int32_t jump_front(const uint8_t *in, int32_t L, uint16_t *cells, int32_t C, uint32_t lane, uint2 *list,
                               uint32_t list_cap, uint32_t *nlist, uint2 *lits, uint32_t lits_cap, uint32_t *nseq) {
     if (C == 0) return (L == 1 && in[0] == 0) ? 0 : -1;
