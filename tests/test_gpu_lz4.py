@@ -264,9 +264,9 @@ def test_decode_size_classes(tc):
     assert bool((rv == plen).all()) and torch.equal(out, pages)
 
 
-@pytest.mark.parametrize("target", [1, 8192, 65536])
+@pytest.mark.parametrize("target", [1, 20000, 65536])
 def test_decode_lane_path_fixtures(tc, target):
-    """The decoder is picked by batch size: below 4,096 pages the jump decoder (workgroup per
+    """The decoder is picked by batch size: below 16,384 pages the jump decoder (workgroup per
     page, pointer-jumping match resolution), below 32,768 the wave decoder, from there the
     lane-per-page decoder (lz4_decode_lane.hip).  The reference-generated, sample and malformed
     fixtures, repeated to each size, give the reference's return values and bytes on all three."""
@@ -304,10 +304,10 @@ def test_decode_lane_path_roundtrip(tc, dist):
     assert bool((rv == plen).all()) and torch.equal(out, pages)
 
 
-@pytest.mark.parametrize("n", [600, 8192, 65536])
+@pytest.mark.parametrize("n", [600, 20000, 65536])
 def test_decode_lane_path_corruptions(tc, oracle_mod, n):
     """Seeded corruptions (byte flips, truncations) through the jump (600 pages), wave
-    (8,192) and lane-per-page (64K) decoders: every return value is the restated
+    (20,000) and lane-per-page (64K) decoders: every return value is the restated
     LZ4_decompress_safe's (lz4.c:1251), and the untouched pages decode bit-exactly."""
     plen = 4096
     pages = tc.pagegen(n, plen, seed=99, dist=0, device=DEV)

@@ -832,7 +832,7 @@ __device__ __forceinline__ void put_literals(uint16_t *cells, const uint8_t *in,
 // lane l's i-th sequence | its output offset within the lane's part << 16, and
 // per lane the sequence count, the output base and the first sequence number.
 struct JumpLanes {
-    uint32_t cnt[kWave], base_o[kWave], base_k[kWave];
+    uint32_t cnt[kWave], base_o[kWave], base_k[kWave];   // column items, output base, first sequence number
 };
 constexpr int32_t kJumpPending = INT32_MIN + 2;   // rv decided by the workgroup's checks
 constexpr uint32_t kJumpOvf = 512;                // overflow items (sequences past a lane's rows)
@@ -847,51 +847,115 @@ __device__ int32_t jump_walk(const uint8_t *in, int32_t L, uint16_t *cells, int3
                              uint32_t list_cap, uint32_t *nlist) {
     if (C == 0) return (L == 1 && in[0] == 0) ? 0 : -1;
     if (L <= 0) return -1;
-    uint32_t entry, y;
-    chain_entries(in, L, (uint8_t *)cells, lane, entry, y);
+    // chain_entries' speculative walks and bridges, recording every token a lane
+    // visits as an item (position | output bytes before it in the lane's walk,
+    // mod 2^16): the true chain enters a lane's walk at a position that lane
+    // stamped, so its part of the chain is a suffix of its items -- no second walk
+    uint8_t *owner = (uint8_t *)cells;
+    const uint32_t S = ((uint32_t)L + kWave - 1) / kWave;
+    const uint32_t seg0 = lane * S;
+    const uint32_t seg1 = min(seg0 + S, (uint32_t)L);
+    for (uint32_t w = lane; w < ((uint32_t)L + 3) / 4; w += kWave) ((uint32_t *)owner)[w] = 0;
+    WAVE_SYNC();
+    uint32_t cum = 0, cnt = 0, q_over = 0, c_over = 0;
+    auto record = [&](uint32_t q, const SeqIn &sq) {
+        if (cnt < rows) items[cnt * kWave + lane] = q | (cum << 16);
+        if (cnt == rows) {
+            q_over = q;
+            c_over = cum;
+        }
+        cnt++;
+        cum += (uint32_t)(sq.in_term ? sq.lit : sq.lit + sq.ml);
+    };
+    uint32_t p = seg0;
+    while (p < seg1) {
+        owner[p] = (uint8_t)(lane + 1);
+        const SeqIn sq = decode_seq_in(in, L, (int32_t)p);
+        record(p, sq);
+        p = sq.in_term || sq.ml_err ? kEnd : (uint32_t)sq.q2;
+    }
+    WAVE_SYNC();
     PROF_DECL
+    constexpr uint32_t kBridgeSteps = TYCHE_BRIDGE_STEPS;
+    uint32_t y = p, o = 0;
+    bool done = seg0 >= seg1 || y >= (uint32_t)L;
+    uint32_t entry = kEnd, cur = 0, e = 0;
+    for (bool fin = false; !fin;) {
+        for (uint32_t it = 0; it < kBridgeSteps; it++) {
+            if (!done) {
+                const uint32_t ow = owner[y];
+                if (ow > lane + 1) {
+                    o = ow;
+                    done = true;
+                } else {
+                    const SeqIn sq = decode_seq_in(in, L, (int32_t)y);
+                    record(y, sq);
+                    y = sq.in_term || sq.ml_err ? kEnd : (uint32_t)sq.q2;
+                    done = y >= (uint32_t)L;
+                }
+            }
+        }
+        for (;;) {
+            if (lane == cur) entry = e;
+            if (!rdlane((uint32_t)done, cur)) break;
+            e = rdlane(y, cur);
+            const uint32_t nx = rdlane(o, cur);
+            if (nx == 0) { fin = true; break; }
+            cur = nx - 1;
+        }
+        if (lane < cur) done = true;
+    }
+    WAVE_SYNC();
+    PROF_MARK(3);
     {
         const uint32_t nv = (((uint32_t)C + 63u) & ~63u) / 8u;
         u32x4 *c4 = (u32x4 *)cells;
         const u32x4 z = {0u, 0u, 0u, 0u};
         for (uint32_t v = lane; v < nv; v += kWave) c4[v] = z;
     }
-    uint32_t olen = 0, cnt = 0, q_over = 0, o_over = 0;
-    bool over = false;
-    for (uint32_t q = entry; q < (uint32_t)L && q != y;) {
-        const SeqIn s = decode_seq_in(in, L, (int32_t)q);
-        over |= olen >= 0x10000u;
-        if (cnt < rows) items[cnt * kWave + lane] = q | (olen << 16);
-        if (cnt == rows) { q_over = q; o_over = olen; }
-        cnt++;
-        if (s.in_term) { olen += (uint32_t)s.lit; break; }
-        if (s.ml_err) break;
-        olen += (uint32_t)(s.lit + s.ml);
-        q = (uint32_t)s.q2;
+    // this lane's part: items [first, cnt), found by binary search (positions grow)
+    const bool on = entry != kEnd;
+    const uint32_t nrec = min(cnt, rows);
+    uint32_t first = 0;
+    bool bad = false;
+    if (on) {
+        uint32_t lo = 0, hi = nrec;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if ((items[mid * kWave + lane] & 0xFFFFu) < entry) lo = mid + 1;
+            else hi = mid;
+        }
+        first = lo;
+        bad = first >= nrec || (items[first * kWave + lane] & 0xFFFFu) != entry || cum >= 0x10000u;
     }
-    WAVE_SYNC();
-    PROF_MARK(4);
-    // a lane's part can span several segments (the walks after it had not met
-    // the true chain): its sequences past `rows` go to the overflow items
-    const uint32_t extra = cnt > rows ? cnt - rows : 0u;
+    uint32_t cum_entry = 0;
+    if (on && !bad) cum_entry = items[first * kWave + lane] >> 16;
+    const uint32_t extra = on && cnt > rows ? cnt - rows : 0u;
     const uint32_t xi = (uint32_t)wave_incl_sum((int32_t)extra);
     const uint32_t nx = rdlane(xi, kWave - 1);
-    if (__ballot(over) || nx > ovf_cap)
+    if (__ballot(bad) || nx > ovf_cap)
         return jump_front(in, L, cells, C, lane, list, list_cap, nlist, nullptr, 0u, nullptr);
+    const uint32_t ncol = on ? nrec - first : 0u;
+    for (uint32_t k = 0; k < ncol; k++) {
+        const uint32_t it = items[(first + k) * kWave + lane];
+        items[k * kWave + lane] = (it & 0xFFFFu) | (((it >> 16) - cum_entry) << 16);
+    }
     if (lane == 0) *novf = nx;
     if (extra) {
-        uint32_t at = xi - extra, q = q_over, o = o_over;
-        for (uint32_t i = rows; i < cnt; i++) {
-            const SeqIn s = decode_seq_in(in, L, (int32_t)q);
-            ovf[at++] = make_uint2(q | (o << 16), lane | (i << 8));
-            o += (uint32_t)(s.in_term ? s.lit : s.lit + s.ml);
-            q = (uint32_t)s.q2;
+        uint32_t at = xi - extra, q = q_over, oc = c_over;
+        for (uint32_t i = rows - first; i < cnt - first; i++) {
+            const SeqIn sq = decode_seq_in(in, L, (int32_t)q);
+            ovf[at++] = make_uint2(q | ((oc - cum_entry) << 16), lane | (i << 8));
+            oc += (uint32_t)(sq.in_term ? sq.lit : sq.lit + sq.ml);
+            q = (uint32_t)sq.q2;
         }
     }
-    const int32_t oi = wave_incl_sum((int32_t)olen), ci = wave_incl_sum((int32_t)cnt);
-    lanes->cnt[lane] = cnt;
+    const uint32_t part = on ? cnt - first : 0u, olen = on ? cum - cum_entry : 0u;
+    const int32_t oi = wave_incl_sum((int32_t)olen), ci = wave_incl_sum((int32_t)part);
+    lanes->cnt[lane] = ncol;
     lanes->base_o[lane] = (uint32_t)oi - olen;
-    lanes->base_k[lane] = (uint32_t)ci - cnt;
+    lanes->base_k[lane] = (uint32_t)ci - part;
+    PROF_MARK(4);
     return kJumpPending;
 }
 
@@ -901,7 +965,7 @@ __device__ __forceinline__ bool jump_item(const uint32_t *items, const uint2 *ov
     if (j < rows * kWave) {
         l = j & (kWave - 1);
         i = j / kWave;
-        if (i >= min(lanes->cnt[l], rows)) return false;
+        if (i >= lanes->cnt[l]) return false;   // cnt: the lane's column items
         it = items[j];
         return true;
     }
@@ -1171,7 +1235,7 @@ __global__ __launch_bounds__(kJumpThreads) void lz4_decode_jump_kernel(tyche_bat
 
 // Batches below this many pages (TYCHE_LZ4_JUMP_MAX) take the jump decoder when
 // the page fits its layout (16-bit cells: pages <= 32 KiB).
-constexpr long kJumpMax = 1024;
+constexpr long kJumpMax = 16384;
 static hipError_t launch_lz4_decode_jump(const tyche_batch_t &b, uint32_t in_cap, uint32_t out_cap, hipStream_t s,
                                          bool &launched) {
     launched = false;
