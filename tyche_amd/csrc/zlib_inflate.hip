@@ -1257,10 +1257,10 @@ hipError_t launch_zlib_inflate(const tyche_batch_t &b, uint32_t out_cap, hipStre
         const uint32_t off_stage = off_m + ((((out_cap + 31u) / 32u) * 4u + 15u) & ~15u);
         const uint32_t stage_cap = (std::max(2048u, out_cap / 2u) + 63u) & ~15u;
         // small batches (restores) resolve matches by pointer jumping: 2 bytes of LDS per
-        // output byte more (below TYCHE_ZLIB_JUMP_MAX pages, default 512: at 512 x 32 KiB the smaller residency
-        // already costs more than the frontier copies; 0 = never)
+        // output byte more (below TYCHE_ZLIB_JUMP_MAX pages, default 1,024: on the workgroup
+        // kernel 512-page batches still gain, 459 vs 698 us at 16 KiB; 0 = never)
         const char *jenv = getenv("TYCHE_ZLIB_JUMP_MAX");
-        const long jmax = jenv ? atol(jenv) : 512;
+        const long jmax = jenv ? atol(jenv) : 1024;
         const uint32_t off_cells = (long)b.count < jmax && out_cap <= 32768u ? off_stage + stage_cap : 0u;
         const size_t lds = (size_t)off_stage + stage_cap + (off_cells ? 2u * ((out_cap + 7u) & ~7u) : 0u);
         // the jump path on a workgroup of kZThreads per page (TYCHE_ZLIB_JUMP_WG=0: one wave)
