@@ -73,8 +73,8 @@ def main():
         print(r.stdout.strip() or r.stderr.strip()[-1500:], flush=True)
     if os.environ.get("LZ4", "1") == "0":
         return
-    for mode, jmax in (("jump", "32767"), ("wave", "0")):
-        env = dict(os.environ, MODE=mode, TYCHE_LZ4_JUMP_MAX=jmax)
+    for mode, jmax, wide in (("jump", "32767", "1"), ("jump512", "32767", "0"), ("wave", "0", "1")):
+        env = dict(os.environ, MODE=mode, TYCHE_LZ4_JUMP_MAX=jmax, TYCHE_LZ4_JUMP_WIDE=wide)
         r = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=600)
         print(r.stdout.strip() or r.stderr.strip()[-1500:], flush=True)
 

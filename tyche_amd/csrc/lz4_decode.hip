@@ -664,7 +664,8 @@ __global__ __launch_bounds__(64) void lz4_decode_wave_kernel(tyche_batch_t b, ui
 // fills).  Then all waves jump, pack cells to bytes and store.  Pages whose
 // lane parts overflow the items take jump_front: the same checks and fills as
 // a second per-lane walk.
-constexpr uint32_t kJumpThreads = 512;
+// 512 threads per page, 1,024 when the batch has no more pages than the device has CUs
+// (one page per CU: the parallel phases take half the time; 512 fits two pages per CU)
 constexpr int32_t kJumpLong = 16;
 
 constexpr uint32_t kLitFlag = 0x8000u;
@@ -998,10 +999,11 @@ __device__ __forceinline__ int32_t seq_check(const SeqIn &s, int32_t o, int32_t 
 // max-scan of the keys (positions grow, so the max is the nearest marker to the
 // left), (C) each chunk rewrites its cells with the carried-in run: byte d + j of
 // a run with offset off points at d - off + (j mod off).
+template <uint32_t kT>
 __device__ __forceinline__ void jump_scan(uint16_t *cells, uint32_t n64, uint32_t *keys, uint32_t tid) {
     u32x4 *c4 = (u32x4 *)cells;
     const uint32_t nch = n64 / 64u;
-    for (uint32_t c = tid; c < nch; c += kJumpThreads) {
+    for (uint32_t c = tid; c < nch; c += kT) {
         uint32_t key = 0;
 #pragma unroll
         for (uint32_t j = 0; j < 8; j++) {
@@ -1026,7 +1028,7 @@ __device__ __forceinline__ void jump_scan(uint16_t *cells, uint32_t n64, uint32_
         }
     }
     __syncthreads();
-    for (uint32_t c = tid; c < nch; c += kJumpThreads) {
+    for (uint32_t c = tid; c < nch; c += kT) {
         const uint32_t key = c ? keys[c - 1] : 0u;
         uint32_t d = key >> 16, off = key & 0xFFFFu;
         uint32_t k = off ? mod_small(64u * c - d, off) : 0u;
@@ -1064,6 +1066,7 @@ __device__ __forceinline__ uint32_t jump_pair(const uint16_t *cells, uint32_t w,
     return lo | (hi << 16);
 }
 
+template <uint32_t kJumpThreads>
 __global__ __launch_bounds__(kJumpThreads) void lz4_decode_jump_kernel(tyche_batch_t b, uint32_t in_cap,
                                                                        uint32_t out_cap, uint32_t cells_bytes,
                                                                        uint32_t list_cap, uint32_t rows,
@@ -1159,7 +1162,7 @@ __global__ __launch_bounds__(kJumpThreads) void lz4_decode_jump_kernel(tyche_bat
             __syncthreads();
             PROF_ADD(10, nl);
             PROF_MARK(6);
-            jump_scan(cells, n64, shared_words + 8, tid);
+            jump_scan<kJumpThreads>(cells, n64, shared_words + 8, tid);
             __syncthreads();
             PROF_MARK(7);
             // pointer jumping, 8 cells per group
@@ -1250,17 +1253,22 @@ static hipError_t launch_lz4_decode_jump(const tyche_batch_t &b, uint32_t in_cap
     const size_t lds = kJumpHdr + (size_t)cells_bytes + 8u * list_cap + 4u * 64u * rows + 8u * kJumpOvf +
                        ((in_cap + 16u + kPad + 15u) & ~15u);
     if (lds > 150 * 1024) return hipSuccess;
-    const void *k = (const void *)lz4_decode_jump_kernel;
-    const size_t ncu = prepare_launch(k);
+    static const int wide_env = getenv("TYCHE_LZ4_JUMP_WIDE") ? atoi(getenv("TYCHE_LZ4_JUMP_WIDE")) : 1;
+    const void *k512 = (const void *)lz4_decode_jump_kernel<512>, *k1024 = (const void *)lz4_decode_jump_kernel<1024>;
+    const size_t ncu = prepare_launch(k512);
+    const bool wide = wide_env && b.count <= ncu;
+    const void *k = wide ? k1024 : k512;
+    const uint32_t threads = wide ? 1024u : 512u;
+    if (wide) (void)prepare_launch(k1024);
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kJumpThreads, lds) != hipSuccess || per_cu < 1)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, (int)threads, lds) != hipSuccess || per_cu < 1)
         per_cu = 1;
     const size_t grid = std::min<size_t>(b.count, ncu * (size_t)per_cu);
     WorkCounter ctr(s, grid < b.count);
     if (grid < b.count && !ctr.get()) return hipErrorOutOfMemory;
     unsigned *cp = grid < b.count ? ctr.get() : nullptr;
-    hipLaunchKernelGGL(lz4_decode_jump_kernel, dim3((unsigned)grid), dim3(kJumpThreads), lds, s, b, in_cap, out_cap,
-                       cells_bytes, list_cap, rows, cp);
+    void *args[] = {(void *)&b, &in_cap, &out_cap, (void *)&cells_bytes, (void *)&list_cap, (void *)&rows, &cp};
+    (void)hipLaunchKernel(k, dim3((unsigned)grid), dim3(threads), args, lds, s);
     launched = true;
     return hipGetLastError();
 }
