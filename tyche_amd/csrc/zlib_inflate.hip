@@ -1061,9 +1061,11 @@ __global__ __launch_bounds__(64) void zlib_inflate_par_kernel(tyche_batch_t b, u
 // (par_matches_jump's cells, spread over the workgroup: the one-wave version
 // spent ~250 k cycles of a 16 KiB page there); wave 0 checks the adler32
 // trailer and takes the serial decoder on any fallback; all waves store the page.
-constexpr uint32_t kZThreads = 256;
+// 256 threads per page, 512 when the batch has no more pages than the device has
+// CUs (at 211 VGPRs a CU holds 8 waves: two 256-thread pages or one 512-thread one)
 
-// wg: 16 scratch words (round flags [0..2], wave maxima [4..7])
+// wg: 32 scratch words (round flags [0..2], wave maxima [16..16 + waves))
+template <uint32_t kZThreads>
 __device__ void par_matches_jump_wg(uint8_t *out, uint32_t total, const uint32_t *M, uint16_t *cells, uint32_t *wg,
                                     uint32_t tid) {
     const uint32_t lane = tid & (kWave - 1), wave = tid / kWave;
@@ -1076,11 +1078,11 @@ __device__ void par_matches_jump_wg(uint8_t *out, uint32_t total, const uint32_t
         if (m) last = 32u * w + 31u - (uint32_t)__builtin_clz(m);
     }
     const int32_t incl = wave_incl_max((int32_t)last);
-    if (lane == kWave - 1) wg[4 + wave] = (uint32_t)incl;
+    if (lane == kWave - 1) wg[16 + wave] = (uint32_t)incl;
     if (tid == 0) wg[0] = 0;
     __syncthreads();
     uint32_t carry = 0;
-    for (uint32_t w = 0; w < wave; w++) carry = max(carry, wg[4 + w]);
+    for (uint32_t w = 0; w < wave; w++) carry = max(carry, wg[16 + w]);
     const int32_t before = __shfl_up(incl, 1);
     if (lane) carry = max(carry, (uint32_t)before);
     uint32_t d = 0, dist = 1, end = 0, k = 0;
@@ -1162,7 +1164,8 @@ __device__ void par_matches_jump_wg(uint8_t *out, uint32_t total, const uint32_t
     __syncthreads();
 }
 
-// LDS: output window | lens/sorted | LT | DT | M | stage | cells | wg (16 words)
+// LDS: output window | lens/sorted | LT | DT | M | stage | cells | wg (32 words)
+template <uint32_t kZThreads>
 __global__ __launch_bounds__(kZThreads) void zlib_inflate_jump_kernel(tyche_batch_t b, uint32_t out_cap,
                                                                        uint32_t off_lens, uint32_t off_lt,
                                                                        uint32_t off_m, uint32_t off_stage,
@@ -1179,7 +1182,7 @@ __global__ __launch_bounds__(kZThreads) void zlib_inflate_jump_kernel(tyche_batc
     uint32_t *M = (uint32_t *)(smem + off_m);
     uint8_t *stage = smem + off_stage;
     uint16_t *cells = (uint16_t *)(smem + off_cells);
-    uint32_t *wg = (uint32_t *)(smem + off_wg);   // [0..2] flags, [4..7] wave maxima, [8] rv, [9] want, [10] page
+    uint32_t *wg = (uint32_t *)(smem + off_wg);   // [0..2] flags, [8] rv, [9] want, [10] page, [16..] wave maxima
     size_t page = blockIdx.x;
     while (page < b.count) {
         const PageRef p = batch_page(b, page);
@@ -1204,7 +1207,7 @@ __global__ __launch_bounds__(kZThreads) void zlib_inflate_jump_kernel(tyche_batc
         }
         __syncthreads();
         int32_t rv = (int32_t)wg[8];
-        if (rv > 0) par_matches_jump_wg(out, (uint32_t)rv, M, cells, wg, tid);
+        if (rv > 0) par_matches_jump_wg<kZThreads>(out, (uint32_t)rv, M, cells, wg, tid);
         if (wave == 0) {
             if (rv >= 0 && lds_adler32(out, (uint32_t)rv, lane) != wg[9]) rv = kZData;
             if (rv == kFallback) {
@@ -1265,19 +1268,26 @@ hipError_t launch_zlib_inflate(const tyche_batch_t &b, uint32_t out_cap, hipStre
         const size_t lds = (size_t)off_stage + stage_cap + (off_cells ? 2u * ((out_cap + 7u) & ~7u) : 0u);
         // the jump path on a workgroup of kZThreads per page (TYCHE_ZLIB_JUMP_WG=0: one wave)
         const char *wenv = getenv("TYCHE_ZLIB_JUMP_WG");
-        if (off_cells && par == 1 && (!wenv || atoi(wenv)) && lds + 64u <= 160 * 1024) {
-            const void *k = (const void *)zlib_inflate_jump_kernel;
-            const size_t ncu = prepare_launch(k);
+        if (off_cells && par == 1 && (!wenv || atoi(wenv)) && lds + 128u <= 160 * 1024) {
+            const void *k256 = (const void *)zlib_inflate_jump_kernel<256>;
+            const void *k512 = (const void *)zlib_inflate_jump_kernel<512>;
+            const size_t ncu = prepare_launch(k256);
+            const bool wide = b.count <= ncu;
+            const void *k = wide ? k512 : k256;
+            const uint32_t threads = wide ? 512u : 256u;
+            if (wide) (void)prepare_launch(k512);
             int per_cu = 0;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kZThreads, lds + 64u) != hipSuccess ||
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, (int)threads, lds + 128u) != hipSuccess ||
                 per_cu < 1)
                 per_cu = 1;
             const size_t grid = std::min<size_t>(b.count, ncu * (size_t)per_cu);
             WorkCounter ctr(s, grid < b.count);
             if (grid < b.count && !ctr.get()) return hipErrorOutOfMemory;
             unsigned *cp = grid < b.count ? ctr.get() : nullptr;
-            hipLaunchKernelGGL(zlib_inflate_jump_kernel, dim3((unsigned)grid), dim3(kZThreads), lds + 64u, s, b,
-                               out_cap, off_lens, off_lt, off_m, off_stage, stage_cap, off_cells, (uint32_t)lds, cp);
+            const uint32_t off_wg = (uint32_t)lds;
+            void *args[] = {(void *)&b, &out_cap, (void *)&off_lens, (void *)&off_lt, (void *)&off_m, (void *)&off_stage,
+                            (void *)&stage_cap, (void *)&off_cells, (void *)&off_wg, &cp};
+            (void)hipLaunchKernel(k, dim3((unsigned)grid), dim3(threads), args, lds + 128u, s);
             return hipGetLastError();
         }
         if (lds <= 160 * 1024) {
