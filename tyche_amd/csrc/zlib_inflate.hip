@@ -640,8 +640,14 @@ __device__ __forceinline__ void par_tables(ParTabs &t, const Table &L, const Tab
 // new output length and the bit position after end-of-block (yend), or
 // kFallback.  V: bitmap scratch inside the output window (out + vo, above op);
 // M: match-start bitmap.
+// items (optional, the jump path's cells region, rows per lane): every symbol a
+// lane visits is recorded (bit position - base | output bytes before it << 17),
+// so an on-chain lane's output count is its total minus the count at its entry
+// (a binary search) instead of a second decode pass; lanes whose walks leave
+// the items or 15 bits of output take the counting pass.
 __device__ __forceinline__ int32_t par_block(const ParTabs &t, const uint32_t *S32, uint32_t P0, uint32_t E, uint8_t *out, int32_t op,
-                             int32_t cap, uint32_t W, uint32_t *M, uint32_t lane, uint32_t &yend) {
+                             int32_t cap, uint32_t W, uint32_t *M, uint32_t lane, uint32_t &yend,
+                             uint32_t *items = nullptr, uint32_t rows = 0) {
     if (P0 >= E) return kFallback;
     ZPROF_DECL
     const uint32_t base = P0 & ~31u;
@@ -655,10 +661,17 @@ __device__ __forceinline__ int32_t par_block(const ParTabs &t, const uint32_t *S
     // 1. walk the own segment
     const uint32_t a = base + lane * S, b = min(a + S, E);
     uint32_t y = lane == 0 ? P0 : a, stop = 0, val, dist;
+    uint32_t ni = 0, cum = 0;   // items recorded, output bytes so far (items)
+    const bool rec = items && E - base < (1u << 17);
     if (a < E) {
         while (y < b) {
             atomicOr(&V[(y - base) >> 5], 1u << (y & 31u));
+            if (rec) {
+                if (ni < rows) items[ni * kWave + lane] = (y - base) | (min(cum, 0x7FFFu) << 17);
+                ni++;
+            }
             const uint32_t k = par_sym(t, S32, y, val, dist);
+            cum += k == kSymLit ? 1u : k == kSymMatch ? val : 0u;
             if (k >= kSymEob) {
                 stop = k;
                 break;
@@ -684,7 +697,12 @@ __device__ __forceinline__ int32_t par_block(const ParTabs &t, const uint32_t *S
                     o = (y - base) / S + 1u;
                     done = true;
                 } else {
+                    if (rec) {
+                        if (ni < rows) items[ni * kWave + lane] = (y - base) | (min(cum, 0x7FFFu) << 17);
+                        ni++;
+                    }
                     const uint32_t k = par_sym(t, S32, y, val, dist);
+                    cum += k == kSymLit ? 1u : k == kSymMatch ? val : 0u;
                     if (k >= kSymEob) stop = k;
                     done = k >= kSymEob || y >= E;
                 }
@@ -707,7 +725,22 @@ __device__ __forceinline__ int32_t par_block(const ParTabs &t, const uint32_t *S
     // 4. count, place, write
     const bool on = entry != 0xFFFFFFFFu;
     uint32_t nout = 0;
-    if (on) {
+    bool counted = false;
+    if (on && rec && ni <= rows && cum < 0x8000u) {
+        // the entry is a symbol start this lane's walk visited: its item
+        uint32_t lo = 0, hi = ni;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if ((items[mid * kWave + lane] & 0x1FFFFu) < entry - base) lo = mid + 1;
+            else hi = mid;
+        }
+        if (lo < ni && (items[lo * kWave + lane] & 0x1FFFFu) == entry - base) {
+            // the lane's part ends at its hand-off (or at end-of-block, which adds no output)
+            nout = cum - (items[lo * kWave + lane] >> 17);
+            counted = true;
+        }
+    }
+    if (on && !counted) {
         for (uint32_t q = entry; q < y;) {
             const uint32_t k = par_sym(t, S32, q, val, dist);
             if (k == kSymLit) nout++;
@@ -915,7 +948,8 @@ __device__ __forceinline__ int32_t inflate_par(BitReader &r, const PageRef &p, c
         WAVE_SYNC();
         ZPROF_MARK(1);
         const uint32_t P0 = h8 + (uint32_t)p.src_len * 8u - (uint32_t)r.avail;
-        op = par_block(t, S32, P0, E, out, op, cap, W, M, lane, yend);
+        op = par_block(t, S32, P0, E, out, op, cap, W, M, lane, yend, (uint32_t *)cells,
+                       cells ? (uint32_t)(((cap + 7) & ~7) * 2 / (4 * kWave)) : 0u);
         if (op < 0) return kFallback;
         WAVE_SYNC();
         if (!last) seek_bits(r, yend - h8, p.src_len, lane);
