@@ -191,9 +191,56 @@ def e2e_host(pages_dev: torch.Tensor, n: int) -> dict:
         best_c, best_d = min(best_c, t1 - t0), min(best_d, t2 - t1)
     assert (rv == plen).all() and np.array_equal(out, host), "host-path round trip failed"
     nbytes = n * plen
-    return {"pages": n, "compress_gib_s": round(nbytes / best_c / GIB, 3),
-            "decompress_gib_s": round(nbytes / best_d / GIB, 3),
-            "combined_gib_s": round(nbytes / (best_c + best_d) / GIB, 3)}
+    res = {"pages": n, "compress_gib_s": round(nbytes / best_c / GIB, 3),
+           "decompress_gib_s": round(nbytes / best_d / GIB, 3),
+           "combined_gib_s": round(nbytes / (best_c + best_d) / GIB, 3)}
+    link = pcie_probe(pages_dev.device, nbytes)
+    res["link_probe"] = link
+    # the ceiling each direction could reach if only the link moved bytes: compress sends the pages
+    # and brings back ~1/ratio of them, decompress the reverse (both directions run at once)
+    ratio = nbytes / float(sum(int(x) for x in clen))
+    h2d, d2h = link["h2d_gib_s"], link["d2h_gib_s"]
+    res["link_bound_compress_gib_s"] = round(min(h2d, d2h * ratio), 3)
+    res["link_bound_decompress_gib_s"] = round(min(d2h, h2d * ratio), 3)
+    res["frac_of_link_bound"] = {"compress": round(res["compress_gib_s"] / res["link_bound_compress_gib_s"], 3),
+                                 "decompress": round(res["decompress_gib_s"] / res["link_bound_decompress_gib_s"], 3)}
+    return res
+
+
+def pcie_probe(dev, nbytes: int, reps: int = 5) -> dict:
+    """Raw pinned-host <-> HBM copy rates (hipMemcpyAsync through torch, 64 MiB copies back to back on one
+    stream per direction, best of `reps`): the PCIe ceiling for the host path."""
+    chunk = 64 << 20
+    k = max(1, nbytes // chunk)
+    h = [torch.empty(chunk, dtype=torch.uint8).pin_memory() for _ in range(2)]
+    d = [torch.empty(chunk, dtype=torch.uint8, device=dev) for _ in range(2)]
+    s_up, s_dn = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+
+    def timed(fn):
+        best = float("inf")
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            fn()
+            torch.cuda.synchronize()
+            best = min(best, time.perf_counter() - t0)
+        return k * chunk / best / GIB
+
+    def up():
+        with torch.cuda.stream(s_up):
+            for i in range(k):
+                d[0].copy_(h[0], non_blocking=True)
+
+    def down():
+        with torch.cuda.stream(s_dn):
+            for i in range(k):
+                h[1].copy_(d[1], non_blocking=True)
+
+    def both():
+        up()
+        down()
+    return {"h2d_gib_s": round(timed(up), 3), "d2h_gib_s": round(timed(down), 3),
+            "bidir_each_gib_s": round(timed(both), 3), "bytes_per_direction": k * chunk}
 
 
 def pmc_traffic(kernel: str, pages: int, page_len: int):

@@ -190,6 +190,12 @@ int tyche_active_devices(void);
  * and returns the number of ranges k >= 1.  The engine uses
  * min_part_bytes = TYCHE_FANOUT_MIN_BYTES (default 64 MiB, one staging chunk). */
 size_t tyche_plan_split(size_t n, const uint32_t *src_lengths, int ndev, uint64_t min_part_bytes, size_t *cuts);
+/* Kernel-path switches and tunables (names without the TYCHE_ prefix, e.g.
+ * "LZ4_LANE_MIN", "ZLIB_PAR"): the library reads TYCHE_<name> from the
+ * environment once and checks for an override on every launch.  Set / drop an
+ * in-process override; for tests and A/B timing -- no knob changes a result. */
+int tyche_set_knob(const char *name, long value);
+int tyche_clear_knob(const char *name);
 /* message for the last TYCHE_E_DEVICE on this thread */
 const char *tyche_last_error(void);
 /* 1 if the library's gfx950 code object is usable on the calling thread's

@@ -22,6 +22,22 @@ def unpack(data: np.ndarray, offs: np.ndarray, lens: np.ndarray, i: int) -> byte
     return data[offs[i]:offs[i] + lens[i]].tobytes()
 
 
+@pytest.fixture
+def knobs():
+    """Sets engine switches for one test through tyche_set_knob (read on every launch) and
+    drops the overrides afterwards: knobs(ZLIB_PAR=0, LZ4_LANE_MIN=0)."""
+    from tyche_amd import _lib
+    names = set()
+
+    def setter(**kv):
+        for k, v in kv.items():
+            _lib.set_knob(k, int(v))
+            names.add(k)
+    yield setter
+    for k in names:
+        _lib.clear_knob(k)
+
+
 @pytest.fixture(scope="session")
 def oracle_mod():
     from oracle import oracle as O

@@ -14,9 +14,11 @@ time.
   errno after opendir), and the app starts, scans its pages and reaches the
   codec, which refuses loudly without a GPU.
 * GPU: `tyche -t compression -c lz4|zlib|zstd` (src/tests.c:340-443) passes
-  through the GPU codec, and a short `-c lz4 -p sample_data/16k -w 1` run
-  compresses and restores pages through list.c's own callers
-  (list.c:1051, 572).
+  through the GPU codec; short `-c lz4|zlib|zstd -p sample_data/16k -w 1`
+  runs compress and restore pages through list.c's own callers
+  (list.c:1051, 572), every run checked; and an injected device failure shows
+  what the unchanged sweep caller does with it and what INTEGRATION.md's
+  one-line change does.
 """
 import hashlib
 import os
@@ -30,6 +32,7 @@ from conftest import ROOT, load_golden
 
 APP = os.path.join(ROOT, "integration", "_app", "tyche")
 APP_Q = os.path.join(ROOT, "integration", "_app", "tyche_q")
+APP_FIXED = os.path.join(ROOT, "integration", "_app", "tyche_fixed")
 LIB_DIR = os.path.join(ROOT, "tyche_amd")
 
 
@@ -96,48 +99,114 @@ def test_reference_app_compression_test(sample_dir, codec):
     assert m and 0 < int(m.group(1)) < 4096, out
 
 
-@pytest.mark.gpu
-def test_reference_app_benchmark_run_lz4(sample_dir):
-    """A short benchmark run of the reference app (`-c lz4 -p sample_data/16k -w 1 -d 3`, a 20 % fixed raw
-    ratio of 512,000 bytes so the sweeper has to compress): its compressor pool (one thread per CPU, 256
-    on the GPU box) and its restore path call the engine, and pages are compressed and restored.
+ENGINE_CALLS = ("buffer__compress", "buffer__decompress", "tyche_buffers_compress", "tyche_buffers_decompress",
+                "tyche_buffer_restore")
 
-    Two defects of the reference's own list code can keep the process from exiting, so the harness
-    watchdog (integration/quarantine.c, TYCHE_APP_WATCHDOG) dumps every thread's stack and exits 3 after
-    15 s; the run then counts only if the dump shows one of them and no thread inside the engine:
+
+def _bench_attempt(app, codec, sample_dir, extra_env=None, extra_args=()):
+    """One short benchmark run of the reference app; returns a record of what it did.  Raises on
+    anything the engine could be blamed for: a fatal signal, an engine error line (TYCHE_LOG_ERRORS),
+    an app ERROR line, an unexpected exit status, or a watchdog dump with a thread inside an engine
+    entry point.  A watchdog exit (3) is accepted only as one of the reference's own two wedges,
+    classified from the dump:
       * shutdown: list__destroy "stops" the compressors by setting runnable = 1 (list.c:972-973) and
         joins them forever (list.c:979-980) -- the results block has been printed by then;
       * mid-run: list__sweep's clock scan (list.c:795-816) spins until it meets an unpopular raw buffer
         that is not already pending, and on a 20-page data set there may be none, so the worker waits in
         list__search (list.c:509-522); the app's status line (manager.c:193) still shows its counters."""
-    _need(APP_Q)
-    env = dict(os.environ, TYCHE_APP_WATCHDOG="15")
-    # the reference's list code is racy (SURVEY §4): a run can wedge before its first restore; up to
-    # three runs, the first that restored anything is checked
-    for attempt in range(3):
-        p = subprocess.run([APP_Q, "-c", "lz4", "-p", str(sample_dir / "16k"), "-w", "1", "-d", "3", "-m", "512000",
-                            "-f", "20"], stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=90, env=env)
-        out, err = p.stdout.decode(errors="replace"), p.stderr.decode(errors="replace")
-        if re.search(r"Restorations\s*:\s*[1-9]", out) or re.search(r"\(([1-9][\d.,]*)\S? Res\)", err):
-            break
+    env = dict(os.environ, TYCHE_APP_WATCHDOG="15", TYCHE_LOG_ERRORS="1")
+    env.update(extra_env or {})
+    p = subprocess.run([app, "-c", codec, "-p", str(sample_dir / "16k"), "-w", "1", "-d", "3", "-m", "512000",
+                        "-f", "20", *extra_args], stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=90, env=env)
+    out, err = p.stdout.decode(errors="replace"), p.stderr.decode(errors="replace")
+    rec = {"codec": codec, "app": os.path.basename(app), "rc": p.returncode, "out": out[-3000:], "err": err[-6000:]}
+    assert p.returncode >= 0 and "fatal signal" not in err, ("crash", rec)
+    assert "tyche-engine:" not in err, ("engine error", rec)
+    assert "ERROR:" not in err, ("app error", rec)
+    assert p.returncode in (0, 3), ("exit status", rec)
     comp = re.search(r"Compressions\s*:\s*([\d,]+) compressions", out)
     rest = re.search(r"Restorations\s*:\s*([\d,]+) restorations", out)
     if comp and rest:
-        comps, rests = int(comp.group(1).replace(",", "")), int(rest.group(1).replace(",", ""))
+        rec["comps"], rec["rests"] = int(comp.group(1).replace(",", "")), int(rest.group(1).replace(",", ""))
     else:
         status = re.findall(r"([\d.,]+)(\S?) Comps \(([\d.,]+)(\S?) Res\)", err)
-        assert status, (p.returncode, out[-2000:], err[-2000:])
         scale = {"": 1, "K": 1e3, "M": 1e6, "B": 1e9}
-        comps = float(status[-1][0].replace(",", "")) * scale.get(status[-1][1], 1)
-        rests = float(status[-1][2].replace(",", "")) * scale.get(status[-1][3], 1)
-    assert comps > 0 and rests > 0, (comps, rests, out[-2000:])
+        rec["comps"] = float(status[-1][0].replace(",", "")) * scale.get(status[-1][1], 1) if status else 0
+        rec["rests"] = float(status[-1][2].replace(",", "")) * scale.get(status[-1][3], 1) if status else 0
+    rec["kind"] = "clean"
     if p.returncode == 3:
         dump = err[err.find("--- thread"):]
-        assert "--- thread" in dump, err[-2000:]
-        assert "buffer__compress" not in dump and "buffer__decompress" not in dump   # no thread in the engine
+        assert "--- thread" in dump, ("watchdog without a dump", rec)
+        threads = dump.split("--- thread")[1:]
+        stuck = [t for t in threads if any(c in t for c in ENGINE_CALLS)]
+        assert not stuck, ("a thread is inside an engine call", rec, stuck[0][-2000:])
         if comp and rest:
-            assert "list__destroy" in dump, dump[-3000:]    # the reference's shutdown hang
+            assert "list__destroy" in dump, ("unclassified hang after the results", rec)
+            rec["kind"] = "reference shutdown hang (list.c:972-980)"
         else:
-            assert "list__sweep" in dump, dump[-3000:]      # the reference's sweep wedge
+            assert "list__sweep" in dump, ("unclassified hang", rec)
+            rec["kind"] = "reference sweep wedge (list.c:795-816)"
     else:
-        assert p.returncode == 0 and comp and rest, (p.returncode, out[-2000:], err[-2000:])
+        assert comp and rest, ("no results block", rec)
+    return rec
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("codec", ["lz4", "zlib", "zstd"])
+def test_reference_app_benchmark_run(sample_dir, codec):
+    """A short benchmark run of the reference app (`-c <codec> -p sample_data/16k -w 1 -d 3`, a 20 % fixed
+    raw ratio of 512,000 bytes so the sweeper has to compress): its compressor pool (one thread per CPU,
+    256 on the GPU box) and its restore path call the engine (list.c:1051, 572), and pages are compressed
+    and restored.  The reference's list code is racy and a run can wedge before its first
+    restore, so up to three runs are made -- but EVERY run is checked (_bench_attempt: no crash, no
+    engine or app error, any hang classified as one of the reference's own), and the first run that
+    restored pages must show compressions and restorations."""
+    _need(APP_Q)
+    attempts = []
+    for _ in range(3):
+        rec = _bench_attempt(APP_Q, codec, sample_dir)
+        attempts.append(rec)
+        if rec["rests"] > 0:
+            break
+    summary = [(a["rc"], a["kind"], a["comps"], a["rests"]) for a in attempts]
+    print(f"{codec}: attempts (rc, kind, compressions, restorations): {summary}")
+    assert attempts[-1]["comps"] > 0 and attempts[-1]["rests"] > 0, summary
+
+
+@pytest.mark.gpu
+def test_reference_app_device_failure(sample_dir):
+    """What a device failure does at the unchanged sweep caller, and what the INTEGRATION.md change does.
+
+    TYCHE_FAIL_COMPRESS_EVERY=2 makes every second encode launch fail as a lost device would
+    (TYCHE_E_DEVICE, *compressed_data = NULL).  With -U 100 every worker round rewrites the pages it
+    read (manager.c:353-359: memcpy from buf->data).
+
+    * Unchanged list.c (tyche_q): list__compressor_start skips a victim only on 124 (list.c:1052), so a
+      failed one is installed with data = NULL and flagged compressed (list.c:1058-1060); the restore
+      site sees comp_length == 0 and just clears the flag (list.c:568-587), leaving a raw page with no
+      data, and the next rewrite of it faults in memcpy -- the page is lost.
+    * The one-line change (tyche_fixed, built from list.c with line 1052 as INTEGRATION.md gives it):
+      the victim stays raw and intact, the run completes, and the pages that did compress restore."""
+    _need(APP_Q)
+    _need(APP_FIXED)
+    fault = {"TYCHE_FAIL_COMPRESS_EVERY": "2"}
+    env = dict(os.environ, TYCHE_APP_WATCHDOG="15", TYCHE_LOG_ERRORS="1", **fault)
+    p = subprocess.run([APP_Q, "-c", "lz4", "-p", str(sample_dir / "16k"), "-w", "1", "-d", "3", "-m", "512000",
+                        "-f", "20", "-U", "100"], stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=90, env=env)
+    err = p.stderr.decode(errors="replace")
+    print(f"unchanged caller: rc {p.returncode}; {err.count('tyche-engine:')} injected failures logged")
+    assert "tyche-engine:" in err                       # the failures happened and were reported
+    assert p.returncode == -11 and "fatal signal" in err, (p.returncode, err[-3000:])   # SIGSEGV ...
+    bt = err[err.find("fatal signal"):]
+    assert "manager__" in bt or "memcpy" in bt, bt[-3000:]                              # ... in the rewrite
+
+    attempts = []
+    for _ in range(3):
+        env_fixed = dict(fault, TYCHE_LOG_ERRORS="0")   # the injected failures are expected here
+        rec = _bench_attempt(APP_FIXED, "lz4", sample_dir, extra_env=env_fixed, extra_args=("-U", "100"))
+        attempts.append(rec)
+        if rec["rests"] > 0:
+            break
+    summary = [(a["rc"], a["kind"], a["comps"], a["rests"]) for a in attempts]
+    print(f"fixed caller: attempts (rc, kind, compressions, restorations): {summary}")
+    assert attempts[-1]["comps"] > 0 and attempts[-1]["rests"] > 0, summary

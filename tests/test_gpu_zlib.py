@@ -411,14 +411,12 @@ def _bench_streams(tc, oracle_mod, plen, n):
 
 
 @pytest.mark.parametrize("par,jump,wg", [("0", "512", "1"), ("1", "512", "1"), ("1", "512", "0"), ("1", "0", "1")])
-def test_inflate_serial_and_parallel_kernels(tc, oracle_mod, monkeypatch, par, jump, wg):
+def test_inflate_serial_and_parallel_kernels(tc, oracle_mod, knobs, par, jump, wg):
     """Both inflate kernels (TYCHE_ZLIB_PAR=0: one symbol at a time; 1: lane-parallel symbol
     decode with the serial decoder as its fallback), the parallel one with either match phase
     (TYCHE_ZLIB_JUMP_MAX=0: frontier copies; otherwise pointer jumping for batches below it),
     restore every page of every size exactly."""
-    monkeypatch.setenv("TYCHE_ZLIB_PAR", par)
-    monkeypatch.setenv("TYCHE_ZLIB_JUMP_MAX", jump)
-    monkeypatch.setenv("TYCHE_ZLIB_JUMP_WG", wg)   # 1: workgroup per page, 0: one wave
+    knobs(ZLIB_PAR=par, ZLIB_JUMP_MAX=jump, ZLIB_JUMP_WG=wg)   # WG 1: workgroup per page, 0: one wave
     for plen in (4096, 16384, 32768):
         pages, streams = _bench_streams(tc, oracle_mod, plen, 24)
         rv, outs = ragged_inflate(tc, streams, [plen] * len(streams), shift=plen % 7)
@@ -426,13 +424,12 @@ def test_inflate_serial_and_parallel_kernels(tc, oracle_mod, monkeypatch, par, j
 
 
 @pytest.mark.parametrize("jump,wg", [("512", "1"), ("512", "0"), ("0", "1")])
-def test_inflate_parallel_corruptions(tc, oracle_mod, monkeypatch, jump, wg):
+def test_inflate_parallel_corruptions(tc, oracle_mod, knobs, jump, wg):
     """Seeded corruptions of bench streams (byte flips anywhere, flips inside the compressed data,
     truncations, short capacities) through the lane-parallel kernel: the return value of every
     stream and the bytes of every success equal the oracle's -- the parallel path hands every page
     it cannot finish cleanly to the serial decoder, which gives the exact verdict."""
-    monkeypatch.setenv("TYCHE_ZLIB_JUMP_MAX", jump)
-    monkeypatch.setenv("TYCHE_ZLIB_JUMP_WG", wg)
+    knobs(ZLIB_JUMP_MAX=jump, ZLIB_JUMP_WG=wg)
     rng = np.random.default_rng(5150)
     pages, streams = _bench_streams(tc, oracle_mod, 16384, 16)
     cases, caps = [], []

@@ -32,10 +32,10 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(autouse=True)
-def _split_for_every_batch(monkeypatch):
+def _split_for_every_batch(knobs):
     """Batches below TYCHE_ZSTD_SPLIT_MIN (4096 pages) take the one-launch kernels; the tests
     here run the multi-pass codec on every batch size (the fused kernels get their own tests)."""
-    monkeypatch.setenv("TYCHE_ZSTD_SPLIT_MIN", "1")
+    knobs(ZSTD_SPLIT_MIN=1)
 
 DEV = torch.device("cuda:0")
 ZSTD = 3
@@ -507,36 +507,33 @@ def test_decode_huffman_tablelog12(tc, oracle_mod):
 
 
 @pytest.mark.parametrize("mode", ["fused", "chunked", "inline"])
-def test_zstd_fused_kernel_and_chunked_split(tc, oracle_mod, monkeypatch, mode):
+def test_zstd_fused_kernel_and_chunked_split(tc, oracle_mod, knobs, mode):
     """The fused one-kernel decoder (TYCHE_ZSTD_SPLIT=0), the split decoder on every batch size
     (TYCHE_ZSTD_SPLIT_MIN=1) run through a 1 MiB pass-1 buffer (TYCHE_ZSTD_SCRATCH_MB=1: a handful of
     pages per chunk) and the split decoder with the sequence chains inline in pass 1
     (TYCHE_ZSTD_JOBS=0) give the verdicts and bytes of the default path on the reference frames,
     the malformed set and the fuzz corpus."""
     if mode == "fused":
-        monkeypatch.setenv("TYCHE_ZSTD_SPLIT", "0")
+        knobs(ZSTD_SPLIT=0)
     elif mode == "chunked":
-        monkeypatch.setenv("TYCHE_ZSTD_SCRATCH_MB", "1")
-        monkeypatch.setenv("TYCHE_ZSTD_SPLIT_MIN", "1")   # every batch, however small, through the split
+        knobs(ZSTD_SCRATCH_MB=1, ZSTD_SPLIT_MIN=1)   # every batch, however small, through the split
     else:
-        monkeypatch.setenv("TYCHE_ZSTD_JOBS", "0")
-        monkeypatch.setenv("TYCHE_ZSTD_SPLIT_MIN", "1")
+        knobs(ZSTD_JOBS=0, ZSTD_SPLIT_MIN=1)
     test_zstd_reference_frames(tc, 3)
     test_zstd_malformed(tc, oracle_mod)
     test_zstd_fuzz_vs_oracle(tc, oracle_mod)
 
 
 @pytest.mark.parametrize("mode", ["fused", "chunked"])
-def test_zstd_encode_fused_kernel_and_chunked_split(tc, oracle_mod, monkeypatch, mode):
+def test_zstd_encode_fused_kernel_and_chunked_split(tc, oracle_mod, knobs, mode):
     """The one-kernel encoder (TYCHE_ZSTD_ENC_SPLIT=0) and the three-pass encoder run through a
     1 MiB work area (TYCHE_ZSTD_SCRATCH_MB=1: a few pages per chunk) produce frames the reference
     decodes: round trips over several distributions and sizes, multi-block and incompressible
     pages, tight capacities."""
     if mode == "fused":
-        monkeypatch.setenv("TYCHE_ZSTD_ENC_SPLIT", "0")
+        knobs(ZSTD_ENC_SPLIT=0)
     else:
-        monkeypatch.setenv("TYCHE_ZSTD_SCRATCH_MB", "1")
-        monkeypatch.setenv("TYCHE_ZSTD_SPLIT_MIN", "1")
+        knobs(ZSTD_SCRATCH_MB=1, ZSTD_SPLIT_MIN=1)
     for dist in (0, 3):
         for plen in (8192, 32768):
             test_encode_roundtrip_reference_decoder(tc, oracle_mod, dist, plen)

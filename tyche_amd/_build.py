@@ -77,7 +77,7 @@ def build_tools(verbose: bool = False) -> list:
     out_dir = os.path.join(root, "tools", "bin")
     os.makedirs(out_dir, exist_ok=True)
     outs = []
-    for name in ("cycle", "stress", "latency"):
+    for name in ("cycle", "cycle_live", "stress", "latency"):
         src = os.path.join(root, "tools", name + ".c")
         out = os.path.join(out_dir, name)
         outs.append(out)

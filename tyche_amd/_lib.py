@@ -119,6 +119,8 @@ SIGNATURES = {
     "tyche_active_devices": (ctypes.c_int, []),
     "tyche_plan_split": (ctypes.c_size_t, [ctypes.c_size_t, _u32p, ctypes.c_int, ctypes.c_uint64,
                                            ctypes.POINTER(ctypes.c_size_t)]),
+    "tyche_set_knob": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_long]),
+    "tyche_clear_knob": (ctypes.c_int, [ctypes.c_char_p]),
     "tyche_last_error": (ctypes.c_char_p, []),
     "tyche_device_ready": (ctypes.c_int, []),
     "tyche_pagegen": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
@@ -146,6 +148,15 @@ def load(build_if_missing: bool = False) -> ctypes.CDLL:
         f.argtypes = args
     _lib = lib
     return lib
+
+
+def set_knob(name: str, value: int) -> None:
+    """In-process override of a TYCHE_<name> switch (include/tyche_codec.h: tyche_set_knob)."""
+    check(load().tyche_set_knob(name.encode(), int(value)), f"tyche_set_knob({name})")
+
+
+def clear_knob(name: str) -> None:
+    check(load().tyche_clear_knob(name.encode()), f"tyche_clear_knob({name})")
 
 
 def last_error() -> str:

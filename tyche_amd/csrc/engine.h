@@ -123,10 +123,18 @@ class ScratchLease {
     int dev_ = -1, idx_ = -1;
     void *p_ = nullptr;
 };
+// Bytes held by the current device's scratch pool in leases no launch uses
+// (freed on demand: callers sizing work by hipMemGetInfo may count them as free).
+size_t scratch_idle_bytes();
 // Per-device, thread-safe launch preparation: raises `kernel`'s dynamic-LDS
 // limit to the CU's 160 KiB once per (device, kernel) and returns the current
 // device's CU count.
 size_t prepare_launch(const void *kernel);
+// Tunables and kernel-path switches: TYCHE_<name> from the environment (read
+// once per name), overridden in-process by tyche_set_knob -- read on every
+// launch, so one process can A/B the paths (the parity tests switch them this
+// way rather than with setenv, which would race getenv in other threads).
+long knob(const char *name, long dflt);
 __device__ __forceinline__ size_t claim_page(unsigned *counter, uint32_t lane) {
     unsigned v = 0;
     if (lane == 0) v = atomicAdd(counter, 1u);

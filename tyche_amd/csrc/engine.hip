@@ -22,6 +22,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <functional>
+#include <map>
 #include <mutex>
 #include <set>
 #include <string>
@@ -125,22 +126,66 @@ struct ScratchPool {
 ScratchPool g_scratch[kMaxDevices];
 }  // namespace
 
+// Leases are sized by the request (1 MiB granules) and reused best-fit, never
+// for a request under a quarter of their size (a small launch must not pin a
+// chunked zstd decode's gigabytes).  Idle entries beyond kPoolKeep bytes per
+// device are freed, largest first, whenever a lease is taken, and a failed
+// allocation frees every idle entry and tries once more.
+constexpr size_t kPoolKeep = size_t(2) << 30;
+
+namespace {
+bool entry_idle(ScratchPool::Entry &x) {
+    return x.state == 0 || (x.state == 2 && hipEventQuery(x.ev) == hipSuccess && ((x.state = 0), true));
+}
+// frees idle entries (largest first) until the pool holds at most `keep` bytes; under P.mu
+void pool_trim(ScratchPool &P, size_t keep) {
+    size_t total = 0;
+    for (auto &x : P.e) total += x.bytes;
+    while (total > keep) {
+        size_t best = P.e.size();
+        for (size_t i = 0; i < P.e.size(); i++)
+            if (entry_idle(P.e[i]) && (best == P.e.size() || P.e[i].bytes > P.e[best].bytes)) best = i;
+        if (best == P.e.size()) return;
+        (void)hipFree(P.e[best].p);
+        (void)hipEventDestroy(P.e[best].ev);
+        total -= P.e[best].bytes;
+        P.e.erase(P.e.begin() + (long)best);
+    }
+}
+}  // namespace
+
+size_t tyche::scratch_idle_bytes() {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return 0;
+    ScratchPool &P = g_scratch[dev];
+    std::lock_guard<std::mutex> g(P.mu);
+    size_t idle = 0;
+    for (auto &x : P.e)
+        if (entry_idle(x)) idle += x.bytes;
+    return idle;
+}
+
 tyche::ScratchLease::ScratchLease(hipStream_t s, size_t bytes) : s_(s) {
+    if (bytes == 0) return;   // nothing asked: get() is null
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return;
     ScratchPool &P = g_scratch[dev];
     std::lock_guard<std::mutex> g(P.mu);
+    const size_t want = (std::max<size_t>(bytes, 1) + 0xFFFFF) & ~size_t(0xFFFFF);
     size_t take = P.e.size();
-    for (size_t i = 0; i < P.e.size(); i++) {
+    for (size_t i = 0; i < P.e.size(); i++) {   // best fit among idle entries of at most 4x the request
         ScratchPool::Entry &x = P.e[i];
-        if (x.state == 1 || x.bytes < bytes) continue;
-        if (x.state == 2 && hipEventQuery(x.ev) != hipSuccess) continue;
-        take = i;
-        break;
+        if (x.state == 1 || x.bytes < want || x.bytes / 4 > want) continue;
+        if (!entry_idle(x)) continue;
+        if (take == P.e.size() || x.bytes < P.e[take].bytes) take = i;
     }
     if (take == P.e.size()) {
-        ScratchPool::Entry x{nullptr, (bytes + 0xFFFFF) & ~size_t(0xFFFFF), nullptr, 0};
-        if (hipMalloc(&x.p, x.bytes) != hipSuccess) return;
+        pool_trim(P, kPoolKeep > want ? kPoolKeep - want : 0);
+        ScratchPool::Entry x{nullptr, want, nullptr, 0};
+        if (hipMalloc(&x.p, x.bytes) != hipSuccess) {
+            pool_trim(P, 0);
+            if (hipMalloc(&x.p, x.bytes) != hipSuccess) return;
+        }
         if (hipEventCreateWithFlags(&x.ev, hipEventDisableTiming) != hipSuccess) {
             (void)hipFree(x.p);
             return;
@@ -157,7 +202,11 @@ tyche::ScratchLease::~ScratchLease() {
     if (idx_ < 0) return;
     ScratchPool &P = g_scratch[dev_];
     std::lock_guard<std::mutex> g(P.mu);
-    ScratchPool::Entry &x = P.e[(size_t)idx_];
+    // by address: pool_trim may have erased (idle) entries before this one since the lease
+    size_t i = 0;
+    while (i < P.e.size() && P.e[i].p != p_) i++;
+    if (i == P.e.size()) return;
+    ScratchPool::Entry &x = P.e[i];
     if (hipEventRecord(x.ev, s_) == hipSuccess) {
         x.state = 2;
     } else {
@@ -185,18 +234,51 @@ size_t tyche::prepare_launch(const void *kernel) {
 }
 
 namespace {
+struct KnobTable {
+    std::mutex mu;
+    std::map<std::string, long> over;                    // tyche_set_knob
+    std::map<std::string, std::pair<bool, long>> env;    // TYCHE_<name>: (present, value)
+};
+KnobTable &knob_table() {
+    static KnobTable *t = new KnobTable;   // never destroyed: detached pool threads may still read it at exit
+    return *t;
+}
+}  // namespace
+
+long tyche::knob(const char *name, long dflt) {
+    KnobTable &T = knob_table();
+    std::lock_guard<std::mutex> g(T.mu);
+    const auto o = T.over.find(name);
+    if (o != T.over.end()) return o->second;
+    auto e = T.env.find(name);
+    if (e == T.env.end()) {
+        const char *v = getenv((std::string("TYCHE_") + name).c_str());
+        e = T.env.emplace(name, std::make_pair(v != nullptr && *v, v ? strtol(v, nullptr, 10) : 0L)).first;
+    }
+    return e->second.first ? e->second.second : dflt;
+}
+
+namespace {
 
 // -1: the host API spreads work over every usable device (the default);
 // >= 0: tyche_set_device pinned the calling thread to that device
 thread_local int t_device = -1;
 thread_local std::string t_error;
 
+// TYCHE_LOG_ERRORS=1: every engine failure is also printed to stderr (one
+// "tyche-engine: ..." line), so a caller that drops the status -- list.c:1051
+// keeps going on any rv but 124 -- still leaves a trace (the C1 tests fail on it).
+void log_error(const std::string &m) {
+    if (knob("LOG_ERRORS", 0)) fprintf(stderr, "tyche-engine: %s\n", m.c_str());
+}
 int fail(const char *what, hipError_t e) {
     t_error = std::string(what) + ": " + hipGetErrorString(e);
+    log_error(t_error);
     return TYCHE_E_DEVICE;
 }
 int fail_msg(const std::string &m) {
     t_error = m;
+    log_error(t_error);
     return TYCHE_E_DEVICE;
 }
 
@@ -248,6 +330,22 @@ const DeviceSet &device_set() {
     return ds;
 }
 
+// Restores the calling thread's current device when it goes out of scope: the
+// host entry points switch devices to run a batch, and a caller (a torch rank
+// after set_device, say) must find its own device current afterwards.
+struct DeviceGuard {
+    int saved = -1;
+    DeviceGuard() {
+        if (hipGetDevice(&saved) != hipSuccess) saved = -1;
+    }
+    ~DeviceGuard() {
+        int now = -1;
+        if (saved >= 0 && hipGetDevice(&now) == hipSuccess && now != saved) (void)hipSetDevice(saved);
+    }
+    DeviceGuard(const DeviceGuard &) = delete;
+    DeviceGuard &operator=(const DeviceGuard &) = delete;
+};
+
 // makes `dev` current on this thread after checking it (cached per device)
 int ensure_device(int dev) {
     static std::atomic<int> ok[kMaxDevices];   // 0 unknown, 1 gfx950, 2 unusable
@@ -262,10 +360,12 @@ int ensure_device(int dev) {
     return TYCHE_E_OK;
 }
 
-// the device for a thread's device-side work: its pinned one, else the first of the set
+int rank_device();
+
+// the device for a thread's device-side work: its pinned one, the rank's, else the first of the set
 int current_device(int *dev) {
-    if (t_device >= 0) {
-        *dev = t_device;
+    if (t_device >= 0 || rank_device() >= 0) {
+        *dev = t_device >= 0 ? t_device : rank_device();
         return TYCHE_E_OK;
     }
     const DeviceSet &ds = device_set();
@@ -281,6 +381,12 @@ bool valid_codec(int id) {
 
 // the encoder kernel for a codec id (valid_codec)
 hipError_t launch_encode(int id, const tyche_batch_t &b, uint32_t in_cap, hipStream_t s) {
+    // Test hook (TYCHE_FAIL_COMPRESS_EVERY=N or the knob): every Nth encode launch
+    // fails as a lost device would, so the callers' TYCHE_E_DEVICE handling
+    // (list.c:1051-1060 and the INTEGRATION.md change) can be exercised.
+    static std::atomic<unsigned long> launches{0};
+    const long every = knob("FAIL_COMPRESS_EVERY", 0);
+    if (every > 0 && (launches.fetch_add(1) + 1) % (unsigned long)every == 0) return hipErrorLaunchFailure;
     if (id == TYCHE_ZSTD_COMPRESSOR_ID) return launch_zstd_encode(b, in_cap, s);
     if (id == TYCHE_ZLIB_COMPRESSOR_ID) return launch_zlib_deflate(b, in_cap, s);
     return launch_lz4_encode(b, in_cap, s);
@@ -578,17 +684,12 @@ std::atomic<int> g_inflight[kMaxDevices];   // host batches running per device
 // path's small batches); the kernels stage their input in LDS with 16-byte
 // loads and write whole 16-byte vectors, which PCIe carries well.
 // TYCHE_ZERO_COPY_BYTES=0 turns it off.
-size_t zero_copy_bytes() {
-    static const size_t v = [] {
-        const char *env = getenv("TYCHE_ZERO_COPY_BYTES");
-        return env ? (size_t)strtoull(env, nullptr, 10) : (size_t)(4u << 20);
-    }();
-    return v;
-}
+size_t zero_copy_bytes() { return (size_t)std::max(0L, knob("ZERO_COPY_BYTES", 4L << 20)); }
 
 template <typename Launch>
 int run_host_batch(int dev, size_t n, const void *const *src, const uint32_t *src_len, void *const *dst,
                    const uint32_t *dst_cap, int32_t *results, Launch launch, bool zc_ok = false) {
+    DeviceGuard keep;   // the caller's device is current again on every return
     int rc = ensure_device(dev);
     if (rc) return rc;
     struct Inflight {
@@ -691,11 +792,16 @@ int run_host_batch(int dev, size_t n, const void *const *src, const uint32_t *sr
 
     size_t first = 0;
     int si = 0;
+    // chunks hold ~chunk_bytes of input AND of output capacity: a decompress batch's
+    // output is ~2.6x its input, so cutting by input alone made 3 chunks of 170 MiB
+    // of D2H each out of a 32K-page batch, too few to overlap the two copy directions
+    const size_t chunk_bytes = (size_t)std::max(1L, knob("HOST_CHUNK_MB", (long)(kChunkBytes >> 20))) << 20;
     while (first < n) {
-        // ---- chunk [first, last): ~kChunkBytes of input
+        // ---- chunk [first, last)
         size_t last = first, in_bytes = 0, out_bytes = 0;
         uint32_t max_in = 0, max_out = 0;
-        while (last < n && (last == first || in_bytes + up16(src_len[last]) <= kChunkBytes)) {
+        while (last < n && (last == first || (in_bytes + up16(src_len[last]) <= chunk_bytes &&
+                                              out_bytes + up16(dst_cap[last]) <= chunk_bytes))) {
             in_bytes += up16(src_len[last]);
             out_bytes += up16(dst_cap[last]);
             max_in = std::max(max_in, src_len[last]);
@@ -766,12 +872,22 @@ int run_host_batch(int dev, size_t n, const void *const *src, const uint32_t *sr
 }
 
 // minimum input bytes per device before a host batch is split across devices
-uint64_t fanout_min_bytes() {
-    static const uint64_t v = [] {
-        const char *env = getenv("TYCHE_FANOUT_MIN_BYTES");
-        return env ? (uint64_t)strtoull(env, nullptr, 10) : (uint64_t)kChunkBytes;
+uint64_t fanout_min_bytes() { return (uint64_t)std::max(0L, knob("FANOUT_MIN_BYTES", (long)kChunkBytes)); }
+
+// A process launched one per GPU (torch.distributed.run sets WORLD_SIZE and
+// LOCAL_RANK) keeps its host work on its own device -- LOCAL_RANK modulo the
+// visible devices, torch's convention, whichever thread calls -- unless
+// TYCHE_DEVICES / TYCHE_DEVICE_IDS ask for the fan-out.  -1: not such a process.
+int rank_device() {
+    static const int d = [] {
+        if (getenv("TYCHE_DEVICES") || getenv("TYCHE_DEVICE_IDS")) return -1;
+        const char *w = getenv("WORLD_SIZE"), *lr = getenv("LOCAL_RANK");
+        if (!lr && !(w && atoi(w) > 1)) return -1;
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return -1;
+        return lr ? atoi(lr) % n : 0;
     }();
-    return v;
+    return d;
 }
 
 // the device with the fewest host batches in flight (ties rotate)
@@ -796,6 +912,8 @@ template <typename Launch>
 int run_host(size_t n, const void *const *src, const uint32_t *src_len, void *const *dst, const uint32_t *dst_cap,
              int32_t *results, Launch launch, bool zc_ok = false) {
     if (t_device >= 0) return run_host_batch(t_device, n, src, src_len, dst, dst_cap, results, launch, zc_ok);
+    if (rank_device() >= 0)   // one process per GPU: its own device only
+        return run_host_batch(rank_device(), n, src, src_len, dst, dst_cap, results, launch, zc_ok);
     const DeviceSet &ds = device_set();
     if (ds.ids.empty()) return fail_msg(ds.why);
     std::vector<size_t> cuts(ds.ids.size() + 1);
@@ -826,6 +944,22 @@ int run_host(size_t n, const void *const *src, const uint32_t *src_len, void *co
 extern "C" {
 
 // ------------------------------------------------------------------ runtime
+int tyche_set_knob(const char *name, long value) {
+    if (!name || !*name) return TYCHE_E_BAD_ARGS;
+    KnobTable &T = knob_table();
+    std::lock_guard<std::mutex> g(T.mu);
+    T.over[name] = value;
+    return TYCHE_E_OK;
+}
+
+int tyche_clear_knob(const char *name) {
+    if (!name || !*name) return TYCHE_E_BAD_ARGS;
+    KnobTable &T = knob_table();
+    std::lock_guard<std::mutex> g(T.mu);
+    T.over.erase(name);
+    return TYCHE_E_OK;
+}
+
 int tyche_device_count(void) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;
@@ -839,7 +973,7 @@ int tyche_set_device(int device) {
 }
 
 int tyche_active_devices(void) {
-    if (t_device >= 0) return 1;
+    if (t_device >= 0 || rank_device() >= 0) return 1;
     return (int)device_set().ids.size();
 }
 
@@ -868,6 +1002,7 @@ size_t tyche_plan_split(size_t n, const uint32_t *src_lengths, int ndev, uint64_
 const char *tyche_last_error(void) { return t_error.c_str(); }
 
 int tyche_device_ready(void) {
+    DeviceGuard keep;
     int dev = 0;
     int rc = current_device(&dev);
     if (rc == TYCHE_E_OK) rc = ensure_device(dev);
@@ -882,6 +1017,18 @@ uint32_t tyche_compress_bound(int compressor_id, uint32_t n) {
 }
 
 // ------------------------------------------------------- device-resident API
+// Launches, counters and scratch follow the current device (hipGetDevice); a
+// stream created on another device makes that device current for the call
+// (DeviceGuard puts the caller's back).
+static int stream_device(hipStream_t s) {
+    if (!s) return TYCHE_E_OK;
+    int sd = -1, cur = -1;
+    if (hipStreamGetDevice(s, &sd) != hipSuccess || sd < 0) return TYCHE_E_OK;
+    if (hipGetDevice(&cur) == hipSuccess && cur == sd) return TYCHE_E_OK;
+    hipError_t e = hipSetDevice(sd);
+    return e == hipSuccess ? TYCHE_E_OK : fail("hipSetDevice (stream's device)", e);
+}
+
 int tyche_compress_batch(int compressor_id, int compressor_level, const tyche_batch_t *batch, void *stream) {
     (void)compressor_level;   // level is fixed at 1 by tyche (src/options.c:68); LZ4 has no level
     if (!batch) return TYCHE_E_BAD_ARGS;
@@ -891,6 +1038,8 @@ int tyche_compress_batch(int compressor_id, int compressor_level, const tyche_ba
     uint32_t in_cap = batch->src_lengths ? batch->max_src_length : batch->src_length;
     if (batch->src_lengths && in_cap == 0) in_cap = 65535;
     if (in_cap > 65535) { t_error = "pages above 64 KiB are not supported by the device encoders"; return TYCHE_E_BAD_ARGS; }
+    DeviceGuard keep;
+    if (int rc = stream_device((hipStream_t)stream)) return rc;
     hipError_t e = launch_encode(compressor_id, *batch, in_cap, (hipStream_t)stream);
     if (e != hipSuccess) return fail("encode launch", e);
     return TYCHE_E_OK;
@@ -901,6 +1050,8 @@ int tyche_decompress_batch(int compressor_id, const tyche_batch_t *batch, void *
     if (!valid_decode_codec(compressor_id)) { t_error = codec_msg(compressor_id); return TYCHE_E_BAD_ARGS; }
     if (batch->count == 0) return TYCHE_E_OK;
     if (!batch->src || !batch->dst || !batch->results) return TYCHE_E_BAD_ARGS;
+    DeviceGuard keep;
+    if (int rc = stream_device((hipStream_t)stream)) return rc;
     uint32_t out_cap = batch->dst_capacity;
     if (compressor_id == TYCHE_ZLIB_COMPRESSOR_ID) {
         hipError_t e = launch_zlib_inflate(*batch, out_cap, (hipStream_t)stream);
@@ -1260,8 +1411,7 @@ int tyche_restore_queue_start(int max_batch, int max_wait_us) {
     g_rq.stop = false;
     for (bool &c : g_rq.collecting) c = false;
     g_rq.running = true;
-    const char *env = getenv("TYCHE_RESTORE_DISPATCHERS");
-    int k = env ? atoi(env) : std::max(1, tyche_active_devices());
+    int k = (int)knob("RESTORE_DISPATCHERS", std::max(1, tyche_active_devices()));
     k = std::max(1, std::min(k, 64));
     for (int codec = 1; codec <= 3; codec++)
         for (int i = 0; i < k; i++) g_rq.th.emplace_back([codec] { g_rq.loop(codec); });

@@ -1242,7 +1242,7 @@ constexpr long kJumpMax = 16384;
 static hipError_t launch_lz4_decode_jump(const tyche_batch_t &b, uint32_t in_cap, uint32_t out_cap, hipStream_t s,
                                          bool &launched) {
     launched = false;
-    static const long jmax = getenv("TYCHE_LZ4_JUMP_MAX") ? atol(getenv("TYCHE_LZ4_JUMP_MAX")) : kJumpMax;
+    const long jmax = knob("LZ4_JUMP_MAX", kJumpMax);
     if ((long)b.count >= jmax || out_cap > 32768u) return hipSuccess;
     const uint32_t cells_bytes = std::max(2u * ((out_cap + 63u) & ~63u), (in_cap + 4u + 15u) & ~15u);
     const uint32_t list_cap = out_cap / (uint32_t)(kJumpLong + 1) + 2u;
@@ -1253,7 +1253,7 @@ static hipError_t launch_lz4_decode_jump(const tyche_batch_t &b, uint32_t in_cap
     const size_t lds = kJumpHdr + (size_t)cells_bytes + 8u * list_cap + 4u * 64u * rows + 8u * kJumpOvf +
                        ((in_cap + 16u + kPad + 15u) & ~15u);
     if (lds > 150 * 1024) return hipSuccess;
-    static const int wide_env = getenv("TYCHE_LZ4_JUMP_WIDE") ? atoi(getenv("TYCHE_LZ4_JUMP_WIDE")) : 1;
+    const long wide_env = knob("LZ4_JUMP_WIDE", 1);
     const void *k512 = (const void *)lz4_decode_jump_kernel<512>, *k1024 = (const void *)lz4_decode_jump_kernel<1024>;
     const size_t ncu = prepare_launch(k512);
     const bool wide = wide_env && b.count <= ncu;
@@ -1331,7 +1331,7 @@ hipError_t launch_lz4_decode(const tyche_batch_t &b, uint32_t in_cap, uint32_t o
     // chunk of the long-stream class (1M bench pages, ms: static 118.9, chunks of
     // 64: 117.4, 8: 111.1, 2: 110.2, 1: 109.9 -- skipped claims are cheap)
     constexpr uint32_t kClassChunk = TYCHE_CLASS_CHUNK;   // static striding when 0
-    static const int split_env = getenv("TYCHE_DECODE_CLASSES") ? atoi(getenv("TYCHE_DECODE_CLASSES")) : 1;
+    const long split_env = knob("DECODE_CLASSES", 1);
     const size_t waves = split_env && b.src_lengths && b.count >= 8192
                              ? waves_per_cu((const void *)lz4_decode_wave_kernel, lds) : 32;
     if (waves < 16) {

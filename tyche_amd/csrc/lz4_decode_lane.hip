@@ -405,6 +405,202 @@ __device__ int32_t decode_ring(const uint8_t *__restrict__ in, int32_t L, uint8_
     }
 }
 
+// ---- round 3: the stream through a per-lane line buffer.
+//
+// decode_ring reads one unaligned 16-byte window straight from HBM per
+// sequence: with 512 lanes per CU each walking its own stream, a lane's line
+// is evicted between its windows (the calibration probe's "seq16" pattern
+// fetches every line 2.3x) and every sequence waits on a global load.  Here
+// the stream is fetched in whole aligned 64-byte lines (four 16-byte loads
+// issued together: one L2 miss per line) one line ahead of the parse, and
+// stored into a per-lane LDS window sb of 80 bytes = stream bytes
+// [lb - 16, lb + 64) (zero outside [0, L)); a sequence's window is one LDS
+// read.  Only far matches (and long literal runs / length bytes past the
+// window) still read HBM on the serial chain.
+
+// bytes [a, a + 16) of the stream, zero outside [0, L); never reads outside it
+__device__ __forceinline__ u128 chunk16z(const uint8_t *__restrict__ in, int32_t a, int32_t L) {
+    if (a >= L || a + 16 <= 0) return 0;
+    if (a >= 0 && a + 16 <= L) return ld16(in + a);
+    if (L >= 16) {
+        if (a < 0) return ld16(in) << (8 * (-a));                   // a + 16 < 16 <= L
+        return ld16(in + L - 16) >> (8 * (a - (L - 16)));          // 0 < a - (L - 16) < 16
+    }
+    u128 v = 0;
+    for (int32_t j = 15; j >= 0; j--) {
+        const int32_t x = a + j;
+        v = (v << 8) | ((x >= 0 && x < L) ? ld1(in + x) : 0u);
+    }
+    return v;
+}
+struct Line {
+    u128 c[4];
+};
+__device__ __forceinline__ Line line_load(const uint8_t *__restrict__ in, int32_t a, int32_t L) {
+    Line l;
+    if (a >= 0 && a + 64 <= L) {
+#pragma unroll
+        for (int32_t j = 0; j < 4; j++) l.c[j] = ld16(in + a + 16 * j);
+    } else {
+#pragma unroll
+        for (int32_t j = 0; j < 4; j++) l.c[j] = chunk16z(in, a + 16 * j, L);
+    }
+    return l;
+}
+struct LineBuf {
+    uint8_t *sb;    // 80 LDS bytes: stream [lb - 16, lb + 64)
+    int32_t lb;     // stream position of the buffered line (in + lb is 64-byte aligned)
+    int32_t ofs;    // (uintptr_t)in & 63
+    u128 tail;      // stream [lb + 48, lb + 64): the next window's front slack
+    Line pre;       // stream [lb + 64, lb + 128), in flight
+};
+__device__ __forceinline__ void lb_store(const LineBuf &s, u128 front, const Line &l) {
+    lds16(s.sb, front);
+#pragma unroll
+    for (int32_t j = 0; j < 4; j++) lds16(s.sb + 16 + 16 * j, l.c[j]);
+}
+__device__ __forceinline__ void lb_init(LineBuf &s, const uint8_t *__restrict__ in, int32_t L, uint8_t *sb) {
+    s.sb = sb;
+    s.ofs = (int32_t)((uintptr_t)in & 63u);
+    s.lb = -s.ofs;
+    const Line l = line_load(in, s.lb, L);
+    lb_store(s, 0, l);
+    s.tail = l.c[3];
+    s.pre = line_load(in, s.lb + 64, L);
+}
+// make [ip, ip + 16) readable from sb (ip >= lb - 16 holds: ip never decreases)
+__device__ __forceinline__ void lb_reach(LineBuf &s, const uint8_t *__restrict__ in, int32_t ip, int32_t L) {
+    if (ip <= s.lb + 48) return;
+    if (ip <= s.lb + 112) {   // the next line, already in flight
+        lb_store(s, s.tail, s.pre);
+        s.tail = s.pre.c[3];
+        s.lb += 64;
+        s.pre = line_load(in, s.lb + 64, L);
+        return;
+    }
+    // a long literal run jumped past it: reload around ip
+    int32_t nl = ((ip + s.ofs) & ~63) - s.ofs;
+    if (ip > nl + 48) nl += 64;
+    const u128 front = chunk16z(in, nl - 16, L);
+    const Line l = line_load(in, nl, L);
+    lb_store(s, front, l);
+    s.tail = l.c[3];
+    s.lb = nl;
+    s.pre = line_load(in, nl + 64, L);
+}
+__device__ __forceinline__ u128 lb_window(const LineBuf &s, int32_t ip) { return lds16(s.sb + (ip - s.lb + 16)); }
+
+template <int32_t kRing>
+__device__ int32_t decode_ring_lb(const uint8_t *__restrict__ in, int32_t L, uint8_t *__restrict__ out, int32_t C,
+                                  uint8_t *rb, uint8_t *sb) {
+    if (C == 0) return (L == 1 && ld1(in) == 0) ? 0 : -1;
+    if (L <= 0) return -1;
+    int32_t ip = 0, op = 0, fl = 0;   // fl: bytes of the page already in HBM
+    LineBuf s;
+    lb_init(s, in, L, sb);
+    lb_reach(s, in, 0, L);   // a page starting late in its 64-byte line
+    Win w;
+    w.hi = 0;
+    w.lo = lb_window(s, 0);
+    for (;;) {
+        const uint32_t token = (uint32_t)w.lo & 0xFFu;
+        int32_t lit = (int32_t)(token >> 4);
+        int32_t pos = 1;
+        if (lit == kRunMask) {
+            uint32_t b;
+            do {
+                b = getbN<16>(w, in, ip, pos, L);
+                pos++;
+                lit += (int32_t)b;
+            } while (ip + pos < L - kRunMask && b == 255);
+        }
+        if (op + lit > C - kMfLimit || ip + pos + lit > L - 8) {   // lz4.c:1147-1163
+            ip += pos;
+            if (ip + lit != L || op + lit > C) return -ip - 1;
+            ring_flush_all<kRing>(rb, out, fl, op);
+            copy_run(out + op, in + ip, lit, C - op, L - ip);
+            return op + lit;
+        }
+        if (pos + lit <= 16) {
+            ring_wr<kRing>(rb, op, w.lo >> (8 * pos));
+        } else {
+            for (int32_t k = 0; k < lit; k += 16) {
+                ring_wr<kRing>(rb, op + k, stream16(in, ip + pos + k, L));
+                ring_flush<kRing>(rb, out, fl, op + min(k + 16, lit));
+            }
+        }
+        pos += lit;
+        const int32_t off = (int32_t)(getbN<16>(w, in, ip, pos, L) | (getbN<16>(w, in, ip, pos + 1, L) << 8));
+        pos += 2;
+        op += lit;
+        if (off > op) return -(ip + pos) - 1;                   // lz4.c:1168
+        int32_t ml = (int32_t)(token & 15u);
+        if (ml == 15) {
+            uint32_t b;
+            do {
+                b = getbN<16>(w, in, ip, pos, L);
+                pos++;
+                if (ip + pos > L - kLastLiterals) return -(ip + pos) - 1;   // lz4.c:1176
+                ml += (int32_t)b;
+            } while (b == 255);
+        }
+        ml += kMinMatch;
+        if (op + ml > C - kLastLiterals) return -(ip + pos) - 1;   // lz4.c:1225
+        const bool far = off > kRing - 32;   // as decode_ring: far sources are already in HBM
+        u128 m = far ? ld16(out + op - off) : ring_rd<kRing>(rb, op - off);
+        ip += pos;
+        lb_reach(s, in, ip, L);
+        w.lo = lb_window(s, ip);
+        if (off >= 16) {
+            ring_wr<kRing>(rb, op, m);
+            for (int32_t k = 16; k < ml; k += 16) {
+                ring_flush<kRing>(rb, out, fl, op + k);
+                m = far ? ld16(out + op + k - off) : ring_rd<kRing>(rb, op + k - off);
+                ring_wr<kRing>(rb, op + k, m);
+            }
+        } else {
+            u128 p = 0;
+            int32_t step = 16;
+            if (off > 0) {
+                p = m & ((((u128)1) << (8 * off)) - 1);
+                for (int32_t len = off; len < 16; len <<= 1) p |= p << (8 * len);
+                step = 16 - (int32_t)mod_small(16u, (uint32_t)off);
+            }
+            for (int32_t k = 0; k < ml; k += step) {
+                ring_flush<kRing>(rb, out, fl, op + k);
+                ring_wr<kRing>(rb, op + k, p);
+            }
+        }
+        op += ml;
+        ring_flush<kRing>(rb, out, fl, op);
+    }
+}
+
+template <int32_t kRing>
+__global__ __launch_bounds__(64) void lz4_decode_ringlb_kernel(tyche_batch_t b, uint32_t in_cap, uint32_t out_cap,
+                                                               unsigned *ctr) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint8_t *rb = smem + threadIdx.x * (kRing + 48) + 16;
+    uint8_t *sb = smem + 64 * (kRing + 48) + threadIdx.x * 80;
+    const size_t nthreads = (size_t)gridDim.x * blockDim.x;
+    size_t page = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    while (page < b.count) {
+        const uint64_t so = b.src_offsets ? b.src_offsets[page] : (uint64_t)page * b.src_stride;
+        const uint64_t dof = b.dst_offsets ? b.dst_offsets[page] : (uint64_t)page * b.dst_stride;
+        const uint32_t L = b.src_lengths ? b.src_lengths[page] : b.src_length;
+        const uint32_t C = b.dst_capacities ? b.dst_capacities[page] : b.dst_capacity;
+        int32_t rv;
+        if (L > in_cap || C > out_cap) {
+            rv = kResultTooLarge;
+        } else {
+            rv = decode_ring_lb<kRing>((const uint8_t *)b.src + so, (int32_t)L, (uint8_t *)b.dst + dof, (int32_t)C, rb,
+                                       sb);
+        }
+        b.results[page] = rv;
+        page = (size_t)atomicAdd(ctr, 1u) + nthreads;
+    }
+}
+
 template <int32_t kRing, int32_t kWin>
 __global__ __launch_bounds__(64) void lz4_decode_ring_kernel(tyche_batch_t b, uint32_t in_cap, uint32_t out_cap,
                                                              unsigned *ctr) {
@@ -465,7 +661,7 @@ constexpr long kLaneMin = 32768;
 // decoders, whose LDS sizing rejects them.
 constexpr uint32_t kLaneMaxStream = 4u << 20;
 bool lz4_lane_decode_wanted(size_t count, uint32_t in_cap, uint32_t out_cap) {
-    static const long min_pages = getenv("TYCHE_LZ4_LANE_MIN") ? atol(getenv("TYCHE_LZ4_LANE_MIN")) : kLaneMin;
+    const long min_pages = knob("LZ4_LANE_MIN", kLaneMin);
     return min_pages >= 0 && count >= (size_t)min_pages && in_cap <= kLaneMaxStream && out_cap <= kLaneMaxStream;
 }
 
@@ -479,10 +675,29 @@ constexpr int kDefaultWin = 16;
 
 hipError_t launch_lz4_decode_lane(const tyche_batch_t &b, uint32_t in_cap, uint32_t out_cap, hipStream_t s) {
     if (b.count == 0) return hipSuccess;
-    static const long env_waves = getenv("TYCHE_LZ4_LANE_WAVES") ? atol(getenv("TYCHE_LZ4_LANE_WAVES")) : 0;
-    static const int ring = getenv("TYCHE_LZ4_LANE_RING") ? atoi(getenv("TYCHE_LZ4_LANE_RING")) : kDefaultRing;
+    const long env_waves = knob("LZ4_LANE_WAVES", 0);
+    const long ring = knob("LZ4_LANE_RING", kDefaultRing);
+    const long lbuf = knob("LZ4_LANE_LB", 0);
+    if (ring && lbuf) {
+        const void *k = ring == 128   ? (const void *)lz4_decode_ringlb_kernel<128>
+                        : ring == 192 ? (const void *)lz4_decode_ringlb_kernel<192>
+                        : ring == 224 ? (const void *)lz4_decode_ringlb_kernel<224>
+                                      : (const void *)lz4_decode_ringlb_kernel<256>;
+        const int32_t rbytes = ring == 128 ? 128 : ring == 192 ? 192 : ring == 224 ? 224 : 256;
+        const size_t lds = 64 * (size_t)(rbytes + 48 + 80);
+        const size_t ncu = prepare_launch(k);
+        size_t waves = waves_per_cu(k, lds);
+        if (env_waves > 0) waves = std::min<size_t>(waves, (size_t)env_waves);
+        const size_t grid = std::min<size_t>((b.count + 63) / 64, ncu * waves);
+        WorkCounter ctr(s, grid * 64 < b.count);
+        unsigned *cp = ctr.get();
+        if (!cp) return hipErrorOutOfMemory;
+        void *args[] = {(void *)&b, &in_cap, &out_cap, &cp};
+        (void)hipLaunchKernel(k, dim3((unsigned)grid), dim3(64), args, lds, s);
+        return hipGetLastError();
+    }
     if (ring) {
-        static const int win = getenv("TYCHE_LZ4_LANE_WIN") ? atoi(getenv("TYCHE_LZ4_LANE_WIN")) : kDefaultWin;
+        const long win = knob("LZ4_LANE_WIN", kDefaultWin);
         const void *k = win == 16 ? (ring == 128   ? (const void *)lz4_decode_ring_kernel<128, 16>
                                      : ring == 256 ? (const void *)lz4_decode_ring_kernel<256, 16>
                                                    : (const void *)lz4_decode_ring_kernel<512, 16>)

@@ -604,7 +604,7 @@ hipError_t launch_lz4_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream_
     if (b.count == 0) return hipSuccess;
     if (in_cap > 65535u) return hipErrorInvalidValue;    // 16-bit positions (byU16 regime)
     // TYCHE_LZ4_ENC=1: the one-wave kernel for every batch (A/B timing)
-    static const int one_wave = getenv("TYCHE_LZ4_ENC") ? atoi(getenv("TYCHE_LZ4_ENC")) == 1 : 0;
+    const bool one_wave = knob("LZ4_ENC", 0) == 1;
     if (!one_wave && in_cap >= kSplitMin) {
         const size_t lds = kSplitStage + ((in_cap + 16u + kPad + 15u) & ~15u);
         const size_t ncu = prepare_launch((const void *)lz4_encode_split_kernel);
@@ -616,11 +616,13 @@ hipError_t launch_lz4_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream_
         // B's scratch: its half's worst case (LZ4_compressBound of L - H < in_cap / 2 + 64), 256-byte aligned
         const uint32_t ws_stride = (lz4_bound(in_cap / 2u + kWave) + 64u + 255u) & ~255u;
         ScratchLease ws(s, grid * (size_t)ws_stride);
-        WorkCounter ctr(s, grid < b.count);
-        if (!ctr.get() || !ws.get()) return hipErrorOutOfMemory;
-        hipLaunchKernelGGL(lz4_encode_split_kernel, dim3((unsigned)grid), dim3(2 * kWave), lds, s, b, in_cap,
-                           ctr.get(), (uint8_t *)ws.get(), ws_stride);
-        return hipGetLastError();
+        if (ws.get()) {   // else the one-wave kernel below, which needs no scratch
+            WorkCounter ctr(s, grid < b.count);
+            if (!ctr.get()) return hipErrorOutOfMemory;
+            hipLaunchKernelGGL(lz4_encode_split_kernel, dim3((unsigned)grid), dim3(2 * kWave), lds, s, b, in_cap,
+                               ctr.get(), (uint8_t *)ws.get(), ws_stride);
+            return hipGetLastError();
+        }
     }
     const size_t lds = kHashSize * sizeof(uint16_t) + 4 * kWave + kWave * 8 + kWave * 16 +
                        ((in_cap + 16u + kPad + 15u) & ~15u);

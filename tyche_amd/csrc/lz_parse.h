@@ -273,7 +273,9 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
         // position <= mflimit, so the window stays inside the page's zero pad.
         uint32_t cand = cands[0];
         Window cw = lds_window(A, cand + ib);
-        bool ok = live & (cand < pos) & (((cw.w0 ^ v) & vm) == 0u);
+        // deflate (kMin3): a candidate beyond the 32 KiB window cannot be coded; rejecting it here
+        // lets a nearer bucket entry win (pages over 32 KiB)
+        bool ok = live & (cand < pos) & (!kMin3 || pos - cand <= 32768u) & (((cw.w0 ^ v) & vm) == 0u);
         uint32_t n = 4u + kProbe;
 #pragma unroll
         for (int k = (int)kProbeWords - 1; k >= 0; k--) {
@@ -286,7 +288,7 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
             // older bucket entries: taken only when strictly longer
             const uint32_t cw2 = cands[w];
             const Window ww = lds_window(A, cw2 + ib);
-            const bool okw = live & (cw2 < pos) & (((ww.w0 ^ v) & vm) == 0u);
+            const bool okw = live & (cw2 < pos) & (!kMin3 || pos - cw2 <= 32768u) & (((ww.w0 ^ v) & vm) == 0u);
             uint32_t nw = 4u + kProbe;
 #pragma unroll
             for (int k = (int)kProbeWords - 1; k >= 0; k--) {

@@ -1285,8 +1285,7 @@ extern "C" int tyche_debug_zlib_profile(unsigned long long *host16, int reset) {
 // parallel path without its fallback (diagnostics: such pages report INT32_MIN + 1)
 hipError_t launch_zlib_inflate(const tyche_batch_t &b, uint32_t out_cap, hipStream_t s) {
     if (b.count == 0) return hipSuccess;
-    const char *env = getenv("TYCHE_ZLIB_PAR");   // read per call: the parity tests switch it in-process
-    const int par = env ? atoi(env) : 1;
+    const long par = knob("ZLIB_PAR", 1);   // per call: the parity tests switch it in-process
     const uint32_t off_lens = (out_cap + 64u + 15u) & ~15u;
     if (par && out_cap <= 65535u) {
         const uint32_t off_lt = (off_lens + 320u + 2u * 320u + 2u * 32u + 15u) & ~15u;
@@ -1296,13 +1295,11 @@ hipError_t launch_zlib_inflate(const tyche_batch_t &b, uint32_t out_cap, hipStre
         // small batches (restores) resolve matches by pointer jumping: 2 bytes of LDS per
         // output byte more (below TYCHE_ZLIB_JUMP_MAX pages, default 1,024: on the workgroup
         // kernel 512-page batches still gain, 459 vs 698 us at 16 KiB; 0 = never)
-        const char *jenv = getenv("TYCHE_ZLIB_JUMP_MAX");
-        const long jmax = jenv ? atol(jenv) : 1024;
+        const long jmax = knob("ZLIB_JUMP_MAX", 1024);
         const uint32_t off_cells = (long)b.count < jmax && out_cap <= 32768u ? off_stage + stage_cap : 0u;
         const size_t lds = (size_t)off_stage + stage_cap + (off_cells ? 2u * ((out_cap + 7u) & ~7u) : 0u);
         // the jump path on a workgroup of kZThreads per page (TYCHE_ZLIB_JUMP_WG=0: one wave)
-        const char *wenv = getenv("TYCHE_ZLIB_JUMP_WG");
-        if (off_cells && par == 1 && (!wenv || atoi(wenv)) && lds + 128u <= 160 * 1024) {
+        if (off_cells && par == 1 && knob("ZLIB_JUMP_WG", 1) && lds + 128u <= 160 * 1024) {
             const void *k256 = (const void *)zlib_inflate_jump_kernel<256>;
             const void *k512 = (const void *)zlib_inflate_jump_kernel<512>;
             const size_t ncu = prepare_launch(k256);

@@ -1937,26 +1937,24 @@ hipError_t launch_zstd_decode(const tyche_batch_t &b, uint32_t in_cap, uint32_t 
     if (b.count == 0) return hipSuccess;
     // small batches (restores) take the one-launch kernel: the split's extra
     // launches cost more latency than its throughput gains on a few pages
-    const char *env = getenv("TYCHE_ZSTD_SPLIT");
-    const char *mn = getenv("TYCHE_ZSTD_SPLIT_MIN");
-    const size_t split_min = mn && atol(mn) > 0 ? (size_t)atol(mn) : 4096;
-    const bool split = !(env && env[0] == '0') && b.count >= split_min;
+    const long mn = knob("ZSTD_SPLIT_MIN", 4096);
+    const size_t split_min = mn > 0 ? (size_t)mn : 4096;
+    const bool split = knob("ZSTD_SPLIT", 1) != 0 && b.count >= split_min;
     const Layout l1 = make_layout(in_cap, out_cap, false);
-    const char *jenv = getenv("TYCHE_ZSTD_JOBS");   // 0: sequence chains inline in pass 1
-    const bool use_jobs = !(jenv && jenv[0] == '0');
+    const bool use_jobs = knob("ZSTD_JOBS", 1) != 0;   // 0: sequence chains inline in pass 1
     const uint32_t lds2 = (out_cap + kWinPad + 15u) & ~15u;
     if (!split || l1.total > 160u * 1024u || lds2 > 160u * 1024u) return launch_fused(b, in_cap, out_cap, s);
     const size_t page_bytes = ent_page_bytes(in_cap, out_cap);
     // the sequence kernel's time per chunk is one page's chain (latency-bound, one
     // lane per page), so chunks are made as large as memory allows: 16 GiB or a
     // quarter of the free memory, whichever is less
-    const char *mb = getenv("TYCHE_ZSTD_SCRATCH_MB");
+    const long mb = knob("ZSTD_SCRATCH_MB", 0);
     size_t budget = (size_t)16 << 30;
     size_t free_b = 0, total_b = 0;
-    if (b.count * page_bytes > ((size_t)1 << 30) && hipMemGetInfo(&free_b, &total_b) == hipSuccess &&
+    if (b.count * page_bytes > ((size_t)1 << 30) && hipMemGetInfo(&free_b, &total_b) == hipSuccess && ((free_b += scratch_idle_bytes()), true) &&
         free_b / 4 < budget)
         budget = free_b / 4;
-    if (mb && atol(mb) > 0) budget = (size_t)atol(mb) << 20;
+    if (mb > 0) budget = (size_t)mb << 20;
     const size_t chunk = std::max<size_t>(1, std::min<size_t>(b.count, budget / page_bytes));
     const size_t st_bytes = (chunk * 4u + 255u) & ~(size_t)255u;
     ScratchLease ws(s, st_bytes + chunk * page_bytes);

@@ -1101,18 +1101,17 @@ hipError_t launch_zstd_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream
     const size_t page_lds = (in_cap + 16u + kPad + 15u) & ~15u;
     const size_t lds = kTableSlots * sizeof(uint16_t) + kWave + kWave * 8 + kSeqCap * 8 + kHtab * 4 + 256 + page_lds;
     const size_t lds1 = kTableSlots * sizeof(uint16_t) + kWave + kWave * 8 + page_lds;   // pass A1
-    const char *env = getenv("TYCHE_ZSTD_ENC_SPLIT");
-    const char *mn = getenv("TYCHE_ZSTD_SPLIT_MIN");   // small batches: one launch (latency)
-    const size_t split_min = mn && atol(mn) > 0 ? (size_t)atol(mn) : 4096;
-    const bool split = !(env && env[0] == '0') && b.count >= split_min;
+    const long mn = knob("ZSTD_SPLIT_MIN", 4096);   // small batches: one launch (latency)
+    const size_t split_min = mn > 0 ? (size_t)mn : 4096;
+    const bool split = knob("ZSTD_ENC_SPLIT", 1) != 0 && b.count >= split_min;
     const size_t page_bytes = enc_area_bytes(in_cap);
     size_t budget = (size_t)8 << 30;
     size_t free_b = 0, total_b = 0;
-    if (b.count * page_bytes > ((size_t)1 << 30) && hipMemGetInfo(&free_b, &total_b) == hipSuccess &&
+    if (b.count * page_bytes > ((size_t)1 << 30) && hipMemGetInfo(&free_b, &total_b) == hipSuccess && ((free_b += scratch_idle_bytes()), true) &&
         free_b / 8 < budget)
         budget = free_b / 8;
-    const char *mb = getenv("TYCHE_ZSTD_SCRATCH_MB");
-    if (mb && atol(mb) > 0) budget = (size_t)atol(mb) << 20;
+    const long mb = knob("ZSTD_SCRATCH_MB", 0);
+    if (mb > 0) budget = (size_t)mb << 20;
     const size_t chunk = split ? std::max<size_t>(1, std::min<size_t>(b.count, budget / page_bytes)) : b.count;
     const size_t st_bytes = (chunk * 4u + 255u) & ~(size_t)255u;
     ScratchLease lease(s, split ? st_bytes + chunk * page_bytes : 0);
