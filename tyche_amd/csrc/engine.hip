@@ -688,7 +688,8 @@ size_t zero_copy_bytes() { return (size_t)std::max(0L, knob("ZERO_COPY_BYTES", 4
 
 template <typename Launch>
 int run_host_batch(int dev, size_t n, const void *const *src, const uint32_t *src_len, void *const *dst,
-                   const uint32_t *dst_cap, int32_t *results, Launch launch, bool zc_ok = false) {
+                   const uint32_t *dst_cap, int32_t *results, Launch launch, bool zc_ok = false,
+                   bool direct_out = false) {
     DeviceGuard keep;   // the caller's device is current again on every return
     int rc = ensure_device(dev);
     if (rc) return rc;
@@ -851,7 +852,11 @@ int run_host_batch(int dev, size_t n, const void *const *src, const uint32_t *sr
         b.src_offsets = (const uint64_t *)dmeta;
         b.src_lengths = (const uint32_t *)(dmeta + ((uint8_t *)m_slen - (uint8_t *)m_soff));
         b.max_src_length = max_in;
-        b.dst = S.d_out.p;
+        // direct_out (LZ4 compress): the kernel writes its streams straight into the pinned
+        // arena over PCIe, so only the compressed bytes cross the link -- a D2H of the arena
+        // would move every page's full capacity (16 KiB+ per 16 KiB page at ratio 2.6)
+        const bool direct = direct_out && S.h_out.dp != nullptr;
+        b.dst = direct ? S.h_out.dp : S.d_out.p;
         b.dst_offsets = (const uint64_t *)(dmeta + ((uint8_t *)m_doff - (uint8_t *)m_soff));
         b.dst_capacities = (const uint32_t *)(dmeta + ((uint8_t *)m_dcap - (uint8_t *)m_soff));
         b.dst_capacity = max_out;
@@ -859,7 +864,7 @@ int run_host_batch(int dev, size_t n, const void *const *src, const uint32_t *sr
         if ((e = launch(b, S.stream)) != hipSuccess) return bail(fail("kernel launch", e));
         if ((e = hipMemcpyAsync(m_res, b.results, k * 4, hipMemcpyDeviceToHost, S.stream)) != hipSuccess)
             return bail(fail("hipMemcpyAsync(results)", e));
-        if (dof && (e = hipMemcpyAsync(S.h_out.p, S.d_out.p, dof, hipMemcpyDeviceToHost, S.stream)) != hipSuccess)
+        if (dof && !direct && (e = hipMemcpyAsync(S.h_out.p, S.d_out.p, dof, hipMemcpyDeviceToHost, S.stream)) != hipSuccess)
             return bail(fail("hipMemcpyAsync(out)", e));
         first = last;
         si = (si + 1) % kSlots;
@@ -910,22 +915,23 @@ int pick_device(const std::vector<int> &ids) {
 // restores) spread over all devices.
 template <typename Launch>
 int run_host(size_t n, const void *const *src, const uint32_t *src_len, void *const *dst, const uint32_t *dst_cap,
-             int32_t *results, Launch launch, bool zc_ok = false) {
-    if (t_device >= 0) return run_host_batch(t_device, n, src, src_len, dst, dst_cap, results, launch, zc_ok);
+             int32_t *results, Launch launch, bool zc_ok = false, bool direct_out = false) {
+    if (t_device >= 0) return run_host_batch(t_device, n, src, src_len, dst, dst_cap, results, launch, zc_ok, direct_out);
     if (rank_device() >= 0)   // one process per GPU: its own device only
-        return run_host_batch(rank_device(), n, src, src_len, dst, dst_cap, results, launch, zc_ok);
+        return run_host_batch(rank_device(), n, src, src_len, dst, dst_cap, results, launch, zc_ok, direct_out);
     const DeviceSet &ds = device_set();
     if (ds.ids.empty()) return fail_msg(ds.why);
     std::vector<size_t> cuts(ds.ids.size() + 1);
     const size_t parts = tyche_plan_split(n, src_len, (int)ds.ids.size(), fanout_min_bytes(), cuts.data());
     if (parts <= 1)
-        return run_host_batch(pick_device(ds.ids), n, src, src_len, dst, dst_cap, results, launch, zc_ok);
+        return run_host_batch(pick_device(ds.ids), n, src, src_len, dst, dst_cap, results, launch, zc_ok, direct_out);
     std::vector<int> rcs(parts, TYCHE_E_OK);
     std::vector<std::string> errs(parts);
     std::vector<std::thread> th;
     auto part = [&](size_t p) {
         const size_t a = cuts[p], m = cuts[p + 1] - cuts[p];
-        rcs[p] = run_host_batch(ds.ids[p], m, src + a, src_len + a, dst + a, dst_cap + a, results + a, launch, zc_ok);
+        rcs[p] = run_host_batch(ds.ids[p], m, src + a, src_len + a, dst + a, dst_cap + a, results + a, launch, zc_ok,
+                                direct_out);
         if (rcs[p]) errs[p] = t_error;
     };
     for (size_t p = 1; p < parts; p++) th.emplace_back(part, p);
@@ -1078,10 +1084,13 @@ int tyche_compress_host(int compressor_id, int compressor_level, size_t n, const
     if (n == 0) return TYCHE_E_OK;
     for (size_t i = 0; i < n; i++)
         if (src_lengths[i] > 65535u) { t_error = "pages above 64 KiB are not supported by the device encoders"; return TYCHE_E_BAD_ARGS; }
+    // LZ4's encoders only store to their destination (never read it back), so their streams may go
+    // straight into the pinned staging arena (HOST_DIRECT_OUT=0: stage through HBM and D2H instead)
+    const bool direct = compressor_id == TYCHE_LZ4_COMPRESSOR_ID && knob("HOST_DIRECT_OUT", 1) != 0;
     return run_host(n, src, src_lengths, dst, dst_capacities, results,
                           [compressor_id](const tyche_batch_t &b, hipStream_t s) {
                               return launch_encode(compressor_id, b, std::max(b.max_src_length, 1u), s);
-                          });
+                          }, false, direct);
 }
 
 int tyche_decompress_host(int compressor_id, size_t n, const void *const *src, const uint32_t *src_lengths,

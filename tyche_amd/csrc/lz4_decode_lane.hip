@@ -523,6 +523,13 @@ __device__ int32_t decode_ring_lb(const uint8_t *__restrict__ in, int32_t L, uin
         }
         if (pos + lit <= 16) {
             ring_wr<kRing>(rb, op, w.lo >> (8 * pos));
+        } else if (ip + pos + ((lit - 1) & ~15) <= s.lb + 48) {
+            // a longer run that the line buffer still holds (every 16-byte read inside it): LDS reads,
+            // no HBM round trip per 16 bytes
+            for (int32_t k = 0; k < lit; k += 16) {
+                ring_wr<kRing>(rb, op + k, lb_window(s, ip + pos + k));
+                ring_flush<kRing>(rb, out, fl, op + min(k + 16, lit));
+            }
         } else {
             for (int32_t k = 0; k < lit; k += 16) {
                 ring_wr<kRing>(rb, op + k, stream16(in, ip + pos + k, L));
@@ -546,16 +553,46 @@ __device__ int32_t decode_ring_lb(const uint8_t *__restrict__ in, int32_t L, uin
         }
         ml += kMinMatch;
         if (op + ml > C - kLastLiterals) return -(ip + pos) - 1;   // lz4.c:1225
-        const bool far = off > kRing - 32;   // as decode_ring: far sources are already in HBM
-        u128 m = far ? ld16(out + op - off) : ring_rd<kRing>(rb, op - off);
+        // as decode_ring: far sources are already in HBM (64: timing-only ablation, far reads from the ring)
+        const bool far = (TYCHE_ABLATE & (64 | 256)) ? false : off > kRing - 32;
+        // A far match's first 64 bytes are fetched together (one wait, not one per 16 bytes: the wave
+        // waits for its slowest lane, and a long far match serialized its loads while 63 lanes idled).
+        // Their sources end at or before op + 64 - (kRing - 31) <= op - 96 (kRing >= 192), and the
+        // unflushed tail is < 80 bytes, so they are in HBM; the ring holds the < 144 unflushed bytes.
+        constexpr bool kGroup = kRing >= 192;
+        u128 m = 0, m1 = 0, m2 = 0, m3 = 0;
+        if (far) {
+            m = ld16(out + op - off);
+            if (kGroup && ml > 16) m1 = ld16(out + op + 16 - off);
+            if (kGroup && ml > 32) m2 = ld16(out + op + 32 - off);
+            if (kGroup && ml > 48) m3 = ld16(out + op + 48 - off);
+        } else if (!(TYCHE_ABLATE & 256)) {
+            m = ring_rd<kRing>(rb, op - off);
+        }
         ip += pos;
         lb_reach(s, in, ip, L);
         w.lo = lb_window(s, ip);
-        if (off >= 16) {
+        if (kGroup && far) {
+            ring_wr<kRing>(rb, op, m);
+            if (ml > 16) ring_wr<kRing>(rb, op + 16, m1);
+            if (ml > 32) ring_wr<kRing>(rb, op + 32, m2);
+            if (ml > 48) ring_wr<kRing>(rb, op + 48, m3);
+            for (int32_t k = 64; k < ml; k += 64) {
+                ring_flush<kRing>(rb, out, fl, op + k);
+                m = ld16(out + op + k - off);
+                if (k + 16 < ml) m1 = ld16(out + op + k + 16 - off);
+                if (k + 32 < ml) m2 = ld16(out + op + k + 32 - off);
+                if (k + 48 < ml) m3 = ld16(out + op + k + 48 - off);
+                ring_wr<kRing>(rb, op + k, m);
+                if (k + 16 < ml) ring_wr<kRing>(rb, op + k + 16, m1);
+                if (k + 32 < ml) ring_wr<kRing>(rb, op + k + 32, m2);
+                if (k + 48 < ml) ring_wr<kRing>(rb, op + k + 48, m3);
+            }
+        } else if (off >= 16) {
             ring_wr<kRing>(rb, op, m);
             for (int32_t k = 16; k < ml; k += 16) {
                 ring_flush<kRing>(rb, out, fl, op + k);
-                m = far ? ld16(out + op + k - off) : ring_rd<kRing>(rb, op + k - off);
+                m = far ? ld16(out + op + k - off) : (TYCHE_ABLATE & 256) ? (u128)0 : ring_rd<kRing>(rb, op + k - off);
                 ring_wr<kRing>(rb, op + k, m);
             }
         } else {

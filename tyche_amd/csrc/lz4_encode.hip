@@ -220,7 +220,7 @@ __device__ __forceinline__ void out_flush_all(const uint8_t *ring, OutRing &r, u
 // The sink of the default emission: n records (stream order) after the literal
 // run that starts at `anchor`; op counts the bytes already in dst.  Returns
 // false if the output would exceed cap.
-__device__ bool emit_staged(const uint2 *rec, uint32_t n, uint32_t anchor, const uint8_t *in, uint8_t *dst,
+__device__ __forceinline__ bool emit_staged(const uint2 *rec, uint32_t n, uint32_t anchor, const uint8_t *in, uint8_t *dst,
                             uint32_t &op, uint32_t cap, uint8_t *ring, OutRing &r, uint8_t *map, uint32_t lane) {
     const bool is_sel = lane < n;
     const uint2 rc = rec[is_sel ? lane : 0];

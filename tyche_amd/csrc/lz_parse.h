@@ -197,7 +197,7 @@ __host__ __device__ constexpr uint32_t table_slots() {
 template <int kWays>
 __device__ __forceinline__ uint32_t bucket_of(uint32_t v, uint32_t v2 = 0, uint32_t nbytes = 4) {
     constexpr uint32_t nb = table_slots<kWays>() / kWays;
-    constexpr uint32_t lg = nb >= 4096 ? 12 : nb >= 2048 ? 11 : nb >= 1024 ? 10 : 9;
+    constexpr uint32_t lg = nb >= 4096 ? 12 : nb >= 2048 ? 11 : nb >= 1024 ? 10 : nb >= 512 ? 9 : 8;
     static_assert((1u << lg) == nb, "bucket count is a power of two");
     if (nbytes > 4) {   // 5 or 6 bytes: zstd's fast parse hashes searchLength bytes (ZSTD_hashPtr)
         const uint64_t x = ((uint64_t)(v2 & (nbytes == 5 ? 0xFFu : 0xFFFFu)) << 32) | v;
@@ -214,7 +214,7 @@ __device__ __forceinline__ uint32_t bucket_of(uint32_t v, uint32_t v2 = 0, uint3
 template <bool kRepCand = false, bool kMin3 = false, int kWays = 1, typename Sink>
 __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *table, uint2 *rec, uint32_t lane,
                                       Sink &sink, uint32_t start = 0) {
-    static_assert(kWays == 1 || kWays == 2 || kWays == 4, "1, 2 or 4 ways");
+    static_assert(kWays == 1 || kWays == 2 || kWays == 4 || kWays == 8, "1, 2, 4 or 8 ways");
     uint32_t anchor = start;
     if (L < (uint32_t)(kMfLimit + 1) || start > L - kMfLimit) return start;
     const uint32_t mflimit = L - kMfLimit;          // last position a match may start
@@ -256,7 +256,7 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
             cands[kWays > 1 ? 1 : 0] = bk >> 16;
             __builtin_amdgcn_wave_barrier();
             T[h] = pos | (bk << 16);
-        } else {
+        } else if (kWays == 4) {
             uint2 *T = (uint2 *)table;
             const uint32_t h = kRepCand ? bucket_of<kWays>(v, pw.fw[0], TYCHE_HASH_BYTES)
                                         : bucket_of<kWays>(kMin3 && TYCHE_HASH3 ? v & 0xFFFFFFu : v);
@@ -267,6 +267,25 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
             cands[kWays > 3 ? 3 : 0] = bk.y >> 16;
             __builtin_amdgcn_wave_barrier();
             T[h] = make_uint2(pos | (bk.x << 16), (bk.x >> 16) | (bk.y << 16));
+        } else {
+            // 8 ways (deflate): a bucket is one aligned 16-byte LDS word of 8 positions, most
+            // recent first -- deflate_fast's chain of 4 over a 2^15-head table keeps more
+            // distinct candidates than 4 ways over 2^10 buckets (tools/parse_sim.c: 16 KiB
+            // pages 4.29 -> 4.35 in the cost model, zlib level 1's own parse 4.34)
+            uint4 *T = (uint4 *)table;
+            const uint32_t h = bucket_of<kWays>(kMin3 && TYCHE_HASH3 ? v & 0xFFFFFFu : v);
+            const uint4 bk = T[h];
+            cands[0] = bk.x & 0xFFFFu;
+            cands[kWays > 1 ? 1 : 0] = bk.x >> 16;
+            cands[kWays > 2 ? 2 : 0] = bk.y & 0xFFFFu;
+            cands[kWays > 3 ? 3 : 0] = bk.y >> 16;
+            cands[kWays > 4 ? 4 : 0] = bk.z & 0xFFFFu;
+            cands[kWays > 5 ? 5 : 0] = bk.z >> 16;
+            cands[kWays > 6 ? 6 : 0] = bk.w & 0xFFFFu;
+            cands[kWays > 7 ? 7 : 0] = bk.w >> 16;
+            __builtin_amdgcn_wave_barrier();
+            T[h] = make_uint4(pos | (bk.x << 16), (bk.x >> 16) | (bk.y << 16), (bk.y >> 16) | (bk.z << 16),
+                              (bk.z >> 16) | (bk.w << 16));
         }
         // ---- the candidate's window: 4-byte verify, forward probe (MINMATCH + up
         // to kProbe bytes) and backward probe (up to 4 bytes).  A candidate is a

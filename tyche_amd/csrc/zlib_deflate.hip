@@ -42,7 +42,7 @@
 #define TYCHE_ZLIB_MIN3 1
 #endif
 #ifndef TYCHE_ZLIB_WAYS
-#define TYCHE_ZLIB_WAYS 4   // candidates per hash bucket (lz_parse.h kWays)
+#define TYCHE_ZLIB_WAYS 8   // candidates per hash bucket (lz_parse.h kWays; 4 before round 3)
 #endif
 
 namespace tyche {
