@@ -292,6 +292,7 @@ def run_c4(args, info, dev):
     total = runner.sum_over_ranks(info, float(n))
     algo = n * plen + comp_bytes
     achieved = algo / (d_ms * 1e-3) / 1e9
+    traffic = pmc_traffic("lz4_decode", n, plen)
     result = {
         "metric": "GiB/s device-resident LZ4 decompress, 8M x 8 KiB pages split over the GPUs (BASELINE configs[3])",
         "value": round(total * plen * args.steps / elapsed / GIB, 3), "unit": "GiB/s", "n_gpus": info.world,
@@ -302,7 +303,9 @@ def run_c4(args, info, dev):
                    "total_pages": args.c4_pages, "pages_this_rank": n, "page_len": plen, "codec": "lz4",
                    "parallelism": f"page-range x{info.world}"},
         "roofline": {"bound": "hbm", "kernel": "lz4_decode", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": traffic["bytes"] if traffic else None,
+                     "traffic_source": traffic["source"] if traffic else None,
                      "algorithmic_bytes_per_launch": algo},
         "kernel_ms": {"lz4_decode": round(d_ms, 4)}, "ratio": round(n * plen / comp_bytes, 4),
     }

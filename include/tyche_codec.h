@@ -196,6 +196,10 @@ size_t tyche_plan_split(size_t n, const uint32_t *src_lengths, int ndev, uint64_
  * in-process override; for tests and A/B timing -- no knob changes a result. */
 int tyche_set_knob(const char *name, long value);
 int tyche_clear_knob(const char *name);
+/* Diagnostics: host-path stage clocks since the last call, then reset -- out[0..6] = ns waiting for
+ * streams, ns scattering, ns gathering, ns enqueuing, bytes gathered, bytes scattered, chunks.
+ * Returns the number of values written (at most n). */
+int tyche_host_profile(uint64_t *out, int n);
 /* message for the last TYCHE_E_DEVICE on this thread */
 const char *tyche_last_error(void);
 /* 1 if the library's gfx950 code object is usable on the calling thread's

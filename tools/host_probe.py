@@ -46,23 +46,36 @@ def main():
     slen = u32(*([plen] * n))
     ccap = u32(*([cap] * n))
     i32p = ctypes.POINTER(ctypes.c_int32)
+    def stages():
+        prof = (ctypes.c_uint64 * 8)()
+        lib.tyche_host_profile(prof, 8)
+        return {"stream_wait_ms": prof[0] / 3e6, "scatter_ms": prof[1] / 3e6, "gather_ms": prof[2] / 3e6,
+                "enqueue_ms": prof[3] / 3e6, "gather_gib": prof[4] / 3 / GIB, "scatter_gib": prof[5] / 3 / GIB,
+                "chunks": prof[6] // 3}
+
     for mb in chunks:
         _lib.set_knob("HOST_CHUNK_MB", mb)
-        bc = bd = float("inf")
+        nb = n * plen
+        stages()
+        bc = float("inf")
         for _ in range(3):
             t0 = time.perf_counter()
             _lib.check(lib.tyche_compress_host(1, 1, n, src_p, slen, comp_p, ccap, res.ctypes.data_as(i32p)), "c")
-            t1 = time.perf_counter()
-            clen = u32(*[int(x) for x in res])
-            t2 = time.perf_counter()
+            bc = min(bc, time.perf_counter() - t0)
+        sc = stages()
+        clen = u32(*[int(x) for x in res])
+        bd = float("inf")
+        for _ in range(3):
+            t0 = time.perf_counter()
             _lib.check(lib.tyche_decompress_host(1, n, comp_p, clen, out_p, slen, rv.ctypes.data_as(i32p)), "d")
-            t3 = time.perf_counter()
-            bc, bd = min(bc, t1 - t0), min(bd, t3 - t2)
+            bd = min(bd, time.perf_counter() - t0)
+        sd = stages()
         assert (rv == plen).all() and np.array_equal(out, host)
-        nb = n * plen
         print(json.dumps({"pages": n, "chunk_mb": mb, "compress_gib_s": round(nb / bc / GIB, 2),
                           "decompress_gib_s": round(nb / bd / GIB, 2),
-                          "combined_gib_s": round(nb / (bc + bd) / GIB, 2)}), flush=True)
+                          "combined_gib_s": round(nb / (bc + bd) / GIB, 2),
+                          "compress_ms": round(bc * 1e3, 2), "decompress_ms": round(bd * 1e3, 2),
+                          "compress_stages_per_call": sc, "decompress_stages_per_call": sd}), flush=True)
     _lib.clear_knob("HOST_CHUNK_MB")
     # host memcpy rate of the copy pool's work alone (numpy, one thread): scatter-sized copies
     a = np.ones(256 << 20, dtype=np.uint8)

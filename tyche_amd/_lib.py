@@ -119,6 +119,7 @@ SIGNATURES = {
     "tyche_active_devices": (ctypes.c_int, []),
     "tyche_plan_split": (ctypes.c_size_t, [ctypes.c_size_t, _u32p, ctypes.c_int, ctypes.c_uint64,
                                            ctypes.POINTER(ctypes.c_size_t)]),
+    "tyche_host_profile": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]),
     "tyche_set_knob": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_long]),
     "tyche_clear_knob": (ctypes.c_int, [ctypes.c_char_p]),
     "tyche_last_error": (ctypes.c_char_p, []),

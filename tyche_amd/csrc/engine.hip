@@ -671,6 +671,21 @@ class CopyPool {
 
 std::atomic<int> g_inflight[kMaxDevices];   // host batches running per device
 
+// run_host_batch's direct_out modes (see there)
+enum { kDirectNone = 0, kDirectAlways = 1, kDirectLz4Decode = 2 };
+
+// Host-path stage clocks (diagnostics, tyche_host_profile): ns spent by calling threads waiting for a
+// slot's stream, scattering results, gathering inputs, and enqueuing copies and kernels; bytes gathered
+// and scattered.
+enum { kHpWait, kHpScatter, kHpGather, kHpEnqueue, kHpGatherBytes, kHpScatterBytes, kHpChunks, kHpCount };
+std::atomic<uint64_t> g_hprof[kHpCount];
+struct HpClock {
+    int slot;
+    uint64_t t0;
+    explicit HpClock(int s) : slot(s), t0(now_ns()) {}
+    ~HpClock() { g_hprof[slot] += now_ns() - t0; }
+};
+
 // Moves n host pages through `launch` on device dev, chunk by chunk (see
 // above).  results[i] gets the kernel's per-page result; for results in
 // (0, dst_cap[i]] that many output bytes land in dst[i].  On any failure the
@@ -689,7 +704,7 @@ size_t zero_copy_bytes() { return (size_t)std::max(0L, knob("ZERO_COPY_BYTES", 4
 template <typename Launch>
 int run_host_batch(int dev, size_t n, const void *const *src, const uint32_t *src_len, void *const *dst,
                    const uint32_t *dst_cap, int32_t *results, Launch launch, bool zc_ok = false,
-                   bool direct_out = false) {
+                   int direct_out = kDirectNone) {
     DeviceGuard keep;   // the caller's device is current again on every return
     int rc = ensure_device(dev);
     if (rc) return rc;
@@ -713,17 +728,27 @@ int run_host_batch(int dev, size_t n, const void *const *src, const uint32_t *sr
     auto finish = [&](Slot &S) -> int {
         if (!S.busy) return TYCHE_E_OK;
         S.busy = false;
-        if ((e = hipStreamSynchronize(S.stream)) != hipSuccess) return fail("hipStreamSynchronize", e);
+        {
+            HpClock hc(kHpWait);
+            if ((e = hipStreamSynchronize(S.stream)) != hipSuccess) return fail("hipStreamSynchronize", e);
+        }
+        HpClock hc(kHpScatter);
         const size_t k = S.count;
         const uint64_t *m_doff = (const uint64_t *)S.h_meta.p + k;
         const int32_t *m_res = (const int32_t *)((const uint8_t *)S.h_meta.p + k * 24);
         const uint8_t *hout = (const uint8_t *)S.h_out.p;
         const size_t f0 = S.first;
+        std::atomic<uint64_t> moved{0};
         pool.run(k, [&](size_t j) {
             const int32_t r = m_res[j];
             results[f0 + j] = r;
-            if (r > 0 && (uint32_t)r <= dst_cap[f0 + j]) memcpy(dst[f0 + j], hout + m_doff[j], (size_t)r);
+            if (r > 0 && (uint32_t)r <= dst_cap[f0 + j]) {
+                memcpy(dst[f0 + j], hout + m_doff[j], (size_t)r);
+                moved.fetch_add((uint64_t)r, std::memory_order_relaxed);
+            }
         });
+        g_hprof[kHpScatterBytes] += moved.load();
+        g_hprof[kHpChunks]++;
         return TYCHE_E_OK;
     };
 
@@ -833,9 +858,14 @@ int run_host_batch(int dev, size_t n, const void *const *src, const uint32_t *sr
             dof += up16(dst_cap[first + j]);
         }
         uint8_t *hin = (uint8_t *)S.h_in.p;
-        pool.run(k, [&](size_t j) {
-            if (m_slen[j]) memcpy(hin + m_soff[j], src[first + j], m_slen[j]);
-        });
+        {
+            HpClock hc(kHpGather);
+            pool.run(k, [&](size_t j) {
+                if (m_slen[j]) memcpy(hin + m_soff[j], src[first + j], m_slen[j]);
+            });
+            g_hprof[kHpGatherBytes] += so;
+        }
+        HpClock enq(kHpEnqueue);
         // ---- H2D -> kernel -> D2H on the slot's stream
         uint8_t *dmeta = (uint8_t *)S.d_meta.p;
         const size_t head_bytes = (uint8_t *)m_res - (uint8_t *)m_soff;
@@ -852,10 +882,15 @@ int run_host_batch(int dev, size_t n, const void *const *src, const uint32_t *sr
         b.src_offsets = (const uint64_t *)dmeta;
         b.src_lengths = (const uint32_t *)(dmeta + ((uint8_t *)m_slen - (uint8_t *)m_soff));
         b.max_src_length = max_in;
-        // direct_out (LZ4 compress): the kernel writes its streams straight into the pinned
-        // arena over PCIe, so only the compressed bytes cross the link -- a D2H of the arena
-        // would move every page's full capacity (16 KiB+ per 16 KiB page at ratio 2.6)
-        const bool direct = direct_out && S.h_out.dp != nullptr;
+        // direct_out: the kernel writes its results straight into the pinned arena over PCIe, as
+        // posted writes that overlap its own work, and no D2H of the arena follows.  LZ4 compress
+        // (kDirectAlways): only the compressed bytes cross the link -- a D2H of the arena would move
+        // every page's full capacity (16 KiB+ per 16 KiB page at ratio 2.6).  LZ4 decompress
+        // (kDirectLz4Decode): the jump and wave decoders write each page once, whole, from LDS; the
+        // lane decoder (chunks of >= kLaneMin pages) reads its own output back, so it keeps the D2H.
+        const bool direct = S.h_out.dp != nullptr &&
+                            (direct_out == kDirectAlways ||
+                             (direct_out == kDirectLz4Decode && !lz4_lane_decode_wanted(k, max_in, max_out)));
         b.dst = direct ? S.h_out.dp : S.d_out.p;
         b.dst_offsets = (const uint64_t *)(dmeta + ((uint8_t *)m_doff - (uint8_t *)m_soff));
         b.dst_capacities = (const uint32_t *)(dmeta + ((uint8_t *)m_dcap - (uint8_t *)m_soff));
@@ -915,7 +950,7 @@ int pick_device(const std::vector<int> &ids) {
 // restores) spread over all devices.
 template <typename Launch>
 int run_host(size_t n, const void *const *src, const uint32_t *src_len, void *const *dst, const uint32_t *dst_cap,
-             int32_t *results, Launch launch, bool zc_ok = false, bool direct_out = false) {
+             int32_t *results, Launch launch, bool zc_ok = false, int direct_out = kDirectNone) {
     if (t_device >= 0) return run_host_batch(t_device, n, src, src_len, dst, dst_cap, results, launch, zc_ok, direct_out);
     if (rank_device() >= 0)   // one process per GPU: its own device only
         return run_host_batch(rank_device(), n, src, src_len, dst, dst_cap, results, launch, zc_ok, direct_out);
@@ -950,6 +985,12 @@ int run_host(size_t n, const void *const *src, const uint32_t *src_len, void *co
 extern "C" {
 
 // ------------------------------------------------------------------ runtime
+int tyche_host_profile(uint64_t *out, int n) {
+    const int k = std::min(n, (int)kHpCount);
+    for (int i = 0; i < k; i++) out[i] = g_hprof[i].exchange(0);
+    return k;
+}
+
 int tyche_set_knob(const char *name, long value) {
     if (!name || !*name) return TYCHE_E_BAD_ARGS;
     KnobTable &T = knob_table();
@@ -1086,7 +1127,7 @@ int tyche_compress_host(int compressor_id, int compressor_level, size_t n, const
         if (src_lengths[i] > 65535u) { t_error = "pages above 64 KiB are not supported by the device encoders"; return TYCHE_E_BAD_ARGS; }
     // LZ4's encoders only store to their destination (never read it back), so their streams may go
     // straight into the pinned staging arena (HOST_DIRECT_OUT=0: stage through HBM and D2H instead)
-    const bool direct = compressor_id == TYCHE_LZ4_COMPRESSOR_ID && knob("HOST_DIRECT_OUT", 1) != 0;
+    const int direct = compressor_id == TYCHE_LZ4_COMPRESSOR_ID && knob("HOST_DIRECT_OUT", 1) ? kDirectAlways : kDirectNone;
     return run_host(n, src, src_lengths, dst, dst_capacities, results,
                           [compressor_id](const tyche_batch_t &b, hipStream_t s) {
                               return launch_encode(compressor_id, b, std::max(b.max_src_length, 1u), s);
@@ -1110,7 +1151,7 @@ int tyche_decompress_host(int compressor_id, size_t n, const void *const *src, c
     return run_host(n, src, src_lengths, dst, dst_capacities, results,
                           [](const tyche_batch_t &b, hipStream_t s) {
                               return launch_lz4_decode(b, b.max_src_length, b.dst_capacity, s);
-                          }, true);
+                          }, true, knob("HOST_DIRECT_OUT", 1) ? kDirectLz4Decode : kDirectNone);
 }
 
 // ------------------------------------------------------- Buffer entry points

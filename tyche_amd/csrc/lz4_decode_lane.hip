@@ -491,7 +491,7 @@ __device__ __forceinline__ void lb_reach(LineBuf &s, const uint8_t *__restrict__
 __device__ __forceinline__ u128 lb_window(const LineBuf &s, int32_t ip) { return lds16(s.sb + (ip - s.lb + 16)); }
 
 template <int32_t kRing>
-__device__ int32_t decode_ring_lb(const uint8_t *__restrict__ in, int32_t L, uint8_t *__restrict__ out, int32_t C,
+__device__ __forceinline__ int32_t decode_ring_lb(const uint8_t *__restrict__ in, int32_t L, uint8_t *__restrict__ out, int32_t C,
                                   uint8_t *rb, uint8_t *sb) {
     if (C == 0) return (L == 1 && ld1(in) == 0) ? 0 : -1;
     if (L <= 0) return -1;
@@ -553,42 +553,15 @@ __device__ int32_t decode_ring_lb(const uint8_t *__restrict__ in, int32_t L, uin
         }
         ml += kMinMatch;
         if (op + ml > C - kLastLiterals) return -(ip + pos) - 1;   // lz4.c:1225
-        // as decode_ring: far sources are already in HBM (64: timing-only ablation, far reads from the ring)
+        // as decode_ring: far sources are already in HBM (64: timing-only ablation, far reads from the ring).
+        // (Round 3 tried fetching a far match's first 64 bytes together instead of one 16-byte load per
+        // step: 36.7 vs 33.5 ms per 1M pages -- the loads' count, not their latency, is what costs.)
         const bool far = (TYCHE_ABLATE & (64 | 256)) ? false : off > kRing - 32;
-        // A far match's first 64 bytes are fetched together (one wait, not one per 16 bytes: the wave
-        // waits for its slowest lane, and a long far match serialized its loads while 63 lanes idled).
-        // Their sources end at or before op + 64 - (kRing - 31) <= op - 96 (kRing >= 192), and the
-        // unflushed tail is < 80 bytes, so they are in HBM; the ring holds the < 144 unflushed bytes.
-        constexpr bool kGroup = kRing >= 192;
-        u128 m = 0, m1 = 0, m2 = 0, m3 = 0;
-        if (far) {
-            m = ld16(out + op - off);
-            if (kGroup && ml > 16) m1 = ld16(out + op + 16 - off);
-            if (kGroup && ml > 32) m2 = ld16(out + op + 32 - off);
-            if (kGroup && ml > 48) m3 = ld16(out + op + 48 - off);
-        } else if (!(TYCHE_ABLATE & 256)) {
-            m = ring_rd<kRing>(rb, op - off);
-        }
+        u128 m = far ? ld16(out + op - off) : (TYCHE_ABLATE & 256) ? (u128)0 : ring_rd<kRing>(rb, op - off);
         ip += pos;
         lb_reach(s, in, ip, L);
         w.lo = lb_window(s, ip);
-        if (kGroup && far) {
-            ring_wr<kRing>(rb, op, m);
-            if (ml > 16) ring_wr<kRing>(rb, op + 16, m1);
-            if (ml > 32) ring_wr<kRing>(rb, op + 32, m2);
-            if (ml > 48) ring_wr<kRing>(rb, op + 48, m3);
-            for (int32_t k = 64; k < ml; k += 64) {
-                ring_flush<kRing>(rb, out, fl, op + k);
-                m = ld16(out + op + k - off);
-                if (k + 16 < ml) m1 = ld16(out + op + k + 16 - off);
-                if (k + 32 < ml) m2 = ld16(out + op + k + 32 - off);
-                if (k + 48 < ml) m3 = ld16(out + op + k + 48 - off);
-                ring_wr<kRing>(rb, op + k, m);
-                if (k + 16 < ml) ring_wr<kRing>(rb, op + k + 16, m1);
-                if (k + 32 < ml) ring_wr<kRing>(rb, op + k + 32, m2);
-                if (k + 48 < ml) ring_wr<kRing>(rb, op + k + 48, m3);
-            }
-        } else if (off >= 16) {
+        if (off >= 16) {
             ring_wr<kRing>(rb, op, m);
             for (int32_t k = 16; k < ml; k += 16) {
                 ring_flush<kRing>(rb, out, fl, op + k);
@@ -717,10 +690,11 @@ hipError_t launch_lz4_decode_lane(const tyche_batch_t &b, uint32_t in_cap, uint3
     const long lbuf = knob("LZ4_LANE_LB", 0);
     if (ring && lbuf) {
         const void *k = ring == 128   ? (const void *)lz4_decode_ringlb_kernel<128>
+                        : ring == 160 ? (const void *)lz4_decode_ringlb_kernel<160>
                         : ring == 192 ? (const void *)lz4_decode_ringlb_kernel<192>
                         : ring == 224 ? (const void *)lz4_decode_ringlb_kernel<224>
                                       : (const void *)lz4_decode_ringlb_kernel<256>;
-        const int32_t rbytes = ring == 128 ? 128 : ring == 192 ? 192 : ring == 224 ? 224 : 256;
+        const int32_t rbytes = ring == 128 ? 128 : ring == 160 ? 160 : ring == 192 ? 192 : ring == 224 ? 224 : 256;
         const size_t lds = 64 * (size_t)(rbytes + 48 + 80);
         const size_t ncu = prepare_launch(k);
         size_t waves = waves_per_cu(k, lds);

@@ -183,7 +183,10 @@ constexpr uint32_t kOutRing = 1024;   // bytes; head is always a multiple of 256
 #ifndef TYCHE_LIT_LANE
 #define TYCHE_LIT_LANE 8
 #endif
-constexpr uint32_t kLitLane = TYCHE_LIT_LANE;   // literal bytes a sequence's lane copies itself (emit_staged)
+constexpr uint32_t kLitLane = TYCHE_LIT_LANE;
+#ifndef TYCHE_LIT_GATHER
+#define TYCHE_LIT_GATHER 1
+#endif   // literal bytes a sequence's lane copies itself (emit_staged)
 struct OutRing {
     uint32_t head, pend;   // wave-uniform: ring position of the first unflushed byte, unflushed bytes
 };
@@ -259,7 +262,22 @@ __device__ __forceinline__ bool emit_staged(const uint2 *rec, uint32_t n, uint32
         // batch's longest run kept every other lane idle (the sink was 56 % of
         // the parse's cycles, tools/phase_prof.py)
         const uint32_t ls = min(lit, kLitLane);
+#if TYCHE_LIT_GATHER
+        // the run's first 8 bytes from three aligned dwords (the staged page has 64 zero bytes of
+        // padding), then up to 8 byte stores that wait on nothing: the byte-at-a-time copy put one
+        // LDS read latency per literal byte on the sink's critical path
+        static_assert(kLitLane == 8, "two gathered dwords");
+        const uint32_t ib = (uint32_t)(uintptr_t)in & 3u;
+        const uint32_t *A = (const uint32_t *)(in - ib);
+        const uint32_t q0 = lstart + ib, i0 = q0 >> 2, sh = q0 & 3u;
+        const uint32_t d0 = A[i0], d1 = A[i0 + 1], d2 = A[i0 + 2];
+        const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, sh), w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+#pragma unroll
+        for (uint32_t t = 0; t < 8; t++)
+            if (t < ls) ring[(q_lit + t) & m] = (uint8_t)((t < 4 ? w0 : w1) >> (8 * (t & 3u)));
+#else
         for (uint32_t t = 0; t < ls; t++) ring[(q_lit + t) & m] = in[lstart + t];
+#endif
         q = q_lit + lit;
         ring[q & m] = (uint8_t)off;
         ring[(q + 1) & m] = (uint8_t)(off >> 8);
