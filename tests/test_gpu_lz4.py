@@ -293,6 +293,33 @@ def test_decode_lane_path_fixtures(tc, target):
             assert hashlib.sha256(outs[j]).digest() == want_dig[i], (j, i)
 
 
+@pytest.mark.parametrize("lb,ring", [(1, 128), (1, 160), (1, 192), (1, 256), (0, 256), (0, 128)])
+def test_decode_lane_kernels_all_rings(tc, oracle_mod, knobs, lb, ring):
+    """Every lane-per-page kernel variant (LZ4_LANE_LB=1: the stream through a per-lane line buffer,
+    the default, at each ring size; 0: the round-2 ring kernel), selected in-process with
+    tyche_set_knob and forced on every batch size (LZ4_LANE_MIN=0): the fixtures with their exact
+    return values, and seeded corruptions against the restated LZ4_decompress_safe."""
+    knobs(LZ4_LANE_LB=lb, LZ4_LANE_RING=ring, LZ4_LANE_MIN=0)
+    test_decode_lane_path_fixtures(tc, 1)
+    rng = np.random.default_rng(1000 + ring + lb)
+    pages = oracle_mod.pagegen(256, 16384, seed=9, first=ring, dist=0)
+    streams, caps = [], []
+    for i in range(256):
+        c = bytearray(oracle_mod.lz4_compress(pages[i].tobytes()))
+        if i % 4 == 1:
+            c[int(rng.integers(0, len(c)))] ^= 1 << int(rng.integers(0, 8))
+        elif i % 4 == 2:
+            c = c[: int(rng.integers(1, len(c)))]
+        streams.append(bytes(c))
+        caps.append(16384 if i % 4 != 3 else int(rng.integers(100, 16384)))
+    rv, outs = ragged_decode(tc, streams, caps)
+    for i in range(256):
+        r, want = oracle_mod.lz4_decompress(streams[i], caps[i])
+        assert rv[i] == r, (i, rv[i], r)
+        if r > 0 and i % 4 in (0, 3):   # untouched streams (a flipped one may hold an offset-0 match: undefined bytes)
+            assert outs[i][:r] == want[:r], i
+
+
 @pytest.mark.parametrize("dist", [0, 1, 2, 3, 4, 5])
 def test_decode_lane_path_roundtrip(tc, dist):
     """64K x 4 KiB pages of every pagegen distribution through the lane-per-page decoder."""

@@ -26,13 +26,15 @@ from collections import defaultdict
 # codec call -> the kernel symbols its dispatches carry (the split zstd codec runs several
 # kernels per chunk of pages and several chunks per call: give --calls for it)
 KERNELS = {"lz4_encode": ("lz4_encode_",), "lz4_decode": ("lz4_decode_",),
-           "zstd_encode": ("zstd_encode_kernel", "zstd_block_kernel", "zstd_fse_kernel", "zstd_pack_kernel"),
+           "zstd_encode": ("zstd_encode_kernel", "zstd_parse_split_kernel", "zstd_block_kernel", "zstd_fse_kernel",
+                           "zstd_pack_kernel"),
            "zstd_decode": ("zstd_decode_kernel", "zstd_entropy_kernel", "zstd_seq_kernel", "zstd_exec_kernel"),
            "zlib_encode": ("zlib_deflate_kernel",), "zlib_decode": ("zlib_inflate_kernel",)}
 
 
 # read-byte factor per FETCH_SIZE byte, by kernel symbol (see the module docstring)
-SCATTERED = ("lz4_decode_ring_kernel", "lz4_decode_lane_kernel", "zstd_seq_kernel", "zstd_fse_kernel")
+SCATTERED = ("lz4_decode_ring_kernel", "lz4_decode_ringlb_kernel", "lz4_decode_lane_kernel", "zstd_seq_kernel",
+             "zstd_fse_kernel")
 
 
 def per_dispatch(path, counter):

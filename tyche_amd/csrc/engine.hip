@@ -31,6 +31,8 @@
 
 #include "engine.h"
 
+#include <immintrin.h>
+
 using namespace tyche;
 
 namespace {
@@ -191,6 +193,7 @@ tyche::ScratchLease::ScratchLease(hipStream_t s, size_t bytes) : s_(s) {
             return;
         }
         P.e.push_back(x);
+        take = P.e.size() - 1;   // pool_trim may have erased entries: the new one is the last
     }
     P.e[take].state = 1;
     dev_ = dev;
@@ -457,8 +460,8 @@ struct Arena {
     }
 };
 
-constexpr int kSlots = 3;
-constexpr size_t kChunkBytes = size_t(64) << 20;
+constexpr int kSlots = 4;   // round 3: 4 x 32 MiB (was 3 x 64 MiB): the host path waited on streams ~30 % of a call
+constexpr size_t kChunkBytes = size_t(32) << 20;
 constexpr int kContextsPerDevice = 8;
 
 struct Slot {
@@ -582,6 +585,34 @@ void release_ctx(int dev, HostCtx *c) {
 
 inline size_t up16(size_t x) { return (x + 15) & ~size_t(15); }
 
+// Page copies between malloc'd Buffers and the pinned staging arenas.  The host
+// path is bound by these copies (r03 stage clocks: gather + scatter ~10 of the
+// 15 ms of a 32K-page decompress call), and a plain memcpy of a 16 KiB page
+// reads its destination's lines before writing them (read-for-ownership): three
+// DRAM transfers per byte.  Non-temporal 16-byte stores skip that read; the
+// caller of a pool job fences once at its end (copy_fence) before handing the
+// arena to a DMA or the caller.
+inline void copy_nt(void *dst, const void *src, size_t n) {
+    if (n < 512 || ((uintptr_t)dst & 15u)) {
+        memcpy(dst, src, n);
+        return;
+    }
+    __m128i *d = (__m128i *)dst;
+    const __m128i *p = (const __m128i *)src;
+    size_t k = n >> 6;
+    for (; k; k--, d += 4, p += 4) {
+        const __m128i a = _mm_loadu_si128(p), b = _mm_loadu_si128(p + 1), c = _mm_loadu_si128(p + 2),
+                      e = _mm_loadu_si128(p + 3);
+        _mm_stream_si128(d, a);
+        _mm_stream_si128(d + 1, b);
+        _mm_stream_si128(d + 2, c);
+        _mm_stream_si128(d + 3, e);
+    }
+    const size_t done = n & ~(size_t)63;
+    if (done < n) memcpy((uint8_t *)dst + done, (const uint8_t *)src + done, n - done);
+}
+inline void copy_fence() { _mm_sfence(); }
+
 // A persistent worker pool for the host-side page copies (memcpy of scattered
 // malloc'd pages into and out of pinned staging).  Several callers (one per
 // device of a fanned-out batch, concurrent tyche threads) may run jobs at once:
@@ -599,10 +630,12 @@ class CopyPool {
     void run(size_t n, F f) {
         if (n < 64 || workers_.empty()) {
             for (size_t i = 0; i < n; i++) f(i);
+            copy_fence();
             return;
         }
         std::function<void(size_t, size_t)> body = [&f](size_t a, size_t b) {
             for (size_t i = a; i < b; i++) f(i);
+            copy_fence();   // the job's non-temporal stores are globally visible before it completes
         };
         Job j;
         j.body = &body;
@@ -670,6 +703,7 @@ class CopyPool {
 };
 
 std::atomic<int> g_inflight[kMaxDevices];   // host batches running per device
+
 
 // run_host_batch's direct_out modes (see there)
 enum { kDirectNone = 0, kDirectAlways = 1, kDirectLz4Decode = 2 };
@@ -743,7 +777,7 @@ int run_host_batch(int dev, size_t n, const void *const *src, const uint32_t *sr
             const int32_t r = m_res[j];
             results[f0 + j] = r;
             if (r > 0 && (uint32_t)r <= dst_cap[f0 + j]) {
-                memcpy(dst[f0 + j], hout + m_doff[j], (size_t)r);
+                copy_nt(dst[f0 + j], hout + m_doff[j], (size_t)r);
                 moved.fetch_add((uint64_t)r, std::memory_order_relaxed);
             }
         });
@@ -784,7 +818,7 @@ int run_host_batch(int dev, size_t n, const void *const *src, const uint32_t *sr
                 }
                 uint8_t *hin = (uint8_t *)S.h_in.p;
                 pool.run(n, [&](size_t j) {
-                    if (m_slen[j]) memcpy(hin + m_soff[j], src[j], m_slen[j]);
+                    if (m_slen[j]) copy_nt(hin + m_soff[j], src[j], m_slen[j]);
                 });
                 uint8_t *dm = (uint8_t *)S.h_meta.dp;
                 tyche_batch_t b{};
@@ -808,7 +842,7 @@ int run_host_batch(int dev, size_t n, const void *const *src, const uint32_t *sr
                 pool.run(n, [&](size_t j) {
                     const int32_t r = m_res[j];
                     results[j] = r;
-                    if (r > 0 && (uint32_t)r <= dst_cap[j]) memcpy(dst[j], hout + m_doff[j], (size_t)r);
+                    if (r > 0 && (uint32_t)r <= dst_cap[j]) copy_nt(dst[j], hout + m_doff[j], (size_t)r);
                 });
                 release_ctx(dev, cp);
                 return TYCHE_E_OK;
@@ -861,7 +895,7 @@ int run_host_batch(int dev, size_t n, const void *const *src, const uint32_t *sr
         {
             HpClock hc(kHpGather);
             pool.run(k, [&](size_t j) {
-                if (m_slen[j]) memcpy(hin + m_soff[j], src[first + j], m_slen[j]);
+                if (m_slen[j]) copy_nt(hin + m_soff[j], src[first + j], m_slen[j]);
             });
             g_hprof[kHpGatherBytes] += so;
         }
@@ -912,7 +946,7 @@ int run_host_batch(int dev, size_t n, const void *const *src, const uint32_t *sr
 }
 
 // minimum input bytes per device before a host batch is split across devices
-uint64_t fanout_min_bytes() { return (uint64_t)std::max(0L, knob("FANOUT_MIN_BYTES", (long)kChunkBytes)); }
+uint64_t fanout_min_bytes() { return (uint64_t)std::max(0L, knob("FANOUT_MIN_BYTES", 64L << 20)); }
 
 // A process launched one per GPU (torch.distributed.run sets WORLD_SIZE and
 // LOCAL_RANK) keeps its host work on its own device -- LOCAL_RANK modulo the

@@ -686,8 +686,11 @@ constexpr int kDefaultWin = 16;
 hipError_t launch_lz4_decode_lane(const tyche_batch_t &b, uint32_t in_cap, uint32_t out_cap, hipStream_t s) {
     if (b.count == 0) return hipSuccess;
     const long env_waves = knob("LZ4_LANE_WAVES", 0);
-    const long ring = knob("LZ4_LANE_RING", kDefaultRing);
-    const long lbuf = knob("LZ4_LANE_LB", 0);
+    // line-buffered stream (round 3, default): 128-byte rings, 10 waves per CU -- 32.7 vs 34.3 ms per
+    // 1M x 16 KiB pages for the ring kernel's 256-byte rings (r03 lane timing; 160 / 192-byte rings
+    // 33.5 / 33.6)
+    const long lbuf = knob("LZ4_LANE_LB", 1);
+    const long ring = knob("LZ4_LANE_RING", lbuf ? 128 : kDefaultRing);
     if (ring && lbuf) {
         const void *k = ring == 128   ? (const void *)lz4_decode_ringlb_kernel<128>
                         : ring == 160 ? (const void *)lz4_decode_ringlb_kernel<160>

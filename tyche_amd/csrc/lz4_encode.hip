@@ -553,6 +553,222 @@ __global__ __launch_bounds__(128, 3) void lz4_encode_split_kernel(tyche_batch_t 
     }
 }
 
+// ---- N-wave split encoder (round 3, the default for pages >= kSplitMin).
+//
+// The two-wave kernel above runs 12 waves per CU; its counters (r03 PMC) show
+// the waves waiting ~42 % of their cycles with no unit saturated (VALU ~35 %,
+// the CU's scalar unit ~42 %): latency-bound.  Here kNW waves share one staged
+// page, wave w parsing part [b_w, b_{w+1}) with b_w = (w L / kNW) rounded down
+// to 64; every wave but the first seeds its table with the kSeed positions
+// before its part (block order, as the one-wave parse would have inserted
+// them; the 2^10-slot table holds little older than that anyway) and holds back
+// its first sequence.  Matches of part w end by b_{w+1} (its parse sees
+// L' = b_{w+1} + LASTLITERALS).  After a barrier wave 0 lays out the page:
+// part 0's stream (already in dst), then for each later part the joint
+// sequence (literals from the previous part's last match end, then the part's
+// held-back first match), then the part's stream from its scratch; a part with
+// no match joins the literal run.  The waves then copy their streams into place.
+// Per page LDS: header + kNW x (table, map, records, ring) + the stage: 31.5 KiB
+// for 4 waves at 16 KiB pages, 5 pages (20 waves) per CU by LDS.
+#ifndef TYCHE_LZ4_SEED
+#define TYCHE_LZ4_SEED 4096   // positions seeded before a part (a multiple of 64)
+#endif
+constexpr uint32_t kSeed = TYCHE_LZ4_SEED;
+template <uint32_t kNW>
+struct SplitHdrN {
+    uint32_t next_lo, next_hi, next2_lo, next2_hi;
+    int32_t result;
+    uint32_t pad0[3];
+    uint32_t len[kNW];        // bytes of part w's stream (part 0: in dst, the rest in their scratch)
+    uint32_t cursor[kNW];     // end of part w's last match (its parse's final anchor)
+    uint32_t has_first[kNW];  // part w > 0: its first record was held back
+    uint32_t ok[kNW];         // part 0: its emission fit the capacity
+    uint32_t seg[kNW];        // part w > 0: its stream's offset in dst
+    uint2 first[kNW];         // part w > 0: the held-back record
+};
+template <uint32_t kNW>
+constexpr size_t split_hdr_bytes() { return (sizeof(SplitHdrN<kNW>) + 63) & ~(size_t)63; }
+template <uint32_t kNW>
+constexpr size_t split_stage_off() { return split_hdr_bytes<kNW>() + kNW * kWaveRegion; }
+template <uint32_t kNW>
+__host__ __device__ constexpr uint32_t part_scratch(uint32_t in_cap) {   // a part's worst-case stream, 256-aligned
+    return (lz4_bound(in_cap / kNW + 2u * kWave) + 64u + 255u) & ~255u;
+}
+template <uint32_t kNW>
+constexpr uint32_t split_prefetch() { return (16384u / 16u + kNW * kWave - 1u) / (kNW * kWave); }   // 16 KiB per page
+
+template <uint32_t kNW>
+__global__ __launch_bounds__(kNW * 64) void lz4_encode_splitn_kernel(tyche_batch_t b, uint32_t in_cap, unsigned *ctr,
+                                                                     uint8_t *ws, uint32_t ws_stride, uint32_t seed) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    constexpr uint32_t kT = kNW * kWave;                 // threads per page
+    constexpr uint32_t kPf = split_prefetch<kNW>();       // 16-byte vectors per thread prefetched
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t wave = rfl(tid >> 6);
+    SplitHdrN<kNW> *hdr = (SplitHdrN<kNW> *)smem;
+    uint8_t *region = smem + split_hdr_bytes<kNW>() + wave * kWaveRegion;
+    uint16_t *table = (uint16_t *)region;
+    uint8_t *map = region + kHashSize * sizeof(uint16_t);
+    uint2 *rec = (uint2 *)(map + 4 * kWave);
+    uint4 *fld = (uint4 *)(rec + kWave);
+    uint8_t *ring = (uint8_t *)fld;
+    uint8_t *stage = smem + split_stage_off<kNW>();
+    const uint32_t part_ws = part_scratch<kNW>(in_cap);
+    uint8_t *scratch = ws + (size_t)blockIdx.x * ws_stride + (size_t)(wave ? wave - 1u : 0u) * part_ws;
+
+    size_t page = blockIdx.x;
+    if (page >= b.count) return;
+    PageRef p = batch_page(b, page);
+    uint32_t head = stage_in(p.src, p.src_len <= in_cap ? p.src_len : 0, stage, tid, kT);
+    if (tid == 0) {
+        const size_t nx = (size_t)atomicAdd(ctr, 1u) + gridDim.x;   // dynamic assignment (engine.h)
+        hdr->next_lo = (uint32_t)nx;
+        hdr->next_hi = (uint32_t)(nx >> 32);
+    }
+    for (;;) {
+        for (uint32_t w = lane; w < kHashSize / 8; w += kWave) ((u32x4 *)table)[w] = u32x4{0, 0, 0, 0};
+        if (tid < kWave) stage[head + p.src_len + tid] = 0;
+        __syncthreads();
+        const size_t next = (size_t)rfl(hdr->next_lo) | ((size_t)rfl(hdr->next_hi) << 32);
+        PageRef pn;
+        u32x4 pf[kPf];
+        uint32_t nhead = 0, nvec = 0;
+        if (next < b.count) {
+            pn = batch_page(b, next);
+            if (pn.src_len <= in_cap && pn.src_len > 0) {
+                const uintptr_t a = (uintptr_t)pn.src;
+                nhead = (uint32_t)(a & 15u);
+                nvec = (nhead + pn.src_len + 15u) >> 4;
+                const u32x4 *g = (const u32x4 *)(a - nhead);
+#pragma unroll
+                for (uint32_t k = 0; k < kPf; k++) pf[k] = gload_nt(g + min(tid + k * kT, nvec - 1u));
+            }
+        }
+        const uint8_t *in = stage + head;
+        const uint32_t L = p.src_len;
+        const bool fits = L <= in_cap;
+        const uint32_t b0 = wave == 0 ? 0u : ((L * wave) / kNW) & ~(kWave - 1u);
+        const uint32_t b1 = wave + 1 == kNW ? L : ((L * (wave + 1)) / kNW) & ~(kWave - 1u);
+        const uint32_t Lp = wave + 1 == kNW ? L : b1 + kLastLiterals;   // part w's matches end by b1
+        if (fits) {
+            if (wave == 0) {
+                uint32_t op = 0;
+                OutRing r{0u, 0u};
+                auto sink = [&](const uint2 *rr, uint32_t n, uint32_t anchor) -> bool {
+                    return emit_staged(rr, n, anchor, in, p.dst, op, p.dst_cap, ring, r, map, lane);
+                };
+                const uint32_t cur = lzp::parse_page(in, Lp, table, rec, lane, sink);
+                const bool ok = cur != 0xFFFFFFFFu;
+                if (ok) out_flush_all(ring, r, p.dst, op, lane);
+                if (lane == 0) {
+                    hdr->ok[0] = ok ? 1u : 0u;
+                    hdr->len[0] = op;
+                    hdr->cursor[0] = ok ? cur : 0u;
+                    const size_t nx = (size_t)atomicAdd(ctr, 1u) + gridDim.x;
+                    hdr->next2_lo = (uint32_t)nx;
+                    hdr->next2_hi = (uint32_t)(nx >> 32);
+                }
+            } else {
+                // the positions before the part, in block order (later blocks overwrite earlier ones)
+                const uint32_t ib = (uint32_t)(uintptr_t)in & 3u;
+                const uint32_t *A = (const uint32_t *)(in - ib);
+                for (uint32_t blk = b0 > seed ? b0 - seed : 0u; blk < b0; blk += kWave) {
+                    const uint32_t pos = blk + lane;
+                    table[lzp::hash4(lzp::lds_word(A, pos + ib))] = (uint16_t)pos;
+                    __builtin_amdgcn_wave_barrier();
+                }
+                uint32_t op = 0;
+                OutRing r{0u, 0u};
+                bool first = true;
+                if (lane == 0) hdr->has_first[wave] = 0;
+                auto sink = [&](const uint2 *rr, uint32_t n, uint32_t anchor) -> bool {
+                    if (first) {
+                        first = false;
+                        if (lane == 0) {
+                            hdr->first[wave] = rr[0];
+                            hdr->has_first[wave] = 1;
+                        }
+                        if (n == 1) return true;
+                        const uint32_t a = (rr[0].x & 0xFFFFu) + (rr[0].y & 0xFFFFu);
+                        return emit_staged(rr + 1, n - 1, a, in, scratch, op, 0xFFFFFFFFu, ring, r, map, lane);
+                    }
+                    return emit_staged(rr, n, anchor, in, scratch, op, 0xFFFFFFFFu, ring, r, map, lane);
+                };
+                const uint32_t cur = lzp::parse_page(in, Lp, table, rec, lane, sink, b0);
+                out_flush_all(ring, r, scratch, op, lane);
+                if (!first && wave + 1 == kNW) (void)write_last_literals(in, cur, L, scratch, op, 0xFFFFFFFFu, lane);
+                if (lane == 0) {
+                    hdr->len[wave] = first ? 0u : op;
+                    hdr->cursor[wave] = cur;
+                }
+            }
+        }
+        __syncthreads();   // every part parsed
+        if (wave == 0) {
+            int32_t rv = 0;
+            if (!fits) {
+                rv = kResultTooLarge;
+            } else if (rfl(hdr->ok[0])) {
+                // layout: part 0's stream, then per later part the joint sequence and its stream
+                uint32_t op = rfl(hdr->len[0]), cur = rfl(hdr->cursor[0]);
+                bool ok = true, tail_done = false;
+                OutRing r{0u, 0u};
+                for (uint32_t w = 1; w < kNW && ok; w++) {
+                    if (!rfl(hdr->has_first[w])) {
+                        if (lane == 0) hdr->seg[w] = op;
+                        continue;
+                    }
+                    if (lane == 0) rec[0] = hdr->first[w];
+                    __builtin_amdgcn_wave_barrier();
+                    ok = emit_staged(rec, 1, cur, in, p.dst, op, p.dst_cap, ring, r, map, lane);
+                    if (ok) out_flush_all(ring, r, p.dst, op, lane);
+                    if (lane == 0) hdr->seg[w] = op;
+                    op += rfl(hdr->len[w]);
+                    cur = rfl(hdr->cursor[w]);
+                    tail_done = w + 1 == kNW;
+                }
+                if (ok && !tail_done) ok = write_last_literals(in, cur, L, p.dst, op, p.dst_cap, lane);
+                if (ok && op <= p.dst_cap) rv = (int32_t)op;
+            }
+            if (lane == 0) {
+                hdr->result = rv;
+                b.results[page] = rv;
+            }
+        }
+        __syncthreads();
+        if (wave > 0 && fits) {   // part w's stream into place
+            const int32_t res = (int32_t)rfl((uint32_t)hdr->result);
+            const uint32_t lw = rfl(hdr->len[wave]);
+            if (res > 0 && lw) {
+                uint8_t *d = p.dst + rfl(hdr->seg[wave]);
+                const uint32_t nv = lw >> 4;
+                for (uint32_t v = lane; v < nv; v += kWave)
+                    *(g_u32x4_ua *)(uintptr_t)(d + 16 * v) = gload_nt((const u32x4 *)(scratch + 16 * v));
+                for (uint32_t j = (nv << 4) + lane; j < lw; j += kWave) d[j] = scratch[j];
+            }
+        }
+        __syncthreads();   // the stage, the tables and the header are free
+        if (next >= b.count) break;
+        page = next;
+        p = pn;
+        head = nhead;
+        if (p.src_len <= in_cap && p.src_len > 0) {
+            u32x4 *l = (u32x4 *)stage;
+#pragma unroll
+            for (uint32_t k = 0; k < kPf; k++) {
+                const uint32_t v = tid + k * kT;
+                if (v < nvec) l[v] = pf[k];
+            }
+            const u32x4 *g = (const u32x4 *)((uintptr_t)p.src - nhead);
+            for (uint32_t v = tid + kPf * kT; v < nvec; v += kT) l[v] = gload_nt(g + v);
+        }
+        if (tid == 0) {
+            hdr->next_lo = hdr->next2_lo;
+            hdr->next_hi = hdr->next2_hi;
+        }
+    }
+}
+
 __global__ __launch_bounds__(64) void lz4_encode_kernel(tyche_batch_t b, uint32_t in_cap, unsigned *ctr) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t lane = threadIdx.x;
@@ -623,6 +839,32 @@ hipError_t launch_lz4_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream_
     if (in_cap > 65535u) return hipErrorInvalidValue;    // 16-bit positions (byU16 regime)
     // TYCHE_LZ4_ENC=1: the one-wave kernel for every batch (A/B timing)
     const bool one_wave = knob("LZ4_ENC", 0) == 1;
+    const long nw = knob("LZ4_ENC_WAVES", 2);   // waves per page of the split encoders (2: the two-wave kernel)
+    if (!one_wave && in_cap >= kSplitMin && (nw == 3 || nw == 4 || nw == 8)) {
+        const void *k = nw == 8   ? (const void *)lz4_encode_splitn_kernel<8>
+                        : nw == 4 ? (const void *)lz4_encode_splitn_kernel<4>
+                                  : (const void *)lz4_encode_splitn_kernel<3>;
+        const uint32_t T = (uint32_t)nw * kWave;
+        const size_t lds = (nw == 8 ? split_stage_off<8>() : nw == 4 ? split_stage_off<4>() : split_stage_off<3>()) +
+                           ((in_cap + 16u + kPad + 15u) & ~15u);
+        const size_t ncu = prepare_launch(k);
+        int per_cu = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, (int)T, lds) != hipSuccess || per_cu < 1) per_cu = 1;
+        const size_t grid = std::min<size_t>(b.count, ncu * (size_t)per_cu);
+        const uint32_t pws = nw == 8 ? part_scratch<8>(in_cap) : nw == 4 ? part_scratch<4>(in_cap) : part_scratch<3>(in_cap);
+        uint32_t seed = (uint32_t)std::max(0L, knob("LZ4_ENC_SEED", kSeed)) & ~(kWave - 1u);   // positions seeded before a part
+        const uint32_t ws_stride = (uint32_t)(nw - 1) * pws;
+        ScratchLease ws(s, grid * (size_t)ws_stride);
+        if (ws.get()) {
+            WorkCounter ctr(s, grid < b.count);
+            if (!ctr.get()) return hipErrorOutOfMemory;
+            unsigned *cp = ctr.get();
+            uint8_t *wp = (uint8_t *)ws.get();
+            void *args[] = {(void *)&b, &in_cap, &cp, &wp, (void *)&ws_stride, &seed};
+            (void)hipLaunchKernel(k, dim3((unsigned)grid), dim3(T), args, lds, s);
+            return hipGetLastError();
+        }
+    }
     if (!one_wave && in_cap >= kSplitMin) {
         const size_t lds = kSplitStage + ((in_cap + 16u + kPad + 15u) & ~15u);
         const size_t ncu = prepare_launch((const void *)lz4_encode_split_kernel);

@@ -893,6 +893,182 @@ __global__ __launch_bounds__(64) void zstd_encode_kernel(tyche_batch_t b, size_t
     }
 }
 
+// ---- pass A1 on kNW waves per page (round 3, TYCHE_ZSTD_PARSE_WAVES, default 4).
+//
+// The one-wave A1 holds page + hash table (40.8 KiB at 32 KiB pages: 4 waves per
+// CU, one per SIMD) and was 737 of the encoder's 995 ms per 1M x 32 KiB pages --
+// latency-bound.  Here kNW waves share the staged page as the LZ4 split encoder
+// does (lz4_encode.hip): wave w parses part [b_w, b_{w+1}) (64-aligned) with its
+// own table, seeded with the kZSeed positions before the part, matches of part w
+// ending by b_{w+1}.  Each wave writes its sequences to its own slice of the
+// area's code region (pass B's, unused until A2 runs); after a barrier every
+// wave copies its slice to its place in the page's sequence list (the first
+// sequence's literal length extended back to the previous part's last match end,
+// whose catch-up it did not see -- any catch-up <= the one taken is valid), and
+// wave 0 cuts the list into parse blocks of kZBlk sequences.  Repeat candidates
+// restart at zstd's {1, 4} in each part; the repeat codes themselves are
+// assigned by A2 over the whole list, as before.
+#ifndef TYCHE_ZSTD_SEED
+#define TYCHE_ZSTD_SEED 8192   // positions seeded before a part (multiple of 64)
+#endif
+constexpr uint32_t kZSeed = TYCHE_ZSTD_SEED;
+constexpr uint32_t kZBlk = kSeqCap - kWave;   // sequences per parse block (parse_to_area cuts after > 960)
+template <uint32_t kNW>
+struct ZSplitHdr {
+    uint32_t next_lo, next_hi, next2_lo, next2_hi;
+    uint32_t n[kNW];        // sequences of part w
+    uint32_t cursor[kNW];   // end of part w's last match (its start if none)
+    uint32_t ok[kNW];       // part w's sequences fit its slice
+};
+template <uint32_t kNW>
+constexpr size_t zsplit_hdr_bytes() { return (sizeof(ZSplitHdr<kNW>) + 63) & ~(size_t)63; }
+constexpr size_t kZWaveRegion = kTableSlots * sizeof(uint16_t) + kWave * 8;   // table, 64 records
+template <uint32_t kNW>
+constexpr size_t zsplit_stage_off() { return zsplit_hdr_bytes<kNW>() + kNW * kZWaveRegion; }
+
+template <uint32_t kNW>
+__global__ __launch_bounds__(kNW * 64) void zstd_parse_split_kernel(tyche_batch_t b, size_t first, size_t count,
+                                                                    uint32_t in_cap, unsigned *ctr, uint8_t *ws,
+                                                                    size_t ws_page, int32_t *st) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    constexpr uint32_t kT = kNW * kWave;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t wave = rfl(tid >> 6);
+    ZSplitHdr<kNW> *hdr = (ZSplitHdr<kNW> *)smem;
+    uint8_t *region = smem + zsplit_hdr_bytes<kNW>() + wave * kZWaveRegion;
+    uint16_t *table = (uint16_t *)region;
+    uint2 *rec = (uint2 *)(region + kTableSlots * sizeof(uint16_t));
+    uint8_t *stage = smem + zsplit_stage_off<kNW>();
+    const uint32_t rec_cap = enc_rec_cap(in_cap);
+    const uint32_t slice = (2u * rec_cap) / kNW;   // the code region holds 2 rec_cap sequences of 8 bytes
+
+    size_t page = blockIdx.x;   // chunk-local
+    if (page >= count) return;
+    PageRef p = batch_page(b, first + page);
+    uint32_t head = stage_in(p.src, p.src_len <= in_cap ? p.src_len : 0, stage, tid, kT);
+    if (tid == 0) {
+        const size_t nx = (size_t)atomicAdd(ctr, 1u) + gridDim.x;
+        hdr->next_lo = (uint32_t)nx;
+        hdr->next_hi = (uint32_t)(nx >> 32);
+    }
+    for (;;) {
+        for (uint32_t w = lane; w < kTableSlots / 8; w += kWave) ((u32x4 *)table)[w] = u32x4{0, 0, 0, 0};
+        if (tid < kWave) stage[head + p.src_len + tid] = 0;
+        __syncthreads();
+        const size_t next = (size_t)rfl(hdr->next_lo) | ((size_t)rfl(hdr->next_hi) << 32);
+        const uint8_t *in = stage + head;
+        const uint32_t L = p.src_len;
+        const bool fits = L <= in_cap;
+        uint8_t *area = ws + page * ws_page;
+        uint2 *W = (uint2 *)area_rec(area) + (size_t)wave * slice;
+        const uint32_t b0 = wave == 0 ? 0u : ((L * wave) / kNW) & ~(kWave - 1u);
+        const uint32_t b1 = wave + 1 == kNW ? L : ((L * (wave + 1)) / kNW) & ~(kWave - 1u);
+        const uint32_t Lp = wave + 1 == kNW ? L : b1 + kLastLiterals;
+        if (fits) {
+            if (wave > 0) {   // seed: the positions before the part, block order, as the parse inserts them
+                const uint32_t ib = (uint32_t)(uintptr_t)in & 3u;
+                const uint32_t *A = (const uint32_t *)(in - ib);
+                uint32_t *T = (uint32_t *)table;
+                for (uint32_t blk = b0 > kZSeed ? b0 - kZSeed : 0u; blk < b0; blk += kWave) {
+                    const uint32_t pos = blk + lane;
+                    const uint32_t h = lzp::bucket_of<kZWays>(lzp::lds_word(A, pos + ib), lzp::lds_word(A, pos + 4u + ib),
+                                                              TYCHE_HASH_BYTES);
+                    const uint32_t bk = T[h];
+                    __builtin_amdgcn_wave_barrier();
+                    T[h] = pos | (bk << 16);
+                    __builtin_amdgcn_wave_barrier();
+                }
+            }
+            uint32_t nseq = 0;
+            auto sink = [&](const uint2 *r, uint32_t n, uint32_t anchor) -> bool {
+                uint32_t ls, ll, ml, off;
+                lzp::decode_record(r, n, anchor, lane, ls, ll, ml, off);
+                if (nseq + n > slice) return false;
+                if (lane < n) W[nseq + lane] = make_uint2(ll | (off << 16), ml);
+                nseq += n;
+                __builtin_amdgcn_wave_barrier();
+                return true;
+            };
+            const uint32_t cur = lzp::parse_page<true, false, kZWays>(in, Lp, table, rec, lane, sink, b0);
+            if (lane == 0) {
+                hdr->ok[wave] = cur != 0xFFFFFFFFu ? 1u : 0u;
+                hdr->n[wave] = nseq;
+                hdr->cursor[wave] = nseq ? cur : b0;
+                if (wave == 0) {
+                    const size_t nx = (size_t)atomicAdd(ctr, 1u) + gridDim.x;
+                    hdr->next2_lo = (uint32_t)nx;
+                    hdr->next2_hi = (uint32_t)(nx >> 32);
+                }
+            }
+        }
+        __syncthreads();   // every part parsed
+        bool ok = fits;
+        uint32_t off_w = 0, prev_end = 0, total = 0;
+        for (uint32_t w = 0; w < kNW; w++) {
+            const uint32_t nw = rfl(hdr->n[w]);
+            ok = ok && rfl(hdr->ok[w]);
+            if (w < wave) {
+                off_w += nw;
+                if (nw) prev_end = rfl(hdr->cursor[w]);
+            }
+            total += nw;
+        }
+        uint2 *S = area_seq(area, rec_cap);
+        if (ok) {   // the slices into place; the part's first literal run starts at the previous part's end
+            const uint32_t nw = rfl(hdr->n[wave]);
+            for (uint32_t j = lane; j < nw; j += kWave) {
+                uint2 q = W[j];
+                if (j == 0 && wave > 0) q.x += b0 - prev_end;   // ll (low 16 bits): cannot carry out (< 2^16)
+                S[off_w + j] = q;
+            }
+        }
+        __syncthreads();
+        if (wave == 0) {
+            if (!fits) {
+                if (lane == 0) st[page] = kResultTooLarge;
+            } else if (!ok || (total + kZBlk - 1) / kZBlk + 1 > kMaxBlk) {
+                if (lane == 0) st[page] = 0;
+            } else {
+                // parse blocks of kZBlk sequences over the whole list: page spans from the sequences' sizes
+                uint32_t npb = 0, pos = 0;
+                for (uint32_t bs = 0; bs < total || npb == 0; bs += kZBlk) {
+                    const uint32_t cnt = min(kZBlk, total - bs);
+                    uint32_t span = 0;
+                    for (uint32_t j = lane; j < cnt; j += kWave) {
+                        const uint2 q = S[bs + j];
+                        span += (q.x & 0xFFFFu) + q.y;
+                    }
+                    span = huf::wave_sum(span);
+                    const bool last = bs + kZBlk >= total;
+                    if (lane == 0) {
+                        uint32_t *P = area_pblk(area, npb);
+                        P[0] = pos;
+                        P[1] = last ? L : pos + span;
+                        P[2] = bs;
+                        P[3] = cnt;
+                    }
+                    pos += span;
+                    npb++;
+                    if (last) break;
+                }
+                if (lane == 0) {
+                    ((uint32_t *)area)[1] = npb;
+                    st[page] = 1;
+                }
+            }
+        }
+        __syncthreads();   // the stage, the tables and the header are free
+        if (next >= count) break;
+        page = next;
+        p = batch_page(b, first + page);
+        head = stage_in(p.src, p.src_len <= in_cap ? p.src_len : 0, stage, tid, kT);
+        if (tid == 0) {
+            hdr->next_lo = hdr->next2_lo;
+            hdr->next_hi = hdr->next2_hi;
+        }
+    }
+}
+
 // ---- pass A2
 constexpr uint32_t kA2Lds = kWave + kWave * 8u + kHtab * 4u + 256u;   // map, stage, htab, weights
 __global__ __launch_bounds__(64) void zstd_block_kernel(tyche_batch_t b, size_t first, size_t count, uint32_t in_cap,
@@ -1133,9 +1309,31 @@ hipError_t launch_zstd_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream
     (void)prepare_launch((const void *)zstd_fse_kernel);
     (void)prepare_launch((const void *)zstd_pack_kernel);
     const size_t cu1 = waves_per_cu(k1, lds1), cu2 = waves_per_cu((const void *)zstd_block_kernel, kA2Lds);
+    // pass A1's waves per page (1: the one-wave parse)
+    const long pw = knob("ZSTD_PARSE_WAVES", 1);
+    size_t cup = 1;
+    if (pw == 2 || pw == 4) {
+        const void *kp = pw == 4 ? (const void *)zstd_parse_split_kernel<4> : (const void *)zstd_parse_split_kernel<2>;
+        const size_t ldsp = (pw == 4 ? zsplit_stage_off<4>() : zsplit_stage_off<2>()) + page_lds;
+        (void)prepare_launch(kp);
+        int per = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kp, (int)(pw * kWave), ldsp) == hipSuccess && per > 0)
+            cup = (size_t)per;
+    }
     for (size_t first = 0; first < b.count; first += chunk) {
         const size_t n = std::min(chunk, b.count - first);
-        {
+        if (pw == 2 || pw == 4) {   // pass A1 on pw waves per page
+            const void *kp = pw == 4 ? (const void *)zstd_parse_split_kernel<4> : (const void *)zstd_parse_split_kernel<2>;
+            const size_t ldsp = (pw == 4 ? zsplit_stage_off<4>() : zsplit_stage_off<2>()) + page_lds;
+            const size_t g = std::min<size_t>(n, ncu * cup);
+            WorkCounter ctr(s, g < n);
+            if (!ctr.get()) return hipErrorOutOfMemory;
+            unsigned *cp = ctr.get();
+            size_t fst = first, cnt = n, wpage = page_bytes;
+            uint32_t icap = in_cap;
+            void *args[] = {(void *)&b, &fst, &cnt, &icap, &cp, &ws, &wpage, &st};
+            (void)hipLaunchKernel(kp, dim3((unsigned)g), dim3((unsigned)(pw * kWave)), args, ldsp, s);
+        } else {
             const size_t g = std::min<size_t>(n, ncu * cu1);
             WorkCounter ctr(s, g < n);
             if (!ctr.get()) return hipErrorOutOfMemory;
