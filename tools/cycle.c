@@ -175,7 +175,7 @@ int main(int argc, char **argv) {
     const double t1 = now_s();
     const size_t comp_bytes = (size_t)g_comp_bytes, fails = (size_t)g_fails;
     /* ---- restore: biased searches from worker threads through the queue */
-    tyche_restore_queue_start(1024, 100);
+    tyche_restore_queue_start(1024, getenv("CYCLE_WAIT_US") ? atoi(getenv("CYCLE_WAIT_US")) : 100);
     pthread_t th[1024];
     const int nt = threads < 1024 ? threads : 1024;
     for (int t = 0; t < nt; t++) pthread_create(&th[t], NULL, restorer, (void *)(uintptr_t)t);

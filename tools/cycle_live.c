@@ -284,7 +284,7 @@ int main(int argc, char **argv) {
     g_max_raw = (int64_t)(total * (size_t)budget_pct / 100u);
 
     /* ---- the live cycle */
-    tyche_restore_queue_start(1024, 100);
+    tyche_restore_queue_start(1024, getenv("CYCLE_WAIT_US") ? atoi(getenv("CYCLE_WAIT_US")) : 100);
     pthread_t cth[256], sth, rth[1024];
     const int nc = ncomp < 1 ? 1 : ncomp < 256 ? ncomp : 256;
     const int nt = nr < 1 ? 1 : nr < 1024 ? nr : 1024;

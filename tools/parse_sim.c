@@ -338,12 +338,40 @@ static double parse_zstd_fast(uint32_t hbits, uint32_t mls) {
 }
 
 /* the device parse with repeat candidates (lz_parse.h kRepCand): nb buckets x ways, hash of hb bytes */
+static uint32_t opt_parts = 1, opt_seed = 1u << 20, opt_carry_rep = 0, gR = 1, gR2 = 4, opt_warm = 0;
 static double parse_zstd_device(uint32_t nb, uint32_t ways, uint32_t hb) {
     static uint32_t T[1 << 16][8];
-    for (uint32_t i = 0; i < nb; i++) for (int w = 0; w < 8; w++) T[i][w] = 0;
     zreset();
-    const uint32_t mflimit = L - 12, matchlimit = L - 5;
-    uint32_t cursor = 0, anchor = 0, blk = 0, R = 1, R2 = 4;
+    uint32_t anchor = 0;
+    const uint32_t Lfull = L;
+  for (uint32_t part = 0; part < opt_parts; part++) {
+    const uint32_t b0 = part == 0 ? 0 : ((Lfull * part) / opt_parts) & ~63u;
+    const uint32_t b1 = part + 1 == opt_parts ? Lfull : ((Lfull * (part + 1)) / opt_parts) & ~63u;
+    const uint32_t Lp = part + 1 == opt_parts ? Lfull : b1 + 5;
+    for (uint32_t i = 0; i < nb; i++) for (int w = 0; w < 8; w++) T[i][w] = 0;
+    for (uint32_t blk = b0 > opt_seed ? b0 - opt_seed : 0; blk < b0; blk += 64)
+        for (int l = 0; l < 64; l++) {
+            const uint32_t pos = blk + l;
+            const uint64_t x = read64(pos) & (hb >= 8 ? ~0ull : ((1ull << (8 * hb)) - 1));
+            const uint32_t h = (uint32_t)((((x * 0xCF1BBCDCB7A56463ull) >> 32) * (uint64_t)nb) >> 32);
+            for (int w = (int)ways - 1; w > 0; w--) T[h][w] = T[h][w - 1];
+            T[h][0] = pos + 1;
+        }
+    const uint32_t mflimit = Lp - 12, matchlimit = Lp - 5;
+    uint32_t R = 1, R2 = 4;
+    if (opt_carry_rep && part > 0) { R = gR; R2 = gR2; }
+    const uint32_t saved_nzs = nzs, saved_zlits = zlits, saved_anchor = anchor;
+    uint32_t saved_zlit[256];
+    int warm = part > 0 && opt_warm > 0;
+  for (int pass = warm ? 0 : 1; pass < 2; pass++) {
+    uint32_t cursor = pass == 0 ? (b0 > opt_warm ? b0 - opt_warm : 0) & ~63u : b0;
+    uint32_t blk = cursor;
+    if (pass == 0) memcpy(saved_zlit, zlit, sizeof zlit);
+    const uint32_t plim = pass == 0 ? b0 + 5 : Lp;
+    const uint32_t mflimit2 = plim - 12, matchlimit2 = plim - 5;
+    (void)mflimit; (void)matchlimit;
+#define mflimit mflimit2
+#define matchlimit matchlimit2
     while (blk <= mflimit) {
         uint32_t cand[64], len[64], back[64], ok[64], rok[64], h[64];
         for (int l = 0; l < 64; l++) {
@@ -400,8 +428,46 @@ static double parse_zstd_device(uint32_t nb, uint32_t ways, uint32_t hb) {
         if ((cursor & ~63u) > nbk) nbk = cursor & ~63u;
         blk = nbk;
     }
+#undef mflimit
+#undef matchlimit
+    if (pass == 0) {   /* warm-up: keep R, R2 and the table, drop the sequences */
+        nzs = saved_nzs; zlits = saved_zlits; anchor = saved_anchor;
+        memcpy(zlit, saved_zlit, sizeof zlit);
+    }
+  }
+    gR = R; gR2 = R2;
+  }
     zlit_add(anchor, L);
     return zstd_cost();
+}
+
+static int main_zstd_split(int n) {
+    double raw = 0, d[4] = {0}, dw[4] = {0};
+    const uint32_t warms[4] = {256, 512, 1024, 2048};
+    const uint32_t parts[4] = {1, 2, 4, 4}, seeds[4] = {1u << 20, 1u << 20, 1u << 20, 1u << 20};
+    for (int i = 0; i < n; i++) {
+        pg_page_t p;
+        pg_page_init(&p, 20170303ull, (uint64_t)i, L, 0);
+        for (uint32_t b = 0; b < L; b++) pg[b] = (uint8_t)pg_page_byte(&p, b);
+        memset(pg + L, 0, 64);
+        raw += L;
+        for (int c = 0; c < 4; c++) {
+            opt_parts = parts[c];
+            opt_seed = seeds[c];
+            opt_carry_rep = c == 3;
+            d[c] += parse_zstd_device(1856, 2, 5);
+        }
+        for (int c = 0; c < 4; c++) {
+            opt_parts = 4; opt_seed = 1u << 20; opt_carry_rep = 0; opt_warm = warms[c];
+            dw[c] += parse_zstd_device(1856, 2, 5);
+        }
+        opt_warm = 0;
+    }
+    opt_parts = 1;
+    opt_seed = 1u << 20;
+    for (int c = 0; c < 4; c++) printf("model: device parse in %u parts, seed %u%s: ratio %.3f\n", parts[c], seeds[c], c == 3 ? ", repeat offsets carried" : "", raw / d[c]);
+    for (int c = 0; c < 4; c++) printf("model: device parse in 4 parts, warm-up parse of %u bytes before each: ratio %.3f\n", warms[c], raw / dw[c]);
+    return 0;
 }
 
 static int main_zstd(int n) {
@@ -429,6 +495,7 @@ int main(int argc, char **argv) {
     const int n = argc > 1 ? atoi(argv[1]) : 200;
     L = argc > 2 ? (uint32_t)atoi(argv[2]) : 16384;
     if (argc > 3 && !strcmp(argv[3], "zstd")) return main_zstd(n);
+    if (argc > 3 && !strcmp(argv[3], "zsplit")) return main_zstd_split(n);
     static const uint32_t grid[][2] = {{1024, 4}, {2048, 4}, {512, 8}, {1024, 8}, {2048, 8}, {1024, 6}, {4096, 8}};
     const int ng = (int)(sizeof grid / sizeof grid[0]);
     double raw = 0, zl = 0, zf = 0, var[16] = {0}, var_r[16] = {0};

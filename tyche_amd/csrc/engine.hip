@@ -752,7 +752,9 @@ int run_host_batch(int dev, size_t n, const void *const *src, const uint32_t *sr
     HostCtx &c = *cp;
     CopyPool &pool = CopyPool::get();
     hipError_t e;
+    std::function<void()> before_bail;   // stops the async finisher (below) before the slots are drained
     auto bail = [&](int r) {
+        if (before_bail) before_bail();
         c.abandon();
         release_ctx(dev, cp);
         return r;
@@ -852,6 +854,92 @@ int run_host_batch(int dev, size_t n, const void *const *src, const uint32_t *sr
 
     size_t first = 0;
     int si = 0;
+    // Async finishing (round 3): with three or more chunks a helper thread waits for each slot's
+    // stream and scatters its results while the caller gathers and enqueues the next chunk -- the
+    // r03 stage clocks had the caller waiting on streams ~25 % of a call, between its copies.
+    // A slot is reused only after the helper has scattered it (S.busy false, under fm).
+    size_t nchunks_est = 0;
+    {
+        size_t inb = 0;
+        for (size_t j = 0; j < n; j++) inb += up16(src_len[j]) + up16(dst_cap[j]);
+        nchunks_est = inb / std::max<size_t>(1, (size_t)std::max(1L, knob("HOST_CHUNK_MB", (long)(kChunkBytes >> 20))) << 20);
+    }
+    const bool async = nchunks_est >= 3 && knob("HOST_ASYNC_SCATTER", 1) != 0;
+    std::mutex fm;
+    std::condition_variable fcv;
+    std::vector<int> fq;   // slots to finish, in issue order
+    bool fstop = false;
+    int frc = TYCHE_E_OK;
+    std::string ferr;
+    std::thread fth;
+    auto finish_async = [&](Slot &S) -> int {   // helper thread: sync, scatter, then free the slot
+        hipError_t fe;
+        {
+            HpClock hc(kHpWait);
+            if ((fe = hipStreamSynchronize(S.stream)) != hipSuccess) return fail("hipStreamSynchronize", fe);
+        }
+        HpClock hc(kHpScatter);
+        const size_t k = S.count;
+        const uint64_t *m_doff = (const uint64_t *)S.h_meta.p + k;
+        const int32_t *m_res = (const int32_t *)((const uint8_t *)S.h_meta.p + k * 24);
+        const uint8_t *hout = (const uint8_t *)S.h_out.p;
+        const size_t f0 = S.first;
+        std::atomic<uint64_t> moved{0};
+        pool.run(k, [&](size_t j) {
+            const int32_t r = m_res[j];
+            results[f0 + j] = r;
+            if (r > 0 && (uint32_t)r <= dst_cap[f0 + j]) {
+                copy_nt(dst[f0 + j], hout + m_doff[j], (size_t)r);
+                moved.fetch_add((uint64_t)r, std::memory_order_relaxed);
+            }
+        });
+        g_hprof[kHpScatterBytes] += moved.load();
+        g_hprof[kHpChunks]++;
+        return TYCHE_E_OK;
+    };
+    if (async) {
+        fth = std::thread([&] {
+            for (;;) {
+                int idx;
+                {
+                    std::unique_lock<std::mutex> g(fm);
+                    fcv.wait(g, [&] { return !fq.empty() || fstop; });
+                    if (fq.empty()) return;
+                    idx = fq.front();
+                    fq.erase(fq.begin());
+                }
+                const int r = finish_async(c.slot[idx]);
+                std::lock_guard<std::mutex> g(fm);
+                if (r) {
+                    frc = r;
+                    ferr = t_error;   // the helper's thread-local message
+                    fcv.notify_all();
+                    return;
+                }
+                c.slot[idx].busy = false;
+                fcv.notify_all();
+            }
+        });
+    }
+    auto stop_helper = [&] {
+        if (!fth.joinable()) return;
+        {
+            std::lock_guard<std::mutex> g(fm);
+            fstop = true;
+        }
+        fcv.notify_all();
+        fth.join();
+    };
+    struct HelperJoin {   // every return path stops the helper (bail() does so before draining the streams)
+        std::function<void()> f;
+        ~HelperJoin() { f(); }
+    } helper_join{stop_helper};
+    before_bail = stop_helper;
+    auto async_fail = [&]() -> int {
+        stop_helper();
+        t_error = ferr;
+        return frc;
+    };
     // chunks hold ~chunk_bytes of input AND of output capacity: a decompress batch's
     // output is ~2.6x its input, so cutting by input alone made 3 chunks of 170 MiB
     // of D2H each out of a 32K-page batch, too few to overlap the two copy directions
@@ -870,7 +958,16 @@ int run_host_batch(int dev, size_t n, const void *const *src, const uint32_t *sr
         }
         const size_t k = last - first;
         Slot &S = c.slot[si];
-        if ((rc = finish(S))) return bail(rc);   // the slot's previous chunk
+        if (async) {   // the helper has scattered the slot's previous chunk
+            std::unique_lock<std::mutex> g(fm);
+            fcv.wait(g, [&] { return !S.busy || frc != TYCHE_E_OK; });
+            if (frc != TYCHE_E_OK) {
+                g.unlock();
+                return bail(async_fail());
+            }
+        } else if ((rc = finish(S))) {
+            return bail(rc);   // the slot's previous chunk
+        }
         // meta layout: soff[k] u64, doff[k] u64, slen[k] u32, dcap[k] u32, res[k] i32
         const size_t meta_bytes = k * 28 + 64;
         if ((rc = S.h_in.grow(in_bytes + 16)) || (rc = S.h_out.grow(out_bytes + 16)) ||
@@ -905,7 +1002,10 @@ int run_host_batch(int dev, size_t n, const void *const *src, const uint32_t *sr
         const size_t head_bytes = (uint8_t *)m_res - (uint8_t *)m_soff;
         S.first = first;
         S.count = k;
-        S.busy = true;   // from the first enqueued copy on, the slot must be drained on failure
+        {
+            std::lock_guard<std::mutex> g(fm);
+            S.busy = true;   // from the first enqueued copy on, the slot must be drained on failure
+        }
         if ((e = hipMemcpyAsync(dmeta, S.h_meta.p, head_bytes, hipMemcpyHostToDevice, S.stream)) != hipSuccess)
             return bail(fail("hipMemcpyAsync(meta)", e));
         if (so && (e = hipMemcpyAsync(S.d_in.p, hin, so, hipMemcpyHostToDevice, S.stream)) != hipSuccess)
@@ -935,8 +1035,22 @@ int run_host_batch(int dev, size_t n, const void *const *src, const uint32_t *sr
             return bail(fail("hipMemcpyAsync(results)", e));
         if (dof && !direct && (e = hipMemcpyAsync(S.h_out.p, S.d_out.p, dof, hipMemcpyDeviceToHost, S.stream)) != hipSuccess)
             return bail(fail("hipMemcpyAsync(out)", e));
+        if (async) {
+            std::lock_guard<std::mutex> g(fm);
+            fq.push_back(si);
+            fcv.notify_all();
+        }
         first = last;
         si = (si + 1) % kSlots;
+    }
+    if (async) {   // the helper drains the queue, then stops
+        stop_helper();
+        if (frc != TYCHE_E_OK) {
+            t_error = ferr;
+            return bail(frc);
+        }
+        release_ctx(dev, cp);
+        return TYCHE_E_OK;
     }
     // drain in issue order
     for (int j = 0; j < kSlots; j++)

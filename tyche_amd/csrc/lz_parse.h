@@ -211,12 +211,15 @@ __device__ __forceinline__ uint32_t bucket_of(uint32_t v, uint32_t v2 = 0, uint3
 #define TYCHE_HASH_BYTES 5   // kRepCand (zstd): bytes hashed -- zstd level 1 hashes searchLength bytes
 #endif
 
+//
+// rep (kRepCand, optional): the repeat offsets {R, R2} to start from, and where the final ones go -- a
+// part of a split parse (zstd_encode.hip) warms them up by parsing the bytes before it.
 template <bool kRepCand = false, bool kMin3 = false, int kWays = 1, typename Sink>
 __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *table, uint2 *rec, uint32_t lane,
-                                      Sink &sink, uint32_t start = 0) {
+                                      Sink &sink, uint32_t start = 0, uint32_t *rep = nullptr) {
     static_assert(kWays == 1 || kWays == 2 || kWays == 4 || kWays == 8, "1, 2, 4 or 8 ways");
     uint32_t anchor = start;
-    if (L < (uint32_t)(kMfLimit + 1) || start > L - kMfLimit) return start;
+    if (L < (uint32_t)(kMfLimit + 1) || start > L - kMfLimit) return start;   // (rep unchanged)
     const uint32_t mflimit = L - kMfLimit;          // last position a match may start
     const uint32_t matchlimit = L - kLastLiterals;  // matches end at or before this
     const uint32_t ib = (uint32_t)(uintptr_t)in & 3u;               // in's offset from a dword boundary
@@ -224,7 +227,7 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
     uint32_t cursor = start; // matches may start here (end of the last match)
     uint32_t nacc = 0;       // records accumulated since the last hand-off
     uint32_t blk = start;    // current 64-position block
-    uint32_t R = 1, R2 = 4;  // repeat offsets 1 and 2 (kRepCand): zstd's initial {1, 4}
+    uint32_t R = rep ? rep[0] : 1u, R2 = rep ? rep[1] : 4u;   // repeat offsets 1 and 2 (kRepCand): zstd's initial {1, 4}
     bool done = false;
     PHASE_INIT();
     for (; !done && blk <= mflimit; blk = max(blk + kWave, cursor & ~(kWave - 1))) {
@@ -481,6 +484,10 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
         __builtin_amdgcn_wave_barrier();
         if (!sink(rec, nacc, anchor)) return 0xFFFFFFFFu;
         anchor = cursor;
+    }
+    if (rep) {
+        rep[0] = R;
+        rep[1] = R2;
     }
     PHASE(3);
     PHASE_FLUSH();

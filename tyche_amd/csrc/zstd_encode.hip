@@ -912,6 +912,7 @@ __global__ __launch_bounds__(64) void zstd_encode_kernel(tyche_batch_t b, size_t
 #define TYCHE_ZSTD_SEED 8192   // positions seeded before a part (multiple of 64)
 #endif
 constexpr uint32_t kZSeed = TYCHE_ZSTD_SEED;
+constexpr uint32_t kZWarm = 256;   // bytes parsed (and dropped) before a part, for its repeat offsets
 constexpr uint32_t kZBlk = kSeqCap - kWave;   // sequences per parse block (parse_to_area cuts after > 960)
 template <uint32_t kNW>
 struct ZSplitHdr {
@@ -929,7 +930,7 @@ constexpr size_t zsplit_stage_off() { return zsplit_hdr_bytes<kNW>() + kNW * kZW
 template <uint32_t kNW>
 __global__ __launch_bounds__(kNW * 64) void zstd_parse_split_kernel(tyche_batch_t b, size_t first, size_t count,
                                                                     uint32_t in_cap, unsigned *ctr, uint8_t *ws,
-                                                                    size_t ws_page, int32_t *st) {
+                                                                    size_t ws_page, int32_t *st, uint32_t seed) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr uint32_t kT = kNW * kWave;
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
@@ -965,11 +966,13 @@ __global__ __launch_bounds__(kNW * 64) void zstd_parse_split_kernel(tyche_batch_
         const uint32_t b1 = wave + 1 == kNW ? L : ((L * (wave + 1)) / kNW) & ~(kWave - 1u);
         const uint32_t Lp = wave + 1 == kNW ? L : b1 + kLastLiterals;
         if (fits) {
+            uint32_t rep[2] = {1u, 4u};
             if (wave > 0) {   // seed: the positions before the part, block order, as the parse inserts them
                 const uint32_t ib = (uint32_t)(uintptr_t)in & 3u;
                 const uint32_t *A = (const uint32_t *)(in - ib);
                 uint32_t *T = (uint32_t *)table;
-                for (uint32_t blk = b0 > kZSeed ? b0 - kZSeed : 0u; blk < b0; blk += kWave) {
+                const uint32_t wstart = b0 > kZWarm ? b0 - kZWarm : 0u;
+                for (uint32_t blk = wstart > seed ? wstart - seed : 0u; blk < wstart; blk += kWave) {
                     const uint32_t pos = blk + lane;
                     const uint32_t h = lzp::bucket_of<kZWays>(lzp::lds_word(A, pos + ib), lzp::lds_word(A, pos + 4u + ib),
                                                               TYCHE_HASH_BYTES);
@@ -978,6 +981,11 @@ __global__ __launch_bounds__(kNW * 64) void zstd_parse_split_kernel(tyche_batch_
                     T[h] = pos | (bk << 16);
                     __builtin_amdgcn_wave_barrier();
                 }
+                // warm-up: parse the kZWarm bytes before the part, sequences dropped, for the repeat
+                // offsets the part's parse starts from (a cold {1, 4} cost the 4-wave split 1.7 % of
+                // ratio; tools/parse_sim.c zsplit: 4.999 -> 5.069 of 5.100)
+                auto drop = [&](const uint2 *, uint32_t, uint32_t) -> bool { return true; };
+                (void)lzp::parse_page<true, false, kZWays>(in, b0 + kLastLiterals, table, rec, lane, drop, wstart, rep);
             }
             uint32_t nseq = 0;
             auto sink = [&](const uint2 *r, uint32_t n, uint32_t anchor) -> bool {
@@ -989,7 +997,7 @@ __global__ __launch_bounds__(kNW * 64) void zstd_parse_split_kernel(tyche_batch_
                 __builtin_amdgcn_wave_barrier();
                 return true;
             };
-            const uint32_t cur = lzp::parse_page<true, false, kZWays>(in, Lp, table, rec, lane, sink, b0);
+            const uint32_t cur = lzp::parse_page<true, false, kZWays>(in, Lp, table, rec, lane, sink, b0, rep);
             if (lane == 0) {
                 hdr->ok[wave] = cur != 0xFFFFFFFFu ? 1u : 0u;
                 hdr->n[wave] = nseq;
@@ -1331,7 +1339,8 @@ hipError_t launch_zstd_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream
             unsigned *cp = ctr.get();
             size_t fst = first, cnt = n, wpage = page_bytes;
             uint32_t icap = in_cap;
-            void *args[] = {(void *)&b, &fst, &cnt, &icap, &cp, &ws, &wpage, &st};
+            uint32_t seed = (uint32_t)std::max(0L, knob("ZSTD_PARSE_SEED", kZSeed)) & ~(kWave - 1u);
+            void *args[] = {(void *)&b, &fst, &cnt, &icap, &cp, &ws, &wpage, &st, &seed};
             (void)hipLaunchKernel(kp, dim3((unsigned)g), dim3((unsigned)(pw * kWave)), args, ldsp, s);
         } else {
             const size_t g = std::min<size_t>(n, ncu * cu1);
