@@ -193,7 +193,12 @@ size_t tyche_plan_split(size_t n, const uint32_t *src_lengths, int ndev, uint64_
 /* Kernel-path switches and tunables (names without the TYCHE_ prefix, e.g.
  * "LZ4_LANE_MIN", "ZLIB_PAR"): the library reads TYCHE_<name> from the
  * environment once and checks for an override on every launch.  Set / drop an
- * in-process override; for tests and A/B timing -- no knob changes a result. */
+ * in-process override; for tests and A/B timing.  No knob changes a decode
+ * result; encoder-shape knobs (LZ4_ENC_WAVES, ZSTD_PARSE_WAVES, ZSTD_FSE_LOG)
+ * change the compressed bytes and ratio, never whether they decode to the page.
+ * Two are test hooks: FAIL_COMPRESS_EVERY=N fails every Nth compress launch
+ * (TYCHE_E_DEVICE, the device-failure test) and LOG_ERRORS=1 prints engine
+ * errors to stderr. */
 int tyche_set_knob(const char *name, long value);
 int tyche_clear_knob(const char *name);
 /* Diagnostics: host-path stage clocks since the last call, then reset -- out[0..6] = ns waiting for

@@ -506,34 +506,98 @@ def test_decode_huffman_tablelog12(tc, oracle_mod):
     assert all(out[i].cpu().numpy().tobytes() == want for i in range(4))
 
 
-@pytest.mark.parametrize("mode", ["fused", "chunked", "inline"])
+DECODE_MODES = {
+    "fused": dict(ZSTD_SPLIT=0),
+    "chunked": dict(ZSTD_SCRATCH_MB=1, ZSTD_SPLIT_MIN=1),   # every batch, however small, through the split
+    "inline": dict(ZSTD_JOBS=0, ZSTD_SPLIT_MIN=1),
+    # pass 2 one page per lane at every batch size: chains and execution fused (the default for
+    # large batches), with log-6 LDS slots, through 1 MiB chunks; and the entry-plane lane kernel
+    "seqexec": dict(ZSTD_EXEC_LANE_MIN=0),
+    "seqexec_slots6": dict(ZSTD_EXEC_LANE_MIN=0, ZSTD_SEQ_SLOTS=6),
+    "seqexec_chunked": dict(ZSTD_EXEC_LANE_MIN=0, ZSTD_SCRATCH_MB=1),
+    "lane_exec": dict(ZSTD_EXEC_LANE_MIN=0, ZSTD_SEQEXEC=0),
+}
+
+
+@pytest.mark.parametrize("mode", list(DECODE_MODES))
 def test_zstd_fused_kernel_and_chunked_split(tc, oracle_mod, knobs, mode):
-    """The fused one-kernel decoder (TYCHE_ZSTD_SPLIT=0), the split decoder on every batch size
-    (TYCHE_ZSTD_SPLIT_MIN=1) run through a 1 MiB pass-1 buffer (TYCHE_ZSTD_SCRATCH_MB=1: a handful of
-    pages per chunk) and the split decoder with the sequence chains inline in pass 1
-    (TYCHE_ZSTD_JOBS=0) give the verdicts and bytes of the default path on the reference frames,
-    the malformed set and the fuzz corpus."""
-    if mode == "fused":
-        knobs(ZSTD_SPLIT=0)
-    elif mode == "chunked":
-        knobs(ZSTD_SCRATCH_MB=1, ZSTD_SPLIT_MIN=1)   # every batch, however small, through the split
-    else:
-        knobs(ZSTD_JOBS=0, ZSTD_SPLIT_MIN=1)
+    """Every decode path gives the verdicts and bytes of the oracle on the reference frames, the
+    malformed set and the fuzz corpus: the fused one-kernel decoder (TYCHE_ZSTD_SPLIT=0), the split
+    decoder through a 1 MiB pass-1 buffer (TYCHE_ZSTD_SCRATCH_MB=1: a handful of pages per chunk),
+    with the sequence chains inline in pass 1 (TYCHE_ZSTD_JOBS=0), and the lane-per-page second
+    passes (zstd_seqexec_kernel with both LDS slot sizes, zstd_exec_lane_kernel) on batches of
+    any size."""
+    knobs(**DECODE_MODES[mode])
     test_zstd_reference_frames(tc, 3)
     test_zstd_malformed(tc, oracle_mod)
     test_zstd_fuzz_vs_oracle(tc, oracle_mod)
 
 
-@pytest.mark.parametrize("mode", ["fused", "chunked"])
+def _raw_block_frame(data, nblocks, rle_every=0):
+    """A single-segment zstd frame of `data` cut into nblocks raw blocks (every rle_every-th block an
+    RLE block of its first byte repeated, the data adjusted to match)."""
+    data = bytearray(data)
+    n = len(data)
+    assert 256 <= n < 65536 + 256
+    out = bytearray((0xFD2FB528).to_bytes(4, "little")) + bytes([0x60]) + (n - 256).to_bytes(2, "little")
+    cuts = [n * k // nblocks for k in range(nblocks + 1)]
+    for k in range(nblocks):
+        a, b = cuts[k], cuts[k + 1]
+        last = 1 if k == nblocks - 1 else 0
+        if rle_every and k % rle_every == 0 and b > a:
+            data[a:b] = bytes([data[a]]) * (b - a)
+            out += (last | (1 << 1) | ((b - a) << 3)).to_bytes(3, "little") + bytes([data[a]])
+        else:
+            out += (last | ((b - a) << 3)).to_bytes(3, "little") + bytes(data[a:b])
+    return bytes(out), bytes(data)
+
+
+@pytest.mark.parametrize("mode", ["seqexec", "seqexec_chunked", "lane_exec"])
+def test_zstd_many_block_pages(tc, knobs, mode):
+    """Pages with more block commands than the fused layout holds (kFusedCmds = 64) are left by
+    pass 1 to the one-wave kernel after pass 2 (kRetryFused); mixed with ordinary pages in one batch,
+    every page decodes to its bytes, capacity failures included."""
+    knobs(**DECODE_MODES[mode])
+    rng = np.random.default_rng(77)
+    pages = tc.pagegen(64, 8192, dist=0, device=DEV)
+    comp, clen = tc.compress_pages(pages, compressor_id=ZSTD)
+    torch.cuda.synchronize()
+    host = pages.cpu().numpy()
+    streams, caps, want = [], [], []
+    for i in range(64):
+        if i % 3 == 0:
+            nb = int(rng.choice([60, 63, 64, 65, 100, 300]))
+            f, d = _raw_block_frame(host[i].tobytes(), nb, rle_every=int(rng.choice([0, 4])))
+        else:
+            f, d = comp[i, :int(clen[i])].cpu().numpy().tobytes(), host[i].tobytes()
+        cap = len(d) if i % 7 else len(d) - 1   # every 7th page one byte short: a capacity failure
+        streams.append(f)
+        caps.append(cap)
+        want.append(d)
+    rv, outs = ragged_decode(tc, streams, caps)
+    for i in range(64):
+        if caps[i] < len(want[i]):
+            assert rv[i] < 0, (i, rv[i])
+        else:
+            assert rv[i] == len(want[i]), (i, rv[i])
+            assert outs[i] == want[i], i
+
+
+@pytest.mark.parametrize("mode", ["fused", "chunked", "fse_log6", "fused_fse_log6"])
 def test_zstd_encode_fused_kernel_and_chunked_split(tc, oracle_mod, knobs, mode):
     """The one-kernel encoder (TYCHE_ZSTD_ENC_SPLIT=0) and the three-pass encoder run through a
-    1 MiB work area (TYCHE_ZSTD_SCRATCH_MB=1: a few pages per chunk) produce frames the reference
-    decodes: round trips over several distributions and sizes, multi-block and incompressible
-    pages, tight capacities."""
+    1 MiB work area (TYCHE_ZSTD_SCRATCH_MB=1: a few pages per chunk), each also with round 2's fixed
+    6/5/6 sequence-table logs (TYCHE_ZSTD_FSE_LOG=6), produce frames the reference decodes: round
+    trips over several distributions and sizes, multi-block and incompressible pages, tight
+    capacities."""
     if mode == "fused":
         knobs(ZSTD_ENC_SPLIT=0)
-    else:
+    elif mode == "chunked":
         knobs(ZSTD_SCRATCH_MB=1, ZSTD_SPLIT_MIN=1)
+    elif mode == "fse_log6":
+        knobs(ZSTD_FSE_LOG=6)
+    else:
+        knobs(ZSTD_ENC_SPLIT=0, ZSTD_FSE_LOG=6)
     for dist in (0, 3):
         for plen in (8192, 32768):
             test_encode_roundtrip_reference_decoder(tc, oracle_mod, dist, plen)

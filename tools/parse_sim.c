@@ -5,7 +5,7 @@
  * symbol histograms (optimal code lengths, extra bits, a fixed header estimate), compared with the
  * system zlib's compress2 level 1 (byte-identical to the reference's zlib 1.2.8 at level 1).
  *
- *   gcc -O2 -o /tmp/parse_sim tools/parse_sim.c -lz && /tmp/parse_sim [pages] [page_len] [zstd]
+ *   gcc -O2 -o /tmp/parse_sim tools/parse_sim.c -lz -lm && /tmp/parse_sim [pages] [page_len] [zstd]
  * (zstd: the same for zstd level 1's fast parse, ZSTD_compressBlock_fast_generic, and the device's
  * repeat-candidate parse at several table shapes)
  */
@@ -237,6 +237,54 @@ static double entropy_bits(const uint32_t *h, int n) {
         if (h[i]) b -= h[i] * __builtin_log2((double)h[i] / tot);
     return b;
 }
+/* opt_fse 0: ideal entropy + a fixed 12-byte header per table; otherwise FSE-normalized costs at table
+ * logs (opt_fse 1: ours, LL 6 / OF 5 / ML 6; 2: the reference's FSE_optimalTableLog choice) plus an
+ * estimate of the NCount header (FSE_writeNCount's variable-width fields, zero runs at 2 bits per 3) */
+static int opt_fse;
+static int hb32(uint32_t v) { return 31 - __builtin_clz(v); }
+static double fse_bits(const uint32_t *h, int n, int maxlog) {
+    double tot = 0;
+    int mx = 0;
+    for (int i = 0; i < n; i++) { tot += h[i]; if (h[i]) mx = i; }
+    if (tot == 0) return 0;
+    if (opt_fse == 0) return entropy_bits(h, n) + 12 * 8;
+    int tl = maxlog;
+    if (opt_fse >= 2) {
+        const uint32_t src = (uint32_t)tot;
+        const int maxsrc = src > 1 ? hb32(src - 1) - 2 : 1;
+        const int minb = (hb32(src) + 1) < (hb32((uint32_t)mx ? (uint32_t)mx : 1u) + 2) ? hb32(src) + 1 : hb32((uint32_t)mx ? (uint32_t)mx : 1u) + 2;
+        if (maxsrc < tl) tl = maxsrc;
+        if (minb > tl) tl = minb;
+        if (tl < 5) tl = 5;
+        if (opt_fse == 3 && tl > maxlog - 2) tl = maxlog - 2;   /* capped at 7 / 6 / 7 */
+        if (opt_fse == 4 && tl > maxlog - 1) tl = maxlog - 1;   /* capped at 8 / 7 / 8 */
+    }
+    const int cells = 1 << tl;
+    int norm[64] = {0}, sum = 0, big = 0;
+    for (int i = 0; i < n; i++) {
+        if (!h[i]) continue;
+        int v = (int)(h[i] * (double)cells / tot + 0.5);
+        if (v < 1) v = 1;
+        norm[i] = v;
+        sum += v;
+        if (h[i] > h[big] || !h[big]) big = i;
+    }
+    norm[big] += cells - sum;
+    if (norm[big] < 1) norm[big] = 1;
+    double bits = 0;
+    for (int i = 0; i < n; i++) if (h[i]) bits += h[i] * (tl - __builtin_log2((double)norm[i]));
+    /* header */
+    double hdr = 4;
+    int remaining = cells + 1, nb = tl + 1, zrun = 0;
+    for (int i = 0; i <= mx && remaining > 1; i++) {
+        if (!norm[i]) { zrun++; continue; }
+        if (zrun) { hdr += 2.0 * ((zrun + 2) / 3); zrun = 0; }
+        hdr += nb;
+        remaining -= norm[i];
+        while (remaining < (1 << (nb - 1)) && nb > 1) nb--;
+    }
+    return bits + hdr;
+}
 static void zlit_add(uint32_t a, uint32_t b) {
     for (uint32_t i = a; i < b; i++) zlit[pg[i]]++;
     zlits += b - a;
@@ -276,8 +324,9 @@ static double zstd_cost(void) {
         extra += zll_bits[lc] + zml_bits[mc] + oc;
     }
     const double lit_bits = huff_bits(zlit, 256);
-    const double bits = lit_bits + entropy_bits(hl, 36) + entropy_bits(hm, 53) + entropy_bits(ho, 32) + extra;
-    return bits / 8 + 6 + 3 + 5 + 6 + 45 + 3 * 12;   /* frame + block + literal headers, jump table, HUF + 3 FSE tables */
+    const double bits = lit_bits + fse_bits(hl, 36, opt_fse == 1 ? 6 : 9) + fse_bits(hm, 53, opt_fse == 1 ? 6 : 9) +
+                        fse_bits(ho, 32, opt_fse == 1 ? 5 : 8) + extra;
+    return bits / 8 + 6 + 3 + 5 + 6 + 45;   /* frame + block + literal headers, jump table, HUF table */
 }
 static void zreset(void) { nzs = 0; zlits = 0; memset(zlit, 0, sizeof zlit); }
 
@@ -442,7 +491,8 @@ static double parse_zstd_device(uint32_t nb, uint32_t ways, uint32_t hb) {
 }
 
 static int main_zstd_split(int n) {
-    double raw = 0, d[4] = {0}, dw[4] = {0};
+    double raw = 0, d[4] = {0}, dw[4] = {0}, ds[6] = {0};
+    const uint32_t sp[6] = {2, 2, 2, 4, 4, 4}, ss[6] = {8192, 16384, 1u << 20, 8192, 16384, 1u << 20};
     const uint32_t warms[4] = {256, 512, 1024, 2048};
     const uint32_t parts[4] = {1, 2, 4, 4}, seeds[4] = {1u << 20, 1u << 20, 1u << 20, 1u << 20};
     for (int i = 0; i < n; i++) {
@@ -461,12 +511,17 @@ static int main_zstd_split(int n) {
             opt_parts = 4; opt_seed = 1u << 20; opt_carry_rep = 0; opt_warm = warms[c];
             dw[c] += parse_zstd_device(1856, 2, 5);
         }
+        for (int c = 0; c < 6; c++) {
+            opt_parts = sp[c]; opt_seed = ss[c]; opt_carry_rep = 0; opt_warm = 256;
+            ds[c] += parse_zstd_device(1856, 2, 5);
+        }
         opt_warm = 0;
     }
     opt_parts = 1;
     opt_seed = 1u << 20;
     for (int c = 0; c < 4; c++) printf("model: device parse in %u parts, seed %u%s: ratio %.3f\n", parts[c], seeds[c], c == 3 ? ", repeat offsets carried" : "", raw / d[c]);
     for (int c = 0; c < 4; c++) printf("model: device parse in 4 parts, warm-up parse of %u bytes before each: ratio %.3f\n", warms[c], raw / dw[c]);
+    for (int c = 0; c < 6; c++) printf("model: device parse in %u parts, hash seed %u bytes, warm-up 256: ratio %.3f\n", sp[c], ss[c], raw / ds[c]);
     return 0;
 }
 
@@ -491,11 +546,35 @@ static int main_zstd(int n) {
     return 0;
 }
 
+static int main_zstd_fse(int n) {
+    double raw = 0, d[5] = {0}, r[5] = {0};
+    const uint32_t hbits = L <= 16384 ? 14 : 13;
+    for (int i = 0; i < n; i++) {
+        pg_page_t p;
+        pg_page_init(&p, 20170303ull, (uint64_t)i, L, 0);
+        for (uint32_t b = 0; b < L; b++) pg[b] = (uint8_t)pg_page_byte(&p, b);
+        memset(pg + L, 0, 64);
+        raw += L;
+        for (int m = 0; m < 5; m++) {
+            opt_fse = m;
+            d[m] += parse_zstd_device(1856, 2, 5);
+            r[m] += parse_zstd_fast(hbits, 6);
+        }
+    }
+    opt_fse = 0;
+    static const char *nm[5] = {"ideal entropy", "FSE logs 6/5/6", "FSE optimal logs (<= 9/8/9)",
+                                "FSE optimal logs (<= 7/6/7)", "FSE optimal logs (<= 8/7/8)"};
+    printf("pages %d x %u B (zstd sequence tables)\n", n, L);
+    for (int m = 0; m < 5; m++) printf("model: %-28s device parse %.3f   level-1 parse %.3f\n", nm[m], raw / d[m], raw / r[m]);
+    return 0;
+}
+
 int main(int argc, char **argv) {
     const int n = argc > 1 ? atoi(argv[1]) : 200;
     L = argc > 2 ? (uint32_t)atoi(argv[2]) : 16384;
     if (argc > 3 && !strcmp(argv[3], "zstd")) return main_zstd(n);
     if (argc > 3 && !strcmp(argv[3], "zsplit")) return main_zstd_split(n);
+    if (argc > 3 && !strcmp(argv[3], "zfse")) return main_zstd_fse(n);
     static const uint32_t grid[][2] = {{1024, 4}, {2048, 4}, {512, 8}, {1024, 8}, {2048, 8}, {1024, 6}, {4096, 8}};
     const int ng = (int)(sizeof grid / sizeof grid[0]);
     double raw = 0, zl = 0, zf = 0, var[16] = {0}, var_r[16] = {0};

@@ -404,32 +404,42 @@ __device__ __forceinline__ void bw_flush(BitW &b, uint8_t *dst, uint32_t lane) {
     b.c = nbytes >= 8u ? 0ull : b.c >> (8u * nbytes);
 }
 
-// An FSE table over at most 16 symbols, log <= 6, held in lanes: lane u has
-// state[u]; lane s has the symbol transform of symbol s.
+// An FSE table of log <= 7 (at most 64 symbols) held in lanes: lane u has
+// stateTable[u] (state) and stateTable[64 + u] (state_hi); lane s has the
+// symbol transform of symbol s.
 struct SmallCT {
-    uint32_t state;   // stateTable entry of this lane
-    uint32_t dnb;     // deltaNbBits of symbol `lane`
-    int32_t dfs;      // deltaFindState of symbol `lane`
+    uint32_t state;      // stateTable entry u of this lane
+    uint32_t state_hi;   // stateTable entry 64 + u (log 7)
+    uint32_t dnb;        // deltaNbBits of symbol `lane`
+    int32_t dfs;         // deltaFindState of symbol `lane`
     uint32_t log;
 };
 
-// FSE_buildCTable_wksp (fse_compress.c) for norm[], log <= 6; -1 entries
+// FSE_buildCTable_wksp (fse_compress.c) for norm[], log <= 7; -1 entries
 // (low-probability symbols) take one cell each at the top of the table.
-// norm_l: lane s holds norm[s] (0 beyond max_sv).
-__device__ SmallCT build_small_ct(int32_t norm_l, uint32_t max_sv, uint32_t log, uint32_t lane) {
+// norm_l: lane s holds norm[s] (0 beyond max_sv).  A log-7 table goes through
+// scr (128 LDS bytes of the caller's scratch) for its state scatter.
+__device__ SmallCT build_small_ct(int32_t norm_l, uint32_t max_sv, uint32_t log, uint32_t lane, uint8_t *scr = nullptr) {
     const uint32_t size = 1u << log, mask = size - 1u, step = (size >> 1) + (size >> 3) + 3u;
     // low-probability cells from the top, then the spread (uniform serial walk);
-    // lane u ends up with tableSymbol[u]
-    uint32_t tsym = 0, pos = 0, high = size - 1u;
+    // lane u ends up with tableSymbol[u] (tsym) and tableSymbol[64 + u] (tsym_hi)
+    uint32_t tsym = 0, tsym_hi = 0, pos = 0, high = size - 1u;
+    auto put = [&](uint32_t cell, uint32_t s) {
+        if (cell < 64u) {
+            if (lane == cell) tsym = s;
+        } else if (lane == cell - 64u) {
+            tsym_hi = s;
+        }
+    };
     for (uint32_t s = 0; s <= max_sv; s++)
         if ((int32_t)rdlane((uint32_t)norm_l, s) == -1) {
-            if (lane == high) tsym = s;
+            put(high, s);
             high--;
         }
     for (uint32_t s = 0; s <= max_sv; s++) {
         const int32_t n = (int32_t)rdlane((uint32_t)norm_l, s);
         for (int32_t i = 0; i < n; i++) {
-            if (lane == pos) tsym = s;
+            put(pos, s);
             pos = (pos + step) & mask;
             while (pos > high) pos = (pos + step) & mask;
         }
@@ -438,17 +448,31 @@ __device__ SmallCT build_small_ct(int32_t norm_l, uint32_t max_sv, uint32_t log,
     const int32_t cells = lane <= max_sv ? (norm_l == -1 ? 1 : norm_l) : 0;
     const int32_t incl = wave_incl_sum(cells);
     const uint32_t cum_l = (uint32_t)(incl - cells);
-    // stateTable[cumul[s] + rank of u among cells of s] = size + u
+    // stateTable[cumul[s] + rank of cell u among the cells of s] = size + u
     const uint64_t lt = lane ? (~0ull >> (64u - lane)) : 0ull;
-    uint32_t idx = lane;   // lanes past the table permute onto themselves
+    const bool lo_ok = lane < size, hi_ok = 64u + lane < size;
+    uint32_t idx = lane, idx_hi = 0;   // lanes past the table permute onto themselves
     for (uint32_t s = 0; s <= max_sv; s++) {
-        const uint64_t m = __ballot(lane < size && tsym == s);
-        if (lane < size && tsym == s) idx = rdlane(cum_l, s) + (uint32_t)__popcll(m & lt);
+        const uint64_t m = __ballot(lo_ok && tsym == s);
+        const uint64_t mh = __ballot(hi_ok && tsym_hi == s);
+        if (lo_ok && tsym == s) idx = rdlane(cum_l, s) + (uint32_t)__popcll(m & lt);
+        if (hi_ok && tsym_hi == s) idx_hi = rdlane(cum_l, s) + (uint32_t)__popcll(m) + (uint32_t)__popcll(mh & lt);
     }
     SmallCT t;
-    // scatter: lane idx receives size + u (ds_permute: the value goes to lane `addr / 4`)
-    t.state = (uint32_t)__builtin_amdgcn_ds_permute((int32_t)(idx * 4u), (int32_t)(size + lane));
-    if (lane >= size) t.state = 0;
+    if (size <= 64u) {
+        // scatter: lane idx receives size + u (ds_permute: the value goes to lane `addr / 4`)
+        t.state = (uint32_t)__builtin_amdgcn_ds_permute((int32_t)(idx * 4u), (int32_t)(size + lane));
+        if (lane >= size) t.state = 0;
+        t.state_hi = 0;
+    } else {
+        __builtin_amdgcn_wave_barrier();
+        scr[idx] = (uint8_t)(size + lane);
+        scr[idx_hi] = (uint8_t)(size + 64u + lane);
+        __builtin_amdgcn_wave_barrier();
+        t.state = scr[lane];
+        t.state_hi = scr[64u + lane];
+        __builtin_amdgcn_wave_barrier();
+    }
     // symbol transforms
     t.dnb = 0;
     t.dfs = 0;
@@ -467,16 +491,31 @@ __device__ SmallCT build_small_ct(int32_t norm_l, uint32_t max_sv, uint32_t log,
     return t;
 }
 
+// stateTable[i] for a wave-uniform i
+__device__ __forceinline__ uint32_t ct_state(const SmallCT &t, uint32_t i) {
+    return i < 64u ? rdlane(t.state, i) : rdlane(t.state_hi, i - 64u);
+}
 __device__ __forceinline__ uint32_t ct_init2(const SmallCT &t, uint32_t sym) {
     const uint32_t dnb = rdlane(t.dnb, sym);
     const uint32_t nbo = (dnb + (1u << 15)) >> 16;
     const uint32_t v = (nbo << 16) - dnb;
-    return rdlane(t.state, (uint32_t)((int32_t)(v >> nbo) + (int32_t)rdlane((uint32_t)t.dfs, sym)));
+    return ct_state(t, (uint32_t)((int32_t)(v >> nbo) + (int32_t)rdlane((uint32_t)t.dfs, sym)));
 }
 __device__ __forceinline__ void ct_encode(BitW &b, uint32_t &st, const SmallCT &t, uint32_t sym) {
     const uint32_t nbo = (st + rdlane(t.dnb, sym)) >> 16;
     bw_add(b, st, nbo);
-    st = rdlane(t.state, (uint32_t)((int32_t)(st >> nbo) + (int32_t)rdlane((uint32_t)t.dfs, sym)));
+    st = ct_state(t, (uint32_t)((int32_t)(st >> nbo) + (int32_t)rdlane((uint32_t)t.dfs, sym)));
+}
+
+// FSE_optimalTableLog_internal (fse_compress.c:479-498) for n >= 2 symbols
+// coded, max_sv the largest, the accuracy capped at max_log
+__device__ __forceinline__ uint32_t optimal_log(uint32_t max_log, uint32_t n, uint32_t max_sv, uint32_t minus) {
+    uint32_t log = max_log;
+    const uint32_t max_bits_src = hb(n - 1u) - minus;
+    const uint32_t min_bits = min(hb(n - 1u) + 1u, hb(max_sv ? max_sv : 1u) + 2u);
+    if (max_bits_src < log) log = max_bits_src;
+    if (min_bits > log) log = min_bits;
+    return min(max(log, 5u), 12u);
 }
 
 // FSE_writeNCount (fse_compress.c, generic path) for norm_l (lane s = norm[s],
@@ -581,13 +620,7 @@ __device__ uint32_t compress_weights(const uint8_t *w, uint32_t n, uint8_t *dst,
     const uint32_t max_cnt = (uint32_t)wave_max((int32_t)cnt);
     if (max_cnt == n) return 1;
     if (max_cnt == 1u) return 0;
-    // FSE_optimalTableLog(6, n, max_sv)
-    uint32_t log = 6;
-    const uint32_t max_bits_src = hb(n - 1u) - 2u;
-    const uint32_t min_bits = min(hb(n - 1u) + 1u, hb(max_sv) + 2u);
-    if (max_bits_src < log) log = max_bits_src;
-    if (min_bits > log) log = min_bits;
-    log = min(max(log, 5u), 12u);
+    const uint32_t log = optimal_log(6, n, max_sv, 2);   // FSE_optimalTableLog(6, n, max_sv)
     int32_t norm;
     if (!normalize(cnt, n, log, norm, lane)) return 0;
     uint32_t op = o + write_ncount(norm, max_sv, log, dst, o, lane);

@@ -35,6 +35,7 @@
 #include <hip/hip_runtime.h>
 
 #include "engine.h"
+#include "lane_ring.h"
 #include "lds_io.h"
 
 #include <algorithm>
@@ -43,41 +44,6 @@
 namespace tyche {
 
 namespace {
-
-typedef unsigned __int128 u128;
-typedef u32x4 u32x4_ua __attribute__((aligned(1)));
-typedef __attribute__((address_space(1))) u32x4_ua g_u32x4_ua;
-typedef __attribute__((address_space(1))) uint8_t g_u8;
-typedef __attribute__((address_space(1))) uint64_t g_u64_ua __attribute__((aligned(1)));
-
-__device__ __forceinline__ u128 ld16(const uint8_t *p) {
-    u32x4 v = *(const g_u32x4_ua *)(uintptr_t)p;
-    return __builtin_bit_cast(u128, v);
-}
-// Cache-policy experiments (-DTYCHE_ABLATE, tools/time_decode.py over
-// libtyche_codec_ablN.so): 16 = non-temporal stream loads, 32 = non-temporal
-// line flushes.
-#ifndef TYCHE_ABLATE
-#define TYCHE_ABLATE 0
-#endif
-__device__ __forceinline__ u128 ld16s(const uint8_t *p) {
-    if (TYCHE_ABLATE & 16) return __builtin_bit_cast(u128, __builtin_nontemporal_load((const g_u32x4_ua *)(uintptr_t)p));
-    return ld16(p);
-}
-__device__ __forceinline__ uint64_t ld8(const uint8_t *p) { return *(const g_u64_ua *)(uintptr_t)p; }
-__device__ __forceinline__ void st16(uint8_t *p, u128 v) {
-    *(g_u32x4_ua *)(uintptr_t)p = __builtin_bit_cast(u32x4, v);
-}
-__device__ __forceinline__ void st16f(uint8_t *p, u128 v) {
-    if (TYCHE_ABLATE & (128 | 256)) return;   // 128: no line flushes, 256: parse only (timing; wrong output)
-    if (TYCHE_ABLATE & 32) {
-        __builtin_nontemporal_store(__builtin_bit_cast(u32x4, v), (g_u32x4_ua *)(uintptr_t)p);
-        return;
-    }
-    st16(p, v);
-}
-__device__ __forceinline__ uint32_t ld1(const uint8_t *p) { return *(const g_u8 *)(uintptr_t)p; }
-__device__ __forceinline__ void st1(uint8_t *p, uint32_t v) { *(g_u8 *)(uintptr_t)p = (uint8_t)v; }
 
 // 32-byte stream window at ip, zero past L (windowN<16> below is the default
 // 16-byte one).  The parse of a sequence reads its token, length bytes, short
@@ -241,56 +207,7 @@ __device__ int32_t decode_lane(const uint8_t *__restrict__ in, int32_t L, uint8_
 // bench pages: offset <= kRing - 32) never touch HBM; the others read the
 // page's already-flushed bytes back from HBM.
 // kRing: ring bytes per lane (a multiple of 16); stride adds 16 B front slack and
-// 32 B tail slack; offsets up to kRing - 32 read the ring
-#ifndef TYCHE_LANE_LINE
-#define TYCHE_LANE_LINE 64
-#endif
-// HBM flush granule (128-byte lines at the 256-byte ring: 34.04-34.08 vs
-// 34.14-34.65 ms per 1M pages with 64, within noise): the unflushed tail stays below kLine + 16 bytes, so far
-// reads (offset > kRing - 32) need kRing >= kLine + 64
-template <int32_t kRing>
-constexpr int32_t line_for() { return kRing >= TYCHE_LANE_LINE + 64 ? TYCHE_LANE_LINE : 64; }
-
-typedef __attribute__((address_space(3))) u32x4_ua l_u32x4_ua;
-__device__ __forceinline__ u128 lds16(const uint8_t *p) {
-    return __builtin_bit_cast(u128, *(const l_u32x4_ua *)(const __attribute__((address_space(3))) uint8_t *)p);
-}
-__device__ __forceinline__ void lds16(uint8_t *p, u128 v) {
-    *(l_u32x4_ua *)(__attribute__((address_space(3))) uint8_t *)p = __builtin_bit_cast(u32x4, v);
-}
-// 16 bytes of the ring at page position x (valid for any x: the 16 bytes past
-// the ring's end mirror its first 16)
-template <int32_t kRing>
-__device__ __forceinline__ u128 ring_rd(uint8_t *rb, int32_t x) { return lds16(rb + ((int32_t)((uint32_t)x % (uint32_t)kRing))); }
-template <int32_t kRing>
-__device__ __forceinline__ void ring_wr(uint8_t *rb, int32_t x, u128 v) {
-    if (TYCHE_ABLATE & 256) return;
-    const int32_t q = (int32_t)((uint32_t)x % (uint32_t)kRing);
-    lds16(rb + q, v);
-    if (q + 16 > kRing) lds16(rb + q - kRing, v);   // wrapped part, to the ring's start
-    if (q < 16) lds16(rb + q + kRing, v);           // mirror of the start, past the end
-}
-// write out the whole lines of [fl, fin)
-template <int32_t kRing>
-__device__ __forceinline__ void ring_flush(uint8_t *rb, uint8_t *__restrict__ out, int32_t &fl, int32_t fin) {
-    constexpr int32_t kLine = line_for<kRing>();
-    static_assert(kRing >= kLine + 64, "ring too small for the flush granule");
-    while (fin - fl >= kLine) {
-#pragma unroll
-        for (int32_t j = 0; j < kLine; j += 16) st16f(out + fl + j, ring_rd<kRing>(rb, fl + j));
-        fl += kLine;
-    }
-}
-template <int32_t kRing>
-__device__ __forceinline__ void ring_flush_all(uint8_t *rb, uint8_t *__restrict__ out, int32_t &fl, int32_t fin) {
-    ring_flush<kRing>(rb, out, fl, fin);
-    for (; fl + 16 <= fin; fl += 16) st16(out + fl, ring_rd<kRing>(rb, fl));
-    if (fl < fin) {
-        const u128 v = ring_rd<kRing>(rb, fl);
-        for (int32_t j = 0; fl + j < fin; j++) st1(out + fl + j, (uint32_t)(v >> (8 * j)) & 0xFFu);
-        fl = fin;
-    }
-}
+// 32 B tail slack; offsets up to kRing - 32 read the ring (lane_ring.h)
 __device__ __forceinline__ u128 stream16(const uint8_t *__restrict__ in, int32_t a, int32_t L) {
     return a + 16 <= L ? ld16(in + a) : window(in, a, L).lo;
 }

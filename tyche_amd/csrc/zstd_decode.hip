@@ -35,6 +35,7 @@
 #include <algorithm>
 
 #include "engine.h"
+#include "lane_ring.h"
 #include "lds_io.h"
 
 namespace tyche {
@@ -964,6 +965,8 @@ struct Ent {
     uint32_t ecap, lcap;      // entries, literal bytes
     uint32_t *jobs;           // [0] = job count, then kJobWords words per job
     uint32_t *tabs;           // FSE cells of the tables the jobs use
+    bool fused;               // zstd_seqexec_kernel's layout: commands only, no sequence entries
+    int32_t over;             // pass 1's result when the planes are full (fused: kRetryFused)
 };
 // Sequence jobs: one per compressed block with sequences, decoded by
 // zstd_seq_kernel one page per lane -- the chain is serial within a page, so the
@@ -976,19 +979,26 @@ constexpr uint32_t kTabBytes = 12u * 1024u;                       // two full LL
 constexpr uint32_t kAreaBytes = 13312u;                           // jobs + tables, 256-aligned
 constexpr uint32_t kTabDefault = 0xFFFFFFFFu;
 constexpr int32_t kRetryInline = -1000;
-__host__ __device__ inline uint32_t ent_cap(uint32_t in_cap, uint32_t out_cap) {
+// fused layout: a page with more than kFusedCmds block commands, or whose jobs do not fit
+// (kRetryInline), is decoded by the fused one-wave kernel after pass 2 (kRetryFused)
+constexpr int32_t kRetryFused = -1001;
+constexpr uint32_t kFusedCmds = 64;
+__host__ __device__ inline uint32_t ent_cap(uint32_t in_cap, uint32_t out_cap, bool fused) {
+    if (fused) return kFusedCmds;
     return ((in_cap / 3u + out_cap / 3u + 72u) + 15u) & ~15u;   // multiple of 16: planes and literals 64-aligned
 }
 __host__ __device__ inline uint32_t lit_cap(uint32_t out_cap) { return out_cap + 16u * (out_cap / 64u + 2u) + 64u; }
-__host__ __device__ inline size_t ent_page_bytes(uint32_t in_cap, uint32_t out_cap) {
-    return kAreaBytes + (((size_t)ent_cap(in_cap, out_cap) * 12u + lit_cap(out_cap) + 255u) & ~(size_t)255u);
+__host__ __device__ inline size_t ent_page_bytes(uint32_t in_cap, uint32_t out_cap, bool fused) {
+    return kAreaBytes + (((size_t)ent_cap(in_cap, out_cap, fused) * 12u + lit_cap(out_cap) + 255u) & ~(size_t)255u);
 }
-__device__ inline Ent ent_of(uint8_t *area, uint32_t in_cap, uint32_t out_cap) {
+__device__ inline Ent ent_of(uint8_t *area, uint32_t in_cap, uint32_t out_cap, bool fused) {
     Ent E;
     E.jobs = (uint32_t *)area;
     E.tabs = (uint32_t *)(area + kJobBytes);
+    E.fused = fused;
+    E.over = fused ? kRetryFused : kErr;
     uint8_t *base = area + kAreaBytes;
-    E.ecap = ent_cap(in_cap, out_cap);
+    E.ecap = ent_cap(in_cap, out_cap, fused);
     E.lcap = lit_cap(out_cap);
     E.ll = (uint32_t *)base;
     E.ml = E.ll + E.ecap;
@@ -1148,7 +1158,7 @@ __device__ int32_t decode_block(const Work &W, SeqTables &T, const Ent &E, uint3
     int32_t mlsum = 0;   // kSplit: sum of match lengths (the block's output is lsize + mlsum)
     if constexpr (kSplit) {
         litc = lat + (uint32_t)lsize;
-        if (ecur >= E.ecap) return kErr;
+        if (ecur >= E.ecap) return E.over;
         cmd_at = ecur++;
     }
     if (nbseq) {
@@ -1184,7 +1194,7 @@ __device__ int32_t decode_block(const Work &W, SeqTables &T, const Ent &E, uint3
                     !publish_table(E, T, W.of, (modes >> 4) & 3u, T.of_log, T.of_off, lane) ||
                     !publish_table(E, T, W.ml, (modes >> 2) & 3u, T.ml_log, T.ml_off, lane) || T.njobs >= kMaxJobs)
                     return kRetryInline;
-                if ((uint32_t)nbseq > E.ecap - ecur) return kErr;
+                if (!E.fused && (uint32_t)nbseq > E.ecap - ecur) return kErr;
                 if (lane == 0) {
                     uint32_t *J = E.jobs + 4u + T.njobs * kJobWords;
                     J[0] = (uint32_t)sp;
@@ -1197,7 +1207,7 @@ __device__ int32_t decode_block(const Work &W, SeqTables &T, const Ent &E, uint3
                     J[7] = T.ll_log | (T.of_log << 8) | (T.ml_log << 16);
                 }
                 T.njobs++;
-                ecur += (uint32_t)nbseq;
+                if (!E.fused) ecur += (uint32_t)nbseq;   // entry slots for zstd_seq_kernel
                 T.fse_entropy = true;
                 put_cmd(E, cmd_at, kCmdBlk | (lat << 2), (uint32_t)lsize, nseq_all, lane);
                 return lsize;
@@ -1262,7 +1272,7 @@ __device__ int32_t decode_block(const Work &W, SeqTables &T, const Ent &E, uint3
             SPROF_ADD(9, k);
             if (k == 0) break;
             if constexpr (kSplit) {
-                if (ecur + k > E.ecap) return kErr;
+                if (ecur + k > E.ecap) return E.over;
                 if (lane < k) {
                     E.ll[ecur + lane] = vll;
                     E.ml[ecur + lane] = vml;
@@ -1380,7 +1390,8 @@ __device__ int32_t decode_frame(const Work &W, const Ent &E, int32_t L, int32_t 
             if (csize > cap - op) return kErrDst;
             if constexpr (kSplit) {
                 const uint32_t at = lit_place(litc, (uint32_t)op, (uint32_t)csize);
-                if (at + (uint32_t)csize > E.lcap || ecur >= E.ecap) return kErr;
+                if (at + (uint32_t)csize > E.lcap) return kErr;
+                if (ecur >= E.ecap) return E.over;
                 lds_to_lit(E.lit + at, in, ip, csize, lane);
                 put_cmd(E, ecur++, kCmdRaw | (at << 2), (uint32_t)csize, 0u, lane);
                 litc = at + (uint32_t)csize;
@@ -1392,7 +1403,7 @@ __device__ int32_t decode_frame(const Work &W, const Ent &E, int32_t L, int32_t 
             if ((int64_t)csize0 > (int64_t)(cap - op)) return kErrDst;
             const uint8_t v = in[ip];
             if constexpr (kSplit) {
-                if (ecur >= E.ecap) return kErr;
+                if (ecur >= E.ecap) return E.over;
                 put_cmd(E, ecur++, kCmdRle, csize0, v, lane);
             } else {
                 for (int32_t i = (int32_t)lane; i < (int32_t)csize0; i += (int32_t)kWave) W.win[op + i] = v;
@@ -1416,7 +1427,7 @@ __device__ int32_t decode_frame(const Work &W, const Ent &E, int32_t L, int32_t 
     }
     if (remaining) return kErr;
     if constexpr (kSplit) {
-        if (ecur >= E.ecap) return kErr;
+        if (ecur >= E.ecap) return E.over;
         put_cmd(E, ecur, kCmdEnd | ((uint32_t)checksum << 2), 0u, sum, lane);
         if (lane == 0) E.jobs[0] = T.njobs;
         return 0;
@@ -1445,8 +1456,11 @@ __host__ __device__ inline Layout make_layout(uint32_t in_cap, uint32_t out_cap,
     return l;
 }
 
-__global__ __launch_bounds__(64) void zstd_decode_kernel(tyche_batch_t b, uint32_t in_cap, uint32_t out_cap, Layout lay,
-                                                         unsigned *ctr) {
+// only (optional): decode just the pages of [first, first + count) whose pass-1 status
+// only[j] is kRetryFused (the fused-layout split decode's leftovers)
+__global__ __launch_bounds__(64) void zstd_decode_kernel(tyche_batch_t b, size_t first, size_t count, uint32_t in_cap,
+                                                         uint32_t out_cap, Layout lay, unsigned *ctr,
+                                                         const int32_t *only) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t lane = threadIdx.x;
     Work W;
@@ -1461,8 +1475,8 @@ __global__ __launch_bounds__(64) void zstd_decode_kernel(tyche_batch_t b, uint32
     W.next = (uint16_t *)(smem + lay.off_next);
     W.w = smem + lay.off_w;
     uint8_t *stage = smem + lay.off_in;
-    for (size_t page = blockIdx.x; page < b.count;
-         page = ctr ? claim_page(ctr, lane) : page + gridDim.x) {   // dynamic assignment (engine.h)
+    auto do_page = [&](size_t j) {
+        const size_t page = first + j;
         const PageRef p = batch_page(b, page);
         int32_t rv;
         if (p.src_len > in_cap || p.dst_cap > out_cap) {
@@ -1483,7 +1497,20 @@ __global__ __launch_bounds__(64) void zstd_decode_kernel(tyche_batch_t b, uint32
             if (rv > 0) stage_out(p.dst, W.win, (uint32_t)rv, lane, kWave);
         }
         if (lane == 0) b.results[page] = rv;
+    };
+    if (only) {
+        // 64 statuses per read; the flagged pages in order
+        for (size_t g = (size_t)blockIdx.x * kWave; g < count; g += (size_t)gridDim.x * kWave) {
+            uint64_t m = __ballot(g + lane < count && only[g + lane] == kRetryFused);
+            while (m) {
+                const uint32_t k = (uint32_t)__builtin_ctzll(m);
+                m &= m - 1ull;
+                do_page(g + k);
+            }
+        }
+        return;
     }
+    for (size_t j = blockIdx.x; j < count; j = ctr ? claim_page(ctr, lane) : j + gridDim.x) do_page(j);   // engine.h
 }
 
 // ---- sequence jobs: one page per lane
@@ -1584,37 +1611,46 @@ __device__ __forceinline__ uint32_t gbitd_reload(BitD &b, const uint8_t *in) {
     return r;
 }
 
-// ZSTD_decompressSequences (zstd_decompress.c:1010-1060) for one job, this lane's
-// page.  Writes the decoded (litLength, matchLength, offset) triples as entries.
+// Sequence chains, one page per lane (zstd_seq_kernel, zstd_seqexec_kernel).
 //
-// kSmall (table logs <= 6/5/6, every level-1 frame of this encoder and the
-// predefined tables): the lane's three tables are copied into its LDS slot as
-// 16-bit cells (newState | symbol << 6 | nbBits << 12) and its entries are
-// staged there 16 at a time, so each plane gets whole 64-byte lines; otherwise
-// cells are gathered from the table area and entries stored one by one.
-constexpr uint32_t kSlotCells = 64u + 32u + 64u;   // LL, OF, ML
+// kLog 7 / 6 (a job whose table logs are <= kLog / kLog - 1 / kLog: every frame
+// of this encoder at TYCHE_ZSTD_FSE_LOG 7 / 6, the predefined tables): the lane's
+// three tables are copied into its LDS slot as 16-bit cells (newState | symbol <<
+// 7 | nbBits << 13); kLog 0: cells are gathered from the table area.  The
+// sequence kernel also stages its entries in LDS 16 at a time, so each plane
+// gets whole 64-byte lines (kLog 0: stored one by one).
+template <uint32_t kLog>
+struct Slots {
+    static constexpr uint32_t LL = 0u, OF = 1u << kLog, ML = (1u << kLog) + (1u << kLog >> 1);
+    static constexpr uint32_t cells = 2u * (1u << kLog) + (1u << kLog >> 1);
+};
+template <uint32_t kLog>
+__device__ __forceinline__ bool job_fits(uint32_t logs) {
+    return (logs & 255u) <= kLog && ((logs >> 8) & 255u) + 1u <= kLog && ((logs >> 16) & 255u) <= kLog;
+}
+constexpr uint32_t kSlotCells = Slots<7>::cells;   // zstd_seq_kernel
 constexpr uint32_t kSeqLds = kWave * (kSlotCells * 2u + 3u * 16u * 4u);
-__device__ __forceinline__ uint32_t cell16(uint32_t c) { return (c & 63u) | (((c >> 6) & 63u) << 16) | ((c >> 12) << 24); }
-template <bool kSmall>
-__device__ bool seq_job(const Ent &E, const uint8_t *src, const uint32_t *J, uint32_t &rep0, uint32_t &rep1,
-                        uint32_t &rep2, uint16_t *lt, uint32_t *sg) {
+__device__ __forceinline__ uint32_t cell16(uint32_t c) { return (c & 127u) | (((c >> 7) & 63u) << 16) | ((c >> 13) << 24); }
+__device__ __forceinline__ uint16_t pack16(uint32_t c) {   // area cell: newState | symbol << 16 | nbBits << 24
+    return (uint16_t)((c & 0xFFFFu) | (((c >> 16) & 0xFFu) << 7) | ((c >> 24) << 13));
+}
+// The chain of one job: pre(i) runs right after step i's bitstream load is
+// issued (the plane stores of step i - 1 go there: loads and stores share
+// vmcnt and complete in order, so waiting for the load never waits for them),
+// emit(i, litLength, matchLength, offset) after step i's sequence is decoded
+// (false: the page fails).
+template <uint32_t kLog, typename Pre, typename Emit>
+__device__ __forceinline__ bool seq_chain(const Ent &E, const uint8_t *src, const uint32_t *J, uint32_t &rep0,
+                                          uint32_t &rep1, uint32_t &rep2, uint16_t *lt, Pre &&pre, Emit &&emit) {
     const int32_t start = (int32_t)J[0], len = (int32_t)J[1];
-    const uint32_t nbseq = J[2], e0 = J[3];
+    const uint32_t nbseq = J[2];
     const uint32_t *LL = E.tabs + J[4] / 4u, *OF = E.tabs + J[5] / 4u, *ML = E.tabs + J[6] / 4u;
     const uint32_t lls = J[7] & 255u, ofs = (J[7] >> 8) & 255u, mls = (J[7] >> 16) & 255u;
-    if (kSmall) {
-        for (uint32_t u = 0; u < (1u << lls); u++) {
-            const uint32_t c = gld(LL + u);
-            lt[u] = (uint16_t)((c & 0xFFFFu) | (((c >> 16) & 0xFFu) << 6) | ((c >> 24) << 12));
-        }
-        for (uint32_t u = 0; u < (1u << ofs); u++) {
-            const uint32_t c = gld(OF + u);
-            lt[64u + u] = (uint16_t)((c & 0xFFFFu) | (((c >> 16) & 0xFFu) << 6) | ((c >> 24) << 12));
-        }
-        for (uint32_t u = 0; u < (1u << mls); u++) {
-            const uint32_t c = gld(ML + u);
-            lt[96u + u] = (uint16_t)((c & 0xFFFFu) | (((c >> 16) & 0xFFu) << 6) | ((c >> 24) << 12));
-        }
+    using S = Slots<kLog ? kLog : 7u>;
+    if (kLog) {
+        for (uint32_t u = 0; u < (1u << lls); u++) lt[S::LL + u] = pack16(gld(LL + u));
+        for (uint32_t u = 0; u < (1u << ofs); u++) lt[S::OF + u] = pack16(gld(OF + u));
+        for (uint32_t u = 0; u < (1u << mls); u++) lt[S::ML + u] = pack16(gld(ML + u));
     }
     BitD b;
     if (!gbitd_init(b, src, start, len)) return false;
@@ -1624,15 +1660,12 @@ __device__ bool seq_job(const Ent &E, const uint8_t *src, const uint32_t *J, uin
     gbitd_reload(b, src);
     uint32_t sml = bitd_read(b, mls);
     gbitd_reload(b, src);
-    // loads and stores share vmcnt and complete in order: a step's loads go out
-    // before the previous step's stores, so waiting for them never waits for those
-    uint32_t pll = 0, pml = 0, pof = 0;
     for (uint32_t i = 0; i < nbseq; i++) {
         uint32_t cl_v, cm_v, co_v;
-        if (kSmall) {
-            cl_v = cell16(lt[sll]);
-            cm_v = cell16(lt[96u + sml]);
-            co_v = cell16(lt[64u + sof]);
+        if (kLog) {
+            cl_v = cell16(lt[S::LL + sll]);
+            cm_v = cell16(lt[S::ML + sml]);
+            co_v = cell16(lt[S::OF + sof]);
         } else {
             cl_v = gld(LL + sll);
             cm_v = gld(ML + sml);
@@ -1640,11 +1673,7 @@ __device__ bool seq_job(const Ent &E, const uint8_t *src, const uint32_t *J, uin
         }
         PendLoad pl;
         const uint32_t rs = gbitd_reload_issue(b, src, pl);
-        if (!kSmall && i) {
-            E.ll[e0 + i - 1] = pll;
-            E.ml[e0 + i - 1] = pml;
-            E.of[e0 + i - 1] = pof;
-        }
+        pre(i);
         if (rs > kCompleted) return false;
         gbitd_reload_finish(b, pl);
         const uint32_t cl = cl_v, cm = cm_v, co = co_v;
@@ -1678,6 +1707,26 @@ __device__ bool seq_job(const Ent &E, const uint8_t *src, const uint32_t *J, uin
         sll = cell_state(cl) + bitd_read(b, cell_nb(cl));
         sml = cell_state(cm) + bitd_read(b, cell_nb(cm));
         sof = cell_state(co) + bitd_read(b, cell_nb(co));
+        if (!emit(i, llv, mlv, offv)) return false;
+    }
+    return true;
+}
+
+// ZSTD_decompressSequences (zstd_decompress.c:1010-1060) for one job, this lane's
+// page: the decoded (litLength, matchLength, offset) triples go to the entry planes.
+template <bool kSmall>   // kSmall: Slots<7> tables in LDS
+__device__ bool seq_job(const Ent &E, const uint8_t *src, const uint32_t *J, uint32_t &rep0, uint32_t &rep1,
+                        uint32_t &rep2, uint16_t *lt, uint32_t *sg) {
+    const uint32_t nbseq = J[2], e0 = J[3];
+    uint32_t pll = 0, pml = 0, pof = 0;
+    auto pre = [&](uint32_t i) {
+        if (!kSmall && i) {
+            E.ll[e0 + i - 1] = pll;
+            E.ml[e0 + i - 1] = pml;
+            E.of[e0 + i - 1] = pof;
+        }
+    };
+    auto emit = [&](uint32_t i, uint32_t llv, uint32_t mlv, uint32_t offv) -> bool {
         if (kSmall) {
             // stage; a full 16-entry line (or the job's last entry) goes out
             const uint32_t e = e0 + i, k = e & 15u;
@@ -1706,7 +1755,9 @@ __device__ bool seq_job(const Ent &E, const uint8_t *src, const uint32_t *J, uin
             pml = mlv;
             pof = offv;
         }
-    }
+        return true;
+    };
+    if (!seq_chain<kSmall ? 7u : 0u>(E, src, J, rep0, rep1, rep2, lt, pre, emit)) return false;
     if (!kSmall && nbseq) {
         E.ll[e0 + nbseq - 1] = pll;
         E.ml[e0 + nbseq - 1] = pml;
@@ -1721,7 +1772,7 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(tyche_batch_t b, size_t fi
                                                       uint32_t out_cap, uint8_t *ws, size_t ws_page, int32_t *st) {
     const size_t j = (size_t)blockIdx.x * kWave + threadIdx.x;
     if (j >= count || st[j] < 0) return;
-    const Ent E = ent_of(ws + j * ws_page, in_cap, out_cap);
+    const Ent E = ent_of(ws + j * ws_page, in_cap, out_cap, false);
     const uint32_t njobs = E.jobs[0];
     if (njobs == 0) return;
     const PageRef p = batch_page(b, first + j);
@@ -1732,7 +1783,7 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(tyche_batch_t b, size_t fi
     for (uint32_t q = 0; q < njobs; q++) {
         const uint32_t *J = E.jobs + 4u + q * kJobWords;
         const uint32_t logs = J[7];
-        const bool small = (logs & 255u) <= 6u && ((logs >> 8) & 255u) <= 5u && ((logs >> 16) & 255u) <= 6u;
+        const bool small = job_fits<7>(logs);
         const bool ok = small ? seq_job<true>(E, p.src, J, rep0, rep1, rep2, lt, sg)
                               : seq_job<false>(E, p.src, J, rep0, rep1, rep2, lt, sg);
         if (!ok) {
@@ -1833,10 +1884,294 @@ __device__ int32_t exec_page(uint8_t *win, const Ent &E, int32_t cap, uint32_t l
     }
 }
 
+// ---- pass 2, one page per lane (default for batches of >= TYCHE_ZSTD_EXEC_LANE_MIN pages)
+//
+// exec_page runs a page's sequences 64 at a time across the wave, but a batch's
+// matches depend on each other (the frontier loop above serialises most of
+// them) and the 32 KiB window holds a CU to 4 waves.  Here one lane replays one
+// page's entries in order -- the reference's ZSTD_execSequence loop
+// (zstd_decompress.c:940-1003) -- through a per-lane LDS ring (lane_ring.h):
+// entries and literals stream from the pass-1 buffer in HBM, near matches read
+// the ring, far ones the page's flushed lines.  Results and checks are
+// exec_page's, in the same order.
+
+// A page's entries in order, four at a time: aligned 16-byte loads of each plane
+// (planes are 64-byte aligned), the next quad in flight while this one is used.
+struct EntRd {
+    const uint32_t *ll, *ml, *of;
+    uint32_t q;   // index of quad 0's first entry
+    u32x4 a0, b0, c0, a1, b1, c1;
+};
+__device__ __forceinline__ u32x4 gquad(const uint32_t *p) { return *(g_u32x4 *)(uintptr_t)p; }
+__device__ __forceinline__ uint32_t pick(u32x4 v, uint32_t i) { return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w; }
+__device__ __forceinline__ void er_init(EntRd &r, const Ent &E) {
+    r.ll = E.ll;
+    r.ml = E.ml;
+    r.of = E.of;
+    r.q = 0;
+    r.a0 = gquad(r.ll);
+    r.b0 = gquad(r.ml);
+    r.c0 = gquad(r.of);
+    r.a1 = gquad(r.ll + 4);
+    r.b1 = gquad(r.ml + 4);
+    r.c1 = gquad(r.of + 4);
+}
+// entry i < ecap (i never decreases; the prefetch may read up to 7 entries past
+// a plane's end: the next plane, or for `of` the literal buffer)
+__device__ __forceinline__ void er_get(EntRd &r, uint32_t i, uint32_t &a, uint32_t &b, uint32_t &c) {
+    while (i >= r.q + 4) {
+        r.q += 4;
+        r.a0 = r.a1;
+        r.b0 = r.b1;
+        r.c0 = r.c1;
+        r.a1 = gquad(r.ll + r.q + 4);
+        r.b1 = gquad(r.ml + r.q + 4);
+        r.c1 = gquad(r.of + r.q + 4);
+    }
+    const uint32_t k = i - r.q;
+    a = pick(r.a0, k);
+    b = pick(r.b0, k);
+    c = pick(r.c0, k);
+}
+
+// n bytes from the literal buffer to page position op through the ring (reads
+// up to 15 bytes past the run: inside the page's area, or the lease's slack)
+template <int32_t kRing>
+__device__ __forceinline__ void lit_run(uint8_t *rb, uint8_t *__restrict__ out, int32_t &fl, int32_t op,
+                                        const uint8_t *__restrict__ src, int32_t n) {
+    for (int32_t k = 0; k < n; k += 16) {
+        ring_wr<kRing>(rb, op + k, ld16(src + k));
+        ring_flush<kRing>(rb, out, fl, op + min(k + 16, n));
+    }
+}
+
+// XXH64 (low 32 bits) of out[0, len) in HBM, one lane
+__device__ uint32_t xxh64_lane(const uint8_t *p, uint32_t len) {
+    uint64_t h;
+    uint32_t i = 0;
+    if (len >= 32) {
+        uint64_t v1 = kP1 + kP2, v2 = kP2, v3 = 0, v4 = (uint64_t)0 - kP1;
+        for (; i + 32 <= len; i += 32) {
+            v1 = xround(v1, ld8(p + i));
+            v2 = xround(v2, ld8(p + i + 8));
+            v3 = xround(v3, ld8(p + i + 16));
+            v4 = xround(v4, ld8(p + i + 24));
+        }
+        h = rotl64(v1, 1) + rotl64(v2, 7) + rotl64(v3, 12) + rotl64(v4, 18);
+        h = (h ^ xround(0, v1)) * kP1 + kP4;
+        h = (h ^ xround(0, v2)) * kP1 + kP4;
+        h = (h ^ xround(0, v3)) * kP1 + kP4;
+        h = (h ^ xround(0, v4)) * kP1 + kP4;
+    } else {
+        h = kP5;
+    }
+    h += (uint64_t)len;
+    for (; i + 8 <= len; i += 8) h = rotl64(h ^ xround(0, ld8(p + i)), 27) * kP1 + kP4;
+    if (i + 4 <= len) {
+        const uint64_t w = ld1(p + i) | (ld1(p + i + 1) << 8) | (ld1(p + i + 2) << 16) | ((uint64_t)ld1(p + i + 3) << 24);
+        h ^= w * kP1;
+        h = rotl64(h, 23) * kP2 + kP3;
+        i += 4;
+    }
+    for (; i < len; i++) h = rotl64(h ^ (uint64_t)ld1(p + i) * kP5, 11) * kP1;
+    h ^= h >> 33;
+    h *= kP2;
+    h ^= h >> 29;
+    h *= kP3;
+    h ^= h >> 32;
+    return (uint32_t)h;
+}
+
+// A lane's page on its way out through the ring
+struct LaneOut {
+    uint8_t *rb;                 // the lane's LDS ring (lane_ring.h)
+    uint8_t *__restrict__ out;   // the page's destination
+    int32_t fl, op, cap;         // bytes already in HBM, bytes decoded, capacity
+};
+
+// One sequence: exec_batch's checks (ZSTD_execSequence, zstd_decompress.c:940-954),
+// ll literals from lit + lp, then ml bytes from off back.  False: the page fails.
+template <int32_t kRing>
+__device__ __forceinline__ bool exec_seq(LaneOut &o, const uint8_t *__restrict__ lit, int32_t &lp, int32_t lsize,
+                                         uint32_t ll, uint32_t ml, uint32_t off) {
+    if ((uint64_t)ll + ml > (uint64_t)(o.cap - o.op) || ll > (uint32_t)(lsize - lp) || off > (uint64_t)o.op + ll)
+        return false;
+    const int32_t d = o.op + (int32_t)ll;   // match destination
+    lit_run<kRing>(o.rb, o.out, o.fl, o.op, lit + lp, (int32_t)ll);
+    lp += (int32_t)ll;
+    // the unflushed tail is < kLine bytes here and the ring holds every position above
+    // d + 16 - kRing, so a source more than kRing - 32 back is already in HBM
+    const int32_t f = (int32_t)off, n = (int32_t)ml;
+    const bool far = f > kRing - 32;
+    u128 m = far ? ld16(o.out + d - f) : ring_rd<kRing>(o.rb, d - f);
+    if (f >= 16) {
+        ring_wr<kRing>(o.rb, d, m);
+        for (int32_t k = 16; k < n; k += 16) {
+            ring_flush<kRing>(o.rb, o.out, o.fl, d + k);
+            m = far ? ld16(o.out + d + k - f) : ring_rd<kRing>(o.rb, d + k - f);
+            ring_wr<kRing>(o.rb, d + k, m);
+        }
+    } else {
+        int32_t step;
+        const u128 p = period_pattern(m, f, step);
+        for (int32_t k = 0; k < n; k += step) {
+            ring_flush<kRing>(o.rb, o.out, o.fl, d + k);
+            ring_wr<kRing>(o.rb, d + k, p);
+        }
+    }
+    o.op = d + n;
+    ring_flush<kRing>(o.rb, o.out, o.fl, o.op);
+    return true;
+}
+
+// exec_page for one lane: the page's commands into out[0, cap) through the ring
+// rb.  blk_seqs(r, cur, nseq, lit, lp, lsize, o) runs a compressed block's nseq
+// sequences (cur: the entry after the block's command; the entry source advances
+// it past what it consumes) and returns false when the page fails.
+template <int32_t kRing, typename BlkSeqs>
+__device__ __forceinline__ int32_t exec_cmds(const Ent &E, uint8_t *__restrict__ out, int32_t cap, uint8_t *rb,
+                                             BlkSeqs &&blk_seqs) {
+    EntRd r;
+    er_init(r, E);
+    uint32_t cur = 0;
+    LaneOut o{rb, out, 0, 0, cap};
+    for (;;) {
+        if (cur >= E.ecap) return kErr;
+        uint32_t a, bsz, c;
+        er_get(r, cur, a, bsz, c);
+        cur++;
+        const uint32_t kind = a & 3u;
+        if (kind == kCmdEnd) {
+            ring_flush_all<kRing>(rb, out, o.fl, o.op);
+            if (((a >> 2) & 1u) && c != xxh64_lane(out, (uint32_t)o.op)) return kErr;
+            return o.op;
+        }
+        const int32_t sz = (int32_t)bsz;
+        if (kind == kCmdRaw) {
+            if (sz > cap - o.op) return kErrDst;
+            lit_run<kRing>(rb, out, o.fl, o.op, E.lit + (a >> 2), sz);
+            o.op += sz;
+            continue;
+        }
+        if (kind == kCmdRle) {
+            if (sz > cap - o.op) return kErrDst;
+            const u128 p = (u128)(c & 0xFFu) * (~(u128)0 / 255u);
+            for (int32_t k = 0; k < sz; k += 16) {
+                ring_flush<kRing>(rb, out, o.fl, o.op + k);
+                ring_wr<kRing>(rb, o.op + k, p);
+            }
+            o.op += sz;
+            ring_flush<kRing>(rb, out, o.fl, o.op);
+            continue;
+        }
+        const int32_t lsize = sz;
+        if (o.op + lsize > cap) return kErrDst;
+        const uint8_t *__restrict__ lit = E.lit + (a >> 2);
+        int32_t lp = 0;
+        if (!blk_seqs(r, cur, c, lit, lp, lsize, o)) return kErr;
+        const int32_t last = lsize - lp;
+        if (last > cap - o.op) return kErrDst;
+        lit_run<kRing>(rb, out, o.fl, o.op, lit + lp, last);
+        o.op += last;
+    }
+}
+
+// The page's sequences from the entry planes (zstd_seq_kernel's output)
+template <int32_t kRing>
+__device__ int32_t exec_lane(const Ent &E, uint8_t *__restrict__ out, int32_t cap, uint8_t *rb) {
+    return exec_cmds<kRing>(E, out, cap, rb,
+                            [&](EntRd &r, uint32_t &cur, uint32_t nseq, const uint8_t *lit, int32_t &lp, int32_t lsize,
+                                LaneOut &o) -> bool {
+                                if (nseq > E.ecap - cur) return false;
+                                for (uint32_t q = 0; q < nseq; q++) {
+                                    uint32_t ll, ml, off;
+                                    er_get(r, cur + q, ll, ml, off);
+                                    if (!exec_seq<kRing>(o, lit, lp, lsize, ll, ml, off)) return false;
+                                }
+                                cur += nseq;
+                                return true;
+                            });
+}
+
+template <int32_t kRing>
+__global__ __launch_bounds__(64) void zstd_exec_lane_kernel(tyche_batch_t b, size_t first, size_t count,
+                                                            uint32_t in_cap, uint32_t out_cap, const uint8_t *ws,
+                                                            size_t ws_page, const int32_t *st, unsigned *ctr) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint8_t *rb = smem + threadIdx.x * (kRing + 48) + 16;
+    const size_t nthreads = (size_t)gridDim.x * blockDim.x;
+    size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    while (j < count) {
+        const size_t i = first + j;
+        int32_t rv = st[j];
+        if (rv >= 0) {
+            const uint64_t dof = b.dst_offsets ? b.dst_offsets[i] : (uint64_t)i * b.dst_stride;
+            const uint32_t C = b.dst_capacities ? b.dst_capacities[i] : b.dst_capacity;
+            const Ent E = ent_of(const_cast<uint8_t *>(ws) + j * ws_page, in_cap, out_cap, false);
+            rv = exec_lane<kRing>(E, (uint8_t *)b.dst + dof, (int32_t)C, rb);
+        }
+        b.results[i] = rv;
+        j = (size_t)atomicAdd(ctr, 1u) + nthreads;
+    }
+}
+
+// ---- pass 2, chains and execution fused (default): one page per lane runs each
+// compressed block's sequence chain (the job pass 1 left) and executes every
+// sequence as it is decoded -- the reference's own order (ZSTD_decompressSequences
+// decodes and executes one sequence at a time, zstd_decompress.c:1037-1047).  No
+// entries go through HBM: the pass-1 area holds commands only (kFusedCmds), so a
+// chunk of pages needs ~50 KiB per 32 KiB page instead of ~310 KiB.  Tables of up
+// to kLog / kLog - 1 / kLog are copied to the lane's LDS slot, larger ones gathered.
+template <int32_t kRing, uint32_t kLog>
+__device__ int32_t seqexec_page(const Ent &E, const uint8_t *src, uint8_t *__restrict__ out, int32_t cap, uint8_t *rb,
+                                uint16_t *lt) {
+    const uint32_t njobs = E.jobs[0];
+    uint32_t q = 0, rep0 = 1, rep1 = 4, rep2 = 8;
+    return exec_cmds<kRing>(E, out, cap, rb,
+                            [&](EntRd &, uint32_t &, uint32_t nseq, const uint8_t *lit, int32_t &lp, int32_t lsize,
+                                LaneOut &o) -> bool {
+                                if (nseq == 0) return true;
+                                if (q >= njobs) return false;
+                                const uint32_t *J = E.jobs + 4u + q * kJobWords;
+                                q++;
+                                if (J[2] != nseq) return false;
+                                auto nopre = [](uint32_t) {};
+                                auto run = [&](uint32_t, uint32_t ll, uint32_t ml, uint32_t off) -> bool {
+                                    return exec_seq<kRing>(o, lit, lp, lsize, ll, ml, off);
+                                };
+                                return job_fits<kLog>(J[7]) ? seq_chain<kLog>(E, src, J, rep0, rep1, rep2, lt, nopre, run)
+                                                            : seq_chain<0u>(E, src, J, rep0, rep1, rep2, lt, nopre, run);
+                            });
+}
+
+template <int32_t kRing, uint32_t kLog>
+__global__ __launch_bounds__(64) void zstd_seqexec_kernel(tyche_batch_t b, size_t first, size_t count,
+                                                          uint32_t in_cap, uint32_t out_cap, const uint8_t *ws,
+                                                          size_t ws_page, const int32_t *st, unsigned *ctr) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint8_t *rb = smem + threadIdx.x * (kRing + 48) + 16;
+    uint16_t *lt = (uint16_t *)(smem + 64u * (kRing + 48)) + threadIdx.x * Slots<kLog>::cells;
+    const size_t nthreads = (size_t)gridDim.x * blockDim.x;
+    size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    while (j < count) {
+        const size_t i = first + j;
+        int32_t rv = st[j];
+        if (rv >= 0) {
+            const uint64_t so = b.src_offsets ? b.src_offsets[i] : (uint64_t)i * b.src_stride;
+            const uint64_t dof = b.dst_offsets ? b.dst_offsets[i] : (uint64_t)i * b.dst_stride;
+            const uint32_t C = b.dst_capacities ? b.dst_capacities[i] : b.dst_capacity;
+            const Ent E = ent_of(const_cast<uint8_t *>(ws) + j * ws_page, in_cap, out_cap, true);
+            rv = seqexec_page<kRing, kLog>(E, (const uint8_t *)b.src + so, (uint8_t *)b.dst + dof, (int32_t)C, rb, lt);
+        }
+        if (rv != kRetryFused) b.results[i] = rv;
+        j = (size_t)atomicAdd(ctr, 1u) + nthreads;
+    }
+}
+
 // Pass 1 over pages [first, first + count) of b; page j's entries at ws + j * ws_page.
 __global__ __launch_bounds__(64) void zstd_entropy_kernel(tyche_batch_t b, size_t first, size_t count, uint32_t in_cap,
                                                           uint32_t out_cap, Layout lay, uint8_t *ws, size_t ws_page,
-                                                          int32_t *st, unsigned *ctr, bool use_jobs) {
+                                                          int32_t *st, unsigned *ctr, bool use_jobs, bool fused) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t lane = threadIdx.x;
     Work W;
@@ -1864,11 +2199,13 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(tyche_batch_t b, size_
             if (lane < kStreamPad / 4) lds_st32(in + p.src_len + lane * 4, 0u);
             WAVE_SYNC();
             W.in = in;
-            const Ent E = ent_of(ws + j * ws_page, in_cap, out_cap);
+            const Ent E = ent_of(ws + j * ws_page, in_cap, out_cap, fused);
             SPROF_DECL
-            // jobs first; a page whose jobs do not fit is redone with the chains inline
-            for (bool jobs = use_jobs;; jobs = false) {
+            // jobs first; a page whose jobs do not fit is redone with the chains inline (fused
+            // layout: by the one-wave kernel after pass 2)
+            for (bool jobs = use_jobs || fused;; jobs = false) {
                 rv = decode_frame<true>(W, E, (int32_t)p.src_len, (int32_t)p.dst_cap, lane, jobs);
+                if (rv == kRetryInline && fused) rv = kRetryFused;
                 if (!(rv == kRetryInline && jobs)) break;
             }
             SPROF_MARK(1);
@@ -1888,7 +2225,7 @@ __global__ __launch_bounds__(64) void zstd_exec_kernel(tyche_batch_t b, size_t f
         const PageRef p = batch_page(b, first + j);
         int32_t rv = st[j];
         if (rv >= 0) {
-            const Ent E = ent_of(const_cast<uint8_t *>(ws) + j * ws_page, in_cap, out_cap);
+            const Ent E = ent_of(const_cast<uint8_t *>(ws) + j * ws_page, in_cap, out_cap, false);
             WAVE_SYNC();
 #ifdef TYCHE_PROFILE
             unsigned long long _pt = clock64();
@@ -1928,11 +2265,22 @@ static hipError_t launch_fused(const tyche_batch_t &b, uint32_t in_cap, uint32_t
     const size_t grid = std::min<size_t>(b.count, ncu * per_cu);
     WorkCounter ctr(s, grid < b.count);
     if (!ctr.get()) return hipErrorOutOfMemory;
-    hipLaunchKernelGGL(zstd_decode_kernel, dim3((unsigned)grid), dim3(kWave), lay.total, s, b, in_cap, out_cap, lay,
-                       ctr.get());
+    hipLaunchKernelGGL(zstd_decode_kernel, dim3((unsigned)grid), dim3(kWave), lay.total, s, b, (size_t)0, b.count, in_cap,
+                       out_cap, lay, ctr.get(), (const int32_t *)nullptr);
     return hipGetLastError();
 }
 
+// Pass 2 runs one page per lane from this many pages per batch (lane-per-page
+// kernels need ~512 pages per CU in flight; below that the wave kernel's window
+// in LDS wins).
+constexpr long kExecLaneMin = 16384;
+
+// TYCHE_ZSTD_SEQEXEC: 1 (default) pass 2 = zstd_seqexec_kernel (chains and
+// execution fused, commands-only areas); 0 = zstd_seq_kernel + an execution kernel
+// over sequence entries (lane per page: zstd_exec_lane_kernel, TYCHE_ZSTD_EXEC_RING
+// 128 / 256; wave per page below TYCHE_ZSTD_EXEC_LANE_MIN pages: zstd_exec_kernel).
+// TYCHE_ZSTD_SEQ_SLOTS 7 (default) / 6: the largest table logs pass 2 keeps in LDS
+// (7: LL/ML 7, OF 6, 3 waves per CU; 6: 6 / 5, 5 waves per CU).
 hipError_t launch_zstd_decode(const tyche_batch_t &b, uint32_t in_cap, uint32_t out_cap, hipStream_t s) {
     if (b.count == 0) return hipSuccess;
     // small batches (restores) take the one-launch kernel: the split's extra
@@ -1941,30 +2289,43 @@ hipError_t launch_zstd_decode(const tyche_batch_t &b, uint32_t in_cap, uint32_t 
     const size_t split_min = mn > 0 ? (size_t)mn : 4096;
     const bool split = knob("ZSTD_SPLIT", 1) != 0 && b.count >= split_min;
     const Layout l1 = make_layout(in_cap, out_cap, false);
+    const Layout lf = make_layout(in_cap, out_cap);   // the one-wave kernel (leftovers of the fused layout)
     const bool use_jobs = knob("ZSTD_JOBS", 1) != 0;   // 0: sequence chains inline in pass 1
     const uint32_t lds2 = (out_cap + kWinPad + 15u) & ~15u;
-    if (!split || l1.total > 160u * 1024u || lds2 > 160u * 1024u) return launch_fused(b, in_cap, out_cap, s);
-    const size_t page_bytes = ent_page_bytes(in_cap, out_cap);
-    // the sequence kernel's time per chunk is one page's chain (latency-bound, one
-    // lane per page), so chunks are made as large as memory allows: 16 GiB or a
-    // quarter of the free memory, whichever is less
+    const long lmin = knob("ZSTD_EXEC_LANE_MIN", kExecLaneMin);
+    const bool lane_exec = lmin >= 0 && b.count >= (size_t)lmin;
+    const bool seqexec = lane_exec && use_jobs && knob("ZSTD_SEQEXEC", 1) != 0 && lf.total <= 160u * 1024u;
+    const long ring = knob("ZSTD_EXEC_RING", 128);
+    const bool slots6 = knob("ZSTD_SEQ_SLOTS", 7) == 6;
+    const void *kx = seqexec ? (slots6 ? (const void *)zstd_seqexec_kernel<128, 6> : (const void *)zstd_seqexec_kernel<128, 7>)
+                     : ring == 256 ? (const void *)zstd_exec_lane_kernel<256>
+                                   : (const void *)zstd_exec_lane_kernel<128>;
+    const size_t lds_lane = seqexec ? 64u * (128u + 48u + 2u * (slots6 ? Slots<6>::cells : Slots<7>::cells))
+                                    : 64u * ((ring == 256 ? 256u : 128u) + 48u);
+    if (!split || l1.total > 160u * 1024u || (!lane_exec && lds2 > 160u * 1024u))
+        return launch_fused(b, in_cap, out_cap, s);
+    const size_t page_bytes = ent_page_bytes(in_cap, out_cap, seqexec);
+    // pass 2's time per chunk is a page's chain (latency-bound, one lane per
+    // page), so chunks are made as large as memory allows: 16 GiB or a quarter
+    // of the free memory, whichever is less
     const long mb = knob("ZSTD_SCRATCH_MB", 0);
     size_t budget = (size_t)16 << 30;
     size_t free_b = 0, total_b = 0;
-    if (b.count * page_bytes > ((size_t)1 << 30) && hipMemGetInfo(&free_b, &total_b) == hipSuccess && ((free_b += scratch_idle_bytes()), true) &&
-        free_b / 4 < budget)
+    if (b.count * page_bytes > ((size_t)1 << 30) && hipMemGetInfo(&free_b, &total_b) == hipSuccess &&
+        ((free_b += scratch_idle_bytes()), true) && free_b / 4 < budget)
         budget = free_b / 4;
     if (mb > 0) budget = (size_t)mb << 20;
     const size_t chunk = std::max<size_t>(1, std::min<size_t>(b.count, budget / page_bytes));
     const size_t st_bytes = (chunk * 4u + 255u) & ~(size_t)255u;
-    ScratchLease ws(s, st_bytes + chunk * page_bytes);
+    ScratchLease ws(s, st_bytes + chunk * page_bytes + 64u);   // + the lane pass's literal over-read
     if (!ws.get()) return launch_fused(b, in_cap, out_cap, s);
     int32_t *st = (int32_t *)ws.get();
     uint8_t *ent = (uint8_t *)ws.get() + st_bytes;
     const size_t ncu = prepare_launch((const void *)zstd_entropy_kernel);
-    (void)prepare_launch((const void *)zstd_exec_kernel);
+    (void)prepare_launch(lane_exec ? kx : (const void *)zstd_exec_kernel);
     const size_t cu1 = waves_per_cu((const void *)zstd_entropy_kernel, l1.total);
-    const size_t cu2 = waves_per_cu((const void *)zstd_exec_kernel, lds2);
+    const size_t cu2 = lane_exec ? waves_per_cu(kx, lds_lane) : waves_per_cu((const void *)zstd_exec_kernel, lds2);
+    const size_t cuf = seqexec ? waves_per_cu((const void *)zstd_decode_kernel, lf.total) : 0;
     for (size_t first = 0; first < b.count; first += chunk) {
         const size_t n = std::min(chunk, b.count - first);
         const size_t g1 = std::min<size_t>(n, ncu * cu1);
@@ -1972,16 +2333,34 @@ hipError_t launch_zstd_decode(const tyche_batch_t &b, uint32_t in_cap, uint32_t 
             WorkCounter ctr(s, g1 < n);
             if (!ctr.get()) return hipErrorOutOfMemory;
             hipLaunchKernelGGL(zstd_entropy_kernel, dim3((unsigned)g1), dim3(kWave), l1.total, s, b, first, n, in_cap,
-                               out_cap, l1, ent, page_bytes, st, ctr.get(), use_jobs);
+                               out_cap, l1, ent, page_bytes, st, ctr.get(), use_jobs, seqexec);
         }
-        hipLaunchKernelGGL(zstd_seq_kernel, dim3((unsigned)((n + kWave - 1) / kWave)), dim3(kWave), kSeqLds, s, b, first,
-                           n, in_cap, out_cap, ent, page_bytes, st);
-        const size_t g2 = std::min<size_t>(n, ncu * cu2);
-        {
+        if (!seqexec)
+            hipLaunchKernelGGL(zstd_seq_kernel, dim3((unsigned)((n + kWave - 1) / kWave)), dim3(kWave), kSeqLds, s, b,
+                               first, n, in_cap, out_cap, ent, page_bytes, st);
+        if (lane_exec) {
+            const size_t g2 = std::min<size_t>((n + 63) / 64, ncu * cu2);
+            WorkCounter ctr(s, true);
+            unsigned *cp = ctr.get();
+            if (!cp) return hipErrorOutOfMemory;
+            const uint8_t *wsp = ent;
+            const int32_t *stp = st;
+            size_t f = first, nn = n, pb = page_bytes;
+            void *args[] = {(void *)&b, &f, &nn, &in_cap, &out_cap, &wsp, &pb, &stp, &cp};
+            (void)hipLaunchKernel(kx, dim3((unsigned)g2), dim3(64), args, lds_lane, s);
+        } else {
+            const size_t g2 = std::min<size_t>(n, ncu * cu2);
             WorkCounter ctr(s, g2 < n);
             if (!ctr.get()) return hipErrorOutOfMemory;
             hipLaunchKernelGGL(zstd_exec_kernel, dim3((unsigned)g2), dim3(kWave), lds2, s, b, first, n, in_cap,
                                out_cap, (const uint8_t *)ent, page_bytes, (const int32_t *)st, ctr.get());
+        }
+        if (seqexec) {
+            // the pages pass 1 left to the one-wave kernel (too many blocks or jobs for the
+            // fused layout): every wave skips the others after one status read
+            const size_t gf = std::min<size_t>((n + kWave - 1) / kWave, ncu * cuf);
+            hipLaunchKernelGGL(zstd_decode_kernel, dim3((unsigned)gf), dim3(kWave), lf.total, s, b, first, n, in_cap,
+                               out_cap, lf, (unsigned *)nullptr, (const int32_t *)st);
         }
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;

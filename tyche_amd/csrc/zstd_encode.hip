@@ -144,6 +144,7 @@ struct Enc {
     uint8_t *area;       // split encode: the page's work area (nullptr: the chain runs here)
     uint32_t nblk, nrec; // blocks and sequence records written to the area
     uint32_t rec_cap;
+    uint32_t logcap;     // 7: LL / OF / ML table logs FSE_optimalTableLog's, capped at 7 / 6 / 7; 6: fixed 6 / 5 / 6
     __device__ uint32_t nrec_cap() const { return rec_cap; }
 };
 
@@ -160,11 +161,13 @@ struct Enc {
 // bounds, so a page that pass A2 accepts always fits.
 constexpr uint32_t kMaxBlk = 24;                 // blocks per page (> 65535 / 4 / 960 + 1)
 constexpr uint32_t kBlkWords = 8;                // g_start, g_len, pre, fse (bound, then actual), n, rec, tab, flags
-// one table, packed for pass B's LDS copy: per symbol deltaNbBits | (deltaFindState + 64) << 19
-// (dnb < 2^19: log <= 6, every symbol's maxBitsOut >= 1; dfs in [-64, 63]), then the 64
-// stateTable bytes (values 64..127)
-constexpr uint32_t kCtWords = 64u + 16u;
-constexpr uint32_t kTabBytes = 3u * kCtWords * 4u;   // 960
+// Sequence table logs: FSE_optimalTableLog capped at these (emit_block)
+constexpr uint32_t kStateBits = 7u + 6u + 7u;   // bits one sequence's three states emit at most (LL, OF, ML logs <= 7 / 6 / 7)
+// one table, packed for pass B's LDS copy: per symbol deltaNbBits | (deltaFindState + 128) << 19
+// (dnb < 2^19: log <= 7, every symbol's maxBitsOut >= 1; dfs in [-128, 127]), word 63 the
+// table log, then the 128 stateTable bytes (values < 256)
+constexpr uint32_t kCtWords = 64u + 32u;
+constexpr uint32_t kTabBytes = 3u * kCtWords * 4u;   // 1152
 constexpr uint32_t kPblkWords = 4;   // parse blocks: page start, page end, first sequence, sequences
 constexpr uint32_t kAreaHead = 16u + kMaxBlk * kBlkWords * 4u + kMaxBlk * kPblkWords * 4u;
 // area: [0] emitted blocks, [1] parse blocks | block records | parse blocks | tables |
@@ -473,7 +476,7 @@ __device__ __forceinline__ bool emit_block(Enc &e, uint32_t bend, bool last, uin
     const uint32_t fl = 1u + (lit_total > 31u) + (lit_total > 4095u);
     const uint32_t nsh = n < 0x7Fu ? 1u : (n < 0x7F00u ? 2u : 3u);
     // upper bound of the FSE bitstream: every state emits at most its table log
-    const uint32_t fse_bound = n ? (n * 17u + xbits + 17u + 8u + 7u) / 8u + 1u : 0u;
+    const uint32_t fse_bound = n ? (n * kStateBits + xbits + kStateBits + 8u + 7u) / 8u + 1u : 0u;
     const uint32_t comp_bound = fl + lit_total + nsh + (n ? 1u + 3u * 48u : 0u) + fse_bound;   // + NCount headers
     const uint32_t hdr = e.op;                              // block header position
     if (comp_bound >= blen) {
@@ -535,28 +538,35 @@ __device__ __forceinline__ bool emit_block(Enc &e, uint32_t bend, bool last, uin
             }
         }
         __builtin_amdgcn_wave_barrier();
-        // ---- tables: per-block distributions at the predefined accuracy (LL 6, OF 5,
-        // ML 6 -- one cell per lane) from 64 sequences on (MIN_SEQ_FOR_DYNAMIC_FSE),
-        // the predefined ones below (ZSTD_compressSequences, zstd_compress.c:595-660);
-        // NCount headers follow the mode byte in LL, OF, ML order
+        // ---- tables: per-block distributions from 64 sequences on (MIN_SEQ_FOR_DYNAMIC_FSE)
+        // at FSE_optimalTableLog's accuracy capped at LL 7 / OF 6 / ML 7 (the reference caps at
+        // 9 / 8 / 9; a log-7 table is two cells per lane -- tools/parse_sim.c zfse: the cap costs
+        // 0.3 % of ratio at 32 KiB pages, the old fixed 6 / 5 / 6 cost 1.6 %), the predefined
+        // ones below (ZSTD_compressSequences, zstd_compress.c:595-680); NCount headers follow
+        // the mode byte in LL, OF, ML order
         const uint32_t mpos = o;
         o += 1u;
         const bool dyn = n >= 64u;
         huf::SmallCT tll, tof, tml;
         {
             int32_t nll, nof, nml;
-            uint32_t mll, mof, mml;
+            uint32_t mll, mof, mml, gll = 6, gof = 5, gml = 6;
             if (dyn) {
                 const uint32_t cll = e.htab[lane], cml = e.htab[64u + lane], cof = lane < 32u ? e.htab[128u + lane] : 0u;
                 mll = (uint32_t)huf::wave_max(cll ? (int32_t)lane : -1);
                 mml = (uint32_t)huf::wave_max(cml ? (int32_t)lane : -1);
                 mof = (uint32_t)huf::wave_max(cof ? (int32_t)lane : -1);
-                if (!huf::normalize(cll, n, 6, nll, lane) || !huf::normalize(cof, n, 5, nof, lane) ||
-                    !huf::normalize(cml, n, 6, nml, lane))
+                if (e.logcap == 7u) {
+                    gll = huf::optimal_log(7u, n, mll, 2);
+                    gof = huf::optimal_log(6u, n, mof, 2);
+                    gml = huf::optimal_log(7u, n, mml, 2);
+                }
+                if (!huf::normalize(cll, n, gll, nll, lane) || !huf::normalize(cof, n, gof, nof, lane) ||
+                    !huf::normalize(cml, n, gml, nml, lane))
                     return false;
-                o += huf::write_ncount(nll, mll, 6, e.dst, o, lane);
-                o += huf::write_ncount(nof, mof, 5, e.dst, o, lane);
-                o += huf::write_ncount(nml, mml, 6, e.dst, o, lane);
+                o += huf::write_ncount(nll, mll, gll, e.dst, o, lane);
+                o += huf::write_ncount(nof, mof, gof, e.dst, o, lane);
+                o += huf::write_ncount(nml, mml, gml, e.dst, o, lane);
             } else {
                 nll = lane <= 35u ? (int32_t)c_ll_norm[min(lane, 35u)] : 0;
                 nml = lane <= 52u ? (int32_t)c_ml_norm[min(lane, 52u)] : 0;
@@ -565,9 +575,10 @@ __device__ __forceinline__ bool emit_block(Enc &e, uint32_t bend, bool last, uin
                 mml = 52;
                 mof = 28;
             }
-            tll = huf::build_small_ct(nll, mll, 6, lane);
-            tof = huf::build_small_ct(nof, mof, 5, lane);
-            tml = huf::build_small_ct(nml, mml, 6, lane);
+            uint8_t *scr = (uint8_t *)(e.htab + 256u);   // past the code histograms
+            tll = huf::build_small_ct(nll, mll, gll, lane, scr);
+            tof = huf::build_small_ct(nof, mof, gof, lane, scr);
+            tml = huf::build_small_ct(nml, mml, gml, lane, scr);
         }
         if (lane == 0) e.dst[mpos] = dyn ? (uint8_t)((2u << 6) | (2u << 4) | (2u << 2)) : 0u;
         SPROF_MARK(4);
@@ -587,8 +598,10 @@ __device__ __forceinline__ bool emit_block(Enc &e, uint32_t bend, bool last, uin
             const huf::SmallCT *ts[3] = {&tll, &tof, &tml};
 #pragma unroll
             for (uint32_t t = 0; t < 3; t++) {
-                T[t * kCtWords + lane] = ts[t]->dnb | ((uint32_t)(ts[t]->dfs + 64) << 19);
+                // word 63 (no symbol 63 in any of the three alphabets) holds the table log
+                T[t * kCtWords + lane] = lane == 63u ? ts[t]->log : ts[t]->dnb | ((uint32_t)(ts[t]->dfs + 128) << 19);
                 ((uint8_t *)(T + t * kCtWords + 64u))[lane] = (uint8_t)ts[t]->state;
+                ((uint8_t *)(T + t * kCtWords + 64u))[64u + lane] = (uint8_t)ts[t]->state_hi;
             }
             const uint32_t pre = o - (hdr + 3u);
             const uint32_t glen = 3u + pre + fse_bound;
@@ -671,7 +684,7 @@ __device__ __forceinline__ bool emit_block(Enc &e, uint32_t bend, bool last, uin
 // Encodes one page held in LDS (in[0, L), 64 zero bytes after).  Returns the
 // frame size, or 0 if it does not fit in cap.
 __device__ __forceinline__ int32_t encode_page(const uint8_t *in, uint32_t L, uint16_t *table, uint8_t *map, uint2 *rec, uint2 *seq,
-                               uint32_t *htab, uint8_t *wts, uint8_t *dst, uint32_t cap, uint32_t lane) {
+                               uint32_t *htab, uint8_t *wts, uint8_t *dst, uint32_t cap, uint32_t logcap, uint32_t lane) {
     // ---- frame header: magic, single-segment descriptor with the content size
     const uint32_t fcs_id = L < 256u ? 0u : (L < 65536u + 256u ? 1u : 2u);
     const uint32_t fcs_len = fcs_id == 0u ? 1u : (fcs_id == 1u ? 2u : 4u);
@@ -706,6 +719,7 @@ __device__ __forceinline__ int32_t encode_page(const uint8_t *in, uint32_t L, ui
     e.nblk = 0;
     e.nrec = 0;
     e.rec_cap = 0;
+    e.logcap = logcap;
     auto sink = [&](const uint2 *r, uint32_t n, uint32_t anchor) -> bool {
         uint32_t ls, ll, ml, off;
         lzp::decode_record(r, n, anchor, lane, ls, ll, ml, off);
@@ -775,7 +789,7 @@ __device__ __forceinline__ int32_t parse_to_area(const uint8_t *in, uint32_t L, 
 // itself is read from global memory).  Returns the gapped frame size or 0.
 __device__ __forceinline__ int32_t emit_page(const uint8_t *src, uint32_t L, uint8_t *area, uint32_t rec_cap,
                                              uint8_t *map, uint2 *stage, uint32_t *htab, uint8_t *wts, uint8_t *dst,
-                                             uint32_t cap, uint32_t lane) {
+                                             uint32_t cap, uint32_t logcap, uint32_t lane) {
     const uint32_t fcs_id = L < 256u ? 0u : (L < 65536u + 256u ? 1u : 2u);
     const uint32_t fcs_len = fcs_id == 0u ? 1u : (fcs_id == 1u ? 2u : 4u);
     const uint32_t fh = 5u + fcs_len;
@@ -805,6 +819,7 @@ __device__ __forceinline__ int32_t emit_page(const uint8_t *src, uint32_t L, uin
     e.nblk = 0;
     e.nrec = 0;
     e.rec_cap = rec_cap;
+    e.logcap = logcap;
     e.cursor = 0;
     const uint32_t npb = __builtin_amdgcn_readfirstlane(((const uint32_t *)area)[1]);
     uint2 *S = area_seq(area, rec_cap);
@@ -824,7 +839,8 @@ __device__ __forceinline__ int32_t emit_page(const uint8_t *src, uint32_t L, uin
 // kParse: pass A1 of the split encode instead (the parse only, into ws; status to st).
 template <bool kParse>
 __global__ __launch_bounds__(64) void zstd_encode_kernel(tyche_batch_t b, size_t first, size_t count, uint32_t in_cap,
-                                                         unsigned *ctr, uint8_t *ws, size_t ws_page, int32_t *st) {
+                                                         unsigned *ctr, uint8_t *ws, size_t ws_page, int32_t *st,
+                                                         uint32_t logcap) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t lane = threadIdx.x;
     uint16_t *table = (uint16_t *)smem;
@@ -869,7 +885,7 @@ __global__ __launch_bounds__(64) void zstd_encode_kernel(tyche_batch_t b, size_t
             in[p.src_len + lane] = 0;
             WAVE_SYNC();
             if (kParse) rv = parse_to_area(in, p.src_len, table, rec, ws + page * ws_page, enc_rec_cap(in_cap), lane);
-            else rv = encode_page(in, p.src_len, table, map, rec, seq, htab, wts, p.dst, p.dst_cap, lane);
+            else rv = encode_page(in, p.src_len, table, map, rec, seq, htab, wts, p.dst, p.dst_cap, logcap, lane);
         }
         if (lane == 0) {
             if (kParse) st[page] = rv;
@@ -1080,7 +1096,8 @@ __global__ __launch_bounds__(kNW * 64) void zstd_parse_split_kernel(tyche_batch_
 // ---- pass A2
 constexpr uint32_t kA2Lds = kWave + kWave * 8u + kHtab * 4u + 256u;   // map, stage, htab, weights
 __global__ __launch_bounds__(64) void zstd_block_kernel(tyche_batch_t b, size_t first, size_t count, uint32_t in_cap,
-                                                        uint8_t *ws, size_t ws_page, int32_t *st, unsigned *ctr) {
+                                                        uint8_t *ws, size_t ws_page, int32_t *st, unsigned *ctr,
+                                                        uint32_t logcap) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t lane = threadIdx.x;
     uint8_t *map = smem;
@@ -1093,7 +1110,7 @@ __global__ __launch_bounds__(64) void zstd_block_kernel(tyche_batch_t b, size_t 
         const PageRef p = batch_page(b, first + j);
         WAVE_SYNC();
         const int32_t rv = emit_page(p.src, p.src_len, ws + j * ws_page, enc_rec_cap(in_cap), map, stage, htab, wts,
-                                     p.dst, p.dst_cap, lane);
+                                     p.dst, p.dst_cap, logcap, lane);
         if (lane == 0) st[j] = rv;
     }
 }
@@ -1149,13 +1166,13 @@ __device__ __forceinline__ uint32_t lct_init2(const uint32_t *T, uint32_t sym) {
     const uint32_t pk = T[sym], dnb = pk & 0x7FFFFu;
     const uint32_t nbo = (dnb + (1u << 15)) >> 16;
     const uint32_t v = (nbo << 16) - dnb;
-    return ((const uint8_t *)(T + 64u))[(uint32_t)((int32_t)(v >> nbo) + (int32_t)(pk >> 19) - 64)];
+    return ((const uint8_t *)(T + 64u))[(uint32_t)((int32_t)(v >> nbo) + (int32_t)(pk >> 19) - 128)];
 }
 __device__ __forceinline__ void lct_encode(LaneBits &b, uint32_t &st, const uint32_t *T, uint32_t sym) {
     const uint32_t pk = T[sym];
     const uint32_t nbo = (st + (pk & 0x7FFFFu)) >> 16;
     lb_add(b, st, nbo);
-    st = ((const uint8_t *)(T + 64u))[(uint32_t)((int32_t)(st >> nbo) + (int32_t)(pk >> 19) - 64)];
+    st = ((const uint8_t *)(T + 64u))[(uint32_t)((int32_t)(st >> nbo) + (int32_t)(pk >> 19) - 128)];
 }
 
 // ZSTD_compressSequences' bitstream (zstd_compress.c:695-735) for n >= 1
@@ -1191,11 +1208,11 @@ __device__ uint32_t fse_lane(uint8_t *out, const uint4 *R, uint32_t n, const uin
         lb_add(b, r.w, ofc);
         lb_flush(b, s);
     }
-    lb_add(b, sml, 6u);
+    lb_add(b, sml, tml[63]);
     lb_flush(b, s);
-    lb_add(b, sof, 5u);
+    lb_add(b, sof, tof[63]);
     lb_flush(b, s);
-    lb_add(b, sll, 6u);
+    lb_add(b, sll, tll[63]);
     lb_flush(b, s);
     lb_add(b, 1u, 1u);
     lb_flush(b, s);
@@ -1288,6 +1305,8 @@ hipError_t launch_zstd_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream
     const long mn = knob("ZSTD_SPLIT_MIN", 4096);   // small batches: one launch (latency)
     const size_t split_min = mn > 0 ? (size_t)mn : 4096;
     const bool split = knob("ZSTD_ENC_SPLIT", 1) != 0 && b.count >= split_min;
+    // sequence-table accuracy: FSE_optimalTableLog capped at LL/ML 7, OF 6 (6: fixed 6 / 5 / 6, round 2's)
+    const uint32_t logcap = knob("ZSTD_FSE_LOG", 7) <= 6 ? 6u : 7u;
     const size_t page_bytes = enc_area_bytes(in_cap);
     size_t budget = (size_t)8 << 30;
     size_t free_b = 0, total_b = 0;
@@ -1306,7 +1325,7 @@ hipError_t launch_zstd_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream
         WorkCounter ctr(s, grid < b.count);
         if (!ctr.get()) return hipErrorOutOfMemory;
         hipLaunchKernelGGL(zstd_encode_kernel<false>, dim3((unsigned)grid), dim3(kWave), lds, s, b, (size_t)0, b.count,
-                           in_cap, ctr.get(), (uint8_t *)nullptr, (size_t)0, (int32_t *)nullptr);
+                           in_cap, ctr.get(), (uint8_t *)nullptr, (size_t)0, (int32_t *)nullptr, logcap);
         return hipGetLastError();
     }
     int32_t *st = (int32_t *)lease.get();
@@ -1347,14 +1366,14 @@ hipError_t launch_zstd_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream
             WorkCounter ctr(s, g < n);
             if (!ctr.get()) return hipErrorOutOfMemory;
             hipLaunchKernelGGL(zstd_encode_kernel<true>, dim3((unsigned)g), dim3(kWave), lds1, s, b, first, n, in_cap,
-                               ctr.get(), ws, page_bytes, st);
+                               ctr.get(), ws, page_bytes, st, logcap);
         }
         {
             const size_t g = std::min<size_t>(n, ncu * cu2);
             WorkCounter ctr(s, g < n);
             if (!ctr.get()) return hipErrorOutOfMemory;
             hipLaunchKernelGGL(zstd_block_kernel, dim3((unsigned)g), dim3(kWave), kA2Lds, s, b, first, n, in_cap, ws,
-                               page_bytes, st, ctr.get());
+                               page_bytes, st, ctr.get(), logcap);
         }
         hipLaunchKernelGGL(zstd_fse_kernel, dim3((unsigned)((n + kWave - 1) / kWave)), dim3(kWave), kWave * kTabBytes, s,
                            b, first, n, ws, page_bytes, (const int32_t *)st);
