@@ -181,10 +181,13 @@ def test_reference_app_benchmark_run(sample_dir, codec):
 def test_reference_app_device_failure(sample_dir):
     """What a device failure does at the unchanged sweep caller, and what the INTEGRATION.md change does.
 
-    TYCHE_FAIL_COMPRESS_EVERY=2 makes every second encode launch fail as a lost device would
+    TYCHE_FAIL_COMPRESS_EVERY=N makes every Nth encode launch fail as a lost device would
     (TYCHE_E_DEVICE, *compressed_data = NULL).  With -U 50 half the worker rounds rewrite the pages they
     read (manager.c:353-359: memcpy from buf->data; -U 100 wedges the reference's copy-on-write before
-    the sweeper runs, tools/c1_probe.sh).
+    the sweeper runs, tools/c1_probe.sh).  The unchanged caller runs with N = 1 (every victim of a
+    failed launch is lost, so a rewrite reaches one before the reference's own races wedge the run:
+    with N = 2 four runs in a row once wedged first), the fixed one with N = 2 (half the launches
+    succeed, so pages still compress).
 
     * Unchanged list.c (tyche_q): list__compressor_start skips a victim only on 124 (list.c:1052), so a
       failed one is installed with data = NULL and flagged compressed (list.c:1058-1060); the restore
@@ -197,20 +200,21 @@ def test_reference_app_device_failure(sample_dir):
     _need(APP_FIXED)
     fault = {"TYCHE_FAIL_COMPRESS_EVERY": "2"}
     args = ["-c", "lz4", "-p", str(sample_dir / "16k"), "-w", "1", "-d", "3", "-m", "512000", "-f", "20", "-U", "50"]
-    crashes = []
-    for _ in range(4):   # the reference's list code is racy: a run may wedge before it rewrites a lost page
-        env = dict(os.environ, TYCHE_APP_WATCHDOG="15", TYCHE_LOG_ERRORS="1", **fault)
+    crashes, runs = [], []
+    for _ in range(6):   # the reference's list code is racy: a run may wedge before it rewrites a lost page
+        env = dict(os.environ, TYCHE_APP_WATCHDOG="15", TYCHE_LOG_ERRORS="1", TYCHE_FAIL_COMPRESS_EVERY="1")
         p = subprocess.run([APP_Q] + args, stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=90, env=env)
         err = p.stderr.decode(errors="replace")
         assert "tyche-engine:" in err                 # the injected failures happened and were reported
+        runs.append(p.returncode)
         if p.returncode == -11:
             bt = err[err.find("fatal signal"):]
             assert "manager__spawn_worker" in bt, bt[-3000:]   # the rewrite's memcpy of the NULL page (manager.c:358)
             crashes.append(p.returncode)
             break
         assert p.returncode == 3, (p.returncode, err[-3000:])   # otherwise only the watchdog may end it
-    print(f"unchanged caller: {len(crashes)} crash(es) in the rewrite of a lost page")
-    assert crashes, "the unchanged caller never reached a lost page in 4 runs"
+    print(f"unchanged caller: runs {runs}, {len(crashes)} crash(es) in the rewrite of a lost page")
+    assert crashes, f"the unchanged caller never reached a lost page: runs {runs}"
 
     attempts = []
     for _ in range(3):

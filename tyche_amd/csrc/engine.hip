@@ -858,11 +858,14 @@ int run_host_batch(int dev, size_t n, const void *const *src, const uint32_t *sr
     // stream and scatters its results while the caller gathers and enqueues the next chunk -- the
     // r03 stage clocks had the caller waiting on streams ~25 % of a call, between its copies.
     // A slot is reused only after the helper has scattered it (S.busy false, under fm).
-    size_t nchunks_est = 0;
+    size_t nchunks_est = 0, rem_in = 0, rem_out = 0;   // rem_*: bytes of the batch not yet in a chunk
     {
-        size_t inb = 0;
-        for (size_t j = 0; j < n; j++) inb += up16(src_len[j]) + up16(dst_cap[j]);
-        nchunks_est = inb / std::max<size_t>(1, (size_t)std::max(1L, knob("HOST_CHUNK_MB", (long)(kChunkBytes >> 20))) << 20);
+        for (size_t j = 0; j < n; j++) {
+            rem_in += up16(src_len[j]);
+            rem_out += up16(dst_cap[j]);
+        }
+        nchunks_est = (rem_in + rem_out) /
+                      std::max<size_t>(1, (size_t)std::max(1L, knob("HOST_CHUNK_MB", (long)(kChunkBytes >> 20))) << 20);
     }
     const bool async = nchunks_est >= 3 && knob("HOST_ASYNC_SCATTER", 1) != 0;
     std::mutex fm;
@@ -944,12 +947,25 @@ int run_host_batch(int dev, size_t n, const void *const *src, const uint32_t *sr
     // output is ~2.6x its input, so cutting by input alone made 3 chunks of 170 MiB
     // of D2H each out of a 32K-page batch, too few to overlap the two copy directions
     const size_t chunk_bytes = (size_t)std::max(1L, knob("HOST_CHUNK_MB", (long)(kChunkBytes >> 20))) << 20;
+    // ramp (HOST_RAMP, default on): the first and the last chunk are a quarter chunk, so the
+    // pipeline fills (H2D + kernel before the first D2H) and drains (the last D2H + scatter,
+    // which nothing overlaps) on small chunks
+    const bool ramp = knob("HOST_RAMP", 1) != 0 && nchunks_est >= 3;
+    const size_t quarter = std::max<size_t>(chunk_bytes / 4, 1u << 20);
+    size_t nchunk = 0;
     while (first < n) {
         // ---- chunk [first, last)
+        size_t limit = chunk_bytes;
+        if (ramp) {
+            const size_t rem = std::max(rem_in, rem_out);
+            if (nchunk == 0) limit = quarter;
+            else if (rem <= chunk_bytes + quarter && rem > quarter) limit = rem - quarter;
+        }
+        nchunk++;
         size_t last = first, in_bytes = 0, out_bytes = 0;
         uint32_t max_in = 0, max_out = 0;
-        while (last < n && (last == first || (in_bytes + up16(src_len[last]) <= chunk_bytes &&
-                                              out_bytes + up16(dst_cap[last]) <= chunk_bytes))) {
+        while (last < n && (last == first || (in_bytes + up16(src_len[last]) <= limit &&
+                                              out_bytes + up16(dst_cap[last]) <= limit))) {
             in_bytes += up16(src_len[last]);
             out_bytes += up16(dst_cap[last]);
             max_in = std::max(max_in, src_len[last]);
@@ -957,6 +973,8 @@ int run_host_batch(int dev, size_t n, const void *const *src, const uint32_t *sr
             last++;
         }
         const size_t k = last - first;
+        rem_in -= in_bytes;
+        rem_out -= out_bytes;
         Slot &S = c.slot[si];
         if (async) {   // the helper has scattered the slot's previous chunk
             std::unique_lock<std::mutex> g(fm);
