@@ -4,7 +4,8 @@
 
 Prints JSON lines: the raw pinned H2D / D2H / bidirectional link rates (bench.pcie_probe),
 then tyche_compress_host / tyche_decompress_host over `pages` malloc'd 16 KiB pages for each
-HOST_CHUNK_MB setting (tyche_set_knob, read per call), best of 3 each.
+HOST_CHUNK_MB setting (tyche_set_knob, read per call), best of 3 each; with AB_KNOB / AB_VALUES
+also an interleaved A/B of one knob.
 """
 import ctypes
 import json
@@ -77,6 +78,28 @@ def main():
                           "compress_ms": round(bc * 1e3, 2), "decompress_ms": round(bd * 1e3, 2),
                           "compress_stages_per_call": sc, "decompress_stages_per_call": sd}), flush=True)
     _lib.clear_knob("HOST_CHUNK_MB")
+    # A/B of one knob in this process (AB_KNOB=name AB_VALUES=v1,v2): the values interleaved 5 times,
+    # best call of each -- box-to-box variance of the host copies is larger than most differences
+    ab = os.environ.get("AB_KNOB")
+    if ab:
+        vals = [int(v) for v in os.environ.get("AB_VALUES", "0,1").split(",")]
+        best = {v: [float("inf"), float("inf")] for v in vals}
+        for _ in range(5):
+            for v in vals:
+                _lib.set_knob(ab, v)
+                t0 = time.perf_counter()
+                _lib.check(lib.tyche_compress_host(1, 1, n, src_p, slen, comp_p, ccap, res.ctypes.data_as(i32p)), "c")
+                best[v][0] = min(best[v][0], time.perf_counter() - t0)
+                clen = u32(*[int(x) for x in res])
+                t0 = time.perf_counter()
+                _lib.check(lib.tyche_decompress_host(1, n, comp_p, clen, out_p, slen, rv.ctypes.data_as(i32p)), "d")
+                best[v][1] = min(best[v][1], time.perf_counter() - t0)
+        _lib.clear_knob(ab)
+        nb = n * plen
+        print(json.dumps({"ab_knob": ab, "pages": n, "best_of": 5,
+                          "results": {str(v): {"compress_gib_s": round(nb / c / GIB, 2), "decompress_gib_s": round(nb / d / GIB, 2),
+                                               "combined_gib_s": round(nb / (c + d) / GIB, 2)} for v, (c, d) in best.items()}}),
+              flush=True)
     # host memcpy rate of the copy pool's work alone (numpy, one thread): scatter-sized copies
     a = np.ones(256 << 20, dtype=np.uint8)
     b = np.empty_like(a)

@@ -11,6 +11,7 @@
 // There is no CPU codec in this library: if the HIP device or the gfx950 code
 // object is unavailable every codec entry point returns an error.
 #include <hip/hip_runtime.h>
+#include <unistd.h>
 #include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -271,8 +272,13 @@ thread_local std::string t_error;
 // TYCHE_LOG_ERRORS=1: every engine failure is also printed to stderr (one
 // "tyche-engine: ..." line), so a caller that drops the status -- list.c:1051
 // keeps going on any rv but 124 -- still leaves a trace (the C1 tests fail on it).
+// The line goes straight to fd 2 (one write): the reference app's stderr is a stdio
+// stream it also prints progress to, and a buffered line would be lost when the
+// app then crashes (the unchanged caller's lost page, test_c1_app.py).
 void log_error(const std::string &m) {
-    if (knob("LOG_ERRORS", 0)) fprintf(stderr, "tyche-engine: %s\n", m.c_str());
+    if (!knob("LOG_ERRORS", 0)) return;
+    const std::string line = "tyche-engine: " + m + "\n";
+    (void)!write(2, line.data(), line.size());
 }
 int fail(const char *what, hipError_t e) {
     t_error = std::string(what) + ": " + hipGetErrorString(e);
