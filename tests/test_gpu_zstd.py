@@ -583,21 +583,27 @@ def test_zstd_many_block_pages(tc, knobs, mode):
             assert outs[i] == want[i], i
 
 
-@pytest.mark.parametrize("mode", ["fused", "chunked", "fse_log6", "fused_fse_log6"])
+ENCODE_MODES = {
+    "fused": dict(ZSTD_ENC_SPLIT=0),
+    "chunked": dict(ZSTD_SCRATCH_MB=1, ZSTD_SPLIT_MIN=1),
+    "fse_log6": dict(ZSTD_FSE_LOG=6),
+    "fused_fse_log6": dict(ZSTD_ENC_SPLIT=0, ZSTD_FSE_LOG=6),
+    "piped_parse": dict(ZSTD_PARSE_PIPE=1),
+    "split_parse2": dict(ZSTD_PARSE_WAVES=2),
+    "split_parse4": dict(ZSTD_PARSE_WAVES=4),
+}
+
+
+@pytest.mark.parametrize("mode", list(ENCODE_MODES))
 def test_zstd_encode_fused_kernel_and_chunked_split(tc, oracle_mod, knobs, mode):
-    """The one-kernel encoder (TYCHE_ZSTD_ENC_SPLIT=0) and the three-pass encoder run through a
-    1 MiB work area (TYCHE_ZSTD_SCRATCH_MB=1: a few pages per chunk), each also with round 2's fixed
-    6/5/6 sequence-table logs (TYCHE_ZSTD_FSE_LOG=6), produce frames the reference decodes: round
+    """Every encode path produces frames the reference decodes: the one-kernel encoder
+    (TYCHE_ZSTD_ENC_SPLIT=0) and the multi-pass encoder through a 1 MiB work area
+    (TYCHE_ZSTD_SCRATCH_MB=1: a few pages per chunk), each also with round 2's fixed 6/5/6
+    sequence-table logs (TYCHE_ZSTD_FSE_LOG=6), and pass A1 on two pipelined waves
+    (TYCHE_ZSTD_PARSE_PIPE=1) or split into 2 / 4 parts (TYCHE_ZSTD_PARSE_WAVES): round
     trips over several distributions and sizes, multi-block and incompressible pages, tight
     capacities."""
-    if mode == "fused":
-        knobs(ZSTD_ENC_SPLIT=0)
-    elif mode == "chunked":
-        knobs(ZSTD_SCRATCH_MB=1, ZSTD_SPLIT_MIN=1)
-    elif mode == "fse_log6":
-        knobs(ZSTD_FSE_LOG=6)
-    else:
-        knobs(ZSTD_ENC_SPLIT=0, ZSTD_FSE_LOG=6)
+    knobs(**ENCODE_MODES[mode])
     for dist in (0, 3):
         for plen in (8192, 32768):
             test_encode_roundtrip_reference_decoder(tc, oracle_mod, dist, plen)

@@ -387,7 +387,7 @@ static double parse_zstd_fast(uint32_t hbits, uint32_t mls) {
 }
 
 /* the device parse with repeat candidates (lz_parse.h kRepCand): nb buckets x ways, hash of hb bytes */
-static uint32_t opt_parts = 1, opt_seed = 1u << 20, opt_carry_rep = 0, gR = 1, gR2 = 4, opt_warm = 0;
+static uint32_t opt_parts = 1, opt_seed = 1u << 20, opt_carry_rep = 0, gR = 1, gR2 = 4, opt_warm = 0, opt_all_blocks = 0;
 static double parse_zstd_device(uint32_t nb, uint32_t ways, uint32_t hb) {
     static uint32_t T[1 << 16][8];
     zreset();
@@ -475,6 +475,15 @@ static double parse_zstd_device(uint32_t nb, uint32_t ways, uint32_t hb) {
         }
         uint32_t nbk = blk + 64;
         if ((cursor & ~63u) > nbk) nbk = cursor & ~63u;
+        if (opt_all_blocks)   /* a finder wave running ahead of the walk inserts the blocks it skips too */
+            for (uint32_t sb = blk + 64; sb < nbk; sb += 64)
+                for (int l2 = 0; l2 < 64; l2++) {
+                    const uint32_t q = sb + l2 <= mflimit ? sb + l2 : mflimit;
+                    const uint64_t x = read64(q) & (hb >= 8 ? ~0ull : ((1ull << (8 * hb)) - 1));
+                    const uint32_t h2 = (uint32_t)((((x * 0xCF1BBCDCB7A56463ull) >> 32) * (uint64_t)nb) >> 32);
+                    for (int w = (int)ways - 1; w > 0; w--) T[h2][w] = T[h2][w - 1];
+                    T[h2][0] = q + 1;
+                }
         blk = nbk;
     }
 #undef mflimit
@@ -546,6 +555,25 @@ static int main_zstd(int n) {
     return 0;
 }
 
+static int main_zstd_allblk(int n) {
+    double raw = 0, d0 = 0, d1 = 0;
+    for (int i = 0; i < n; i++) {
+        pg_page_t p;
+        pg_page_init(&p, 20170303ull, (uint64_t)i, L, 0);
+        for (uint32_t b = 0; b < L; b++) pg[b] = (uint8_t)pg_page_byte(&p, b);
+        memset(pg + L, 0, 64);
+        raw += L;
+        opt_all_blocks = 0;
+        d0 += parse_zstd_device(1856, 2, 5);
+        opt_all_blocks = 1;
+        d1 += parse_zstd_device(1856, 2, 5);
+    }
+    opt_all_blocks = 0;
+    printf("pages %d x %u B: device parse %.3f, with every block inserted (finder ahead of the walk) %.3f\n", n, L,
+           raw / d0, raw / d1);
+    return 0;
+}
+
 static int main_zstd_fse(int n) {
     double raw = 0, d[5] = {0}, r[5] = {0};
     const uint32_t hbits = L <= 16384 ? 14 : 13;
@@ -575,6 +603,7 @@ int main(int argc, char **argv) {
     if (argc > 3 && !strcmp(argv[3], "zstd")) return main_zstd(n);
     if (argc > 3 && !strcmp(argv[3], "zsplit")) return main_zstd_split(n);
     if (argc > 3 && !strcmp(argv[3], "zfse")) return main_zstd_fse(n);
+    if (argc > 3 && !strcmp(argv[3], "zallblk")) return main_zstd_allblk(n);
     static const uint32_t grid[][2] = {{1024, 4}, {2048, 4}, {512, 8}, {1024, 8}, {2048, 8}, {1024, 6}, {4096, 8}};
     const int ng = (int)(sizeof grid / sizeof grid[0]);
     double raw = 0, zl = 0, zf = 0, var[16] = {0}, var_r[16] = {0};

@@ -207,6 +207,12 @@ __device__ __forceinline__ uint32_t bucket_of(uint32_t v, uint32_t v2 = 0, uint3
     }
     return (v * 2654435761u) >> (32 - lg);
 }
+#ifndef TYCHE_PW_PREFETCH
+// 1: parse_page loads the next block's window ahead, with the current block's candidate
+// windows.  Measured (round 3, 1M x 16 KiB LZ4 pages): 85.0 ms off, 85.9-86.1 on; zlib 645 /
+// 650 -- the LDS latency it hides is not what bounds the parse, and its 6 VGPRs cost.  Off.
+#define TYCHE_PW_PREFETCH 0
+#endif
 #ifndef TYCHE_HASH_BYTES
 #define TYCHE_HASH_BYTES 5   // kRepCand (zstd): bytes hashed -- zstd level 1 hashes searchLength bytes
 #endif
@@ -229,6 +235,8 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
     uint32_t blk = start;    // current 64-position block
     uint32_t R = rep ? rep[0] : 1u, R2 = rep ? rep[1] : 4u;   // repeat offsets 1 and 2 (kRepCand): zstd's initial {1, 4}
     bool done = false;
+    Window pwn{};                       // TYCHE_PW_PREFETCH: the next block's window, loaded ahead
+    uint32_t pwn_blk = 0xFFFFFFFFu;     // the block it belongs to (none yet)
     PHASE_INIT();
     for (; !done && blk <= mflimit; blk = max(blk + kWave, cursor & ~(kWave - 1))) {
         const uint32_t pos = blk + lane;
@@ -238,7 +246,7 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
         // then insert this block's positions.  Every lane takes part, branch-free:
         // lanes past mflimit only exist in the last block, and no lookup follows
         // their inserts.
-        const Window pw = lds_window(A, (live ? pos : mflimit) + ib);
+        const Window pw = (TYCHE_PW_PREFETCH && pwn_blk == blk) ? pwn : lds_window(A, (live ? pos : mflimit) + ib);
         const uint32_t v = pw.w0;
         constexpr uint32_t vm = kMin3 ? 0xFFFFFFu : 0xFFFFFFFFu;   // the bytes a candidate must match
         uint32_t cands[kWays];
@@ -324,6 +332,15 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
                 n = nw;
                 ok = true;
             }
+        }
+        if (TYCHE_PW_PREFETCH) {
+            // the next block's window goes out with this block's candidate windows: its LDS
+            // latency overlaps this block's compares and walk instead of heading the next
+            // block's chain (window -> hash -> table -> candidate window).  A walk that
+            // jumps past the next block (a match running beyond it) reloads.
+            const uint32_t np = blk + kWave + lane;
+            pwn = lds_window(A, (np <= mflimit ? np : mflimit) + ib);
+            pwn_blk = blk + kWave;
         }
         if (kMin3) {
             // distance 4 straight from this position's window (arrays of 4-byte
@@ -491,6 +508,213 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
     }
     PHASE(3);
     PHASE_FLUSH();
+    return anchor;
+}
+
+// ---- Two-wave pipelined parse (zstd: repeat candidates, 2 ways, 5-byte hash).
+//
+// parse_page's block chain is window -> hash -> table -> candidate windows ->
+// compares -> repeat candidates -> walk, and at one wave per SIMD (the zstd
+// parse's LDS holds a CU to 4 waves) that chain is latency-bound.  Here a
+// workgroup of two waves shares the page: the finder (wave 0) runs block k+1's
+// hash side -- window, bucket read and insert, both bucket candidates' windows
+// and compares -- while the walker (wave 1) runs block k's repeat candidates, the
+// walk and the records; they meet at one workgroup barrier per block, the finder
+// handing over (candidate, length, ok, backward extension) per lane in a
+// two-slot LDS ring.  The finder processes every block: it cannot know which ones
+// the walk will skip, so positions inside long matches are inserted too
+// (tools/parse_sim.c zallblk: ratio unchanged, 5.034 / 4.785 at 32 / 16 KiB).
+// Everything else -- which candidates a position tries, the walk, the records
+// -- is parse_page<true, false, 2>'s.  Measured (round 3, C3 pages): encode
+// 1,205 vs 1,026 ms per 1M pages for the one-wave A1 at the same ratio -- 3 pages
+// per CU instead of 4 (41.9 KiB of LDS) and a barrier per block do not pay for the
+// overlap, as with round 2's LZ4 finder/parser pipeline.  Off by default
+// (TYCHE_ZSTD_PARSE_PIPE=1 selects it).
+struct PipeSlot {
+    uint32_t a[kWave];   // cand | n << 16 (n <= 20) | ok << 24 | back << 25 (0..4)
+};
+
+__device__ __forceinline__ void pipe_find(const uint32_t *A, uint32_t ib, uint32_t blk, uint32_t mflimit,
+                                          uint16_t *table, PipeSlot &sl, uint32_t lane) {
+    const uint32_t pos = blk + lane;
+    const bool live = pos <= mflimit;
+    const Window pw = lds_window(A, (live ? pos : mflimit) + ib);
+    const uint32_t v = pw.w0;
+    uint32_t *T = (uint32_t *)table;
+    const uint32_t h = bucket_of<2>(v, pw.fw[0], TYCHE_HASH_BYTES);
+    const uint32_t bk = T[h];
+    __builtin_amdgcn_wave_barrier();
+    T[h] = pos | (bk << 16);
+    uint32_t cand = bk & 0xFFFFu;
+    Window cw = lds_window(A, cand + ib);
+    const uint32_t cand2 = bk >> 16;
+    const Window ww = lds_window(A, cand2 + ib);
+    bool ok = live & (cand < pos) & (cw.w0 == v);
+    uint32_t n = 4u + kProbe;
+#pragma unroll
+    for (int k = (int)kProbeWords - 1; k >= 0; k--) {
+        const uint32_t x = pw.fw[k] ^ cw.fw[k];
+        if (x) n = 4u + 4u * (uint32_t)k + ((uint32_t)__builtin_ctz(x) >> 3);
+    }
+    const bool okw = live & (cand2 < pos) & (ww.w0 == v);
+    uint32_t nw = 4u + kProbe;
+#pragma unroll
+    for (int k = (int)kProbeWords - 1; k >= 0; k--) {
+        const uint32_t x = pw.fw[k] ^ ww.fw[k];
+        if (x) nw = 4u + 4u * (uint32_t)k + ((uint32_t)__builtin_ctz(x) >> 3);
+    }
+    if (okw && (!ok || nw > n)) {   // the older bucket entry: taken only when strictly longer
+        cand = cand2;
+        cw = ww;
+        n = nw;
+        ok = true;
+    }
+    const uint32_t xb = pw.back ^ cw.back;
+    const uint32_t back = pos < 4 || cand < 4 ? 0u : xb ? (__builtin_clz(xb) >> 3) : 4u;
+    sl.a[lane] = cand | (n << 16) | ((ok ? 1u : 0u) << 24) | (back << 25);
+}
+
+// Both waves of the workgroup call this (wave 0 the finder, wave 1 the walker)
+// with the same in, L; the walker's sink gets the records.  Returns (walker) the
+// anchor of the last literal run, or 0xFFFFFFFF if the sink aborted.  slots:
+// two PipeSlot in LDS; flag: one LDS word.
+template <typename Sink>
+__device__ uint32_t parse_page_piped(const uint8_t *in, uint32_t L, uint16_t *table, uint2 *rec, PipeSlot *slots,
+                                     uint32_t *flag, uint32_t wave, uint32_t lane, Sink &sink) {
+    if (L < (uint32_t)(kMfLimit + 1)) return 0;
+    const uint32_t mflimit = L - kMfLimit;
+    const uint32_t matchlimit = L - kLastLiterals;
+    const uint32_t ib = (uint32_t)(uintptr_t)in & 3u;
+    const uint32_t *A = (const uint32_t *)(in - ib);
+    const uint32_t nblk = mflimit / kWave + 1u;   // blocks 0, 64, ... <= mflimit
+    uint32_t anchor = 0, cursor = 0, nacc = 0, next_blk = 0, R = 1u, R2 = 4u;
+    bool done = false, aborted = false;
+    if (wave == 1 && lane == 0) *flag = 0;
+    __syncthreads();
+    for (uint32_t t = 0; t <= nblk; t++) {
+        if (wave == 0) {
+            if (t < nblk) pipe_find(A, ib, t * kWave, mflimit, table, slots[t & 1u], lane);
+        } else if (t >= 1 && !done && (t - 1u) * kWave == next_blk) {
+            const uint32_t blk = next_blk;
+            const PipeSlot &sl = slots[(t - 1u) & 1u];
+            const uint32_t pos = blk + lane;
+            const bool live = pos <= mflimit;
+            const Window pw = lds_window(A, (live ? pos : mflimit) + ib);
+            const uint32_t v = pw.w0;
+            const uint32_t sa = sl.a[lane];
+            uint32_t cand = sa & 0xFFFFu, n = (sa >> 16) & 0xFFu, back = sa >> 25;
+            bool ok = ((sa >> 24) & 1u) != 0u;
+            // ---- repeat candidates (parse_page's kRepCand block)
+            const uint32_t rc = pos >= R ? pos - R : 0u;
+            const Window rw = lds_window(A, min(rc, mflimit) + ib);
+            bool rok = live & (pos >= R) & (rw.w0 == v);
+            uint32_t rn = 4u + kProbe;
+#pragma unroll
+            for (int k = (int)kProbeWords - 1; k >= 0; k--) {
+                const uint32_t x = pw.fw[k] ^ rw.fw[k];
+                if (x) rn = 4u + 4u * (uint32_t)k + ((uint32_t)__builtin_ctz(x) >> 3);
+            }
+            const uint32_t rc2 = pos >= R2 ? pos - R2 : 0u;
+            const Window rw2 = lds_window(A, min(rc2, mflimit) + ib);
+            const bool rok2 = TYCHE_REP2 && live & (pos >= R2) & (rw2.w0 == v) & (R2 != R);
+            uint32_t rn2 = 4u + kProbe;
+#pragma unroll
+            for (int k = (int)kProbeWords - 1; k >= 0; k--) {
+                const uint32_t x = pw.fw[k] ^ rw2.fw[k];
+                if (x) rn2 = 4u + 4u * (uint32_t)k + ((uint32_t)__builtin_ctz(x) >> 3);
+            }
+            auto back_of = [&](uint32_t c, uint32_t cb) {
+                const uint32_t x = pw.back ^ cb;
+                return pos < 4 || c < 4 ? 0u : x ? (__builtin_clz(x) >> 3) : 4u;
+            };
+            if (rok && (!ok || rn + TYCHE_REP_SLACK >= n)) {
+                cand = rc;
+                back = back_of(rc, rw.back);
+                n = rn;
+                ok = true;
+            }
+            if (rok2 && (!ok || rn2 + TYCHE_REP_SLACK >= n) && !(rok && rn >= rn2)) {
+                cand = rc2;
+                back = back_of(rc2, rw2.back);
+                n = rn2;
+                ok = true;
+            }
+            rok |= rok2;
+            const uint32_t e = min(matchlimit, pos + kMinMatch + kProbe);
+            n = min(n, e - pos);
+            uint32_t len = n;
+            const bool capped = pos + n == e && e < matchlimit;
+            // ---- the walk (parse_page's)
+            uint64_t mall = __ballot(ok);
+            if (TYCHE_REP_NEXT) {
+                const uint64_t mrep = __ballot(rok);
+                mall &= ~(mrep >> 1) | mrep;
+            }
+            const uint32_t at = cursor > blk ? cursor - blk : 0u;
+            const uint64_t rem = mall & (~0ull << at);
+            if (rem != 0) {
+                const uint32_t endp = pos + len;
+                const uint32_t rl = endp - blk;
+                const uint64_t after = rl < kWave ? mall & (~0ull << rl) : 0ull;
+                const uint32_t nxt = capped ? 2u * kWave : after ? (uint32_t)__builtin_ctzll(after) : kWave;
+                uint64_t sel = 0;
+                uint32_t li = (uint32_t)__builtin_ctzll(rem);
+                uint32_t end;
+                for (;;) {
+                    uint32_t at_li;
+                    do {
+                        at_li = li;
+                        sel |= 1ull << li;
+                        const uint32_t off = blk + li - rdlane(cand, li);
+                        if (off != R) {
+                            R2 = R;
+                            R = off;
+                        }
+                        li = rdlane(nxt, li);
+                    } while (li < kWave);
+                    if (li == kWave) {
+                        end = rdlane(endp, at_li);
+                        break;
+                    }
+                    const uint32_t mp = blk + at_li, mc = rdlane(cand, at_li), ln0 = rdlane(endp, at_li) - mp;
+                    const uint32_t ln = ln0 + wave_extend(in, A, ib, mp + ln0, mc + ln0, matchlimit, lane);
+                    if (lane == at_li) len = ln;
+                    end = mp + ln;
+                    const uint32_t rel = end - blk;
+                    const uint64_t r = rel < kWave ? mall & (~0ull << rel) : 0ull;
+                    if (r == 0) break;
+                    li = (uint32_t)__builtin_ctzll(r);
+                }
+                cursor = end;
+                done = cursor > mflimit;
+                const bool is_sel = (sel >> lane) & 1ull;
+                const uint32_t rank = nacc + (uint32_t)__popcll(sel & ((1ull << lane) - 1ull));
+                if (is_sel) rec[rank] = make_uint2(pos | (cand << 16), len | (back << 16));
+                nacc += (uint32_t)__popcll(sel);
+                if (nacc > kWave - 16u || done) {
+                    __builtin_amdgcn_wave_barrier();
+                    if (!sink(rec, nacc, anchor)) {
+                        aborted = true;
+                        done = true;
+                    }
+                    anchor = cursor;
+                    nacc = 0;
+                }
+            }
+            next_blk = max(blk + kWave, cursor & ~(kWave - 1u));
+            if (next_blk > mflimit) done = true;
+            if (done && lane == 0) *flag = 1;
+        }
+        __syncthreads();
+        if (rfl(*flag)) break;   // the walk is over: the finder stops too
+    }
+    if (wave == 0) return 0;
+    if (aborted) return 0xFFFFFFFFu;
+    if (nacc) {
+        __builtin_amdgcn_wave_barrier();
+        if (!sink(rec, nacc, anchor)) return 0xFFFFFFFFu;
+        anchor = cursor;
+    }
     return anchor;
 }
 

@@ -747,8 +747,10 @@ __device__ __forceinline__ int32_t encode_page(const uint8_t *in, uint32_t L, ui
 // Pass A1: the parse of one page (LDS, 64 zero bytes after) into the area: the
 // sequences, and blocks cut where encode_page's sink cuts them.  Returns 1, or
 // 0 when a bound is exceeded (the page is then stored uncompressed by the caller).
-__device__ __forceinline__ int32_t parse_to_area(const uint8_t *in, uint32_t L, uint16_t *table, uint2 *rec,
-                                                 uint8_t *area, uint32_t rec_cap, uint32_t lane) {
+// parse(sink) runs the parse over the page and returns its last anchor.
+template <typename Parse>
+__device__ __forceinline__ int32_t parse_to_area_with(uint32_t L, uint8_t *area, uint32_t rec_cap, uint32_t lane,
+                                                      Parse &&parse) {
     uint2 *S = area_seq(area, rec_cap);
     uint32_t nseq = 0, bseq = 0, bstart = 0, cursor = 0, npb = 0;
     auto put_pblk = [&](uint32_t bend) {
@@ -778,11 +780,17 @@ __device__ __forceinline__ int32_t parse_to_area(const uint8_t *in, uint32_t L, 
         }
         return true;
     };
-    const uint32_t anchor = lzp::parse_page<true, false, kZWays>(in, L, table, rec, lane, sink);
+    const uint32_t anchor = parse(sink);
     if (anchor == 0xFFFFFFFFu) return 0;
     put_pblk(L);
     if (lane == 0) ((uint32_t *)area)[1] = npb;
     return 1;
+}
+__device__ __forceinline__ int32_t parse_to_area(const uint8_t *in, uint32_t L, uint16_t *table, uint2 *rec,
+                                                 uint8_t *area, uint32_t rec_cap, uint32_t lane) {
+    return parse_to_area_with(L, area, rec_cap, lane, [&](auto &sink) {
+        return lzp::parse_page<true, false, kZWays>(in, L, table, rec, lane, sink);
+    });
 }
 
 // Pass A2: frame header and every block of the page from the area (the page
@@ -909,7 +917,77 @@ __global__ __launch_bounds__(64) void zstd_encode_kernel(tyche_batch_t b, size_t
     }
 }
 
-// ---- pass A1 on kNW waves per page (round 3, TYCHE_ZSTD_PARSE_WAVES, default 4).
+// ---- pass A1 on two pipelined waves per page (round 3, TYCHE_ZSTD_PARSE_PIPE=1; not the
+// default: 1,205 vs 1,026 ms per 1M x 32 KiB pages for the one-wave kernel above).  lzp::parse_page_piped: the finder wave hashes block k+1 while
+// the walker wave takes block k's repeat candidates and walk; the records (and so the frames)
+// are the one-wave parse's except that the finder also inserts the blocks the walk skips.
+// LDS: header, the table, the two-slot ring, the walker's records and the page (41.9 KiB at
+// 32 KiB pages: 3 pages, 6 waves per CU).
+struct ZPipeHdr {
+    uint32_t next_lo, next_hi, next2_lo, next2_hi, flag, pad[11];
+};
+static_assert(sizeof(ZPipeHdr) == 64, "pipe header");
+constexpr size_t kZPipeStage = sizeof(ZPipeHdr) + kTableSlots * sizeof(uint16_t) + 2 * sizeof(lzp::PipeSlot) + kWave * 8;
+__global__ __launch_bounds__(128) void zstd_parse_pipe_kernel(tyche_batch_t b, size_t first, size_t count,
+                                                              uint32_t in_cap, unsigned *ctr, uint8_t *ws,
+                                                              size_t ws_page, int32_t *st) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t wave = rfl(tid >> 6);
+    ZPipeHdr *hdr = (ZPipeHdr *)smem;
+    uint16_t *table = (uint16_t *)(smem + sizeof(ZPipeHdr));
+    lzp::PipeSlot *slots = (lzp::PipeSlot *)(smem + sizeof(ZPipeHdr) + kTableSlots * sizeof(uint16_t));
+    uint2 *rec = (uint2 *)(slots + 2);
+    uint8_t *stage = smem + kZPipeStage;
+    const uint32_t rec_cap = enc_rec_cap(in_cap);
+
+    size_t page = blockIdx.x;   // chunk-local
+    if (page >= count) return;
+    PageRef p = batch_page(b, first + page);
+    uint32_t head = stage_in(p.src, p.src_len <= in_cap ? p.src_len : 0, stage, tid, 2 * kWave);
+    if (tid == 0) {
+        const size_t nx = (size_t)atomicAdd(ctr, 1u) + gridDim.x;   // dynamic assignment (engine.h)
+        hdr->next_lo = (uint32_t)nx;
+        hdr->next_hi = (uint32_t)(nx >> 32);
+    }
+    for (;;) {
+        for (uint32_t w = tid; w < kTableSlots / 8; w += 2 * kWave) ((u32x4 *)table)[w] = u32x4{0, 0, 0, 0};
+        if (tid < kWave) stage[head + p.src_len + tid] = 0;
+        __syncthreads();
+        const size_t next = (size_t)rfl(hdr->next_lo) | ((size_t)rfl(hdr->next_hi) << 32);
+        const uint8_t *in = stage + head;
+        const uint32_t L = p.src_len;
+        int32_t rv = kResultTooLarge;
+        if (L <= in_cap) {   // uniform over the workgroup: both waves run the parse's barriers
+            if (wave == 1) {
+                rv = parse_to_area_with(L, ws + page * ws_page, rec_cap, lane, [&](auto &sink) {
+                    return lzp::parse_page_piped(in, L, table, rec, slots, &hdr->flag, 1u, lane, sink);
+                });
+            } else {
+                auto none = [](const uint2 *, uint32_t, uint32_t) -> bool { return true; };
+                (void)lzp::parse_page_piped(in, L, table, rec, slots, &hdr->flag, 0u, lane, none);
+            }
+        }
+        if (tid == 0) {
+            const size_t nx = (size_t)atomicAdd(ctr, 1u) + gridDim.x;
+            hdr->next2_lo = (uint32_t)nx;
+            hdr->next2_hi = (uint32_t)(nx >> 32);
+        }
+        if (wave == 1 && lane == 0) st[page] = rv;
+        __syncthreads();   // the stage, the table and the header are free
+        if (next >= count) break;
+        page = next;
+        p = batch_page(b, first + page);
+        head = stage_in(p.src, p.src_len <= in_cap ? p.src_len : 0, stage, tid, 2 * kWave);
+        if (tid == 0) {
+            hdr->next_lo = hdr->next2_lo;
+            hdr->next_hi = hdr->next2_hi;
+        }
+    }
+}
+
+// ---- pass A1 on kNW waves per page (round 3, TYCHE_ZSTD_PARSE_WAVES 2 / 4; not the default:
+// the parts' parses cost ratio, 4.947 -> 4.910 at 2 waves).
 //
 // The one-wave A1 holds page + hash table (40.8 KiB at 32 KiB pages: 4 waves per
 // CU, one per SIMD) and was 737 of the encoder's 995 ms per 1M x 32 KiB pages --
@@ -1347,9 +1425,26 @@ hipError_t launch_zstd_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kp, (int)(pw * kWave), ldsp) == hipSuccess && per > 0)
             cup = (size_t)per;
     }
+    // pass A1 on two pipelined waves (TYCHE_ZSTD_PARSE_PIPE=1; default 0: one wave per page)
+    const bool pipe = pw != 2 && pw != 4 && knob("ZSTD_PARSE_PIPE", 0) != 0;
+    const size_t ldsq = kZPipeStage + page_lds;
+    size_t cuq = 1;
+    if (pipe) {
+        (void)prepare_launch((const void *)zstd_parse_pipe_kernel);
+        int per = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void *)zstd_parse_pipe_kernel, 2 * (int)kWave, ldsq) ==
+                hipSuccess && per > 0)
+            cuq = (size_t)per;
+    }
     for (size_t first = 0; first < b.count; first += chunk) {
         const size_t n = std::min(chunk, b.count - first);
-        if (pw == 2 || pw == 4) {   // pass A1 on pw waves per page
+        if (pipe) {
+            const size_t g = std::min<size_t>(n, ncu * cuq);
+            WorkCounter ctr(s, g < n);
+            if (!ctr.get()) return hipErrorOutOfMemory;
+            hipLaunchKernelGGL(zstd_parse_pipe_kernel, dim3((unsigned)g), dim3(2 * kWave), ldsq, s, b, first, n, in_cap,
+                               ctr.get(), ws, page_bytes, st);
+        } else if (pw == 2 || pw == 4) {   // pass A1 on pw waves per page
             const void *kp = pw == 4 ? (const void *)zstd_parse_split_kernel<4> : (const void *)zstd_parse_split_kernel<2>;
             const size_t ldsp = (pw == 4 ? zsplit_stage_off<4>() : zsplit_stage_off<2>()) + page_lds;
             const size_t g = std::min<size_t>(n, ncu * cup);
