@@ -42,7 +42,7 @@ namespace tyche {
 namespace {
 
 // Optional phase profile (diagnostic build only: -DTYCHE_PROFILE,
-// tools/zstd_prof.py): shader cycles per phase summed by lane 0.
+// tools/zstd_phases.py): shader cycles per phase summed by lane 0.
 #ifdef TYCHE_PROFILE
 __device__ unsigned long long g_sdprof[16];
 #define SPROF_DECL unsigned long long _pt = clock64();
@@ -1087,6 +1087,7 @@ __device__ int32_t decode_block(const Work &W, SeqTables &T, const Ent &E, uint3
         } else if (single) {
             uint32_t tl;
             const int32_t hs = huf_read_table(W, cs, csize, tl, lane);
+            SPROF_MARK(7);
             ok = hs >= 0 && hs < csize;
             if (ok) {
                 T.huf_log = tl;
@@ -1097,6 +1098,7 @@ __device__ int32_t decode_block(const Work &W, SeqTables &T, const Ent &E, uint3
             if (ok) {
                 uint32_t tl;
                 const int32_t hs = huf_read_table(W, cs, csize, tl, lane);
+                SPROF_MARK(7);
                 ok = hs >= 0 && hs < csize;
                 if (ok) {
                     T.huf_log = tl;
