@@ -515,6 +515,9 @@ DECODE_MODES = {
     "seqexec": dict(ZSTD_EXEC_LANE_MIN=0),
     "seqexec_slots6": dict(ZSTD_EXEC_LANE_MIN=0, ZSTD_SEQ_SLOTS=6),
     "seqexec_chunked": dict(ZSTD_EXEC_LANE_MIN=0, ZSTD_SCRATCH_MB=1),
+    # literal streams: 16 pages per wave, or left in pass 1
+    "seqexec_lit16": dict(ZSTD_EXEC_LANE_MIN=0, ZSTD_LIT_LANES=16),
+    "seqexec_lit_pass1": dict(ZSTD_EXEC_LANE_MIN=0, ZSTD_LIT_LANES=0),
     "lane_exec": dict(ZSTD_EXEC_LANE_MIN=0, ZSTD_SEQEXEC=0),
 }
 
@@ -526,7 +529,8 @@ def test_zstd_fused_kernel_and_chunked_split(tc, oracle_mod, knobs, mode):
     decoder through a 1 MiB pass-1 buffer (TYCHE_ZSTD_SCRATCH_MB=1: a handful of pages per chunk),
     with the sequence chains inline in pass 1 (TYCHE_ZSTD_JOBS=0), and the lane-per-page second
     passes (zstd_seqexec_kernel with both LDS slot sizes, zstd_exec_lane_kernel) on batches of
-    any size."""
+    any size, with the Huffman literal streams lane-per-stream (zstd_lit_kernel, 8 or 16 pages
+    per wave) or in pass 1."""
     knobs(**DECODE_MODES[mode])
     test_zstd_reference_frames(tc, 3)
     test_zstd_malformed(tc, oracle_mod)

@@ -907,6 +907,11 @@ struct SeqTables {
     // none yet), jobs written, table bytes used
     bool jobs;
     uint32_t ll_off, of_off, ml_off, njobs, tb_used;
+    // pass 1 with literal jobs (the Huffman streams run lane-per-stream in zstd_lit_kernel):
+    // the published Huffman table in force (offset in the page's Huffman region, or -1 when
+    // the table in W.huf was not published), tables published, literal jobs written
+    int32_t huf_pub;
+    uint32_t nhuf, nlj;
 };
 
 // ZSTD_buildSeqTable (zstd_decompress.c:693-724).  Returns bytes read or < 0.
@@ -967,6 +972,9 @@ struct Ent {
     uint32_t *tabs;           // FSE cells of the tables the jobs use
     bool fused;               // zstd_seqexec_kernel's layout: commands only, no sequence entries
     int32_t over;             // pass 1's result when the planes are full (fused: kRetryFused)
+    bool defer_lit;           // Huffman literal streams left to zstd_lit_kernel (fused layout)
+    uint32_t *litjobs;        // [0] = literal job count, then kLitJobWords words per job
+    uint16_t *hufs;           // published Huffman decoding tables, kHufCells entries each
 };
 // Sequence jobs: one per compressed block with sequences, decoded by
 // zstd_seq_kernel one page per lane -- the chain is serial within a page, so the
@@ -976,7 +984,17 @@ constexpr uint32_t kJobWords = 8;   // start, length, nbSeq, first entry, ll/of/
 constexpr uint32_t kMaxJobs = 31;
 constexpr uint32_t kJobBytes = 4u * (4u + kMaxJobs * kJobWords);   // 1008
 constexpr uint32_t kTabBytes = 12u * 1024u;                       // two full LL+OF+ML sets and more
-constexpr uint32_t kAreaBytes = 13312u;                           // jobs + tables, 256-aligned
+// Literal jobs (round 3, fused layout): one per Huffman-compressed literals section whose
+// table has at most kHufCells entries (tableLog <= 11), decoded by zstd_lit_kernel one stream
+// per lane; the table is published to the area (at most kMaxHuf per page).  Pages with more
+// sections or tables decode the rest in pass 1 as before.
+constexpr uint32_t kLitJobWords = 8;   // streams' start and length, lsize, literal-buffer position, table, log | single << 8
+constexpr uint32_t kMaxLitJobs = 31;
+constexpr uint32_t kLitJobBytes = 4u * (4u + kMaxLitJobs * kLitJobWords);   // 1008
+constexpr uint32_t kHufCells = 2048;
+constexpr uint32_t kMaxHuf = 4;
+constexpr uint32_t kAreaJobs = 13312u;                            // seq jobs + FSE tables
+constexpr uint32_t kAreaBytes = kAreaJobs + kLitJobBytes + kMaxHuf * kHufCells * 2u + 16u;   // 256-aligned: 30720
 constexpr uint32_t kTabDefault = 0xFFFFFFFFu;
 constexpr int32_t kRetryInline = -1000;
 // fused layout: a page with more than kFusedCmds block commands, or whose jobs do not fit
@@ -995,6 +1013,9 @@ __device__ inline Ent ent_of(uint8_t *area, uint32_t in_cap, uint32_t out_cap, b
     Ent E;
     E.jobs = (uint32_t *)area;
     E.tabs = (uint32_t *)(area + kJobBytes);
+    E.litjobs = (uint32_t *)(area + kAreaJobs);
+    E.hufs = (uint16_t *)(area + kAreaJobs + kLitJobBytes);
+    E.defer_lit = false;
     E.fused = fused;
     E.over = fused ? kRetryFused : kErr;
     uint8_t *base = area + kAreaBytes;
@@ -1082,8 +1103,31 @@ __device__ int32_t decode_block(const Work &W, SeqTables &T, const Ent &E, uint3
         }
         const int32_t cs = ip + lh;
         bool ok;
+        // defer: the streams go to zstd_lit_kernel when the table is (or can be) published
+        auto defer = [&](int32_t at, int32_t len) -> bool {
+            if (!(kSplit && E.defer_lit && T.huf_pub >= 0 && T.nlj < kMaxLitJobs)) return false;
+            if (lane == 0) {
+                uint32_t *J = E.litjobs + 4u + T.nlj * kLitJobWords;
+                J[0] = (uint32_t)at;
+                J[1] = (uint32_t)len;
+                J[2] = (uint32_t)lsize;
+                J[3] = lat;
+                J[4] = (uint32_t)T.huf_pub;
+                J[5] = T.huf_log | ((single ? 1u : 0u) << 8);
+            }
+            T.nlj++;
+            return true;
+        };
+        auto publish = [&](uint32_t tl) {   // after a new table: publish it if it fits a slot
+            T.huf_pub = -1;
+            if (!(kSplit && E.defer_lit) || tl > 11u || T.nhuf >= kMaxHuf) return;
+            uint16_t *g = E.hufs + T.nhuf * kHufCells;
+            for (uint32_t i = lane; i < (1u << tl); i += kWave) g[i] = W.huf[i];
+            T.huf_pub = (int32_t)(T.nhuf * kHufCells);
+            T.nhuf++;
+        };
         if (ltype == 3u) {
-            ok = huf_decode<kSplit>(W, cs, csize, single, (uint32_t)lsize, T.huf_log, dst, lane);
+            ok = defer(cs, csize) || huf_decode<kSplit>(W, cs, csize, single, (uint32_t)lsize, T.huf_log, dst, lane);
         } else if (single) {
             uint32_t tl;
             const int32_t hs = huf_read_table(W, cs, csize, tl, lane);
@@ -1091,7 +1135,8 @@ __device__ int32_t decode_block(const Work &W, SeqTables &T, const Ent &E, uint3
             ok = hs >= 0 && hs < csize;
             if (ok) {
                 T.huf_log = tl;
-                ok = huf_decode<kSplit>(W, cs + hs, csize - hs, true, (uint32_t)lsize, tl, dst, lane);
+                publish(tl);
+                ok = defer(cs + hs, csize - hs) || huf_decode<kSplit>(W, cs + hs, csize - hs, true, (uint32_t)lsize, tl, dst, lane);
             }
         } else {
             ok = lsize != 0 && csize < lsize && csize > 1;
@@ -1102,7 +1147,9 @@ __device__ int32_t decode_block(const Work &W, SeqTables &T, const Ent &E, uint3
                 ok = hs >= 0 && hs < csize;
                 if (ok) {
                     T.huf_log = tl;
-                    ok = huf_decode<kSplit>(W, cs + hs, csize - hs, false, (uint32_t)lsize, tl, dst, lane);
+                    publish(tl);
+                    ok = defer(cs + hs, csize - hs) ||
+                         huf_decode<kSplit>(W, cs + hs, csize - hs, false, (uint32_t)lsize, tl, dst, lane);
                 }
             }
         }
@@ -1374,6 +1421,9 @@ __device__ int32_t decode_frame(const Work &W, const Ent &E, int32_t L, int32_t 
     T.ll_off = T.of_off = T.ml_off = kTabDefault;
     T.njobs = 0;
     T.tb_used = 0;
+    T.huf_pub = -1;
+    T.nhuf = 0;
+    T.nlj = 0;
     int32_t ip = fh, remaining = L - fh, op = 0;
     uint32_t ecur = 0, litc = 0;
     for (;;) {
@@ -1431,7 +1481,10 @@ __device__ int32_t decode_frame(const Work &W, const Ent &E, int32_t L, int32_t 
     if constexpr (kSplit) {
         if (ecur >= E.ecap) return E.over;
         put_cmd(E, ecur, kCmdEnd | ((uint32_t)checksum << 2), 0u, sum, lane);
-        if (lane == 0) E.jobs[0] = T.njobs;
+        if (lane == 0) {
+            E.jobs[0] = T.njobs;
+            E.litjobs[0] = T.nlj;
+        }
         return 0;
     }
     return op;
@@ -2170,10 +2223,122 @@ __global__ __launch_bounds__(64) void zstd_seqexec_kernel(tyche_batch_t b, size_
     }
 }
 
+// ---- literal streams, one per lane (fused layout, TYCHE_ZSTD_LIT_LANES; between pass 1 and
+// zstd_seqexec_kernel).
+//
+// Pass 1 decoded a section's 1 or 4 Huffman streams in lanes 0-3 of its wave, ~480 cycles per
+// symbol (the whole wave's instruction stream for 4 lanes: 60 % of pass 1, tools/zstd_phases.py).
+// Here lane 4g + s decodes stream s of page g of the workgroup, kGroups pages per wave: the
+// page's published table is copied to its group's LDS slot (kHufCells x 16 bit) and each lane
+// walks its stream from global memory (huf_decode's reader, checks and end test), writing
+// whole aligned 8-byte words of the literal buffer.  A failed stream fails the page.
+template <uint32_t kGroups>
+__global__ __launch_bounds__(64) void zstd_lit_kernel(tyche_batch_t b, size_t first, size_t count, uint32_t in_cap,
+                                                      uint32_t out_cap, uint8_t *ws, size_t ws_page, int32_t *st) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint32_t lane = threadIdx.x, g = lane >> 2, s = lane & 3u;
+    uint16_t *tab = (uint16_t *)smem + min(g, kGroups - 1u) * kHufCells;
+    const size_t j = (size_t)blockIdx.x * kGroups + g;
+    const bool act = g < kGroups && j < count && st[j] >= 0;
+    Ent E;
+    const uint8_t *src = nullptr;
+    uint32_t njobs = 0;
+    if (act) {
+        E = ent_of(ws + j * ws_page, in_cap, out_cap, true);
+        njobs = E.litjobs[0];
+        const size_t i = first + j;
+        src = (const uint8_t *)b.src + (b.src_offsets ? b.src_offsets[i] : (uint64_t)i * b.src_stride);
+    }
+    uint32_t maxj = njobs;
+#pragma unroll
+    for (uint32_t m = 1; m < kWave; m <<= 1) maxj = max(maxj, (uint32_t)__shfl_xor((int)maxj, (int)m));
+    bool ok = true;
+    for (uint32_t q = 0; q < maxj; q++) {
+        const bool has = act && q < njobs;
+        uint32_t cs = 0, n = 0, lsize = 0, lat = 0, toff = 0, tlog = 0;
+        bool single = false;
+        if (has) {
+            const uint32_t *J = E.litjobs + 4u + q * kLitJobWords;
+            cs = J[0];
+            n = J[1];
+            lsize = J[2];
+            lat = J[3];
+            toff = J[4];
+            tlog = J[5] & 255u;
+            single = ((J[5] >> 8) & 1u) != 0u;
+            // the group's four lanes copy the table, a quarter each (16-byte pieces; a slot holds
+            // kHufCells entries, so a tiny table copies one whole piece)
+            const uint32_t pieces = max(1u, (2u << tlog) / 16u), per = (pieces + 3u) / 4u;
+            const u32x4 *gt = (const u32x4 *)(E.hufs + toff);
+            for (uint32_t k = s * per; k < min(pieces, (s + 1u) * per); k++) ((u32x4 *)tab)[k] = gt[k];
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (has && ok) {
+            int32_t sstart = 0, slen = 0;
+            uint32_t o0 = 0, cnt = 0;
+            bool good = true;
+            if (single) {
+                sstart = (int32_t)cs;
+                slen = (int32_t)n;
+                cnt = s == 0 ? lsize : 0u;
+            } else {
+                good = n >= 10u;
+                if (good) {
+                    const int32_t l1 = (int32_t)(src[cs] | (src[cs + 1] << 8)), l2 = (int32_t)(src[cs + 2] | (src[cs + 3] << 8)),
+                                  l3 = (int32_t)(src[cs + 4] | (src[cs + 5] << 8));
+                    const int32_t l4 = (int32_t)n - (l1 + l2 + l3 + 6);
+                    good = l4 >= 0 && l4 <= (int32_t)n;
+                    const uint32_t seg = (lsize + 3u) / 4u;
+                    const uint32_t n4 = lsize > 3u * seg ? lsize - 3u * seg : 0u;
+                    sstart = (int32_t)cs + 6 + (s > 0 ? l1 : 0) + (s > 1 ? l2 : 0) + (s > 2 ? l3 : 0);
+                    slen = s == 0 ? l1 : s == 1 ? l2 : s == 2 ? l3 : l4;
+                    o0 = seg * s;
+                    cnt = s < 3u ? seg : n4;
+                }
+            }
+            if (good && (!single || s == 0u)) {
+                BitD bd;
+                good = gbitd_init(bd, src, sstart, slen);
+                uint8_t *out = E.lit + lat;
+                uint64_t acc = 0;
+                uint32_t lo = (uint32_t)((uintptr_t)(out + o0) & 7u);   // first valid byte of the current word
+                for (uint32_t i = 0; good && i < cnt; i++) {
+                    if (bd.used > 52u) gbitd_reload(bd, src);
+                    const uint32_t e = tab[(uint32_t)bitd_look_fast(bd, tlog)];
+                    bd.used += e >> 8;
+                    uint8_t *at = out + o0 + i;
+                    const uint32_t k = (uint32_t)((uintptr_t)at & 7u);
+                    acc |= (uint64_t)(e & 255u) << (8u * k);
+                    if (k == 7u || i + 1u == cnt) {
+                        uint8_t *word = at - k;
+                        if (lo == 0u && k == 7u) {
+                            *(uint64_t *)word = acc;
+                        } else {
+                            for (uint32_t t = lo; t <= k; t++) word[t] = (uint8_t)(acc >> (8u * t));
+                        }
+                        acc = 0;
+                        lo = 0;
+                    }
+                }
+                if (good) {   // BIT_endOfDStream
+                    if (bd.used <= 64u) gbitd_reload(bd, src);
+                    good = bd.ptr == bd.start && bd.used == 64u;
+                }
+            }
+            ok = good;
+        }
+        __builtin_amdgcn_wave_barrier();   // the slot is reused by the next job's table
+    }
+    // a stream that failed fails its page (all four lanes of the group agree on the verdict)
+    const uint32_t grp_bad = (uint32_t)(__ballot(act && !ok) >> (4u * min(g, 15u))) & 15u;
+    if (act && s == 0u && grp_bad) st[j] = kErr;
+}
+
 // Pass 1 over pages [first, first + count) of b; page j's entries at ws + j * ws_page.
 __global__ __launch_bounds__(64) void zstd_entropy_kernel(tyche_batch_t b, size_t first, size_t count, uint32_t in_cap,
                                                           uint32_t out_cap, Layout lay, uint8_t *ws, size_t ws_page,
-                                                          int32_t *st, unsigned *ctr, bool use_jobs, bool fused) {
+                                                          int32_t *st, unsigned *ctr, bool use_jobs, bool fused,
+                                                          bool defer_lit) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t lane = threadIdx.x;
     Work W;
@@ -2201,7 +2366,8 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(tyche_batch_t b, size_
             if (lane < kStreamPad / 4) lds_st32(in + p.src_len + lane * 4, 0u);
             WAVE_SYNC();
             W.in = in;
-            const Ent E = ent_of(ws + j * ws_page, in_cap, out_cap, fused);
+            Ent E = ent_of(ws + j * ws_page, in_cap, out_cap, fused);
+            E.defer_lit = fused && defer_lit;
             SPROF_DECL
             // jobs first; a page whose jobs do not fit is redone with the chains inline (fused
             // layout: by the one-wave kernel after pass 2)
@@ -2299,6 +2465,11 @@ hipError_t launch_zstd_decode(const tyche_batch_t &b, uint32_t in_cap, uint32_t 
     const bool seqexec = lane_exec && use_jobs && knob("ZSTD_SEQEXEC", 1) != 0 && lf.total <= 160u * 1024u;
     const long ring = knob("ZSTD_EXEC_RING", 128);
     const bool slots6 = knob("ZSTD_SEQ_SLOTS", 7) == 6;
+    // literal streams lane-per-stream (zstd_lit_kernel) between pass 1 and zstd_seqexec_kernel
+    const long lit_groups = knob("ZSTD_LIT_LANES", 8);   // pages per wave: 8 / 16; 0 = streams in pass 1
+    const bool lit_lanes = seqexec && lit_groups > 0;
+    const void *kl = lit_groups == 16 ? (const void *)zstd_lit_kernel<16> : (const void *)zstd_lit_kernel<8>;
+    const uint32_t kgroups = lit_groups == 16 ? 16u : 8u;
     const void *kx = seqexec ? (slots6 ? (const void *)zstd_seqexec_kernel<128, 6> : (const void *)zstd_seqexec_kernel<128, 7>)
                      : ring == 256 ? (const void *)zstd_exec_lane_kernel<256>
                                    : (const void *)zstd_exec_lane_kernel<128>;
@@ -2335,7 +2506,16 @@ hipError_t launch_zstd_decode(const tyche_batch_t &b, uint32_t in_cap, uint32_t 
             WorkCounter ctr(s, g1 < n);
             if (!ctr.get()) return hipErrorOutOfMemory;
             hipLaunchKernelGGL(zstd_entropy_kernel, dim3((unsigned)g1), dim3(kWave), l1.total, s, b, first, n, in_cap,
-                               out_cap, l1, ent, page_bytes, st, ctr.get(), use_jobs, seqexec);
+                               out_cap, l1, ent, page_bytes, st, ctr.get(), use_jobs, seqexec, lit_lanes);
+        }
+        if (lit_lanes) {
+            (void)prepare_launch(kl);
+            size_t f = first, nn = n, pb = page_bytes;
+            uint8_t *wsp = ent;
+            int32_t *stp = st;
+            void *args[] = {(void *)&b, &f, &nn, &in_cap, &out_cap, &wsp, &pb, &stp};
+            (void)hipLaunchKernel(kl, dim3((unsigned)((n + kgroups - 1) / kgroups)), dim3(64), args,
+                                  (size_t)kgroups * kHufCells * 2u, s);
         }
         if (!seqexec)
             hipLaunchKernelGGL(zstd_seq_kernel, dim3((unsigned)((n + kWave - 1) / kWave)), dim3(kWave), kSeqLds, s, b,
