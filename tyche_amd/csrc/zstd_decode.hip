@@ -446,13 +446,49 @@ __device__ __forceinline__ uint32_t cell_sym(uint32_t c) { return (c >> 16) & 0x
 __device__ __forceinline__ uint32_t cell_nb(uint32_t c) { return c >> 24; }
 
 // FSE_buildDTable (fse_decompress.c:113-168) from norm[0..max_sv]; cells[] gets
-// 1 << table_log entries.  The symbol spread is a serial walk (wave-uniform);
+// 1 << table_log entries.  The symbol spread is lane-parallel (a serial,
+// wave-uniform walk for alphabets over 64 symbols or tables over 512 cells);
 // lanes then finish the cells of each 64-entry chunk with per-symbol ranks.
 // Returns false on the reference's GENERIC error (spread did not close).
+__device__ bool dtable_states(uint32_t *cells, uint16_t *next, uint32_t table_log, uint32_t lane);
 __device__ bool build_dtable(uint32_t *cells, const int16_t *norm, uint32_t max_sv, uint32_t table_log,
                              uint16_t *next, uint32_t lane) {
     const uint32_t size = 1u << table_log, mask = size - 1u;
     const uint32_t step = (size >> 1) + (size >> 3) + 3u;
+    if (max_sv < kWave && size <= 512u) {
+        // Round 3: the spread lane-parallel.  The serial walk visits positions (k * step) & mask
+        // (k = 0, 1, ...) skipping those above `high`, and the i-th valid position takes the i-th
+        // occurrence in symbol order -- so each lane takes a k, ranks the valid ones with a ballot,
+        // and looks its occurrence's symbol up in an occurrence -> symbol map (in next's bytes
+        // until next is filled).  read_ncount guarantees the counts fill the table; a table that
+        // does not is rejected as the serial walk's `position != 0` rejects it.
+        const uint64_t below = lane ? (~0ull >> (64u - lane)) : 0ull;
+        const bool sym = lane <= max_sv;
+        const int32_t c = sym ? (int32_t)norm[lane] : 0;
+        const bool low = sym && c == -1;
+        const uint64_t mlow = __ballot(low);
+        if (low) cells[size - 1u - (uint32_t)__popcll(mlow & below)] = lane << 16;
+        const uint32_t high = size - 1u - (uint32_t)__popcll(mlow);
+        const int32_t cnt = low || c < 0 ? 0 : c;
+        const int32_t incl = wave_incl_sum(cnt), excl = incl - cnt;
+        if ((uint32_t)rdlane((uint32_t)incl, kWave - 1) != high + 1u) return false;
+        uint8_t *occ = (uint8_t *)next;   // <= 512 entries: next's 256 x 16 bit
+        __builtin_amdgcn_wave_barrier();
+        for (int32_t i = 0; i < cnt; i++) occ[excl + i] = (uint8_t)lane;
+        __builtin_amdgcn_wave_barrier();
+        uint32_t taken = 0;
+        for (uint32_t k0 = 0; k0 < size; k0 += kWave) {
+            const uint32_t k = k0 + lane, p = (k * step) & mask;
+            const bool v = k < size && p <= high;
+            const uint64_t mv = __ballot(v);
+            if (v) cells[p] = (uint32_t)occ[taken + (uint32_t)__popcll(mv & below)] << 16;
+            taken += (uint32_t)__popcll(mv);
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (sym) next[lane] = (uint16_t)(low ? 1 : c);
+        __builtin_amdgcn_wave_barrier();
+        return dtable_states(cells, next, table_log, lane);
+    }
     uint32_t high = size - 1u;
     // symbols are written into bits 16..23 first (cell = sym << 16)
     for (uint32_t s = 0; s <= max_sv; s++) {
@@ -481,7 +517,13 @@ __device__ bool build_dtable(uint32_t *cells, const int16_t *norm, uint32_t max_
     }
     __builtin_amdgcn_wave_barrier();
     if (pos != 0) return false;
-    // nextState = symbolNext[s]++ in cell order: per 64-cell chunk, rank lanes by symbol
+    return dtable_states(cells, next, table_log, lane);
+}
+
+// nextState = symbolNext[s]++ in cell order (FSE_buildDTable): per 64-cell chunk, rank lanes by
+// symbol; cells hold their symbol in bits 16..23, next[s] the symbol's count (-1 as 1).
+__device__ bool dtable_states(uint32_t *cells, uint16_t *next, uint32_t table_log, uint32_t lane) {
+    const uint32_t size = 1u << table_log;
     for (uint32_t u0 = 0; u0 < size; u0 += kWave) {
         const uint32_t u = u0 + lane;
         const bool act = u < size;
