@@ -127,6 +127,58 @@ def test_encode_roundtrip_oracle(tc, oracle_mod, dist, plen):
     assert sum(lh) <= 1.10 * sum(ref_sizes) + 64 * n
 
 
+def _literal_run_pages(n, plen, seed):
+    """Pages mixing random stretches (long literal runs: batches of sequences whose encoding
+    exceeds the encoder's 1 KiB output ring go straight to HBM, lz4_encode.hip emit_direct)
+    with repeated records (matches), in several proportions."""
+    rng = np.random.default_rng(seed)
+    pages = np.zeros((n, plen), np.uint8)
+    for i in range(n):
+        pos = 0
+        rec = rng.integers(0, 256, 24, dtype=np.uint8)
+        while pos < plen:
+            kind = rng.integers(0, 4)
+            m = int(rng.integers(1, [3000, 400, 60, 900][kind]))
+            m = min(m, plen - pos)
+            if kind in (0, 1):
+                pages[i, pos:pos + m] = rng.integers(0, 256, m, dtype=np.uint8)
+            else:
+                pages[i, pos:pos + m] = np.resize(rec, m)
+            pos += m
+    return pages
+
+
+@pytest.mark.parametrize("variant", ["one_wave", "split2", "split3", "split4", "split8"])
+@pytest.mark.parametrize("plen", [8192, 16384, 32768])
+def test_encode_kernels_long_literal_runs(tc, oracle_mod, knobs, variant, plen):
+    """Every LZ4 encoder kernel (TYCHE_LZ4_ENC=1 one wave per page; the two-wave split; the
+    N-wave splits, TYCHE_LZ4_ENC_WAVES) on bench pages and on pages with long literal runs:
+    every stream restores through the reference decoder (oracle/_ref) and the oracle's."""
+    O = oracle_mod
+    if variant == "one_wave":
+        knobs(LZ4_ENC=1)
+    elif variant != "split2":
+        knobs(LZ4_ENC_WAVES=int(variant[-1]))
+    n = 24
+    host = np.concatenate([_literal_run_pages(n, plen, plen + 7),
+                           tc.pagegen(n, plen, seed=77, first=plen, dist=0, device=DEV).cpu().numpy()])
+    pages = torch.from_numpy(host).to(DEV)
+    comp, clen = tc.compress_pages(pages)
+    torch.cuda.synchronize()
+    ch, lh = comp.cpu().numpy(), clen.cpu().numpy()
+    for i in range(2 * n):
+        assert 0 < lh[i] <= O.lz4_bound(plen), (i, lh[i])
+        stream = ch[i, :lh[i]].tobytes()
+        r, dec = O.lz4_decompress(stream, plen)
+        assert r == plen and dec == host[i].tobytes(), i
+        if O.have_ref():
+            r2, dec2 = O.ref_lz4_decompress(stream, plen)
+            assert r2 == plen and dec2 == host[i].tobytes(), i
+    out, rv = tc.decompress_pages(comp, clen, plen)
+    torch.cuda.synchronize()
+    assert bool((rv == plen).all()) and torch.equal(out, pages)
+
+
 def test_pagegen_matches_host(tc, oracle_mod):
     for dist in range(6):
         d = tc.pagegen(8, 16384, seed=11, first=123, dist=dist, device=DEV).cpu().numpy()

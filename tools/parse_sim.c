@@ -285,11 +285,23 @@ static double fse_bits(const uint32_t *h, int n, int maxlog) {
     }
     return bits + hdr;
 }
+static uint32_t opt_blk_seq = 0;   /* > 0: zstd_cost cuts the sequences into blocks of at most this many */
 static void zlit_add(uint32_t a, uint32_t b) {
     for (uint32_t i = a; i < b; i++) zlit[pg[i]]++;
     zlits += b - a;
 }
+static double zstd_cost_range(uint32_t i0, uint32_t i1, uint32_t *rep, uint32_t *lp, int last);
 static double zstd_cost(void) {
+    if (opt_blk_seq) {   /* blocks of <= opt_blk_seq sequences, each with its own literal and sequence tables */
+        uint32_t rep[3] = {1, 4, 8}, lp = 0;
+        double tot = 6;
+        for (uint32_t i = 0; i < nzs || i == 0; i += opt_blk_seq) {
+            const uint32_t i1 = i + opt_blk_seq < nzs ? i + opt_blk_seq : nzs;
+            tot += zstd_cost_range(i, i1, rep, &lp, i1 == nzs);
+            if (i1 == nzs) break;
+        }
+        return tot;
+    }
     uint32_t hl[36] = {0}, hm[53] = {0}, ho[32] = {0};
     double extra = 0;
     uint32_t rep[3] = {1, 4, 8};
@@ -327,6 +339,47 @@ static double zstd_cost(void) {
     const double bits = lit_bits + fse_bits(hl, 36, opt_fse == 1 ? 6 : 9) + fse_bits(hm, 53, opt_fse == 1 ? 6 : 9) +
                         fse_bits(ho, 32, opt_fse == 1 ? 5 : 8) + extra;
     return bits / 8 + 6 + 3 + 5 + 6 + 45;   /* frame + block + literal headers, jump table, HUF table */
+}
+/* one block: sequences [i0, i1), literals from *lp (the last block also takes the page's tail) */
+static double zstd_cost_range(uint32_t i0, uint32_t i1, uint32_t *rep, uint32_t *lp, int last) {
+    uint32_t hl[36] = {0}, hm[53] = {0}, ho[32] = {0}, hlit[256] = {0};
+    double extra = 0;
+    for (uint32_t i = i0; i < i1; i++) {
+        const zseq q = zs[i];
+        for (uint32_t b = 0; b < q.ll; b++) hlit[pg[*lp + b]]++;
+        *lp += q.ll + q.ml;
+        uint32_t ov;
+        if (q.ll) {
+            if (q.off == rep[0]) ov = 1;
+            else if (q.off == rep[1]) ov = 2;
+            else if (q.off == rep[2]) ov = 3;
+            else ov = q.off + 3;
+        } else {
+            if (q.off == rep[1]) ov = 1;
+            else if (q.off == rep[2]) ov = 2;
+            else if (q.off == rep[0] - 1) ov = 3;
+            else ov = q.off + 3;
+        }
+        if (ov > 3) { rep[2] = rep[1]; rep[1] = rep[0]; rep[0] = q.off; }
+        else {
+            const uint32_t idx = ov - 1 + (q.ll == 0);
+            if (idx) {
+                const uint32_t t = idx == 3 ? rep[0] - 1 : rep[idx];
+                if (idx != 1) rep[2] = rep[1];
+                rep[1] = rep[0];
+                rep[0] = t;
+            }
+        }
+        const uint32_t lc = zcode_ll(q.ll), mc = zcode_ml(q.ml - 3);
+        uint32_t oc = 31 - (uint32_t)__builtin_clz(ov);
+        hl[lc]++; hm[mc]++; ho[oc]++;
+        extra += zll_bits[lc] + zml_bits[mc] + oc;
+    }
+    if (last) { for (uint32_t b = *lp; b < L; b++) hlit[pg[b]]++; *lp = L; }
+    const double lit_bits = huff_bits(hlit, 256);
+    const double bits = lit_bits + fse_bits(hl, 36, opt_fse == 1 ? 6 : 9) + fse_bits(hm, 53, opt_fse == 1 ? 6 : 9) +
+                        fse_bits(ho, 32, opt_fse == 1 ? 5 : 8) + extra;
+    return bits / 8 + 3 + 5 + 6 + 45;
 }
 static void zreset(void) { nzs = 0; zlits = 0; memset(zlit, 0, sizeof zlit); }
 
@@ -597,6 +650,32 @@ static int main_zstd_fse(int n) {
     return 0;
 }
 
+/* block cuts: the device encoder starts a new block every 960 sequences (zstd_encode.hip kZBlk);
+ * level 1 puts a whole page (<= 128 KiB) in one block */
+static int main_zstd_blk(int n) {
+    static const uint32_t cuts[5] = {0, 960, 1500, 2000, 4000};
+    double raw = 0, d[5] = {0}, r[5] = {0}, ns = 0;
+    const uint32_t hbits = L <= 16384 ? 14 : 13;
+    opt_fse = 3;
+    for (int i = 0; i < n; i++) {
+        pg_page_t p;
+        pg_page_init(&p, 20170303ull, (uint64_t)i, L, 0);
+        for (uint32_t b = 0; b < L; b++) pg[b] = (uint8_t)pg_page_byte(&p, b);
+        memset(pg + L, 0, 64);
+        raw += L;
+        for (int m = 0; m < 5; m++) {
+            opt_blk_seq = cuts[m];
+            d[m] += parse_zstd_device(1856, 2, 5);
+            if (m == 0) ns += nzs;
+            r[m] += parse_zstd_fast(hbits, 6);
+        }
+    }
+    opt_blk_seq = 0;
+    printf("pages %d x %u B (zstd block cuts, FSE logs <= 7/6/7), %.0f device sequences per page\n", n, L, ns / n);
+    for (int m = 0; m < 5; m++) printf("model: blocks of <= %4u sequences  device parse %.3f   level-1 parse %.3f\n", cuts[m], raw / d[m], raw / r[m]);
+    return 0;
+}
+
 int main(int argc, char **argv) {
     const int n = argc > 1 ? atoi(argv[1]) : 200;
     L = argc > 2 ? (uint32_t)atoi(argv[2]) : 16384;
@@ -604,6 +683,7 @@ int main(int argc, char **argv) {
     if (argc > 3 && !strcmp(argv[3], "zsplit")) return main_zstd_split(n);
     if (argc > 3 && !strcmp(argv[3], "zfse")) return main_zstd_fse(n);
     if (argc > 3 && !strcmp(argv[3], "zallblk")) return main_zstd_allblk(n);
+    if (argc > 3 && !strcmp(argv[3], "zblk")) return main_zstd_blk(n);
     static const uint32_t grid[][2] = {{1024, 4}, {2048, 4}, {512, 8}, {1024, 8}, {2048, 8}, {1024, 6}, {4096, 8}};
     const int ng = (int)(sizeof grid / sizeof grid[0]);
     double raw = 0, zl = 0, zf = 0, var[16] = {0}, var_r[16] = {0};

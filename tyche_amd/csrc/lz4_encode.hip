@@ -599,7 +599,8 @@ constexpr uint32_t split_prefetch() { return (16384u / 16u + kNW * kWave - 1u) /
 
 template <uint32_t kNW>
 __global__ __launch_bounds__(kNW * 64) void lz4_encode_splitn_kernel(tyche_batch_t b, uint32_t in_cap, unsigned *ctr,
-                                                                     uint8_t *ws, uint32_t ws_stride, uint32_t seed) {
+                                                                     uint8_t *ws, uint32_t ws_stride, uint32_t seed,
+                                                                     uint32_t p0) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr uint32_t kT = kNW * kWave;                 // threads per page
     constexpr uint32_t kPf = split_prefetch<kNW>();       // 16-byte vectors per thread prefetched
@@ -647,8 +648,17 @@ __global__ __launch_bounds__(kNW * 64) void lz4_encode_splitn_kernel(tyche_batch
         const uint8_t *in = stage + head;
         const uint32_t L = p.src_len;
         const bool fits = L <= in_cap;
-        const uint32_t b0 = wave == 0 ? 0u : ((L * wave) / kNW) & ~(kWave - 1u);
-        const uint32_t b1 = wave + 1 == kNW ? L : ((L * (wave + 1)) / kNW) & ~(kWave - 1u);
+        // part w starts at bnd(w): equal parts, or (p0 > 0) p0/64 of the page for part 0 -- the one
+        // part that seeds nothing -- and equal shares of the rest for the others
+        auto bnd = [&](uint32_t w) -> uint32_t {
+            if (w == 0) return 0u;
+            if (w == kNW) return L;
+            if (!p0) return ((L * w) / kNW) & ~(kWave - 1u);
+            const uint32_t h = (L * p0 / 64u) & ~(kWave - 1u);
+            return (h + ((L - h) * (w - 1u)) / (kNW - 1u)) & ~(kWave - 1u);
+        };
+        const uint32_t b0 = bnd(wave);
+        const uint32_t b1 = bnd(wave + 1);
         const uint32_t Lp = wave + 1 == kNW ? L : b1 + kLastLiterals;   // part w's matches end by b1
         if (fits) {
             if (wave == 0) {
@@ -853,6 +863,10 @@ hipError_t launch_lz4_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream_
         const size_t grid = std::min<size_t>(b.count, ncu * (size_t)per_cu);
         const uint32_t pws = nw == 8 ? part_scratch<8>(in_cap) : nw == 4 ? part_scratch<4>(in_cap) : part_scratch<3>(in_cap);
         uint32_t seed = (uint32_t)std::max(0L, knob("LZ4_ENC_SEED", kSeed)) & ~(kWave - 1u);   // positions seeded before a part
+        // part 0's share of the page in 64ths (0: equal parts); at least 1/kNW, so the later parts fit
+        // their scratch (part_scratch: a 1/kNW part)
+        uint32_t p0 = (uint32_t)std::max(0L, knob("LZ4_ENC_P0", 0));
+        if (p0) p0 = std::min<uint32_t>(std::max<uint32_t>(p0, (64u + (uint32_t)nw - 1u) / (uint32_t)nw), 48u);
         const uint32_t ws_stride = (uint32_t)(nw - 1) * pws;
         ScratchLease ws(s, grid * (size_t)ws_stride);
         if (ws.get()) {
@@ -860,7 +874,7 @@ hipError_t launch_lz4_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream_
             if (!ctr.get()) return hipErrorOutOfMemory;
             unsigned *cp = ctr.get();
             uint8_t *wp = (uint8_t *)ws.get();
-            void *args[] = {(void *)&b, &in_cap, &cp, &wp, (void *)&ws_stride, &seed};
+            void *args[] = {(void *)&b, &in_cap, &cp, &wp, (void *)&ws_stride, &seed, &p0};
             (void)hipLaunchKernel(k, dim3((unsigned)grid), dim3(T), args, lds, s);
             return hipGetLastError();
         }
