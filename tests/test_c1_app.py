@@ -205,14 +205,22 @@ def test_reference_app_device_failure(sample_dir):
         env = dict(os.environ, TYCHE_APP_WATCHDOG="15", TYCHE_LOG_ERRORS="1", TYCHE_FAIL_COMPRESS_EVERY="1")
         p = subprocess.run([APP_Q] + args, stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=90, env=env)
         err = p.stderr.decode(errors="replace")
-        assert "tyche-engine:" in err                 # the injected failures happened and were reported
         runs.append(p.returncode)
         if p.returncode == -11:
+            assert "tyche-engine:" in err             # the injected failures happened and were reported
             bt = err[err.find("fatal signal"):]
             assert "manager__spawn_worker" in bt, bt[-3000:]   # the rewrite's memcpy of the NULL page (manager.c:358)
             crashes.append(p.returncode)
             break
         assert p.returncode == 3, (p.returncode, err[-3000:])   # otherwise only the watchdog may end it
+        # a watchdog exit: one of the reference's own wedges (copy-on-write or sweep scan), never a thread
+        # inside the engine; it may come before the first sweep, so before any injected failure
+        dump = err[err.find("--- thread"):]
+        assert "--- thread" in dump, ("watchdog without a dump", err[-3000:])
+        stuck = [t for t in dump.split("--- thread")[1:] if any(c in t for c in ENGINE_CALLS)]
+        assert not stuck, ("a thread is inside an engine call", stuck[0][-2000:])
+        assert any(f in dump for f in ("list__add_cow", "list__slaughter_house", "list__sweep", "list__search")), \
+            ("unclassified hang", dump[-3000:])
     print(f"unchanged caller: runs {runs}, {len(crashes)} crash(es) in the rewrite of a lost page")
     assert crashes, f"the unchanged caller never reached a lost page: runs {runs}"
 

@@ -129,7 +129,7 @@ def test_encode_roundtrip_oracle(tc, oracle_mod, dist, plen):
 
 def _literal_run_pages(n, plen, seed):
     """Pages mixing random stretches (long literal runs: batches of sequences whose encoding
-    exceeds the encoder's 1 KiB output ring go straight to HBM, lz4_encode.hip emit_direct)
+    exceeds the encoder's 1 KiB output ring go straight to HBM, lz4_encode.hip emit_records)
     with repeated records (matches), in several proportions."""
     rng = np.random.default_rng(seed)
     pages = np.zeros((n, plen), np.uint8)
@@ -151,13 +151,14 @@ def _literal_run_pages(n, plen, seed):
 @pytest.mark.parametrize("variant", ["one_wave", "split2", "split3", "split4", "split8"])
 @pytest.mark.parametrize("plen", [8192, 16384, 32768])
 def test_encode_kernels_long_literal_runs(tc, oracle_mod, knobs, variant, plen):
-    """Every LZ4 encoder kernel (TYCHE_LZ4_ENC=1 one wave per page; the two-wave split; the
-    N-wave splits, TYCHE_LZ4_ENC_WAVES) on bench pages and on pages with long literal runs:
-    every stream restores through the reference decoder (oracle/_ref) and the oracle's."""
+    """Every LZ4 encoder kernel (TYCHE_LZ4_ENC=1 one wave per page; the two-wave split and the
+    N-wave splits, TYCHE_LZ4_ENC_WAVES, 3 being the default) on bench pages and on pages with
+    long literal runs: every stream restores through the reference decoder (oracle/_ref) and
+    the oracle's."""
     O = oracle_mod
     if variant == "one_wave":
         knobs(LZ4_ENC=1)
-    elif variant != "split2":
+    else:
         knobs(LZ4_ENC_WAVES=int(variant[-1]))
     n = 24
     host = np.concatenate([_literal_run_pages(n, plen, plen + 7),

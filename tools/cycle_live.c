@@ -197,10 +197,14 @@ static void *sweeper(void *arg) {
     return NULL;
 }
 
+#define MIN_LZ4_RESTORES 16
 static void *restorer(void *arg) {
     uint64_t rng = SEED + (uint64_t)(uintptr_t)arg * 1000003u;
     const size_t hot = g_n / 5 ? g_n / 5 : 1;
-    for (long k = 0; k < g_restores; k++) {
+    /* each restorer makes g_restores searches, and more (up to 8x) until the run has restored
+     * MIN_LZ4_RESTORES pages that the sweeper compressed during it: a short run's searches can
+     * otherwise all end before the cold pages the sweeps hit come back */
+    for (long k = 0; k < g_restores || (g_restored_lz4 < MIN_LZ4_RESTORES && k < 8 * g_restores); k++) {
         const uint64_t r = splitmix(&rng);
         const size_t id = (r % 100u) < 80u ? (size_t)((r >> 8) % hot) : hot + (size_t)((r >> 8) % (g_n - hot ? g_n - hot : 1));
         if (id >= g_n) continue;

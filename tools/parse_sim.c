@@ -439,7 +439,9 @@ static double parse_zstd_fast(uint32_t hbits, uint32_t mls) {
     return zstd_cost();
 }
 
-/* the device parse with repeat candidates (lz_parse.h kRepCand): nb buckets x ways, hash of hb bytes */
+/* the device parse with repeat candidates (lz_parse.h kRepCand): nb buckets x ways, hash of hb bytes;
+ * a repeat candidate wins when at most opt_rep_slack bytes shorter than the hash candidate (TYCHE_REP_SLACK) */
+static uint32_t opt_rep_slack = 3;
 static uint32_t opt_parts = 1, opt_seed = 1u << 20, opt_carry_rep = 0, gR = 1, gR2 = 4, opt_warm = 0, opt_all_blocks = 0;
 static double parse_zstd_device(uint32_t nb, uint32_t ways, uint32_t hb) {
     static uint32_t T[1 << 16][8];
@@ -495,8 +497,8 @@ static double parse_zstd_device(uint32_t nb, uint32_t ways, uint32_t hb) {
             uint32_t rn = 0, rn2 = 0;
             if (pos >= R && read32(pos - R) == read32(pos)) rn = mlen(pos, pos - R, matchlimit);
             if (R2 != R && pos >= R2 && read32(pos - R2) == read32(pos)) rn2 = mlen(pos, pos - R2, matchlimit);
-            if (rn >= 4 && rn >= best) { best = rn; bc = pos - R; }
-            if (rn2 >= 4 && rn2 >= best && !(rn >= 4 && rn >= rn2)) { best = rn2; bc = pos - R2; }
+            if (rn >= 4 && rn + opt_rep_slack >= best) { best = rn; bc = pos - R; }
+            if (rn2 >= 4 && rn2 + opt_rep_slack >= best && !(rn >= 4 && rn >= rn2)) { best = rn2; bc = pos - R2; }
             rok[l] = rn >= 4 || rn2 >= 4;
             if (best >= 4) {
                 ok[l] = 1; cand[l] = bc; len[l] = best;
@@ -589,8 +591,9 @@ static int main_zstd_split(int n) {
 
 static int main_zstd(int n) {
     double raw = 0, ref = 0, d[8] = {0};
-    static const uint32_t cfg[][3] = {{1856, 2, 5}, {4096, 2, 5}, {8192, 2, 5}, {16384, 1, 6}, {4096, 2, 6}, {2048, 4, 5}, {4096, 4, 5}};
-    const int nc = 7;
+    static const uint32_t cfg[][3] = {{1856, 2, 5}, {4096, 2, 5}, {8192, 2, 5}, {16384, 1, 6}, {4096, 2, 6}, {2048, 4, 5}, {4096, 4, 5}, {928, 4, 5}};
+    const int nc = 8;
+    opt_fse = 3;   /* sequence tables as the device encodes them (FSE_optimalTableLog capped at 7/6/7) */
     const uint32_t hbits = L <= 16384 ? 14 : 13;
     for (int i = 0; i < n; i++) {
         pg_page_t p;
@@ -601,7 +604,8 @@ static int main_zstd(int n) {
         ref += parse_zstd_fast(hbits, 6);
         for (int c = 0; c < nc; c++) d[c] += parse_zstd_device(cfg[c][0], cfg[c][1], cfg[c][2]);
     }
-    printf("pages %d x %u B (zstd)\n", n, L);
+    opt_fse = 0;
+    printf("pages %d x %u B (zstd, repeat slack %u)\n", n, L, opt_rep_slack);
     printf("model: level-1 fast parse (hashLog %u, mls 6)   ratio %.3f\n", hbits, raw / ref);
     for (int c = 0; c < nc; c++)
         printf("model: device %5u buckets x %u ways, %u-byte hash  ratio %.3f\n", cfg[c][0], cfg[c][1], cfg[c][2], raw / d[c]);

@@ -1045,10 +1045,12 @@ int run_host_batch(int dev, size_t n, const void *const *src, const uint32_t *sr
         // (kDirectAlways): only the compressed bytes cross the link -- a D2H of the arena would move
         // every page's full capacity (16 KiB+ per 16 KiB page at ratio 2.6).  LZ4 decompress
         // (kDirectLz4Decode): the jump and wave decoders write each page once, whole, from LDS; the
-        // lane decoder (chunks of >= kLaneMin pages) reads its own output back, so it keeps the D2H.
+        // lane decoder (chunks of >= kLaneMin pages) reads its own output back, so it keeps the D2H;
+        // TYCHE_HOST_DIRECT_DECODE_MAX: chunks of more pages than this stage through HBM too.
         const bool direct = S.h_out.dp != nullptr &&
                             (direct_out == kDirectAlways ||
-                             (direct_out == kDirectLz4Decode && !lz4_lane_decode_wanted(k, max_in, max_out)));
+                             (direct_out == kDirectLz4Decode && !lz4_lane_decode_wanted(k, max_in, max_out) &&
+                              (long)k <= knob("HOST_DIRECT_DECODE_MAX", 1L << 30)));
         b.dst = direct ? S.h_out.dp : S.d_out.p;
         b.dst_offsets = (const uint64_t *)(dmeta + ((uint8_t *)m_doff - (uint8_t *)m_soff));
         b.dst_capacities = (const uint32_t *)(dmeta + ((uint8_t *)m_dcap - (uint8_t *)m_soff));
@@ -1589,13 +1591,19 @@ struct RestoreQueue {
         std::vector<Buffer *> bufs;
         std::vector<int> st;
         std::vector<RestoreReq *> &cq = q[codec];
+        // TYCHE_RESTORE_WAIT_IDLE (default 1): the wait for company applies only when this
+        // dispatcher found its queue empty -- requests that queued up while its last batch ran
+        // have waited a whole batch already and go out at once (0: every batch waits)
+        const bool wait_idle_only = knob("RESTORE_WAIT_IDLE", 1) != 0;
+        bool idle = true;
         for (;;) {
             {
                 std::unique_lock<std::mutex> g(mu);
+                if (cq.empty()) idle = true;
                 cv.wait(g, [&] { return (stop && cq.empty()) || (!cq.empty() && !collecting[codec]); });
                 if (cq.empty()) return;   // stopping
                 collecting[codec] = true;
-                if ((int)cq.size() < max_batch && max_wait_us > 0)
+                if ((idle || !wait_idle_only) && (int)cq.size() < max_batch && max_wait_us > 0)
                     cv.wait_for(g, std::chrono::microseconds(max_wait_us),
                                 [&] { return stop || (int)cq.size() >= max_batch; });
                 const size_t k = std::min(cq.size(), (size_t)max_batch);
@@ -1616,6 +1624,7 @@ struct RestoreQueue {
                     take[i]->status = st[i];
                     take[i]->done = true;
                 }
+                idle = cq.empty();
             }
             done_cv.notify_all();
         }

@@ -330,7 +330,7 @@ __device__ int32_t encode_page(const uint8_t *in, uint32_t L, uint16_t *table, u
     return (int32_t)(op + total);
 }
 
-// ---- split encoder (the default when the batch's pages may reach kSplitMin bytes).
+// ---- two-wave split encoder (round 2's default for pages >= kSplitMin; TYCHE_LZ4_ENC_WAVES=2).
 //
 // The one-wave encoder is latency-bound: its page, hash table and sequence
 // buffers take 20 KiB of LDS, so a CU holds 8 of them (2 waves per SIMD), and
@@ -553,7 +553,7 @@ __global__ __launch_bounds__(128, 3) void lz4_encode_split_kernel(tyche_batch_t 
     }
 }
 
-// ---- N-wave split encoder (round 3, the default for pages >= kSplitMin).
+// ---- N-wave split encoder (round 3; 3 waves are the default for pages >= kSplitMin).
 //
 // The two-wave kernel above runs 12 waves per CU; its counters (r03 PMC) show
 // the waves waiting ~42 % of their cycles with no unit saturated (VALU ~35 %,
@@ -849,7 +849,11 @@ hipError_t launch_lz4_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream_
     if (in_cap > 65535u) return hipErrorInvalidValue;    // 16-bit positions (byU16 regime)
     // TYCHE_LZ4_ENC=1: the one-wave kernel for every batch (A/B timing)
     const bool one_wave = knob("LZ4_ENC", 0) == 1;
-    const long nw = knob("LZ4_ENC_WAVES", 2);   // waves per page of the split encoders (2: the two-wave kernel)
+    // waves per page of the split encoders (2: the two-wave kernel; default 3 since round 3: 79.4 vs
+    // 85.0 ms per 1M x 16 KiB pages at ratio 2.6193 vs 2.6204, with part 0 taking 27/64 of the page
+    // and the later parts seeded with the 10,240 positions before them -- A/B of seeds 4,096-16,384
+    // and part-0 shares 21-29/64 in DESIGN.md §3.2)
+    const long nw = knob("LZ4_ENC_WAVES", 3);
     if (!one_wave && in_cap >= kSplitMin && (nw == 3 || nw == 4 || nw == 8)) {
         const void *k = nw == 8   ? (const void *)lz4_encode_splitn_kernel<8>
                         : nw == 4 ? (const void *)lz4_encode_splitn_kernel<4>
@@ -862,10 +866,10 @@ hipError_t launch_lz4_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream_
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, (int)T, lds) != hipSuccess || per_cu < 1) per_cu = 1;
         const size_t grid = std::min<size_t>(b.count, ncu * (size_t)per_cu);
         const uint32_t pws = nw == 8 ? part_scratch<8>(in_cap) : nw == 4 ? part_scratch<4>(in_cap) : part_scratch<3>(in_cap);
-        uint32_t seed = (uint32_t)std::max(0L, knob("LZ4_ENC_SEED", kSeed)) & ~(kWave - 1u);   // positions seeded before a part
+        uint32_t seed = (uint32_t)std::max(0L, knob("LZ4_ENC_SEED", nw == 3 ? 10240L : (long)kSeed)) & ~(kWave - 1u);   // positions seeded before a part
         // part 0's share of the page in 64ths (0: equal parts); at least 1/kNW, so the later parts fit
         // their scratch (part_scratch: a 1/kNW part)
-        uint32_t p0 = (uint32_t)std::max(0L, knob("LZ4_ENC_P0", 0));
+        uint32_t p0 = (uint32_t)std::max(0L, knob("LZ4_ENC_P0", nw == 3 ? 27L : 0L));
         if (p0) p0 = std::min<uint32_t>(std::max<uint32_t>(p0, (64u + (uint32_t)nw - 1u) / (uint32_t)nw), 48u);
         const uint32_t ws_stride = (uint32_t)(nw - 1) * pws;
         ScratchLease ws(s, grid * (size_t)ws_stride);

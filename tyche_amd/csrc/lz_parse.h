@@ -183,15 +183,17 @@ __device__ __forceinline__ void decode_record(const uint2 *rec, uint32_t n, uint
 #ifndef TYCHE_WAYS_SCALE
 #define TYCHE_WAYS_SCALE 2   // bucketed tables hold TYCHE_WAYS_SCALE * kHashSize slots
 #endif
-// kRepCand (zstd) with 2 ways: TYCHE_ZSTD_BUCKETS buckets, not a power of two --
-// 1856 buckets (7,424 bytes) keep a 32 KiB page's parse at 40,848 bytes of LDS,
-// 4 waves per CU (zstd_encode.hip); the bucket is the high product of the hash
+// kRepCand (zstd) with 2 or 4 ways: 2 * TYCHE_ZSTD_BUCKETS slots in buckets of
+// kWays, a bucket count that is not a power of two -- 3,712 slots (7,424 bytes)
+// keep a 32 KiB page's parse at 40,848 bytes of LDS, 4 waves per CU
+// (zstd_encode.hip); the bucket is the high product of the hash
 #ifndef TYCHE_ZSTD_BUCKETS
 #define TYCHE_ZSTD_BUCKETS 1856
 #endif
 template <int kWays, bool kRepCand = false>
 __host__ __device__ constexpr uint32_t table_slots() {
-    return kRepCand && kWays == 2 ? 2u * TYCHE_ZSTD_BUCKETS : kWays > 1 ? TYCHE_WAYS_SCALE * kHashSize : kHashSize;
+    return kRepCand && (kWays == 2 || kWays == 4) ? 2u * TYCHE_ZSTD_BUCKETS
+                                                  : kWays > 1 ? TYCHE_WAYS_SCALE * kHashSize : kHashSize;
 }
 
 template <int kWays>
@@ -202,7 +204,7 @@ __device__ __forceinline__ uint32_t bucket_of(uint32_t v, uint32_t v2 = 0, uint3
     if (nbytes > 4) {   // 5 or 6 bytes: zstd's fast parse hashes searchLength bytes (ZSTD_hashPtr)
         const uint64_t x = ((uint64_t)(v2 & (nbytes == 5 ? 0xFFu : 0xFFFFu)) << 32) | v;
         const uint64_t hx = x * 0xCF1BBCDCB7A56463ull;
-        if (kWays == 2) return (uint32_t)(((hx >> 32) * (uint64_t)TYCHE_ZSTD_BUCKETS) >> 32);
+        if (kWays == 2 || kWays == 4) return (uint32_t)(((hx >> 32) * (uint64_t)(2u * TYCHE_ZSTD_BUCKETS / kWays)) >> 32);
         return (uint32_t)(hx >> (64 - lg));
     }
     return (v * 2654435761u) >> (32 - lg);
@@ -375,7 +377,11 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
             }
             if (kMin3 && rw.w0 != v) rn = 3u;
 #ifndef TYCHE_REP_SLACK
-#define TYCHE_REP_SLACK 0
+// a repeat candidate wins when at most this many bytes shorter than the hash candidate: a repeat
+// offset costs a few bits instead of ~10-14 (round 3, 64K bench pages: slack 0 / 2 / 3 / 4 ratio
+// 4.676 / 4.708 / 4.709 / 4.704 at 16 KiB, 4.947 / 4.988 / 4.989 / 4.981 at 32 KiB, encode time
+// unchanged; tools/parse_sim.c zfse put 3 at level 1's ratio)
+#define TYCHE_REP_SLACK 3
 #endif
             // repeat offset 2 (the other offset of two alternating ones)
             const uint32_t rc2 = pos >= R2 ? pos - R2 : 0u;

@@ -786,10 +786,11 @@ __device__ __forceinline__ int32_t parse_to_area_with(uint32_t L, uint8_t *area,
     if (lane == 0) ((uint32_t *)area)[1] = npb;
     return 1;
 }
+template <int kW>
 __device__ __forceinline__ int32_t parse_to_area(const uint8_t *in, uint32_t L, uint16_t *table, uint2 *rec,
                                                  uint8_t *area, uint32_t rec_cap, uint32_t lane) {
     return parse_to_area_with(L, area, rec_cap, lane, [&](auto &sink) {
-        return lzp::parse_page<true, false, kZWays>(in, L, table, rec, lane, sink);
+        return lzp::parse_page<true, false, kW>(in, L, table, rec, lane, sink);
     });
 }
 
@@ -844,8 +845,9 @@ __device__ __forceinline__ int32_t emit_page(const uint8_t *src, uint32_t L, uin
 }
 
 // The one-kernel encode of pages [first, first + count) of b (TYCHE_ZSTD_ENC_SPLIT=0).
-// kParse: pass A1 of the split encode instead (the parse only, into ws; status to st).
-template <bool kParse>
+// kParse: pass A1 of the split encode instead (the parse only, into ws; status to st), its
+// buckets of kW ways (2 or 4: the same 3,712 table slots, lz_parse.h)
+template <bool kParse, int kW = kZWays>
 __global__ __launch_bounds__(64) void zstd_encode_kernel(tyche_batch_t b, size_t first, size_t count, uint32_t in_cap,
                                                          unsigned *ctr, uint8_t *ws, size_t ws_page, int32_t *st,
                                                          uint32_t logcap) {
@@ -892,7 +894,7 @@ __global__ __launch_bounds__(64) void zstd_encode_kernel(tyche_batch_t b, size_t
             WAVE_SYNC();
             in[p.src_len + lane] = 0;
             WAVE_SYNC();
-            if (kParse) rv = parse_to_area(in, p.src_len, table, rec, ws + page * ws_page, enc_rec_cap(in_cap), lane);
+            if (kParse) rv = parse_to_area<kW>(in, p.src_len, table, rec, ws + page * ws_page, enc_rec_cap(in_cap), lane);
             else rv = encode_page(in, p.src_len, table, map, rec, seq, htab, wts, p.dst, p.dst_cap, logcap, lane);
         }
         if (lane == 0) {
@@ -1408,14 +1410,21 @@ hipError_t launch_zstd_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream
     }
     int32_t *st = (int32_t *)lease.get();
     uint8_t *ws = (uint8_t *)lease.get() + st_bytes;
-    const void *k1 = (const void *)zstd_encode_kernel<true>;
+    // pass A1's buckets: 4 ways for pages up to TYCHE_ZSTD_WAYS4_MAX bytes (default 16 KiB), 2 above --
+    // the same LDS (round 3, 64K bench pages with the repeat slack: 16 KiB ratio 4.709 -> see DESIGN
+    // §3.5; tools/parse_sim.c zstd: +0.4 % at 16 KiB, +0.55 % at 32 KiB for the two extra candidates)
+    const bool four = kZWays == 2 && (long)in_cap <= knob("ZSTD_WAYS4_MAX", 16384);
+    const void *k1 = four ? (const void *)zstd_encode_kernel<true, 4> : (const void *)zstd_encode_kernel<true>;
     const size_t ncu = prepare_launch(k1);
     (void)prepare_launch((const void *)zstd_block_kernel);
     (void)prepare_launch((const void *)zstd_fse_kernel);
     (void)prepare_launch((const void *)zstd_pack_kernel);
     const size_t cu1 = waves_per_cu(k1, lds1), cu2 = waves_per_cu((const void *)zstd_block_kernel, kA2Lds);
     // pass A1's waves per page (1: the one-wave parse)
-    const long pw = knob("ZSTD_PARSE_WAVES", 1);
+    // pass A1 on 1, 2 or 4 waves per page: 2 by default for pages over 16 KiB (round 3, with the
+    // repeat slack: C3 876 vs 1,014 ms per 1M pages at ratio 4.951 vs 4.989 -- the reference's level 1
+    // gives 4.915; 4 waves 789 ms at 4.902), 1 wave (4-way buckets, above) up to 16 KiB
+    const long pw = knob("ZSTD_PARSE_WAVES", four ? 1 : 2);
     size_t cup = 1;
     if (pw == 2 || pw == 4) {
         const void *kp = pw == 4 ? (const void *)zstd_parse_split_kernel<4> : (const void *)zstd_parse_split_kernel<2>;
@@ -1460,8 +1469,12 @@ hipError_t launch_zstd_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream
             const size_t g = std::min<size_t>(n, ncu * cu1);
             WorkCounter ctr(s, g < n);
             if (!ctr.get()) return hipErrorOutOfMemory;
-            hipLaunchKernelGGL(zstd_encode_kernel<true>, dim3((unsigned)g), dim3(kWave), lds1, s, b, first, n, in_cap,
-                               ctr.get(), ws, page_bytes, st, logcap);
+            unsigned *cp = ctr.get();
+            uint8_t *wsp = ws;
+            size_t fst = first, cnt = n, wpage = page_bytes;
+            uint32_t icap = in_cap, lc = logcap;
+            void *args[] = {(void *)&b, &fst, &cnt, &icap, &cp, &wsp, &wpage, &st, &lc};
+            (void)hipLaunchKernel(k1, dim3((unsigned)g), dim3(kWave), args, lds1, s);
         }
         {
             const size_t g = std::min<size_t>(n, ncu * cu2);
