@@ -29,7 +29,7 @@ KERNELS = {"lz4_encode": ("lz4_encode_",), "lz4_decode": ("lz4_decode_",),
            "zstd_encode": ("zstd_encode_kernel", "zstd_parse_split_kernel", "zstd_block_kernel", "zstd_fse_kernel",
                            "zstd_pack_kernel"),
            "zstd_decode": ("zstd_decode_kernel", "zstd_entropy_kernel", "zstd_seq_kernel", "zstd_exec_kernel",
-                           "zstd_exec_lane_kernel", "zstd_seqexec_kernel"),
+                           "zstd_exec_lane_kernel", "zstd_seqexec_kernel", "zstd_lit_kernel"),
            "zlib_encode": ("zlib_deflate_kernel",), "zlib_decode": ("zlib_inflate_kernel",)}
 
 

@@ -1026,7 +1026,8 @@ constexpr size_t zsplit_stage_off() { return zsplit_hdr_bytes<kNW>() + kNW * kZW
 template <uint32_t kNW>
 __global__ __launch_bounds__(kNW * 64) void zstd_parse_split_kernel(tyche_batch_t b, size_t first, size_t count,
                                                                     uint32_t in_cap, unsigned *ctr, uint8_t *ws,
-                                                                    size_t ws_page, int32_t *st, uint32_t seed) {
+                                                                    size_t ws_page, int32_t *st, uint32_t seed,
+                                                                    uint32_t p0) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr uint32_t kT = kNW * kWave;
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
@@ -1058,8 +1059,17 @@ __global__ __launch_bounds__(kNW * 64) void zstd_parse_split_kernel(tyche_batch_
         const bool fits = L <= in_cap;
         uint8_t *area = ws + page * ws_page;
         uint2 *W = (uint2 *)area_rec(area) + (size_t)wave * slice;
-        const uint32_t b0 = wave == 0 ? 0u : ((L * wave) / kNW) & ~(kWave - 1u);
-        const uint32_t b1 = wave + 1 == kNW ? L : ((L * (wave + 1)) / kNW) & ~(kWave - 1u);
+        // part w starts at bnd(w): equal parts, or (p0 > 0) p0/64 of the page for part 0 -- the one part
+        // without a seed and a warm-up -- and equal shares of the rest
+        auto bnd = [&](uint32_t w) -> uint32_t {
+            if (w == 0) return 0u;
+            if (w == kNW) return L;
+            if (!p0) return ((L * w) / kNW) & ~(kWave - 1u);
+            const uint32_t h = (L * p0 / 64u) & ~(kWave - 1u);
+            return (h + ((L - h) * (w - 1u)) / (kNW - 1u)) & ~(kWave - 1u);
+        };
+        const uint32_t b0 = bnd(wave);
+        const uint32_t b1 = bnd(wave + 1);
         const uint32_t Lp = wave + 1 == kNW ? L : b1 + kLastLiterals;
         if (fits) {
             uint32_t rep[2] = {1u, 4u};
@@ -1463,7 +1473,13 @@ hipError_t launch_zstd_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream
             size_t fst = first, cnt = n, wpage = page_bytes;
             uint32_t icap = in_cap;
             uint32_t seed = (uint32_t)std::max(0L, knob("ZSTD_PARSE_SEED", kZSeed)) & ~(kWave - 1u);
-            void *args[] = {(void *)&b, &fst, &cnt, &icap, &cp, &ws, &wpage, &st, &seed};
+            // part 0's share in 64ths (0: equal parts), between 1/pw and 2/pw of the page: every part's
+            // sequences (<= a quarter of its bytes) fit its slice of 2 * rec_cap / pw entries
+            uint32_t p0 = (uint32_t)std::max(0L, knob("ZSTD_PARSE_P0", 0));
+            if (p0)
+                p0 = std::min<uint32_t>(std::max<uint32_t>(p0, (64u + (uint32_t)pw - 1u) / (uint32_t)pw),
+                                        std::min<uint32_t>(48u, 128u / (uint32_t)pw));
+            void *args[] = {(void *)&b, &fst, &cnt, &icap, &cp, &ws, &wpage, &st, &seed, &p0};
             (void)hipLaunchKernel(kp, dim3((unsigned)g), dim3((unsigned)(pw * kWave)), args, ldsp, s);
         } else {
             const size_t g = std::min<size_t>(n, ncu * cu1);
