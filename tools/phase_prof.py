@@ -36,3 +36,10 @@ for i, nm in enumerate(names):
     print(f"{nm:14s} {buf[i] / npg:10.0f} cycles/page  {100.0 * buf[i] / tot:5.1f} %")
 print(f"extensions     {buf[6] / npg:10.1f} per page; blocks {buf[8] / npg:.1f}, with a match {buf[10] / npg:.1f}, matches {buf[9] / npg:.1f}")
 print(f"parse total    {tot / npg:10.0f} cycles/page; kernel {e0.elapsed_time(e1):.2f} ms for {n} pages; pages seen {npg}")
+if buf[15]:
+    sub = ["fields + prefix sum", "ring writes", "long literal runs", "ring flush"]
+    st = sum(buf[11 + i] for i in range(4))
+    print(f"sink sub-phases (every 64th workgroup, {buf[15]} calls):")
+    for i, nm in enumerate(sub):
+        print(f"  {nm:20s} {buf[11 + i] / buf[15]:8.0f} cycles/call  {100.0 * buf[11 + i] / st:5.1f} %")
+

@@ -225,6 +225,15 @@ __device__ __forceinline__ void out_flush_all(const uint8_t *ring, OutRing &r, u
 // false if the output would exceed cap.
 __device__ __forceinline__ bool emit_staged(const uint2 *rec, uint32_t n, uint32_t anchor, const uint8_t *in, uint8_t *dst,
                             uint32_t &op, uint32_t cap, uint8_t *ring, OutRing &r, uint8_t *map, uint32_t lane) {
+#if defined(TYCHE_PHASES)
+    // profiling builds: sink sub-phases of every 64th workgroup's calls into g_phase[11..15]
+    const bool sp_rec = blockIdx.x % 64u == 0u && lane == 0u;
+    uint32_t sp_t = (uint32_t)__builtin_amdgcn_s_memtime();
+#define SINK_PHASE(i) do { const uint32_t t_ = (uint32_t)__builtin_amdgcn_s_memtime(); \
+                           if (sp_rec) atomicAdd(&lzp::g_phase[i], (unsigned long long)(t_ - sp_t)); sp_t = t_; } while (0)
+#else
+#define SINK_PHASE(i) do {} while (0)
+#endif
     const bool is_sel = lane < n;
     const uint2 rc = rec[is_sel ? lane : 0];
     const uint2 rp = rec[lane > 0 && is_sel ? lane - 1 : 0];
@@ -250,6 +259,7 @@ __device__ __forceinline__ bool emit_staged(const uint2 *rec, uint32_t n, uint32
         out_flush_all(ring, r, dst, op, lane);
         return emit_records(rec, n, anchor, in, dst, op, cap, map, (uint4 *)ring, lane);
     }
+    SINK_PHASE(11);
     constexpr uint32_t m = kOutRing - 1;
     const uint32_t q_lit = r.head + r.pend + eo + 1 + lext;   // ring position of this sequence's literals
     if (is_sel) {
@@ -284,6 +294,7 @@ __device__ __forceinline__ bool emit_staged(const uint2 *rec, uint32_t n, uint32
         q += 2;
         for (uint32_t t = 0; t < mext; t++) ring[(q + t) & m] = (uint8_t)(t + 1 == mext ? (mc - 15) % 255 : 255);
     }
+    SINK_PHASE(12);
     uint64_t longm = __ballot(is_sel && lit > kLitLane);
     while (longm) {
         const uint32_t k = (uint32_t)__builtin_ctzll(longm);
@@ -292,11 +303,17 @@ __device__ __forceinline__ bool emit_staged(const uint2 *rec, uint32_t n, uint32
         for (uint32_t i = lane; i < kl; i += kWave) ring[(kq + i) & m] = in[ks + i];
     }
     __builtin_amdgcn_wave_barrier();
+    SINK_PHASE(13);
     r.pend += et;
     out_flush_steps(ring, r, dst, op, lane);
     __builtin_amdgcn_wave_barrier();
+    SINK_PHASE(14);
+#if defined(TYCHE_PHASES)
+    if (sp_rec) atomicAdd(&lzp::g_phase[15], 1ull);
+#endif
     return true;
 }
+#undef SINK_PHASE
 
 // Encodes one page held in LDS into dst (global, capacity cap).  Returns the
 // compressed size, or 0 if it does not fit in cap.
