@@ -129,7 +129,7 @@ def test_encode_roundtrip_oracle(tc, oracle_mod, dist, plen):
 
 def _literal_run_pages(n, plen, seed):
     """Pages mixing random stretches (long literal runs: batches of sequences whose encoding
-    exceeds the encoder's 1 KiB output ring go straight to HBM, lz4_encode.hip emit_records)
+    exceeds the encoder's output ring go straight to HBM, lz4_encode.hip emit_records)
     with repeated records (matches), in several proportions."""
     rng = np.random.default_rng(seed)
     pages = np.zeros((n, plen), np.uint8)

@@ -174,12 +174,29 @@ __device__ bool emit_records(const uint2 *rec, uint32_t n, uint32_t anchor, cons
 // stamp, a max-scan, a select chain per byte): ~330 instructions per 256 output
 // bytes, 27 % of the encoder's wave cycles (tools/phase_prof.py, r02).  Here each
 // sequence's lane writes its own bytes -- token, literal-length bytes, literals,
-// offset, match-length bytes -- into a 1 KiB LDS ring with byte stores, and the
-// ring leaves for HBM in 256-byte steps, one dword store per lane.  The ring
+// offset, match-length bytes -- into a 2 KiB LDS ring with byte stores, and the
+// ring leaves for HBM in 512-byte steps, one 8-byte store per lane.  The ring
 // reuses emit_records' field area, so the LDS budget (and 8 waves per CU) is
 // unchanged; a sink too large for the ring (long literal runs: the ring is
 // flushed first) still takes emit_records straight to HBM.
-constexpr uint32_t kOutRing = 1024;   // bytes; head is always a multiple of 256
+// Output ring size and flush width (round 3, 256K x 16 KiB pages, ms per 1M, three-wave encoder):
+// 1 KiB ring, 256-byte dword flushes 79.3-79.4; 2 KiB, 512-byte 8-byte flushes 78.1; 2 KiB, 1 KiB
+// 16-byte flushes 78.2; 1 KiB, 512-byte flushes 80.2 (more batches overflow the ring).  A wave-wide
+// copy of all long literal runs at once (instead of one run after another) ran 80.5.
+#ifndef TYCHE_LZ4_RING
+#define TYCHE_LZ4_RING 2048
+#endif
+#ifndef TYCHE_LZ4_FLUSH_VEC
+#define TYCHE_LZ4_FLUSH_VEC 2
+#endif
+constexpr uint32_t kOutRing = TYCHE_LZ4_RING;        // bytes; head is always a multiple of kFlushStep
+constexpr uint32_t kFlushVec = TYCHE_LZ4_FLUSH_VEC;  // dwords per lane per flush step (1, 2 or 4)
+constexpr uint32_t kFlushStep = 4u * kWave * kFlushVec;
+static_assert(kOutRing >= 1024 && kOutRing % kFlushStep == 0 && (kOutRing & (kOutRing - 1)) == 0, "ring");
+typedef uint32_t u32x2_ua __attribute__((ext_vector_type(2), aligned(1)));
+typedef __attribute__((address_space(1))) u32x2_ua g_u32x2_ua;
+typedef uint32_t u32x4_uaf __attribute__((ext_vector_type(4), aligned(1)));
+typedef __attribute__((address_space(1))) u32x4_uaf g_u32x4_uaf;
 #ifndef TYCHE_LIT_LANE
 #define TYCHE_LIT_LANE 8
 #endif
@@ -193,20 +210,30 @@ struct OutRing {
 
 __device__ __forceinline__ void out_flush_steps(const uint8_t *ring, OutRing &r, uint8_t *dst, uint32_t &op,
                                                 uint32_t lane) {
-    while (r.pend >= 4 * kWave) {
-        const uint32_t w = *(const uint32_t *)(ring + ((r.head + 4 * lane) & (kOutRing - 1)));
-        store_u32_unaligned(dst + op + 4 * lane, w);
-        op += 4 * kWave;
-        r.head = (r.head + 4 * kWave) & (kOutRing - 1);
-        r.pend -= 4 * kWave;
+    while (r.pend >= kFlushStep) {
+        const uint8_t *src = ring + ((r.head + 4u * kFlushVec * lane) & (kOutRing - 1));
+        uint8_t *d = dst + op + 4u * kFlushVec * lane;
+        if (kFlushVec == 4) {
+            *(g_u32x4_uaf *)(uintptr_t)d = *(const u32x4 *)src;
+        } else if (kFlushVec == 2) {
+            const uint2 w = *(const uint2 *)src;
+            u32x2_ua v;
+            v.x = w.x;
+            v.y = w.y;
+            *(g_u32x2_ua *)(uintptr_t)d = v;
+        } else {
+            store_u32_unaligned(d, *(const uint32_t *)src);
+        }
+        op += kFlushStep;
+        r.head = (r.head + kFlushStep) & (kOutRing - 1);
+        r.pend -= kFlushStep;
     }
 }
 
 __device__ __forceinline__ void out_flush_all(const uint8_t *ring, OutRing &r, uint8_t *dst, uint32_t &op,
                                               uint32_t lane) {
     out_flush_steps(ring, r, dst, op, lane);
-    const uint32_t j = 4 * lane;
-    if (j < r.pend) {
+    for (uint32_t j = 4 * lane; j < r.pend; j += 4 * kWave) {   // the rest (< kFlushStep), a dword per lane
         const uint32_t w = *(const uint32_t *)(ring + ((r.head + j) & (kOutRing - 1)));
         if (j + 4 <= r.pend) {
             store_u32_unaligned(dst + op + j, w);
@@ -387,7 +414,7 @@ struct SplitHdr {
 };
 static_assert(sizeof(SplitHdr) == 64, "split header");
 // per-wave region: table | map (256) | records (512) | fields / output ring (1 KiB)
-constexpr size_t kWaveRegion = kHashSize * sizeof(uint16_t) + 4 * kWave + kWave * sizeof(uint2) + kWave * sizeof(uint4);
+constexpr size_t kWaveRegion = kHashSize * sizeof(uint16_t) + 4 * kWave + kWave * sizeof(uint2) + kOutRing;
 constexpr size_t kSplitStage = sizeof(SplitHdr) + 2 * kWaveRegion;
 
 // the last literal run in[anchor, L) at dst + op (encode_page's tail); false if it does not fit cap
@@ -802,8 +829,8 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel(tyche_batch_t b, uint32_
     uint16_t *table = (uint16_t *)smem;
     uint8_t *map = smem + kHashSize * sizeof(uint16_t);                 // 256-byte owner map
     uint2 *rec = (uint2 *)(map + 4 * kWave);                           // 64 sequence records
-    uint4 *fld = (uint4 *)(rec + kWave);                               // 64 packed sequence fields
-    uint8_t *stage = (uint8_t *)(fld + kWave);
+    uint4 *fld = (uint4 *)(rec + kWave);                               // 64 packed sequence fields / output ring
+    uint8_t *stage = (uint8_t *)fld + kOutRing;
     const size_t stride = gridDim.x;
 
     size_t page = blockIdx.x;
@@ -919,7 +946,7 @@ hipError_t launch_lz4_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream_
             return hipGetLastError();
         }
     }
-    const size_t lds = kHashSize * sizeof(uint16_t) + 4 * kWave + kWave * 8 + kWave * 16 +
+    const size_t lds = kHashSize * sizeof(uint16_t) + 4 * kWave + kWave * 8 + kOutRing +
                        ((in_cap + 16u + kPad + 15u) & ~15u);
     const size_t ncu = prepare_launch((const void *)lz4_encode_kernel);
     const size_t per_cu = waves_per_cu((const void *)lz4_encode_kernel, lds);
