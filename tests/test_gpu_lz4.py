@@ -187,10 +187,15 @@ def test_pagegen_matches_host(tc, oracle_mod):
         assert np.array_equal(d, h), dist
 
 
+@pytest.mark.parametrize("kernel", ["default", "split3_all_sizes"])
 @pytest.mark.parametrize("n", [0, 1, 4, 12, 13, 14, 63, 64, 65, 100, 1000, 4095, 65535])
-def test_encode_sizes(tc, oracle_mod, n):
-    """Edge sizes: empty (LZ4 emits one 0x00 token), below MFLIMIT+1, around a wave, max byU16 size."""
+def test_encode_sizes(tc, oracle_mod, knobs, n, kernel):
+    """Edge sizes: empty (LZ4 emits one 0x00 token), below MFLIMIT+1, around a wave, max byU16 size;
+    each also through the three-wave split kernel (TYCHE_LZ4_SPLIT_MIN=0: parts of a tiny page are
+    empty or a few bytes)."""
     O = oracle_mod
+    if kernel != "default":
+        knobs(LZ4_SPLIT_MIN=0)
     rng = np.random.default_rng(n)
     data = (rng.integers(0, 3, n, dtype=np.uint8) * 40).tobytes()
     src = torch.from_numpy(np.frombuffer(data, np.uint8).copy().reshape(1, n) if n else np.zeros((1, 0), np.uint8))

@@ -49,7 +49,8 @@ namespace {
 using lzp::kWave;
 using lzp::kHashSize;
 constexpr uint32_t kPad = 64;
-constexpr uint32_t kPrefetchVec = 16;    // 16-byte vectors per lane prefetched for the next page (16 KiB)
+constexpr uint32_t kPrefetchVec = 16;    // 16-byte vectors per lane prefetched for the next page (16 KiB; 8 or 4
+                                          // take the one-wave kernel to 132 / 119 VGPRs: 70.6 / 70.9 ms per 1M x 8 KiB)
 
 // a sequence's encoding: token, literal-length bytes, literals, offset, match-length bytes
 struct SeqFields {
@@ -342,6 +343,16 @@ __device__ __forceinline__ bool emit_staged(const uint2 *rec, uint32_t n, uint32
 }
 #undef SINK_PHASE
 
+#ifndef TYCHE_LZ4_SINK_CALL
+#define TYCHE_LZ4_SINK_CALL 0
+#endif
+// the one-wave kernel's sink as a call (TYCHE_LZ4_SINK_CALL=1), as in round 2, instead of inlined
+__device__ __noinline__ bool emit_staged_call(const uint2 *rec, uint32_t n, uint32_t anchor, const uint8_t *in, uint8_t *dst,
+                                              uint32_t &op, uint32_t cap, uint8_t *ring, OutRing &r, uint8_t *map,
+                                              uint32_t lane) {
+    return emit_staged(rec, n, anchor, in, dst, op, cap, ring, r, map, lane);
+}
+
 // Encodes one page held in LDS into dst (global, capacity cap).  Returns the
 // compressed size, or 0 if it does not fit in cap.
 __device__ int32_t encode_page(const uint8_t *in, uint32_t L, uint16_t *table, uint8_t *map, uint2 *rec,
@@ -353,6 +364,7 @@ __device__ int32_t encode_page(const uint8_t *in, uint32_t L, uint16_t *table, u
     OutRing r{0u, 0u};
     uint8_t *ring = (uint8_t *)fld;
     auto sink = [&](const uint2 *rr, uint32_t n, uint32_t anchor) -> bool {
+        if (TYCHE_LZ4_STAGED && TYCHE_LZ4_SINK_CALL) return emit_staged_call(rr, n, anchor, in, dst, op, cap, ring, r, map, lane);
         if (TYCHE_LZ4_STAGED) return emit_staged(rr, n, anchor, in, dst, op, cap, ring, r, map, lane);
         return emit_records(rr, n, anchor, in, dst, op, cap, map, fld, lane);
     };
@@ -898,7 +910,13 @@ hipError_t launch_lz4_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream_
     // and the later parts seeded with the 10,240 positions before them -- A/B of seeds 4,096-16,384
     // and part-0 shares 21-29/64 in DESIGN.md §3.2)
     const long nw = knob("LZ4_ENC_WAVES", 3);
-    if (!one_wave && in_cap >= kSplitMin && (nw == 3 || nw == 4 || nw == 8)) {
+    // TYCHE_LZ4_SPLIT_MIN: the smallest in_cap that takes a split kernel.  8 KiB pages split into
+    // three parts too since round 3 (256K x 8 KiB pages, ms per 1M: one wave per page 70.6 -- it holds
+    // 168 VGPRs, 12 waves per CU --, three waves 41.5 at ratio 2.525 vs 2.528, four 37.9 at 2.519);
+    // the two-wave kernel keeps kSplitMin for its own per-page split
+    const uint32_t split_min = (uint32_t)std::max(0L, knob("LZ4_SPLIT_MIN", nw == 3 || nw == 4 || nw == 8 ? 8192L
+                                                                                                       : (long)kSplitMin));
+    if (!one_wave && in_cap >= split_min && (nw == 3 || nw == 4 || nw == 8)) {
         const void *k = nw == 8   ? (const void *)lz4_encode_splitn_kernel<8>
                         : nw == 4 ? (const void *)lz4_encode_splitn_kernel<4>
                                   : (const void *)lz4_encode_splitn_kernel<3>;
@@ -927,7 +945,7 @@ hipError_t launch_lz4_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream_
             return hipGetLastError();
         }
     }
-    if (!one_wave && in_cap >= kSplitMin) {
+    if (!one_wave && in_cap >= split_min) {
         const size_t lds = kSplitStage + ((in_cap + 16u + kPad + 15u) & ~15u);
         const size_t ncu = prepare_launch((const void *)lz4_encode_split_kernel);
         int per_cu = 0;
