@@ -344,12 +344,23 @@ __device__ __forceinline__ bool emit_staged(const uint2 *rec, uint32_t n, uint32
 #undef SINK_PHASE
 
 #ifndef TYCHE_LZ4_SINK_CALL
-#define TYCHE_LZ4_SINK_CALL 0
+// the sink as a call instead of inlined into the parse: bit 0 for the one-wave kernel (encode_page),
+// bit 1 for the N-wave split kernels.  One wave per page, ms per 1M pages: 8 KiB 70.7 inlined ->
+// 44.7 called, 4 KiB 34.8 -> 21.3 (the inlined sink was round 3's 38 -> 70 ms regression at 8 KiB);
+// the three-wave kernel the other way: 16 KiB 77.9 inlined vs 86.9 called, 8 KiB 41.4 vs 46.6
+#define TYCHE_LZ4_SINK_CALL 1
 #endif
-// the one-wave kernel's sink as a call (TYCHE_LZ4_SINK_CALL=1), as in round 2, instead of inlined
+// the sink as a call (as in round 2)
 __device__ __noinline__ bool emit_staged_call(const uint2 *rec, uint32_t n, uint32_t anchor, const uint8_t *in, uint8_t *dst,
                                               uint32_t &op, uint32_t cap, uint8_t *ring, OutRing &r, uint8_t *map,
                                               uint32_t lane) {
+    return emit_staged(rec, n, anchor, in, dst, op, cap, ring, r, map, lane);
+}
+
+__device__ __forceinline__ bool emit_sink_n(const uint2 *rec, uint32_t n, uint32_t anchor, const uint8_t *in, uint8_t *dst,
+                                            uint32_t &op, uint32_t cap, uint8_t *ring, OutRing &r, uint8_t *map,
+                                            uint32_t lane) {
+    if (TYCHE_LZ4_SINK_CALL & 2) return emit_staged_call(rec, n, anchor, in, dst, op, cap, ring, r, map, lane);
     return emit_staged(rec, n, anchor, in, dst, op, cap, ring, r, map, lane);
 }
 
@@ -364,7 +375,7 @@ __device__ int32_t encode_page(const uint8_t *in, uint32_t L, uint16_t *table, u
     OutRing r{0u, 0u};
     uint8_t *ring = (uint8_t *)fld;
     auto sink = [&](const uint2 *rr, uint32_t n, uint32_t anchor) -> bool {
-        if (TYCHE_LZ4_STAGED && TYCHE_LZ4_SINK_CALL) return emit_staged_call(rr, n, anchor, in, dst, op, cap, ring, r, map, lane);
+        if ((TYCHE_LZ4_STAGED != 0) & ((TYCHE_LZ4_SINK_CALL & 1) != 0)) return emit_staged_call(rr, n, anchor, in, dst, op, cap, ring, r, map, lane);
         if (TYCHE_LZ4_STAGED) return emit_staged(rr, n, anchor, in, dst, op, cap, ring, r, map, lane);
         return emit_records(rr, n, anchor, in, dst, op, cap, map, fld, lane);
     };
@@ -721,7 +732,7 @@ __global__ __launch_bounds__(kNW * 64) void lz4_encode_splitn_kernel(tyche_batch
                 uint32_t op = 0;
                 OutRing r{0u, 0u};
                 auto sink = [&](const uint2 *rr, uint32_t n, uint32_t anchor) -> bool {
-                    return emit_staged(rr, n, anchor, in, p.dst, op, p.dst_cap, ring, r, map, lane);
+                    return emit_sink_n(rr, n, anchor, in, p.dst, op, p.dst_cap, ring, r, map, lane);
                 };
                 const uint32_t cur = lzp::parse_page(in, Lp, table, rec, lane, sink);
                 const bool ok = cur != 0xFFFFFFFFu;
@@ -756,9 +767,9 @@ __global__ __launch_bounds__(kNW * 64) void lz4_encode_splitn_kernel(tyche_batch
                         }
                         if (n == 1) return true;
                         const uint32_t a = (rr[0].x & 0xFFFFu) + (rr[0].y & 0xFFFFu);
-                        return emit_staged(rr + 1, n - 1, a, in, scratch, op, 0xFFFFFFFFu, ring, r, map, lane);
+                        return emit_sink_n(rr + 1, n - 1, a, in, scratch, op, 0xFFFFFFFFu, ring, r, map, lane);
                     }
-                    return emit_staged(rr, n, anchor, in, scratch, op, 0xFFFFFFFFu, ring, r, map, lane);
+                    return emit_sink_n(rr, n, anchor, in, scratch, op, 0xFFFFFFFFu, ring, r, map, lane);
                 };
                 const uint32_t cur = lzp::parse_page(in, Lp, table, rec, lane, sink, b0);
                 out_flush_all(ring, r, scratch, op, lane);
@@ -786,7 +797,7 @@ __global__ __launch_bounds__(kNW * 64) void lz4_encode_splitn_kernel(tyche_batch
                     }
                     if (lane == 0) rec[0] = hdr->first[w];
                     __builtin_amdgcn_wave_barrier();
-                    ok = emit_staged(rec, 1, cur, in, p.dst, op, p.dst_cap, ring, r, map, lane);
+                    ok = emit_sink_n(rec, 1, cur, in, p.dst, op, p.dst_cap, ring, r, map, lane);
                     if (ok) out_flush_all(ring, r, p.dst, op, lane);
                     if (lane == 0) hdr->seg[w] = op;
                     op += rfl(hdr->len[w]);
