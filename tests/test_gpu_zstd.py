@@ -284,7 +284,8 @@ def test_encode_sizes(tc, oracle_mod, n):
 
 
 def test_encode_multiblock_and_incompressible(tc, oracle_mod):
-    """Pages with > 1024 sequences span several blocks (kSeqCap); random pages go out as raw blocks."""
+    """Pages with more sequences than a block holds span several blocks (kSeqCap in the one-kernel
+    encoder, kZBlk in the split one); random pages go out as raw blocks."""
     O = oracle_mod
     rng = np.random.default_rng(9)
     pages = []
@@ -300,6 +301,33 @@ def test_encode_multiblock_and_incompressible(tc, oracle_mod):
     _check_frames(O, comp, clen, host, 32768)
     lh = clen.cpu().numpy()
     assert (lh[8:] <= 32768 + 16).all()
+    # 64 KiB - 1 (the device encoders' largest page) of 5-byte words: > 10,000 sequences, several
+    # blocks at every block size the split encoder cuts (TYCHE_ZSTD_AREA_BLK, 4096 by default)
+    words = rng.integers(0, 256, (256, 5), dtype=np.uint8)
+    host = np.stack([words[rng.integers(0, 256, 65535 // 5 + 1)].reshape(-1)[:65535] for _ in range(4)])
+    comp, clen = tc.compress_pages(torch.from_numpy(host).to(DEV), compressor_id=ZSTD)
+    torch.cuda.synchronize()
+    _check_frames(O, comp, clen, host, 65535)
+    for i in range(4):
+        assert _count_blocks(comp[i, :int(clen[i])].cpu().numpy().tobytes()) >= 2, i
+    out, rv = tc.decompress_pages(comp, clen, 65535, compressor_id=ZSTD)
+    torch.cuda.synchronize()
+    assert (rv.cpu() == 65535).all() and torch.equal(out.cpu(), torch.from_numpy(host))
+
+
+def _count_blocks(frame):
+    """Blocks of one of our frames (single segment, no dictionary, no checksum)."""
+    fcs_id = frame[4] >> 6
+    pos = 5 + (1, 2, 4, 8)[fcs_id]
+    nb = 0
+    while True:
+        bh = int.from_bytes(frame[pos:pos + 3], "little")
+        size = bh >> 3
+        pos += 3 + (1 if (bh >> 1) & 3 == 1 else size)
+        nb += 1
+        if bh & 1:
+            assert pos == len(frame)
+            return nb
 
 
 def test_encode_large_batch_deterministic(tc):

@@ -159,7 +159,7 @@ struct Enc {
 // page per lane) writes the bitstreams into the gaps; pass C (zstd_pack_kernel)
 // closes the gaps and patches the block headers.  Capacity decisions use the
 // bounds, so a page that pass A2 accepts always fits.
-constexpr uint32_t kMaxBlk = 24;                 // blocks per page (> 65535 / 4 / 960 + 1)
+constexpr uint32_t kMaxBlk = 24;                 // blocks per page (> 65535 / 4 / 960 + 1; kZBlk below)
 constexpr uint32_t kBlkWords = 8;                // g_start, g_len, pre, fse (bound, then actual), n, rec, tab, flags
 // Sequence table logs: FSE_optimalTableLog capped at these (emit_block)
 constexpr uint32_t kStateBits = 7u + 6u + 7u;   // bits one sequence's three states emit at most (LL, OF, ML logs <= 7 / 6 / 7)
@@ -313,6 +313,7 @@ __device__ uint32_t huf_literals(Enc &e, uint32_t n, uint32_t trail, uint32_t li
     const bool single = lit_total < 256u;
     if (e.cap < lit_total || e.cap - lit_total < o + lh + 272u) return 0;   // room for header + weights below the scratch
     const uint32_t scr = e.cap - lit_total;
+    SPROF_DECL
     // ---- pass 1: scatter to scratch, histogram
     for (uint32_t k = lane; k < 256u; k += kWave) e.htab[k] = 0;
     __builtin_amdgcn_wave_barrier();
@@ -328,7 +329,9 @@ __device__ uint32_t huf_literals(Enc &e, uint32_t n, uint32_t trail, uint32_t li
 #pragma unroll
     for (int j = 0; j < 4; j++) c[j] = e.htab[lane + 64u * j];
     __builtin_amdgcn_wave_barrier();   // htab (now in c) is the Huffman construction's scratch
+    SPROF_MARK(10);   // scatter + histogram
     const uint32_t maxlen = huf::code_lengths(c, lit_total, kHufMaxBits, l, lane, e.htab);
+    SPROF_MARK(11);   // code lengths
     if (maxlen == 0) {
         // a single distinct byte: RLE literals (set_rle)
         const uint32_t fl = 1u + (lit_total > 31u) + (lit_total > 4095u);
@@ -389,6 +392,7 @@ __device__ uint32_t huf_literals(Enc &e, uint32_t n, uint32_t trail, uint32_t li
 #pragma unroll
     for (int j = 0; j < 4; j++) e.htab[lane + 64u * j] = code[j] | (l[j] << 16);
     __builtin_amdgcn_wave_barrier();
+    SPROF_MARK(12);   // weights, size check, codes
     // ---- streams: symbols last to first, bits LSB first (HUF_compress1X_usingCTable), end mark
     uint32_t sp = wpos + whdr + (single ? 0u : 6u);
     const uint32_t seg = (lit_total + 3u) / 4u;
@@ -435,6 +439,7 @@ __device__ uint32_t huf_literals(Enc &e, uint32_t n, uint32_t trail, uint32_t li
         }
         __builtin_amdgcn_wave_barrier();
     }
+    SPROF_MARK(13);   // streams
     const uint32_t clit = sp - (o + lh);
     // ---- literals section header (set_compressed)
     if (lh == 3u) {
@@ -744,6 +749,17 @@ __device__ __forceinline__ int32_t encode_page(const uint8_t *in, uint32_t L, ui
     return (int32_t)e.op;
 }
 
+// Sequences per block of the split encode.  Its blocks live in the area, not in LDS, so
+// they are not held to the one-kernel encode's kSeqCap: 4096 makes a 32 KiB page one
+// block, which halves pass A2's per-block Huffman and FSE table work (1M x 32 KiB:
+// encode 855 -> 793 ms, decode 308 -> 296 ms, ratio 4.946 -> 4.940; 16 KiB pages,
+// mostly one block already, unchanged -- profiles/r03_zstd_block_size_ab.log)
+#ifndef TYCHE_ZSTD_AREA_BLK
+#define TYCHE_ZSTD_AREA_BLK 4096
+#endif
+constexpr uint32_t kZBlk = TYCHE_ZSTD_AREA_BLK;
+static_assert(kZBlk >= kWave && (65536u / 4u + kZBlk - 1u) / kZBlk + 1u <= kMaxBlk, "area blocks");
+
 // Pass A1: the parse of one page (LDS, 64 zero bytes after) into the area: the
 // sequences, and blocks cut where encode_page's sink cuts them.  Returns 1, or
 // 0 when a bound is exceeded (the page is then stored uncompressed by the caller).
@@ -772,7 +788,7 @@ __device__ __forceinline__ int32_t parse_to_area_with(uint32_t L, uint8_t *area,
         const uint2 lastr = r[n - 1];
         cursor = (lastr.x & 0xFFFFu) + (lastr.y & 0xFFFFu);
         __builtin_amdgcn_wave_barrier();
-        if (nseq - bseq > kSeqCap - kWave) {
+        if (nseq - bseq > kZBlk) {
             if (npb + 1u >= kMaxBlk) return false;
             put_pblk(cursor);
             bstart = cursor;
@@ -1009,7 +1025,6 @@ __global__ __launch_bounds__(128) void zstd_parse_pipe_kernel(tyche_batch_t b, s
 #endif
 constexpr uint32_t kZSeed = TYCHE_ZSTD_SEED;
 constexpr uint32_t kZWarm = 256;   // bytes parsed (and dropped) before a part, for its repeat offsets
-constexpr uint32_t kZBlk = kSeqCap - kWave;   // sequences per parse block (parse_to_area cuts after > 960)
 template <uint32_t kNW>
 struct ZSplitHdr {
     uint32_t next_lo, next_hi, next2_lo, next2_hi;
