@@ -1445,22 +1445,25 @@ hipError_t launch_zstd_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream
     (void)prepare_launch((const void *)zstd_fse_kernel);
     (void)prepare_launch((const void *)zstd_pack_kernel);
     const size_t cu1 = waves_per_cu(k1, lds1), cu2 = waves_per_cu((const void *)zstd_block_kernel, kA2Lds);
-    // pass A1's waves per page (1: the one-wave parse)
-    // pass A1 on 1, 2 or 4 waves per page: 2 by default for pages over 16 KiB (round 3, with the
-    // repeat slack: C3 876 vs 1,014 ms per 1M pages at ratio 4.951 vs 4.989 -- the reference's level 1
-    // gives 4.915; 4 waves 789 ms at 4.902), 1 wave (4-way buckets, above) up to 16 KiB
-    const long pw = knob("ZSTD_PARSE_WAVES", four ? 1 : 2);
+    // pass A1 on 1 to 4 waves per page (1: the one-wave parse, 4-way buckets, up to 16 KiB):
+    // 4 by default above 16 KiB.  Round 3, 32 KiB bench pages with one block per page
+    // (profiles/r03_zstd_parse_ab.log): 2 parts 793 ms per 1M pages at ratio 4.940; 3 parts 823
+    // (2 workgroups per CU, the same 6 waves, twice the seeding); 4 parts, part 0 22/64 of the
+    // page and 12,288 seed positions: 709 ms at 4.921 -- the reference's level 1 gives 4.915
+    const long pw = knob("ZSTD_PARSE_WAVES", four ? 1 : 4);
+    const bool psplit = pw >= 2 && pw <= 4;
+    const void *kp = pw == 4 ? (const void *)zstd_parse_split_kernel<4>
+                   : pw == 3 ? (const void *)zstd_parse_split_kernel<3> : (const void *)zstd_parse_split_kernel<2>;
+    const size_t ldsp = (pw == 4 ? zsplit_stage_off<4>() : pw == 3 ? zsplit_stage_off<3>() : zsplit_stage_off<2>()) + page_lds;
     size_t cup = 1;
-    if (pw == 2 || pw == 4) {
-        const void *kp = pw == 4 ? (const void *)zstd_parse_split_kernel<4> : (const void *)zstd_parse_split_kernel<2>;
-        const size_t ldsp = (pw == 4 ? zsplit_stage_off<4>() : zsplit_stage_off<2>()) + page_lds;
+    if (psplit) {
         (void)prepare_launch(kp);
         int per = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kp, (int)(pw * kWave), ldsp) == hipSuccess && per > 0)
             cup = (size_t)per;
     }
     // pass A1 on two pipelined waves (TYCHE_ZSTD_PARSE_PIPE=1; default 0: one wave per page)
-    const bool pipe = pw != 2 && pw != 4 && knob("ZSTD_PARSE_PIPE", 0) != 0;
+    const bool pipe = !psplit && knob("ZSTD_PARSE_PIPE", 0) != 0;
     const size_t ldsq = kZPipeStage + page_lds;
     size_t cuq = 1;
     if (pipe) {
@@ -1478,21 +1481,23 @@ hipError_t launch_zstd_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream
             if (!ctr.get()) return hipErrorOutOfMemory;
             hipLaunchKernelGGL(zstd_parse_pipe_kernel, dim3((unsigned)g), dim3(2 * kWave), ldsq, s, b, first, n, in_cap,
                                ctr.get(), ws, page_bytes, st);
-        } else if (pw == 2 || pw == 4) {   // pass A1 on pw waves per page
-            const void *kp = pw == 4 ? (const void *)zstd_parse_split_kernel<4> : (const void *)zstd_parse_split_kernel<2>;
-            const size_t ldsp = (pw == 4 ? zsplit_stage_off<4>() : zsplit_stage_off<2>()) + page_lds;
+        } else if (psplit) {   // pass A1 on pw waves per page
             const size_t g = std::min<size_t>(n, ncu * cup);
             WorkCounter ctr(s, g < n);
             if (!ctr.get()) return hipErrorOutOfMemory;
             unsigned *cp = ctr.get();
             size_t fst = first, cnt = n, wpage = page_bytes;
             uint32_t icap = in_cap;
-            uint32_t seed = (uint32_t)std::max(0L, knob("ZSTD_PARSE_SEED", kZSeed)) & ~(kWave - 1u);
+            // positions seeded before each part (4 parts: 8,192 -> 12,288 seeds 701 -> 709 ms, ratio
+            // 4.910 -> 4.921; 16,384: 719 ms at 4.921)
+            uint32_t seed = (uint32_t)std::max(0L, knob("ZSTD_PARSE_SEED", pw == 4 ? 12288L : (long)kZSeed)) &
+                            ~(kWave - 1u);
             // part 0's share in 64ths (0: equal parts), between 1/pw and 2/pw of the page: every part's
             // sequences (<= a quarter of its bytes) fit its slice of 2 * rec_cap / pw entries
-            // (default 35/64 for two parts: 843 vs 869 ms per 1M x 32 KiB pages, ratio 4.946 vs 4.951;
-            // 33 / 34: 854 / 847 ms)
-            uint32_t p0 = (uint32_t)std::max(0L, knob("ZSTD_PARSE_P0", pw == 2 ? 35L : 0L));
+            // (two parts: 35/64, 843 vs 869 ms per 1M x 32 KiB pages, ratio 4.946 vs 4.951; 33 / 34:
+            // 854 / 847 ms.  Four parts: 22/64, 700 ms at 4.910 vs 16 (equal) 723 at 4.908, 20 702 at
+            // 4.910, 24 719 at 4.904, 27 772 at 4.893)
+            uint32_t p0 = (uint32_t)std::max(0L, knob("ZSTD_PARSE_P0", pw == 2 ? 35L : pw == 4 ? 22L : 0L));
             if (p0)
                 p0 = std::min<uint32_t>(std::max<uint32_t>(p0, (64u + (uint32_t)pw - 1u) / (uint32_t)pw),
                                         std::min<uint32_t>(48u, 128u / (uint32_t)pw));
