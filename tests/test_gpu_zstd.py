@@ -622,6 +622,7 @@ ENCODE_MODES = {
     "fused_fse_log6": dict(ZSTD_ENC_SPLIT=0, ZSTD_FSE_LOG=6),
     "piped_parse": dict(ZSTD_PARSE_PIPE=1),
     "split_parse2": dict(ZSTD_PARSE_WAVES=2),
+    "split_parse3": dict(ZSTD_PARSE_WAVES=3),
     "split_parse4": dict(ZSTD_PARSE_WAVES=4),
     "ways4_all_sizes": dict(ZSTD_WAYS4_MAX=65535),
     "ways2_all_sizes": dict(ZSTD_WAYS4_MAX=0),
@@ -635,9 +636,9 @@ def test_zstd_encode_fused_kernel_and_chunked_split(tc, oracle_mod, knobs, mode)
     (TYCHE_ZSTD_ENC_SPLIT=0) and the multi-pass encoder through a 1 MiB work area
     (TYCHE_ZSTD_SCRATCH_MB=1: a few pages per chunk), each also with round 2's fixed 6/5/6
     sequence-table logs (TYCHE_ZSTD_FSE_LOG=6), and pass A1 on two pipelined waves
-    (TYCHE_ZSTD_PARSE_PIPE=1) or split into 2 / 4 parts (TYCHE_ZSTD_PARSE_WAVES), and with
+    (TYCHE_ZSTD_PARSE_PIPE=1) or split into 2 / 3 / 4 parts (TYCHE_ZSTD_PARSE_WAVES), and with
     4-way or 2-way buckets at every page size (TYCHE_ZSTD_WAYS4_MAX; default: one wave with 4 ways
-    up to 16 KiB, two waves with 2 ways above), and one wave with 2 ways at every size: round
+    up to 16 KiB, four waves with 2 ways above), and one wave with 2 ways at every size: round
     trips over several distributions and sizes, multi-block and incompressible pages, tight
     capacities."""
     knobs(**ENCODE_MODES[mode])
