@@ -1280,6 +1280,10 @@ __device__ __forceinline__ void lct_encode(LaneBits &b, uint32_t &st, const uint
     st = ((const uint8_t *)(T + 64u))[(uint32_t)((int32_t)(st >> nbo) + (int32_t)(pk >> 19) - 128)];
 }
 
+#ifndef TYCHE_ZSTD_FSE_PF
+#define TYCHE_ZSTD_FSE_PF 8
+#endif
+constexpr uint32_t kFsePf = TYCHE_ZSTD_FSE_PF;   // sequence records in flight per lane (pass B)
 // ZSTD_compressSequences' bitstream (zstd_compress.c:695-735) for n >= 1
 // sequences; the same steps as emit_block's wave-uniform loop.  Returns its size.
 __device__ uint32_t fse_lane(uint8_t *out, const uint4 *R, uint32_t n, const uint32_t *T) {
@@ -1292,26 +1296,37 @@ __device__ uint32_t fse_lane(uint8_t *out, const uint4 *R, uint32_t n, const uin
     b.c = 0;
     b.pos = 0;
     uint32_t sll = 0, sml = 0, sof = 0;
-    uint4 nx = R[n - 1u];
-    for (uint32_t i = n; i-- > 0;) {
-        const uint4 r = nx;
-        if (i) nx = R[i - 1u];   // the next record is loaded a step ahead
-        const uint32_t llc = r.x & 0xFFu, mlc = (r.x >> 8) & 0xFFu, ofc = r.x >> 16;
-        const uint32_t llb = r.y >> 24, mlb = r.z >> 24;
-        if (i == n - 1u) {
-            sml = lct_init2(tml, mlc);
-            sof = lct_init2(tof, ofc);
-            sll = lct_init2(tll, llc);
-        } else {
-            lct_encode(b, sof, tof, ofc);
-            lct_encode(b, sml, tml, mlc);
-            lct_encode(b, sll, tll, llc);
-            if (ofc + mlb + llb >= 64u - 7u - (9u + 9u + 8u)) lb_flush(b, s);
+    // the records are loaded kFsePf steps ahead (a ring of registers, slot u of each pass of
+    // kFsePf steps): at one wave per two SIMDs (the LDS slots) a load one step ahead left
+    // every step waiting on HBM
+    uint4 q[kFsePf];
+#pragma unroll
+    for (uint32_t u = 0; u < kFsePf; u++) q[u] = u < n ? R[n - 1u - u] : make_uint4(0, 0, 0, 0);
+    for (uint32_t base = n; base > 0; base = base > kFsePf ? base - kFsePf : 0u) {
+#pragma unroll
+        for (uint32_t u = 0; u < kFsePf; u++) {
+            const bool live = base > u;
+            const uint32_t i = base - 1u - u;   // wraps when !live: every use below is gated
+            const uint4 r = q[u];
+            if (live && i >= kFsePf) q[u] = R[i - kFsePf];
+            if (!live) continue;
+            const uint32_t llc = r.x & 0xFFu, mlc = (r.x >> 8) & 0xFFu, ofc = r.x >> 16;
+            const uint32_t llb = r.y >> 24, mlb = r.z >> 24;
+            if (i == n - 1u) {
+                sml = lct_init2(tml, mlc);
+                sof = lct_init2(tof, ofc);
+                sll = lct_init2(tll, llc);
+            } else {
+                lct_encode(b, sof, tof, ofc);
+                lct_encode(b, sml, tml, mlc);
+                lct_encode(b, sll, tll, llc);
+                if (ofc + mlb + llb >= 64u - 7u - (9u + 9u + 8u)) lb_flush(b, s);
+            }
+            lb_add(b, r.y & 0xFFFFFFu, llb);
+            lb_add(b, r.z & 0xFFFFFFu, mlb);
+            lb_add(b, r.w, ofc);
+            lb_flush(b, s);
         }
-        lb_add(b, r.y & 0xFFFFFFu, llb);
-        lb_add(b, r.z & 0xFFFFFFu, mlb);
-        lb_add(b, r.w, ofc);
-        lb_flush(b, s);
     }
     lb_add(b, sml, tml[63]);
     lb_flush(b, s);
