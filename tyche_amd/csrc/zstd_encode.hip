@@ -1266,19 +1266,34 @@ __device__ __forceinline__ void lb_flush(LaneBits &b, ByteSink &s) {   // BIT_fl
     b.pos &= 7u;
     b.c = nbytes >= 8u ? 0ull : b.c >> (8u * nbytes);
 }
-// FSE_initCState2 / FSE_encodeSymbol over a packed table (kCtWords) in LDS
-__device__ __forceinline__ uint32_t lct_init2(const uint32_t *T, uint32_t sym) {
-    const uint32_t pk = T[sym], dnb = pk & 0x7FFFFu;
+// FSE_initCState2 / FSE_encodeSymbol over a packed table in LDS: S the symbol words, X the state bytes
+__device__ __forceinline__ uint32_t lct_init2(const uint32_t *S, const uint8_t *X, uint32_t sym) {
+    const uint32_t pk = S[sym], dnb = pk & 0x7FFFFu;
     const uint32_t nbo = (dnb + (1u << 15)) >> 16;
     const uint32_t v = (nbo << 16) - dnb;
-    return ((const uint8_t *)(T + 64u))[(uint32_t)((int32_t)(v >> nbo) + (int32_t)(pk >> 19) - 128)];
+    return X[(uint32_t)((int32_t)(v >> nbo) + (int32_t)(pk >> 19) - 128)];
 }
-__device__ __forceinline__ void lct_encode(LaneBits &b, uint32_t &st, const uint32_t *T, uint32_t sym) {
-    const uint32_t pk = T[sym];
+__device__ __forceinline__ void lct_encode(LaneBits &b, uint32_t &st, const uint32_t *S, const uint8_t *X, uint32_t sym) {
+    const uint32_t pk = S[sym];
     const uint32_t nbo = (st + (pk & 0x7FFFFu)) >> 16;
     lb_add(b, st, nbo);
-    st = ((const uint8_t *)(T + 64u))[(uint32_t)((int32_t)(st >> nbo) + (int32_t)(pk >> 19) - 128)];
+    st = X[(uint32_t)((int32_t)(st >> nbo) + (int32_t)(pk >> 19) - 128)];
 }
+
+// Pass B's LDS slot per lane.  TYCHE_ZSTD_FSE_SLOT 1 (default): only what the alphabets use --
+// 36 LL, 32 OF and 53 ML symbol words, each table's log after its words, then 128 / 64 / 128
+// state bytes (OF log <= 6): 816 bytes, 3 workgroups per CU instead of 2 at the full 1,152.
+#ifndef TYCHE_ZSTD_FSE_SLOT
+#define TYCHE_ZSTD_FSE_SLOT 1
+#endif
+struct FseSlot {
+    uint32_t sll, sof, sml, xll, xof, xml, lll, lof, lml, words;   // word offsets in the slot
+};
+constexpr FseSlot kFseSlot = TYCHE_ZSTD_FSE_SLOT ? FseSlot{0, 37, 70, 124, 156, 172, 36, 69, 123, 204}
+                                                 : FseSlot{0, kCtWords, 2 * kCtWords, 64, kCtWords + 64,
+                                                           2 * kCtWords + 64, 63, kCtWords + 63, 2 * kCtWords + 63,
+                                                           3 * kCtWords};
+static_assert(kFseSlot.words % 4u == 0, "slot of 16-byte pieces");
 
 #ifndef TYCHE_ZSTD_FSE_PF
 #define TYCHE_ZSTD_FSE_PF 8
@@ -1287,7 +1302,9 @@ constexpr uint32_t kFsePf = TYCHE_ZSTD_FSE_PF;   // sequence records in flight p
 // ZSTD_compressSequences' bitstream (zstd_compress.c:695-735) for n >= 1
 // sequences; the same steps as emit_block's wave-uniform loop.  Returns its size.
 __device__ uint32_t fse_lane(uint8_t *out, const uint4 *R, uint32_t n, const uint32_t *T) {
-    const uint32_t *tll = T, *tof = T + kCtWords, *tml = T + 2u * kCtWords;
+    const uint32_t *tll = T + kFseSlot.sll, *tof = T + kFseSlot.sof, *tml = T + kFseSlot.sml;
+    const uint8_t *xll = (const uint8_t *)(T + kFseSlot.xll), *xof = (const uint8_t *)(T + kFseSlot.xof),
+                  *xml = (const uint8_t *)(T + kFseSlot.xml);
     ByteSink s;
     s.addr = (uintptr_t)out;
     s.w = 0;
@@ -1313,13 +1330,13 @@ __device__ uint32_t fse_lane(uint8_t *out, const uint4 *R, uint32_t n, const uin
             const uint32_t llc = r.x & 0xFFu, mlc = (r.x >> 8) & 0xFFu, ofc = r.x >> 16;
             const uint32_t llb = r.y >> 24, mlb = r.z >> 24;
             if (i == n - 1u) {
-                sml = lct_init2(tml, mlc);
-                sof = lct_init2(tof, ofc);
-                sll = lct_init2(tll, llc);
+                sml = lct_init2(tml, xml, mlc);
+                sof = lct_init2(tof, xof, ofc);
+                sll = lct_init2(tll, xll, llc);
             } else {
-                lct_encode(b, sof, tof, ofc);
-                lct_encode(b, sml, tml, mlc);
-                lct_encode(b, sll, tll, llc);
+                lct_encode(b, sof, tof, xof, ofc);
+                lct_encode(b, sml, tml, xml, mlc);
+                lct_encode(b, sll, tll, xll, llc);
                 if (ofc + mlb + llb >= 64u - 7u - (9u + 9u + 8u)) lb_flush(b, s);
             }
             lb_add(b, r.y & 0xFFFFFFu, llb);
@@ -1328,11 +1345,11 @@ __device__ uint32_t fse_lane(uint8_t *out, const uint4 *R, uint32_t n, const uin
             lb_flush(b, s);
         }
     }
-    lb_add(b, sml, tml[63]);
+    lb_add(b, sml, T[kFseSlot.lml]);
     lb_flush(b, s);
-    lb_add(b, sof, tof[63]);
+    lb_add(b, sof, T[kFseSlot.lof]);
     lb_flush(b, s);
-    lb_add(b, sll, tll[63]);
+    lb_add(b, sll, T[kFseSlot.lll]);
     lb_flush(b, s);
     lb_add(b, 1u, 1u);
     lb_flush(b, s);
@@ -1341,7 +1358,7 @@ __device__ uint32_t fse_lane(uint8_t *out, const uint4 *R, uint32_t n, const uin
     return (uint32_t)(s.addr - (uintptr_t)out);
 }
 
-// Each lane copies its block's three tables (960 bytes) into its own LDS slot.
+// Each lane copies its block's three tables into its own LDS slot (kFseSlot).
 __global__ __launch_bounds__(64) void zstd_fse_kernel(tyche_batch_t b, size_t first, size_t count, uint8_t *ws,
                                                       size_t ws_page, const int32_t *st) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -1350,13 +1367,24 @@ __global__ __launch_bounds__(64) void zstd_fse_kernel(tyche_batch_t b, size_t fi
     uint8_t *area = ws + j * ws_page;
     const uint32_t nblk = ((const uint32_t *)area)[0];
     uint8_t *dst = batch_page(b, first + j).dst;
-    uint32_t *lt = (uint32_t *)smem + threadIdx.x * (3u * kCtWords);
+    uint32_t *lt = (uint32_t *)smem + threadIdx.x * kFseSlot.words;
     for (uint32_t k = 0; k < nblk; k++) {
         uint32_t *B = area_blk(area, k);
         if (!(B[7] & 2u)) continue;
-        const u32x4 *g = (const u32x4 *)area_tab(area, B[6]);
-#pragma unroll 4
-        for (uint32_t w = 0; w < 3u * kCtWords / 4u; w++) ((u32x4 *)lt)[w] = g[w];
+        const uint32_t *g = area_tab(area, B[6]);
+        if (TYCHE_ZSTD_FSE_SLOT) {
+            for (uint32_t w = 0; w < 36u; w++) lt[kFseSlot.sll + w] = g[w];
+            for (uint32_t w = 0; w < 32u; w++) lt[kFseSlot.sof + w] = g[kCtWords + w];
+            for (uint32_t w = 0; w < 53u; w++) lt[kFseSlot.sml + w] = g[2u * kCtWords + w];
+            lt[kFseSlot.lll] = g[63];
+            lt[kFseSlot.lof] = g[kCtWords + 63u];
+            lt[kFseSlot.lml] = g[2u * kCtWords + 63u];
+            for (uint32_t w = 0; w < 32u; w++) lt[kFseSlot.xll + w] = g[64u + w];
+            for (uint32_t w = 0; w < 16u; w++) lt[kFseSlot.xof + w] = g[kCtWords + 64u + w];
+            for (uint32_t w = 0; w < 32u; w++) lt[kFseSlot.xml + w] = g[2u * kCtWords + 64u + w];
+        } else {
+            for (uint32_t w = 0; w < 3u * kCtWords / 4u; w++) ((u32x4 *)lt)[w] = ((const u32x4 *)g)[w];
+        }
         B[3] = fse_lane(dst + B[0] + 3u + B[2], area_rec(area) + B[5], B[4], lt);
     }
 }
@@ -1536,8 +1564,8 @@ hipError_t launch_zstd_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream
             hipLaunchKernelGGL(zstd_block_kernel, dim3((unsigned)g), dim3(kWave), kA2Lds, s, b, first, n, in_cap, ws,
                                page_bytes, st, ctr.get(), logcap);
         }
-        hipLaunchKernelGGL(zstd_fse_kernel, dim3((unsigned)((n + kWave - 1) / kWave)), dim3(kWave), kWave * kTabBytes, s,
-                           b, first, n, ws, page_bytes, (const int32_t *)st);
+        hipLaunchKernelGGL(zstd_fse_kernel, dim3((unsigned)((n + kWave - 1) / kWave)), dim3(kWave),
+                           kWave * kFseSlot.words * 4u, s, b, first, n, ws, page_bytes, (const int32_t *)st);
         {
             const size_t g = std::min<size_t>(n, ncu * 8u);
             WorkCounter ctr(s, g < n);
