@@ -424,12 +424,9 @@ __device__ SmallCT build_small_ct(int32_t norm_l, uint32_t max_sv, uint32_t log,
     // low-probability cells from the top, then the spread (uniform serial walk);
     // lane u ends up with tableSymbol[u] (tsym) and tableSymbol[64 + u] (tsym_hi)
     uint32_t tsym = 0, tsym_hi = 0, pos = 0, high = size - 1u;
-    auto put = [&](uint32_t cell, uint32_t s) {
-        if (cell < 64u) {
-            if (lane == cell) tsym = s;
-        } else if (lane == cell - 64u) {
-            tsym_hi = s;
-        }
+    auto put = [&](uint32_t cell, uint32_t s) {   // selects, not stores: keeps tsym / tsym_hi in VGPRs
+        tsym = lane == cell ? s : tsym;
+        tsym_hi = lane + 64u == cell ? s : tsym_hi;
     };
     for (uint32_t s = 0; s <= max_sv; s++)
         if ((int32_t)rdlane((uint32_t)norm_l, s) == -1) {
