@@ -378,6 +378,35 @@ def test_decode_lane_kernels_all_rings(tc, oracle_mod, knobs, lb, ring):
             assert outs[i][:r] == want[:r], i
 
 
+@pytest.mark.parametrize("ring,far", [(1024, 8), (1024, 6), (512, 8), (512, 6), (2048, 8)])
+def test_decode_quad_kernel_variants(tc, oracle_mod, knobs, ring, far):
+    """The quad-per-page chunked decoder (lz4_decode_quad.hip) at every ring / far-entry size,
+    forced on every batch size (LZ4_QUAD=1, LZ4_LANE_MIN=0): the fixtures with their exact return
+    values, seeded corruptions against the restated LZ4_decompress_safe, and pages built for its
+    slow path (incompressible, long literal runs, long and self-overlapping matches)."""
+    knobs(LZ4_QUAD=1, LZ4_QUAD_RING=ring, LZ4_QUAD_FAR=far, LZ4_LANE_MIN=0)
+    test_decode_lane_path_fixtures(tc, 1)
+    rng = np.random.default_rng(2000 + ring + far)
+    pages = oracle_mod.pagegen(256, 16384, seed=11, first=ring + far, dist=0)
+    streams, caps = [], []
+    for i in range(256):
+        c = bytearray(oracle_mod.lz4_compress(pages[i].tobytes()))
+        if i % 4 == 1:
+            c[int(rng.integers(0, len(c)))] ^= 1 << int(rng.integers(0, 8))
+        elif i % 4 == 2:
+            c = c[: int(rng.integers(1, len(c)))]
+        streams.append(bytes(c))
+        caps.append(16384 if i % 4 != 3 else int(rng.integers(100, 16384)))
+    rv, outs = ragged_decode(tc, streams, caps)
+    for i in range(256):
+        r, want = oracle_mod.lz4_decompress(streams[i], caps[i])
+        assert rv[i] == r, (i, rv[i], r)
+        if r > 0 and i % 4 in (0, 3):
+            assert outs[i][:r] == want[:r], i
+    for plen in (8192, 16384, 32768):
+        test_decode_jump_path_page_kinds(tc, oracle_mod, plen, 300)
+
+
 @pytest.mark.parametrize("dist", [0, 1, 2, 3, 4, 5])
 def test_decode_lane_path_roundtrip(tc, dist):
     """64K x 4 KiB pages of every pagegen distribution through the lane-per-page decoder."""
@@ -421,9 +450,9 @@ def test_decode_lane_path_corruptions(tc, oracle_mod, n):
 
 @pytest.mark.parametrize("plen", [8192, 32768, 65535])
 def test_decode_lane_path_page_sizes(tc, oracle_mod, plen):
-    """32K-page batches (the lane decoder's threshold) of 8 KiB, 32 KiB and 65,535-byte
-    pages: round trip on the GPU, and a sample of the streams decodes identically with the
-    oracle restatement."""
+    """32K-page batches (the lane decoder's threshold) of 8 KiB (C4's page size), 32 KiB and
+    65,535-byte pages: round trip on the GPU, and every page's device stream decodes identically
+    with the oracle restatement (oracle_lz4_decompress_pages)."""
     n = 32768
     gen = (plen + 4095) // 4096 * 4096          # pagegen sizes; 65,535 = the byU16 limit, cut from 64 KiB
     pages = tc.pagegen(n, gen, seed=31, first=plen, dist=0, device=DEV)[:, :plen].contiguous()
@@ -431,10 +460,13 @@ def test_decode_lane_path_page_sizes(tc, oracle_mod, plen):
     out, rv = tc.decompress_pages(comp, clen, plen)
     torch.cuda.synchronize()
     assert bool((rv == plen).all()) and torch.equal(out, pages)
-    ch, lh, host = comp[:64].cpu().numpy(), clen[:64].cpu().numpy(), pages[:64].cpu().numpy()
-    for i in range(64):
-        r, dec = oracle_mod.lz4_decompress(ch[i, :lh[i]].tobytes(), plen)
-        assert r == plen and dec == host[i].tobytes(), i
+    # every page's device stream through the C oracle (LZ4_decompress_safe restated) back to the page
+    ch, lh, host = comp.cpu().numpy(), clen.cpu().numpy().astype(np.int32), pages.cpu().numpy()
+    dec = np.zeros_like(host)
+    orv = np.zeros(n, np.int32)
+    oracle_mod.lz4_decompress_pages(ch, lh, dec, orv, 0, n)
+    assert bool((orv == plen).all()), np.nonzero(orv != plen)[0][:10]
+    assert np.array_equal(dec, host)
 
 
 @pytest.mark.parametrize("plen", [8192, 16384, 32768])

@@ -20,6 +20,7 @@ incompressible pages; the encoder is deterministic.
 """
 import ctypes
 import hashlib
+import os
 import zlib
 
 import numpy as np
@@ -38,6 +39,7 @@ def _split_for_every_batch(knobs):
     knobs(ZSTD_SPLIT_MIN=1)
 
 DEV = torch.device("cuda:0")
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ZSTD = 3
 
 
@@ -613,6 +615,57 @@ def test_zstd_many_block_pages(tc, knobs, mode):
         else:
             assert rv[i] == len(want[i]), (i, rv[i])
             assert outs[i] == want[i], i
+
+
+_FRESH_SEQEXEC_CHILD = r'''
+import os, sys, numpy as np, torch
+sys.path.insert(0, os.environ["TYCHE_ROOT"])
+from tyche_amd import codec
+d = np.load(sys.argv[1], allow_pickle=False)
+frames, flen, plen = d["frames"], d["flen"], int(d["plen"])
+comp = torch.from_numpy(frames).cuda()
+clen = torch.from_numpy(flen).cuda()
+out, rv = codec.decompress_pages(comp, clen, plen, compressor_id=3, max_comp_len=int(frames.shape[1]))
+torch.cuda.synchronize()
+np.save(sys.argv[2], np.concatenate([rv.cpu().numpy().astype(np.int64)[:, None],
+                                     out.cpu().numpy().astype(np.int64)], axis=1))
+'''
+
+
+def test_zstd_seqexec_first_call_fresh_process(tc, tmp_path):
+    """A fresh process whose FIRST zstd decode is a large split batch on the lane-per-page second pass
+    (TYCHE_ZSTD_EXEC_LANE_MIN=0) at 32 KiB pages, some of them raw-block frames of more than 64 blocks:
+    those are left to the one-wave kernel after pass 2 at ~70 KiB of dynamic LDS, whose limit the
+    split path raises itself (no earlier fused launch in the process did it)."""
+    import subprocess
+    import sys
+    n, plen = 256, 32768
+    pages = tc.pagegen(n, plen, seed=5, dist=0, device=DEV)
+    comp, clen = tc.compress_pages(pages, compressor_id=ZSTD)
+    torch.cuda.synchronize()
+    host = pages.cpu().numpy()
+    ch, lh = comp.cpu().numpy(), clen.cpu().numpy()
+    frames, want = [], []
+    for i in range(n):
+        if i % 5 == 0:
+            f, dd = _raw_block_frame(host[i].tobytes(), 100 if i % 10 == 0 else 70)
+        else:
+            f, dd = ch[i, :lh[i]].tobytes(), host[i].tobytes()
+        frames.append(f)
+        want.append(dd)
+    width = max(len(f) for f in frames) + 16
+    buf = np.zeros((n, width), np.uint8)
+    for i, f in enumerate(frames):
+        buf[i, :len(f)] = np.frombuffer(f, np.uint8)
+    np.savez(tmp_path / "in.npz", frames=buf, flen=np.array([len(f) for f in frames], np.int32), plen=plen)
+    env = dict(os.environ, TYCHE_ZSTD_EXEC_LANE_MIN="0", TYCHE_ZSTD_SPLIT_MIN="1", TYCHE_ROOT=ROOT)
+    r = subprocess.run([sys.executable, "-c", _FRESH_SEQEXEC_CHILD, str(tmp_path / "in.npz"), str(tmp_path / "out.npy")],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    res = np.load(tmp_path / "out.npy")
+    for i in range(n):
+        assert res[i, 0] == plen, (i, res[i, 0])
+        assert res[i, 1:].astype(np.uint8).tobytes() == want[i], i
 
 
 ENCODE_MODES = {

@@ -14,7 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 BUILD = os.path.join(HERE, "..", "build", "tyche_amd")
 LIB = os.path.join(HERE, "libtyche_codec.so")
-SOURCES = ["engine.hip", "lz4_decode.hip", "lz4_decode_lane.hip", "lz4_encode.hip", "zlib_inflate.hip", "zstd_decode.hip", "zstd_encode.hip", "zlib_deflate.hip", "pagegen.hip",
+SOURCES = ["engine.hip", "lz4_decode.hip", "lz4_decode_lane.hip", "lz4_decode_quad.hip", "lz4_encode.hip", "zlib_inflate.hip", "zstd_decode.hip", "zstd_encode.hip", "zlib_deflate.hip", "pagegen.hip",
            "errno_guard.hip"]   # errno_guard last: its constructor runs after the code-object registrations
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"

@@ -29,7 +29,9 @@ __device__ __forceinline__ u128 ld16(const uint8_t *p) {
 }
 // Cache-policy experiments (-DTYCHE_ABLATE, tools/time_decode.py over
 // libtyche_codec_ablN.so; LZ4 lane decoder only): 16 = non-temporal stream loads,
-// 32 = non-temporal line flushes, 128 = no line flushes, 256 = parse only.
+// 32 = non-temporal line flushes, 128 = no line flushes, 256 = parse only,
+// 512 = ring LDS accesses forced to 16-byte alignment (wrong output, the parse is untouched: prices
+// the per-lane replays of byte-unaligned ds_read/ds_write_b128).
 #ifndef TYCHE_ABLATE
 #define TYCHE_ABLATE 0
 #endif
@@ -71,11 +73,15 @@ __device__ __forceinline__ void lds16(uint8_t *p, u128 v) {
 // 16 bytes of the ring at page position x (valid for any x: the 16 bytes past
 // the ring's end mirror its first 16)
 template <int32_t kRing>
-__device__ __forceinline__ u128 ring_rd(uint8_t *rb, int32_t x) { return lds16(rb + ((int32_t)((uint32_t)x % (uint32_t)kRing))); }
+__device__ __forceinline__ u128 ring_rd(uint8_t *rb, int32_t x) {
+    if (TYCHE_ABLATE & 512) return lds16(rb + ((int32_t)((uint32_t)x % (uint32_t)kRing) & ~15));   // timing only: aligned
+    return lds16(rb + ((int32_t)((uint32_t)x % (uint32_t)kRing)));
+}
 template <int32_t kRing>
 __device__ __forceinline__ void ring_wr(uint8_t *rb, int32_t x, u128 v) {
     if (TYCHE_ABLATE & 256) return;
-    const int32_t q = (int32_t)((uint32_t)x % (uint32_t)kRing);
+    int32_t q = (int32_t)((uint32_t)x % (uint32_t)kRing);
+    if (TYCHE_ABLATE & 512) q &= ~15;   // timing only: 16-byte aligned LDS stores (wrong output)
     lds16(rb + q, v);
     if (q + 16 > kRing) lds16(rb + q - kRing, v);   // wrapped part, to the ring's start
     if (q < 16) lds16(rb + q + kRing, v);           // mirror of the start, past the end

@@ -2538,6 +2538,10 @@ hipError_t launch_zstd_decode(const tyche_batch_t &b, uint32_t in_cap, uint32_t 
     uint8_t *ent = (uint8_t *)ws.get() + st_bytes;
     const size_t ncu = prepare_launch((const void *)zstd_entropy_kernel);
     (void)prepare_launch(lane_exec ? kx : (const void *)zstd_exec_kernel);
+    // the leftovers launch of the one-wave kernel below runs at lf.total bytes of dynamic LDS
+    // (~70 KiB at 32 KiB pages, above the 64 KiB default): its limit must be raised here too, and
+    // before cuf is sized, whether or not launch_fused ran earlier in this process
+    if (seqexec) (void)prepare_launch((const void *)zstd_decode_kernel);
     const size_t cu1 = waves_per_cu((const void *)zstd_entropy_kernel, l1.total);
     const size_t cu2 = lane_exec ? waves_per_cu(kx, lds_lane) : waves_per_cu((const void *)zstd_exec_kernel, lds2);
     const size_t cuf = seqexec ? waves_per_cu((const void *)zstd_decode_kernel, lf.total) : 0;
