@@ -153,6 +153,7 @@ def measure_codec(cid: int, name: str, n: int, plen: int, steps: int, warmup: in
            "algorithmic_bytes_per_launch": algo, "ratio": round(nbytes / cbytes, 4)}
     tr = {k: pmc_traffic(k, n, plen) for k in res["kernel_ms"]}
     res["traffic"] = {k: (v["bytes"] if v else None) for k, v in tr.items()}
+    res["traffic_source"] = {k: ((v.get("source") or ("stale: " + v["stale"])) if v else None) for k, v in tr.items()}
     return res, pages
 
 
@@ -245,14 +246,21 @@ def pcie_probe(dev, nbytes: int, reps: int = 5) -> dict:
 
 def pmc_traffic(kernel: str, pages: int, page_len: int):
     """HBM bytes per launch for `kernel` from the newest committed PMC summary
-    (profiles/rNN_traffic.json, made by tools/pmc_traffic.py from separate
-    FETCH_SIZE / WRITE_SIZE rocprofv3 passes of the same kernels), scaled from
-    bytes per page to this launch's page count; None when no summary matches."""
+    (profiles/rNN_traffic*.json, made by tools/pmc_traffic.py from separate FETCH_SIZE /
+    WRITE_SIZE rocprofv3 passes of the same kernels), scaled from bytes per page to this
+    launch's page count.  A summary counts only if it was taken on the kernel sources this
+    process runs (its kernel_sources_sha16 equals _build.kernel_sources_digest()); otherwise
+    the result is None bytes with the stale file named, never a number from other code."""
+    from tyche_amd._build import kernel_sources_digest
+    cur = kernel_sources_digest()
     files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r*_traffic*.json")))
     for f in reversed(files):
         t = json.load(open(f))
         if t.get("page_len") == page_len and kernel in t.get("bytes_per_page", {}):
-            return {"bytes": int(t["bytes_per_page"][kernel] * pages), "source": os.path.basename(f)}
+            if t.get("kernel_sources_sha16") != cur:
+                return {"bytes": None, "source": None, "stale": os.path.basename(f)}
+            return {"bytes": int(t["bytes_per_page"][kernel] * pages), "source": os.path.basename(f),
+                    "commit": t.get("commit")}
     return None
 
 
@@ -306,6 +314,7 @@ def run_c4(args, info, dev):
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic["bytes"] if traffic else None,
                      "traffic_source": traffic["source"] if traffic else None,
+                     "traffic_stale": traffic.get("stale") if traffic else None,
                      "algorithmic_bytes_per_launch": algo},
         "kernel_ms": {"lz4_decode": round(d_ms, 4)}, "ratio": round(n * plen / comp_bytes, 4),
     }
@@ -401,6 +410,8 @@ def main():
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic["bytes"] if traffic else None,
                      "traffic_source": traffic["source"] if traffic else None,
+                     "traffic_commit": traffic.get("commit") if traffic else None,
+                     "traffic_stale": traffic.get("stale") if traffic else None,
                      "algorithmic_bytes_per_launch": algo_bytes},
         "compress_gib_s": round(page_bytes / (c_ms * 1e-3) / GIB, 3),
         "decompress_gib_s": round(page_bytes / (d_ms * 1e-3) / GIB, 3),

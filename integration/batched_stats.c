@@ -1,0 +1,19 @@
+/* batched_stats.c -- linked into _app/tyche_batched only (TEST INFRASTRUCTURE):
+ * at exit, prints the engine's restore-queue counters (launches and buffers
+ * served, tyche_restore_queue_stats) and the sweep batches (tyche_buffers_compress
+ * calls and buffers) so the C1 batched test can see that the reference's own
+ * callers drove batched GPU work. */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+void tyche_restore_queue_stats(uint64_t *batches, uint64_t *buffers);
+
+static void report(void) {
+    uint64_t batches = 0, buffers = 0;
+    tyche_restore_queue_stats(&batches, &buffers);
+    fprintf(stderr, "tyche-restore-queue: batches %llu buffers %llu\n", (unsigned long long)batches,
+            (unsigned long long)buffers);
+}
+
+__attribute__((constructor)) static void register_report(void) { atexit(report); }

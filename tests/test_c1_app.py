@@ -33,6 +33,7 @@ from conftest import ROOT, load_golden
 APP = os.path.join(ROOT, "integration", "_app", "tyche")
 APP_Q = os.path.join(ROOT, "integration", "_app", "tyche_q")
 APP_FIXED = os.path.join(ROOT, "integration", "_app", "tyche_fixed")
+APP_BATCHED = os.path.join(ROOT, "integration", "_app", "tyche_batched")
 LIB_DIR = os.path.join(ROOT, "tyche_amd")
 
 
@@ -103,7 +104,7 @@ ENGINE_CALLS = ("buffer__compress", "buffer__decompress", "tyche_buffers_compres
                 "tyche_buffer_restore")
 
 
-def _bench_attempt(app, codec, sample_dir, extra_env=None, extra_args=()):
+def _bench_attempt(app, codec, sample_dir, extra_env=None, extra_args=(), workers=1):
     """One short benchmark run of the reference app; returns a record of what it did.  Raises on
     anything the engine could be blamed for: a fatal signal, an engine error line (TYCHE_LOG_ERRORS),
     an app ERROR line, an unexpected exit status, or a watchdog dump with a thread inside an engine
@@ -116,7 +117,7 @@ def _bench_attempt(app, codec, sample_dir, extra_env=None, extra_args=()):
         list__search (list.c:509-522); the app's status line (manager.c:193) still shows its counters."""
     env = dict(os.environ, TYCHE_APP_WATCHDOG="15", TYCHE_LOG_ERRORS="1")
     env.update(extra_env or {})
-    p = subprocess.run([app, "-c", codec, "-p", str(sample_dir / "16k"), "-w", "1", "-d", "3", "-m", "512000",
+    p = subprocess.run([app, "-c", codec, "-p", str(sample_dir / "16k"), "-w", str(workers), "-d", "3", "-m", "512000",
                         "-f", "20", *extra_args], stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=90, env=env)
     out, err = p.stdout.decode(errors="replace"), p.stderr.decode(errors="replace")
     rec = {"codec": codec, "app": os.path.basename(app), "rc": p.returncode, "out": out[-3000:], "err": err[-6000:]}
@@ -133,6 +134,9 @@ def _bench_attempt(app, codec, sample_dir, extra_env=None, extra_args=()):
         scale = {"": 1, "K": 1e3, "M": 1e6, "B": 1e9}
         rec["comps"] = float(status[-1][0].replace(",", "")) * scale.get(status[-1][1], 1) if status else 0
         rec["rests"] = float(status[-1][2].replace(",", "")) * scale.get(status[-1][3], 1) if status else 0
+    q = re.search(r"tyche-restore-queue: batches (\d+) buffers (\d+)", err)
+    if q:
+        rec["queue_batches"], rec["queue_buffers"] = int(q.group(1)), int(q.group(2))
     rec["kind"] = "clean"
     if p.returncode == 3:
         dump = err[err.find("--- thread"):]
@@ -175,6 +179,32 @@ def test_reference_app_benchmark_run(sample_dir, codec):
     summary = [(a["rc"], a["kind"], a["comps"], a["rests"]) for a in attempts]
     print(f"{codec}: attempts (rc, kind, compressions, restorations): {summary}")
     assert attempts[-1]["comps"] > 0 and attempts[-1]["rests"] > 0, summary
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("codec", ["lz4", "zlib", "zstd"])
+def test_reference_app_batched_run(sample_dir, codec):
+    """The reference app with INTEGRATION.md's batch integration applied to its own list.c
+    (integration/patch_batched.py -> _app/tyche_batched): the compressor pool hands each grabbed
+    set of victims to one tyche_buffers_compress call (list.c:1047-1063) and list__search's
+    restore goes through the engine's restore queue (list.c:572, started at list.c:169).  With 16
+    workers hitting compressed pages at once, pages are compressed and restored, and the queue
+    served its restores in fewer GPU launches than buffers (batches < buffers).  Every run is
+    checked as in the unbatched benchmark test (crash, engine error, app error, classified hangs)."""
+    _need(APP_BATCHED)
+    attempts = []
+    for _ in range(3):
+        rec = _bench_attempt(APP_BATCHED, codec, sample_dir, workers=16)
+        attempts.append(rec)
+        if rec["rests"] > 0 and rec.get("queue_buffers", 0) > rec.get("queue_batches", 0) > 0:
+            break
+    summary = [(a["rc"], a["kind"], a["comps"], a["rests"], a.get("queue_batches"), a.get("queue_buffers"))
+               for a in attempts]
+    print(f"{codec} batched: attempts (rc, kind, compressions, restorations, queue batches, queue buffers): {summary}")
+    last = attempts[-1]
+    assert last["comps"] > 0 and last["rests"] > 0, summary
+    assert last.get("queue_buffers", 0) > 0, summary
+    assert last["queue_batches"] < last["queue_buffers"], summary
 
 
 @pytest.mark.gpu

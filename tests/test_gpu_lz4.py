@@ -378,6 +378,38 @@ def test_decode_lane_kernels_all_rings(tc, oracle_mod, knobs, lb, ring):
             assert outs[i][:r] == want[:r], i
 
 
+@pytest.mark.parametrize("ring", [256, 512])
+def test_decode_lc_kernel_variants(tc, oracle_mod, knobs, ring):
+    """The chunked lane-per-page decoder (lz4_decode_lc.hip) at both ring sizes, forced on every
+    batch size (LZ4_LC=1, LZ4_LANE_MIN=0): the fixtures with their exact return values, seeded
+    corruptions against the restated LZ4_decompress_safe, and the page kinds that exercise its
+    split records (incompressible pages: literal runs longer than a window; zero and short-period
+    pages: long self-overlapping matches; deep match chains)."""
+    knobs(LZ4_LC=1, LZ4_LC_RING=ring, LZ4_LANE_MIN=0)
+    test_decode_lane_path_fixtures(tc, 1)
+    rng = np.random.default_rng(3000 + ring)
+    pages = oracle_mod.pagegen(256, 16384, seed=13, first=ring, dist=0)
+    streams, caps = [], []
+    for i in range(256):
+        c = bytearray(oracle_mod.lz4_compress(pages[i].tobytes()))
+        if i % 4 == 1:
+            c[int(rng.integers(0, len(c)))] ^= 1 << int(rng.integers(0, 8))
+        elif i % 4 == 2:
+            c = c[: int(rng.integers(1, len(c)))]
+        streams.append(bytes(c))
+        caps.append(16384 if i % 4 != 3 else int(rng.integers(100, 16384)))
+    rv, outs = ragged_decode(tc, streams, caps)
+    for i in range(256):
+        r, want = oracle_mod.lz4_decompress(streams[i], caps[i])
+        assert rv[i] == r, (i, rv[i], r)
+        if r > 0 and i % 4 in (0, 3):
+            assert outs[i][:r] == want[:r], i
+    for plen in (8192, 16384, 32768):
+        test_decode_jump_path_page_kinds(tc, oracle_mod, plen, 300)
+    test_decode_token_list_near_output(tc, oracle_mod, 6000, 16384, True)
+    test_decode_token_list_near_output(tc, oracle_mod, 20000, 65535, True)
+
+
 @pytest.mark.parametrize("ring,far", [(1024, 8), (1024, 6), (512, 8), (512, 6), (2048, 8)])
 def test_decode_quad_kernel_variants(tc, oracle_mod, knobs, ring, far):
     """The quad-per-page chunked decoder (lz4_decode_quad.hip) at every ring / far-entry size,

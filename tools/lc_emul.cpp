@@ -1,0 +1,161 @@
+// tools/lc_emul.cpp -- host emulator of the chunked lane-per-page LZ4 decoder
+// (tyche_amd/csrc/lz4_decode_lc.hip) for one page at a time: the kernel's own
+// per-lane code (lz4_lc_core.h: record parse, record copies, ring and window
+// handling) driven by the same chunk loop as the kernel, with the cooperative
+// line flush replaced by plain copies of the same lines.  TEST INFRASTRUCTURE:
+// tests/test_lc_emul.py runs it against the oracle on the fixtures and seeded
+// corruptions, on the CPU, so the algorithm is checked before (and apart from)
+// the GPU parity tests.
+//
+//   g++ -O2 -shared -fPIC -o tools/bin/liblcemul.so tools/lc_emul.cpp
+//   int lc_emul_decode(const uint8_t *in, int L, uint8_t *out, int C, int R);
+#include <algorithm>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+
+typedef unsigned __int128 u128;
+using std::min;
+
+#define BF_FN static inline
+#define BF_ALIGNBYTE(a, b, c) ((uint32_t)(((((uint64_t)(a)) << 32) | (uint64_t)(b)) >> (8u * ((c) & 3u))))
+#define LC_FN static inline
+#define LC_RCP(x) (1.0f / (x))
+#define LC_BARRIER() \
+    do {             \
+    } while (0)
+
+constexpr int32_t kMinMatch = 4, kLastLiterals = 5, kMfLimit = 12, kRunMask = 15;
+
+static inline uint64_t lq(const uint8_t *p) {
+    uint64_t v;
+    memcpy(&v, p, 8);
+    return v;
+}
+static inline void lq(uint8_t *p, uint64_t v) { memcpy(p, &v, 8); }
+static inline uint32_t lb(const uint8_t *p) { return *p; }
+static inline uint32_t ld1(const uint8_t *p) { return *p; }
+static inline u128 ld16(const uint8_t *p) {
+    u128 v;
+    memcpy(&v, p, 16);
+    return v;
+}
+static inline uint32_t sbyte(const uint8_t *in, int32_t p, int32_t L) { return p >= 0 && p < L ? in[p] : 0u; }
+static inline u128 chunk16z(const uint8_t *in, int32_t a, int32_t L) {
+    u128 v = 0;
+    for (int32_t k = 15; k >= 0; k--) v = (v << 8) | sbyte(in, a + k, L);
+    return v;
+}
+
+#include "../tyche_amd/csrc/byte_funnel.h"
+#include "../tyche_amd/csrc/lz4_lc_core.h"
+
+long g_stat[8];
+extern "C" long *lc_emul_stats() { return g_stat; }
+static void fetch_far(const LPage &P, int32_t src, u128 *f) {
+    if (src < 0 || src + 32 > P.fl) {
+        fprintf(stderr, "lc_emul: far source [%d, %d) not flushed (fl %d)\n", src, src + 32, P.fl);
+        abort();
+    }
+    f[0] = ld16(P.out + src);
+    f[1] = ld16(P.out + src + 16);
+}
+
+template <int32_t R>
+static int lc_decode(const uint8_t *in, int32_t L, uint8_t *out, int32_t C) {
+    if (C == 0) return (L == 1 && in[0] == 0) ? 0 : -1;
+    if (L <= 0) return -1;
+    alignas(16) uint8_t ring[R + 16];
+    alignas(16) uint8_t win[kLWS + 64];   // reads run up to 24 bytes past the window's slack
+    uint8_t *w16 = win + 16;
+    memset(ring, 0xA5, sizeof(ring));
+    memset(win, 0x5A, sizeof(win));
+    LPage P;
+    memset(&P, 0, sizeof(P));
+    P.in = in;
+    P.out = out;
+    P.L = L;
+    P.C = C;
+    for (int32_t k = 0; k < kLW; k += 16) {
+        const u128 v = chunk16z(in, k, L);
+        memcpy(w16 + k, &v, 16);
+    }
+    for (long chunk = 0; chunk < 100000000; chunk++) {
+        const int32_t op0 = P.op;
+        int32_t st = kLParse, rv = 0, nrec = 0;
+        uint32_t rec[kLC + 1];
+        u128 farv[2 * kLC + 2];
+        bool go = true, gen = false;
+        int32_t need_gen = 0;
+        for (int32_t t = 0; t < kLC; t++) {
+            rec[t] = 0;
+            farv[2 * t] = farv[2 * t + 1] = 0;
+            if (go) {
+                bool far = false;
+                int32_t src = 0;
+                const int32_t k = getenv("LC_SLOW") ? 2 : parse_fast<R>(P, w16, op0, rec[t], far, src);
+                if (k == 1) {
+                    nrec = t + 1;
+                    if (far) fetch_far(P, src, farv + 2 * t);
+                } else {
+                    go = false;
+                    need_gen = (k == 2 || t == 0) ? 1 : 0;
+                    if (k == 0 && t != 0) st = kLCut;
+                }
+            }
+        }
+        rec[kLC] = 0;
+        farv[2 * kLC] = farv[2 * kLC + 1] = 0;
+        if (need_gen) {
+            bool far = false;
+            int32_t src = 0;
+            if (parse_slot<R>(P, w16, op0, nrec == 0, st, rv, rec[kLC], far, src)) {
+                gen = true;
+                if (far) fetch_far(P, src, farv + 2 * kLC);
+            }
+        }
+        const bool ended = st == kLEnd;
+        const int32_t nwb = (P.lrem > 0 ? P.lp : P.ip) & ~15;
+        if (ended && rv < 0) {
+            nrec = 0;
+            gen = false;
+        }
+        if (getenv("LC_TRACE")) {
+            const int32_t lo = atoi(getenv("LC_TRACE"));
+            int32_t d = op0;
+            for (int32_t t = 0; t <= kLC; t++) {
+                if (!(t < kLC ? t < nrec : gen)) continue;
+                const uint32_t r = rec[t];
+                const int32_t lpr = (int32_t)(r & 63u), n1 = (int32_t)((r >> 6) & 15u), n2 = (int32_t)((r >> 10) & 63u),
+                              off = (int32_t)(r >> 16);
+                if (d + n1 + n2 >= lo && d <= lo + 64)
+                    fprintf(stderr, "chunk %ld t %d d %d wb %d lpr %d n1 %d n2 %d off %d far %d\n", chunk, t, d, P.wb, lpr,
+                            n1, n2, off, off > R - 32);
+                d += n1 + n2;
+            }
+        }
+        uint64_t tail = P.tail;
+        copy_records<R>(ring, w16, op0, tail, rec, farv, nrec, gen);
+        P.tail = tail;
+        const int32_t lend = (ended && rv < 0) ? P.fl : (P.op & ~63);
+        for (int32_t f = P.fl; f + 64 <= lend; f += 64) memcpy(out + f, ring + (f & (R - 1)), 64);
+        P.fl = lend > P.fl ? lend : P.fl;
+        if (ended) {
+            if (rv >= 0)
+                for (int32_t a = P.fl; a < P.op; a++) out[a] = ring[a & (R - 1)];
+            return rv;
+        }
+        P.wb = nwb;
+        for (int32_t k = 0; k < kLW; k += 16) {
+            const u128 v = chunk16z(in, nwb + k, L);
+            memcpy(w16 + k, &v, 16);
+        }
+    }
+    fprintf(stderr, "lc_emul: no end\n");
+    abort();
+}
+
+extern "C" int lc_emul_decode(const uint8_t *in, int L, uint8_t *out, int C, int R) {
+    return R == 512 ? lc_decode<512>(in, L, out, C) : lc_decode<256>(in, L, out, C);
+}

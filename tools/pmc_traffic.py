@@ -21,7 +21,13 @@ bench.py scales the per-page figure to its own launch for `roofline.traffic`.
 import argparse
 import csv
 import json
+import os
+import subprocess
+import sys
 from collections import defaultdict
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from tyche_amd._build import kernel_sources_digest  # noqa: E402
 
 # codec call -> the kernel symbols its dispatches carry (the split zstd codec runs several
 # kernels per chunk of pages and several chunks per call: give --calls for it)
@@ -34,7 +40,8 @@ KERNELS = {"lz4_encode": ("lz4_encode_",), "lz4_decode": ("lz4_decode_",),
 
 
 # read-byte factor per FETCH_SIZE byte, by kernel symbol (see the module docstring)
-SCATTERED = ("lz4_decode_ring_kernel", "lz4_decode_ringlb_kernel", "lz4_decode_lane_kernel", "zstd_seq_kernel",
+SCATTERED = ("lz4_decode_ring_kernel", "lz4_decode_ringlb_kernel", "lz4_decode_lane_kernel", "lz4_decode_quad_kernel",
+             "zstd_seq_kernel",
              "zstd_fse_kernel", "zstd_exec_lane_kernel", "zstd_seqexec_kernel", "zstd_lit_kernel")
 
 
@@ -57,6 +64,15 @@ def per_dispatch(path, counter):
     return out
 
 
+def _head():
+    try:
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        return subprocess.run(["git", "-C", root, "rev-parse", "--short=12", "HEAD"], capture_output=True,
+                              text=True, timeout=10).stdout.strip() or None
+    except (OSError, subprocess.SubprocessError):
+        return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("fetch")
@@ -73,7 +89,10 @@ def main():
            "formula": "(c*FETCH_SIZE + WRITE_SIZE) * 1024 / pages; c = 2 for the page-staging kernels (gfx950 "
                       "half count of coalesced streaming reads), 1 for the scattered lane LZ4 decoder (calibrated, "
                       "tools/probes/fetch_calib.hip)",
-           "bytes_per_page": {}, "read_bytes_per_page": {}, "write_bytes_per_page": {}}
+           "bytes_per_page": {}, "read_bytes_per_page": {}, "write_bytes_per_page": {},
+           # the kernel code these counters describe: bench.py reports `traffic` only while this
+           # digest equals the digest of the sources it runs (a stale summary must not look current)
+           "kernel_sources_sha16": kernel_sources_digest(), "commit": _head()}
     for k in KERNELS:
         if not f.get(k) or not w.get(k):
             continue

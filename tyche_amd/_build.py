@@ -14,7 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 BUILD = os.path.join(HERE, "..", "build", "tyche_amd")
 LIB = os.path.join(HERE, "libtyche_codec.so")
-SOURCES = ["engine.hip", "lz4_decode.hip", "lz4_decode_lane.hip", "lz4_decode_quad.hip", "lz4_encode.hip", "zlib_inflate.hip", "zstd_decode.hip", "zstd_encode.hip", "zlib_deflate.hip", "pagegen.hip",
+SOURCES = ["engine.hip", "lz4_decode.hip", "lz4_decode_lane.hip", "lz4_decode_quad.hip", "lz4_decode_lc.hip", "lz4_encode.hip", "zlib_inflate.hip", "zstd_decode.hip", "zstd_encode.hip", "zlib_deflate.hip", "pagegen.hip",
            "errno_guard.hip"]   # errno_guard last: its constructor runs after the code-object registrations
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
@@ -26,6 +26,20 @@ FLAGS = ["--offload-arch=" + ARCH, "-O3", "-fPIC", "-std=c++17", "-Wall", "-Wno-
 # Without it, pairs still become ds_read2_b32 (4-byte alignment suffices).
 NO_LSV = ["-mllvm", "-amdgpu-load-store-vectorizer=false"]
 SOURCE_FLAGS = {"lz4_encode.hip": NO_LSV, "zstd_encode.hip": NO_LSV, "zlib_deflate.hip": NO_LSV, "zstd_decode.hip": NO_LSV}
+
+
+def kernel_sources_digest() -> str:
+    """sha256 (first 16 hex digits) over the kernel sources (csrc/*.hip, csrc/*.h and the ABI
+    header): PMC traffic summaries record it (tools/pmc_traffic.py) so that bench.py can tell a
+    summary of the code it runs from a stale one."""
+    import hashlib
+    h = hashlib.sha256()
+    files = sorted(f for f in os.listdir(CSRC) if f.endswith((".hip", ".h")))
+    for f in files:
+        h.update(f.encode())
+        h.update(open(os.path.join(CSRC, f), "rb").read())
+    h.update(open(os.path.join(HERE, "..", "include", "tyche_codec.h"), "rb").read())
+    return h.hexdigest()[:16]
 
 
 def _newer(target: str, deps: list[str]) -> bool:

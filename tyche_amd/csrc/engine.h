@@ -74,6 +74,8 @@ bool lz4_lane_decode_wanted(size_t count, uint32_t in_cap, uint32_t out_cap);
 hipError_t launch_lz4_decode_lane(const tyche_batch_t &b, uint32_t in_cap, uint32_t out_cap, hipStream_t s);
 // large batches, round 4: one page per quad, chunked (lz4_decode_quad.hip)
 hipError_t launch_lz4_decode_quad(const tyche_batch_t &b, uint32_t in_cap, uint32_t out_cap, hipStream_t s);
+// large batches, round 4: one page per lane, chunked, aligned LDS (lz4_decode_lc.hip)
+hipError_t launch_lz4_decode_lc(const tyche_batch_t &b, uint32_t in_cap, uint32_t out_cap, hipStream_t s);
 hipError_t launch_lz4_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream_t s);
 hipError_t launch_zstd_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream_t s);
 hipError_t launch_zlib_deflate(const tyche_batch_t &b, uint32_t in_cap, hipStream_t s);

@@ -48,6 +48,7 @@
 #include "engine.h"
 #include "lane_ring.h"
 #include "lds_io.h"
+#include "lds_qword.h"
 
 namespace tyche {
 
@@ -88,15 +89,6 @@ struct QL {
     static constexpr uint32_t total = far + (uint32_t)F * 16u * kFarEnt;
 };
 
-typedef __attribute__((address_space(3))) uint64_t l_u64;
-typedef __attribute__((address_space(3))) uint32_t l_u32;
-typedef __attribute__((address_space(3))) uint8_t l_u8;
-__device__ __forceinline__ uint64_t lq(const uint8_t *p) { return *(const l_u64 *)(const l_u8 *)p; }
-__device__ __forceinline__ void lq(uint8_t *p, uint64_t v) { *(l_u64 *)(l_u8 *)p = v; }
-__device__ __forceinline__ uint32_t ld32(const uint8_t *p) { return *(const l_u32 *)(const l_u8 *)p; }
-__device__ __forceinline__ void ld32(uint8_t *p, uint32_t v) { *(l_u32 *)(l_u8 *)p = v; }
-__device__ __forceinline__ uint32_t lb(const uint8_t *p) { return *(const l_u8 *)p; }
-
 // quad_perm [0,0,0,0]: lane 0 of every quad to its four lanes
 __device__ __forceinline__ uint32_t qb0(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x00, 0xF, 0xF, false);
@@ -105,14 +97,6 @@ __device__ __forceinline__ uint64_t qb0(uint64_t v) {
     return (uint64_t)qb0((uint32_t)v) | ((uint64_t)qb0((uint32_t)(v >> 32)) << 32);
 }
 
-// bytes [s, s + 8) of the 16 bytes a (low) : b (high), 0 <= s < 8
-__device__ __forceinline__ uint64_t funnel8(uint64_t a, uint64_t b, uint32_t s) {
-    const uint32_t a0 = (uint32_t)a, a1 = (uint32_t)(a >> 32), b0 = (uint32_t)b, b1 = (uint32_t)(b >> 32);
-    const bool h = (s & 4u) != 0;
-    const uint32_t x0 = h ? a1 : a0, x1 = h ? b0 : a1, x2 = h ? b1 : b0;
-    const uint32_t r = s & 3u;
-    return (uint64_t)__builtin_amdgcn_alignbyte(x1, x0, r) | ((uint64_t)__builtin_amdgcn_alignbyte(x2, x1, r) << 32);
-}
 // 8 bytes at byte offset p (any alignment, p >= -8) of an 8-aligned LDS buffer
 __device__ __forceinline__ uint64_t rd8(const uint8_t *base, int32_t p) {
     const int32_t a = p & ~7;
@@ -124,38 +108,6 @@ __device__ __forceinline__ uint64_t ring8(const uint8_t *ring, int32_t p) {
     const int32_t a = p & ~7;
     return funnel8(lq(ring + (a & (H - 1))), lq(ring + ((a + 8) & (H - 1))), (uint32_t)p & 7u);
 }
-// bytes [0, m) of t, bytes [m, 8) of v
-__device__ __forceinline__ uint64_t keep_low(uint64_t t, uint64_t v, uint32_t m) {
-    const uint32_t mlo = m >= 4u ? 0xFFFFFFFFu : ((1u << (8u * m)) - 1u);
-    const uint32_t mhi = m <= 4u ? 0u : ((1u << (8u * (m - 4u))) - 1u);
-    const uint32_t lo = (mlo & (uint32_t)t) | (~mlo & (uint32_t)v);
-    const uint32_t hi = (mhi & (uint32_t)(t >> 32)) | (~mhi & (uint32_t)(v >> 32));
-    return (uint64_t)lo | ((uint64_t)hi << 32);
-}
-__device__ __forceinline__ uint32_t sel4(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t q) {
-    const uint32_t t0 = (q & 1u) ? w1 : w0, t1 = (q & 1u) ? w3 : w2;
-    return (q & 2u) ? t1 : t0;
-}
-
-// bytes [a, a + 16) of the stream, zero outside [0, L); never reads outside it
-__device__ __forceinline__ u128 chunk16q(const uint8_t *__restrict__ in, int32_t a, int32_t L) {
-    if (a >= L || a + 16 <= 0) return 0;
-    if (a >= 0 && a + 16 <= L) return ld16(in + a);
-    if (L >= 16) {
-        if (a < 0) return ld16(in) << (8 * (-a));
-        return ld16(in + L - 16) >> (8 * (a - (L - 16)));
-    }
-    u128 v = 0;
-    for (int32_t k = 15; k >= 0; k--) {
-        const int32_t x = a + k;
-        v = (v << 8) | ((x >= 0 && x < L) ? ld1(in + x) : 0u);
-    }
-    return v;
-}
-__device__ __forceinline__ uint32_t sbyte(const uint8_t *__restrict__ in, int32_t p, int32_t L) {
-    return p >= 0 && p < L ? ld1(in + p) : 0u;
-}
-
 // ---- slow path: one sequence at (ip, op) straight between HBM buffers
 // (decode_lane's loop body, lz4_decode_lane.hip), every byte of out below op
 // already in HBM.  Lane j of the quad copies the j-th 16 bytes of every 64.
@@ -302,7 +254,7 @@ __device__ __forceinline__ void window_load(uint8_t *sb, const uint8_t *__restri
 #pragma unroll
     for (int32_t c = 0; c < 4; c++) {
         const int32_t k = 16 * ((int32_t)j + 4 * c);
-        lds16(sb + 16 + k, chunk16q(in, ns + k, L));
+        lds16(sb + 16 + k, chunk16z(in, ns + k, L));
     }
 }
 
@@ -492,10 +444,10 @@ __global__ __launch_bounds__(64) void lz4_decode_quad_kernel(tyche_batch_t b, ui
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         u128 pre0 = 0, pre1 = 0, pre2 = 0, pre3 = 0;
         if (cont) {
-            pre0 = chunk16q(P.in, ns + 16 * (int32_t)j, P.L);
-            pre1 = chunk16q(P.in, ns + 16 * ((int32_t)j + 4), P.L);
-            pre2 = chunk16q(P.in, ns + 16 * ((int32_t)j + 8), P.L);
-            pre3 = chunk16q(P.in, ns + 16 * ((int32_t)j + 12), P.L);
+            pre0 = chunk16z(P.in, ns + 16 * (int32_t)j, P.L);
+            pre1 = chunk16z(P.in, ns + 16 * ((int32_t)j + 4), P.L);
+            pre2 = chunk16z(P.in, ns + 16 * ((int32_t)j + 8), P.L);
+            pre3 = chunk16z(P.in, ns + 16 * ((int32_t)j + 12), P.L);
         }
 #pragma unroll
         for (int32_t f = 0; f < F; f++) {
