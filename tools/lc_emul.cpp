@@ -51,23 +51,26 @@ static inline u128 chunk16z(const uint8_t *in, int32_t a, int32_t L) {
 #include "../tyche_amd/csrc/byte_funnel.h"
 #include "../tyche_amd/csrc/lz4_lc_core.h"
 
-long g_stat[8];
-extern "C" long *lc_emul_stats() { return g_stat; }
-static void fetch_far(const LPage &P, int32_t src, u128 *f) {
-    if (src < 0 || src + 32 > P.fl) {
-        fprintf(stderr, "lc_emul: far source [%d, %d) not flushed (fl %d)\n", src, src + 32, P.fl);
+// a far match part's source: its n2 used bytes must be in HBM already (lc_budget); the
+// kernel's loads may run past them (bytes it does not use), the emulator's stop there
+static void fetch_far(const LPage &P, uint32_t rec, int32_t src, u128 *f) {
+    const int32_t n2 = (int32_t)((rec >> 10) & 63u);
+    if (src < 0 || src + n2 > P.fl) {
+        fprintf(stderr, "lc_emul: far source [%d, %d) not flushed (fl %d)\n", src, src + n2, P.fl);
         abort();
     }
-    f[0] = ld16(P.out + src);
-    f[1] = ld16(P.out + src + 16);
+    uint8_t b[32] = {0};
+    memcpy(b, P.out + src, (size_t)n2);
+    f[0] = ld16(b);
+    f[1] = n2 > 16 ? ld16(b + 16) : 0;
 }
 
 template <int32_t R>
 static int lc_decode(const uint8_t *in, int32_t L, uint8_t *out, int32_t C) {
     if (C == 0) return (L == 1 && in[0] == 0) ? 0 : -1;
     if (L <= 0) return -1;
-    alignas(16) uint8_t ring[R + 16];
-    alignas(16) uint8_t win[kLWS + 64];   // reads run up to 24 bytes past the window's slack
+    alignas(16) uint8_t ring[R];
+    alignas(16) uint8_t win[kLWS + 64];   // reads run up to 32 bytes past the window's end
     uint8_t *w16 = win + 16;
     memset(ring, 0xA5, sizeof(ring));
     memset(win, 0x5A, sizeof(win));
@@ -97,7 +100,7 @@ static int lc_decode(const uint8_t *in, int32_t L, uint8_t *out, int32_t C) {
                 const int32_t k = getenv("LC_SLOW") ? 2 : parse_fast<R>(P, w16, op0, rec[t], far, src);
                 if (k == 1) {
                     nrec = t + 1;
-                    if (far) fetch_far(P, src, farv + 2 * t);
+                    if (far) fetch_far(P, rec[t], src, farv + 2 * t);
                 } else {
                     go = false;
                     need_gen = (k == 2 || t == 0) ? 1 : 0;
@@ -112,7 +115,7 @@ static int lc_decode(const uint8_t *in, int32_t L, uint8_t *out, int32_t C) {
             int32_t src = 0;
             if (parse_slot<R>(P, w16, op0, nrec == 0, st, rv, rec[kLC], far, src)) {
                 gen = true;
-                if (far) fetch_far(P, src, farv + 2 * kLC);
+                if (far) fetch_far(P, rec[kLC], src, farv + 2 * kLC);
             }
         }
         const bool ended = st == kLEnd;
@@ -131,15 +134,15 @@ static int lc_decode(const uint8_t *in, int32_t L, uint8_t *out, int32_t C) {
                               off = (int32_t)(r >> 16);
                 if (d + n1 + n2 >= lo && d <= lo + 64)
                     fprintf(stderr, "chunk %ld t %d d %d wb %d lpr %d n1 %d n2 %d off %d far %d\n", chunk, t, d, P.wb, lpr,
-                            n1, n2, off, off > R - 32);
+                            n1, n2, off, off > lc_near<R>());
                 d += n1 + n2;
             }
         }
         uint64_t tail = P.tail;
         copy_records<R>(ring, w16, op0, tail, rec, farv, nrec, gen);
         P.tail = tail;
-        const int32_t lend = (ended && rv < 0) ? P.fl : (P.op & ~63);
-        for (int32_t f = P.fl; f + 64 <= lend; f += 64) memcpy(out + f, ring + (f & (R - 1)), 64);
+        const int32_t lend = (ended && rv < 0) ? P.fl : (P.op & ~15);
+        for (int32_t f = P.fl; f + 16 <= lend; f += 16) memcpy(out + f, ring + (f & (R - 1)), 16);
         P.fl = lend > P.fl ? lend : P.fl;
         if (ended) {
             if (rv >= 0)
@@ -157,5 +160,5 @@ static int lc_decode(const uint8_t *in, int32_t L, uint8_t *out, int32_t C) {
 }
 
 extern "C" int lc_emul_decode(const uint8_t *in, int L, uint8_t *out, int C, int R) {
-    return R == 512 ? lc_decode<512>(in, L, out, C) : lc_decode<256>(in, L, out, C);
+    return R == 256 ? lc_decode<256>(in, L, out, C) : lc_decode<128>(in, L, out, C);
 }

@@ -41,6 +41,7 @@ KERNELS = {"lz4_encode": ("lz4_encode_",), "lz4_decode": ("lz4_decode_",),
 
 # read-byte factor per FETCH_SIZE byte, by kernel symbol (see the module docstring)
 SCATTERED = ("lz4_decode_ring_kernel", "lz4_decode_ringlb_kernel", "lz4_decode_lane_kernel", "lz4_decode_quad_kernel",
+             "lz4_decode_lc_kernel",
              "zstd_seq_kernel",
              "zstd_fse_kernel", "zstd_exec_lane_kernel", "zstd_seqexec_kernel", "zstd_lit_kernel")
 

@@ -69,7 +69,8 @@ inline size_t waves_per_cu(const void *kernel, size_t lds) {
     return granted ? std::max<size_t>(1, std::min<size_t>(32, (160 * 1024) / granted)) : 32;
 }
 
-hipError_t launch_lz4_decode(const tyche_batch_t &b, uint32_t in_cap, uint32_t out_cap, hipStream_t s);
+hipError_t launch_lz4_decode(const tyche_batch_t &b, uint32_t in_cap, uint32_t out_cap, hipStream_t s,
+                             bool allow_lane = true);
 bool lz4_lane_decode_wanted(size_t count, uint32_t in_cap, uint32_t out_cap);
 hipError_t launch_lz4_decode_lane(const tyche_batch_t &b, uint32_t in_cap, uint32_t out_cap, hipStream_t s);
 // large batches, round 4: one page per quad, chunked (lz4_decode_quad.hip)

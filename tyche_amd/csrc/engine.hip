@@ -140,19 +140,28 @@ namespace {
 bool entry_idle(ScratchPool::Entry &x) {
     return x.state == 0 || (x.state == 2 && hipEventQuery(x.ev) == hipSuccess && ((x.state = 0), true));
 }
-// frees idle entries (largest first) until the pool holds at most `keep` bytes; under P.mu
-void pool_trim(ScratchPool &P, size_t keep) {
+// takes idle entries (largest first) out of the pool until it holds at most `keep` bytes; under
+// P.mu.  The caller frees what it returns (free_entries) after releasing P.mu: hipFree synchronises
+// the device, and neither the other streams nor the other lease requests should wait on that.
+std::vector<ScratchPool::Entry> pool_trim(ScratchPool &P, size_t keep) {
+    std::vector<ScratchPool::Entry> out;
     size_t total = 0;
     for (auto &x : P.e) total += x.bytes;
     while (total > keep) {
         size_t best = P.e.size();
         for (size_t i = 0; i < P.e.size(); i++)
             if (entry_idle(P.e[i]) && (best == P.e.size() || P.e[i].bytes > P.e[best].bytes)) best = i;
-        if (best == P.e.size()) return;
-        (void)hipFree(P.e[best].p);
-        (void)hipEventDestroy(P.e[best].ev);
+        if (best == P.e.size()) break;
+        out.push_back(P.e[best]);
         total -= P.e[best].bytes;
         P.e.erase(P.e.begin() + (long)best);
+    }
+    return out;
+}
+void free_entries(const std::vector<ScratchPool::Entry> &v) {
+    for (const auto &x : v) {
+        (void)hipFree(x.p);
+        (void)hipEventDestroy(x.ev);
     }
 }
 }  // namespace
@@ -173,33 +182,44 @@ tyche::ScratchLease::ScratchLease(hipStream_t s, size_t bytes) : s_(s) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return;
     ScratchPool &P = g_scratch[dev];
-    std::lock_guard<std::mutex> g(P.mu);
-    const size_t want = (std::max<size_t>(bytes, 1) + 0xFFFFF) & ~size_t(0xFFFFF);
-    size_t take = P.e.size();
-    for (size_t i = 0; i < P.e.size(); i++) {   // best fit among idle entries of at most 4x the request
-        ScratchPool::Entry &x = P.e[i];
-        if (x.state == 1 || x.bytes < want || x.bytes / 4 > want) continue;
-        if (!entry_idle(x)) continue;
-        if (take == P.e.size() || x.bytes < P.e[take].bytes) take = i;
-    }
-    if (take == P.e.size()) {
-        pool_trim(P, kPoolKeep > want ? kPoolKeep - want : 0);
-        ScratchPool::Entry x{nullptr, want, nullptr, 0};
-        if (hipMalloc(&x.p, x.bytes) != hipSuccess) {
-            pool_trim(P, 0);
-            if (hipMalloc(&x.p, x.bytes) != hipSuccess) return;
+    std::vector<ScratchPool::Entry> victims;   // trimmed under the lock, freed after it
+    {
+        std::lock_guard<std::mutex> g(P.mu);
+        const size_t want = (std::max<size_t>(bytes, 1) + 0xFFFFF) & ~size_t(0xFFFFF);
+        size_t take = P.e.size();
+        for (size_t i = 0; i < P.e.size(); i++) {   // best fit among idle entries of at most 4x the request
+            ScratchPool::Entry &x = P.e[i];
+            if (x.state == 1 || x.bytes < want || x.bytes / 4 > want) continue;
+            if (!entry_idle(x)) continue;
+            if (take == P.e.size() || x.bytes < P.e[take].bytes) take = i;
         }
-        if (hipEventCreateWithFlags(&x.ev, hipEventDisableTiming) != hipSuccess) {
-            (void)hipFree(x.p);
-            return;
+        if (take == P.e.size()) {
+            victims = pool_trim(P, kPoolKeep > want ? kPoolKeep - want : 0);
+            ScratchPool::Entry x{nullptr, want, nullptr, 0};
+            if (hipMalloc(&x.p, x.bytes) != hipSuccess) {
+                // out of memory: every idle entry goes, now (under the lock: this lease needs it)
+                free_entries(victims);
+                victims = pool_trim(P, 0);
+                free_entries(victims);
+                victims.clear();
+                if (hipMalloc(&x.p, x.bytes) != hipSuccess) return;
+            }
+            if (hipEventCreateWithFlags(&x.ev, hipEventDisableTiming) != hipSuccess) {
+                (void)hipFree(x.p);
+                x.p = nullptr;
+            } else {
+                P.e.push_back(x);
+                take = P.e.size() - 1;   // pool_trim may have erased entries: the new one is the last
+            }
         }
-        P.e.push_back(x);
-        take = P.e.size() - 1;   // pool_trim may have erased entries: the new one is the last
+        if (take < P.e.size()) {
+            P.e[take].state = 1;
+            dev_ = dev;
+            idx_ = (int)take;
+            p_ = P.e[take].p;
+        }
     }
-    P.e[take].state = 1;
-    dev_ = dev;
-    idx_ = (int)take;
-    p_ = P.e[take].p;
+    free_entries(victims);
 }
 
 tyche::ScratchLease::~ScratchLease() {
@@ -843,7 +863,7 @@ int run_host_batch(int dev, size_t n, const void *const *src, const uint32_t *sr
                 S.first = 0;
                 S.count = n;
                 S.busy = true;
-                if ((e = launch(b, S.stream)) != hipSuccess) return bail(fail("kernel launch", e));
+                if ((e = launch(b, S.stream, true)) != hipSuccess) return bail(fail("kernel launch", e));
                 S.busy = false;
                 if ((e = hipStreamSynchronize(S.stream)) != hipSuccess) return bail(fail("hipStreamSynchronize", e));
                 const uint8_t *hout = (const uint8_t *)S.h_out.p;
@@ -1046,7 +1066,9 @@ int run_host_batch(int dev, size_t n, const void *const *src, const uint32_t *sr
         // every page's full capacity (16 KiB+ per 16 KiB page at ratio 2.6).  LZ4 decompress
         // (kDirectLz4Decode): the jump and wave decoders write each page once, whole, from LDS; the
         // lane decoder (chunks of >= kLaneMin pages) reads its own output back, so it keeps the D2H;
-        // TYCHE_HOST_DIRECT_DECODE_MAX: chunks of more pages than this stage through HBM too.
+        // TYCHE_HOST_DIRECT_DECODE_MAX: chunks of more pages than this stage through HBM too.  The
+        // choice is made once here and handed to the launch (host_dst), so a knob changed meanwhile
+        // cannot put the lane decoder on a host destination.
         const bool direct = S.h_out.dp != nullptr &&
                             (direct_out == kDirectAlways ||
                              (direct_out == kDirectLz4Decode && !lz4_lane_decode_wanted(k, max_in, max_out) &&
@@ -1056,7 +1078,7 @@ int run_host_batch(int dev, size_t n, const void *const *src, const uint32_t *sr
         b.dst_capacities = (const uint32_t *)(dmeta + ((uint8_t *)m_dcap - (uint8_t *)m_soff));
         b.dst_capacity = max_out;
         b.results = (int32_t *)(dmeta + head_bytes);
-        if ((e = launch(b, S.stream)) != hipSuccess) return bail(fail("kernel launch", e));
+        if ((e = launch(b, S.stream, direct)) != hipSuccess) return bail(fail("kernel launch", e));
         if ((e = hipMemcpyAsync(m_res, b.results, k * 4, hipMemcpyDeviceToHost, S.stream)) != hipSuccess)
             return bail(fail("hipMemcpyAsync(results)", e));
         if (dof && !direct && (e = hipMemcpyAsync(S.h_out.p, S.d_out.p, dof, hipMemcpyDeviceToHost, S.stream)) != hipSuccess)
@@ -1088,20 +1110,24 @@ int run_host_batch(int dev, size_t n, const void *const *src, const uint32_t *sr
 // minimum input bytes per device before a host batch is split across devices
 uint64_t fanout_min_bytes() { return (uint64_t)std::max(0L, knob("FANOUT_MIN_BYTES", 64L << 20)); }
 
-// A process launched one per GPU (torch.distributed.run sets WORLD_SIZE and
-// LOCAL_RANK) keeps its host work on its own device -- LOCAL_RANK modulo the
-// visible devices, torch's convention, whichever thread calls -- unless
-// TYCHE_DEVICES / TYCHE_DEVICE_IDS ask for the fan-out.  -1: not such a process.
+// A process launched one per GPU (torch.distributed.run sets LOCAL_RANK and
+// LOCAL_WORLD_SIZE) keeps its host work on its own device -- LOCAL_RANK modulo
+// the visible devices, torch's convention, whichever thread calls.  Only
+// LOCAL_RANK engages it (a launcher that sets WORLD_SIZE alone gets the
+// fan-out, not device 0), a LOCAL_WORLD_SIZE of 1 does not (the node's only
+// process may use every device), and TYCHE_DEVICES / TYCHE_DEVICE_IDS or the
+// RANK_PIN knob (0, at any time through tyche_set_knob) turn it off, e.g. for a
+// helper process that inherited a worker's environment.  -1: not pinned.
 int rank_device() {
     static const int d = [] {
         if (getenv("TYCHE_DEVICES") || getenv("TYCHE_DEVICE_IDS")) return -1;
-        const char *w = getenv("WORLD_SIZE"), *lr = getenv("LOCAL_RANK");
-        if (!lr && !(w && atoi(w) > 1)) return -1;
+        const char *lr = getenv("LOCAL_RANK"), *lw = getenv("LOCAL_WORLD_SIZE");
+        if (!lr || !*lr || (lw && atoi(lw) == 1)) return -1;
         int n = 0;
         if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return -1;
-        return lr ? atoi(lr) % n : 0;
+        return std::max(0, atoi(lr)) % n;
     }();
-    return d;
+    return d >= 0 && knob("RANK_PIN", 1) != 0 ? d : -1;
 }
 
 // the device with the fewest host batches in flight (ties rotate)
@@ -1303,7 +1329,7 @@ int tyche_compress_host(int compressor_id, int compressor_level, size_t n, const
     // straight into the pinned staging arena (HOST_DIRECT_OUT=0: stage through HBM and D2H instead)
     const int direct = compressor_id == TYCHE_LZ4_COMPRESSOR_ID && knob("HOST_DIRECT_OUT", 1) ? kDirectAlways : kDirectNone;
     return run_host(n, src, src_lengths, dst, dst_capacities, results,
-                          [compressor_id](const tyche_batch_t &b, hipStream_t s) {
+                          [compressor_id](const tyche_batch_t &b, hipStream_t s, bool) {
                               return launch_encode(compressor_id, b, std::max(b.max_src_length, 1u), s);
                           }, false, direct);
 }
@@ -1314,17 +1340,17 @@ int tyche_decompress_host(int compressor_id, size_t n, const void *const *src, c
     if (n == 0) return TYCHE_E_OK;
     if (compressor_id == TYCHE_ZLIB_COMPRESSOR_ID)
         return run_host(n, src, src_lengths, dst, dst_capacities, results,
-                              [](const tyche_batch_t &b, hipStream_t s) {
+                              [](const tyche_batch_t &b, hipStream_t s, bool) {
                                   return launch_zlib_inflate(b, b.dst_capacity, s);
                               }, true);
     if (compressor_id == TYCHE_ZSTD_COMPRESSOR_ID)
         return run_host(n, src, src_lengths, dst, dst_capacities, results,
-                              [](const tyche_batch_t &b, hipStream_t s) {
+                              [](const tyche_batch_t &b, hipStream_t s, bool) {
                                   return launch_zstd_decode(b, b.max_src_length, b.dst_capacity, s);
                               }, true);
     return run_host(n, src, src_lengths, dst, dst_capacities, results,
-                          [](const tyche_batch_t &b, hipStream_t s) {
-                              return launch_lz4_decode(b, b.max_src_length, b.dst_capacity, s);
+                          [](const tyche_batch_t &b, hipStream_t s, bool host_dst) {
+                              return launch_lz4_decode(b, b.max_src_length, b.dst_capacity, s, !host_dst);
                           }, true, knob("HOST_DIRECT_OUT", 1) ? kDirectLz4Decode : kDirectNone);
 }
 

@@ -1273,10 +1273,12 @@ static hipError_t launch_lz4_decode_jump(const tyche_batch_t &b, uint32_t in_cap
     return hipGetLastError();
 }
 
-hipError_t launch_lz4_decode(const tyche_batch_t &b, uint32_t in_cap, uint32_t out_cap, hipStream_t s) {
+hipError_t launch_lz4_decode(const tyche_batch_t &b, uint32_t in_cap, uint32_t out_cap, hipStream_t s,
+                             bool allow_lane) {
     if (b.count == 0) return hipSuccess;
-    // large batches: one page per lane (lz4_decode_lane.hip)
-    if (lz4_lane_decode_wanted(b.count, in_cap, out_cap)) return launch_lz4_decode_lane(b, in_cap, out_cap, s);
+    // large batches: one page per lane (lz4_decode_lane.hip); never into host memory (allow_lane
+    // false): that decoder reads its flushed output back
+    if (allow_lane && lz4_lane_decode_wanted(b.count, in_cap, out_cap)) return launch_lz4_decode_lane(b, in_cap, out_cap, s);
     // small batches: workgroup per page, pointer-jumping match resolution
     {
         bool launched = false;

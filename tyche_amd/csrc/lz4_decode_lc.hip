@@ -19,17 +19,19 @@
 //    checks in the reference's order on the way.  A sequence larger than a
 //    record is cut into parts (long literal runs, long matches); the parse is a
 //    state machine that resumes inside a literal run or a match in the next
-//    chunk.  A far match part (offset > R - 32: its source has left the ring)
+//    chunk.  A far match part (offset > R - 24: its source has left the ring)
 //    issues its 16-byte load right away, into that slot's registers;
 //  * the next chunk's window is loaded behind them; stage 3 then copies the
 //    records window/ring/registers -> ring with aligned LDS qwords only
 //    (byte-unaligned LDS accesses replay per lane, tools/probes/lds_wide.hip):
 //    a run is written as the three qwords from d & ~7, the lane's "tail"
 //    register supplying the bytes below d;
-//  * stage 4 writes the finished 64-byte lines of all 64 pages cooperatively:
-//    four lanes per line, 16 lines per store instruction, so every line leaves
-//    in one instruction (a lane writing its own lines as four 16-byte stores
-//    leaves them partially written for the L2 to merge).
+//  * stage 4 writes the finished 16-byte pieces of all 64 pages cooperatively,
+//    one piece per lane and store instruction, a page's pieces on neighbouring
+//    lanes (a lane storing only its own page's pieces would touch 64 lines per
+//    instruction).  Flushing 16-byte pieces rather than 64-byte lines keeps the
+//    unflushed tail under 16 bytes, which lets a 128-byte ring carry 88-byte
+//    chunks (lz4_lc_core.h, lc_budget): LDS per wave 14 KiB, 11 waves per CU.
 //
 // Results are LZ4_decompress_safe's: the decoded size, or -(input bytes
 // consumed)-1 for a malformed stream (stream bytes past its end read as zero,
@@ -65,16 +67,17 @@ namespace {
 
 #include "lz4_lc_core.h"
 
+// LDS of one wave: the 64 windows first (a parse read may run up to 32 bytes past
+// its window, into the next one or the rings), the 64 rings, the flush tables.
 template <int32_t R>
 struct LCL {
-    static constexpr int32_t rs = R + 16;                                 // ring stride (16-aligned, bank spread)
-    static constexpr uint32_t ring = 0;
-    static constexpr uint32_t win = 64u * rs;
-    static constexpr uint32_t tab_out = win + 64u * kLWS;                 // 64 x u64: page output pointers
-    static constexpr uint32_t tab_fl = tab_out + 64u * 8u;                // 64 x u32: first pending line
-    static constexpr int32_t max_lines = (R - 127 + 63) / 64 + 2;         // whole lines per lane per chunk
-    static constexpr uint32_t own = tab_fl + 64u * 4u;                    // 64 x max_lines x u32
-    static constexpr uint32_t total = own + 64u * (uint32_t)max_lines * 4u;
+    static constexpr uint32_t win = 0;
+    static constexpr uint32_t ring = 64u * kLWS;
+    static constexpr uint32_t tab_out = ring + 64u * (uint32_t)R;         // 64 x u64: page output pointers
+    static constexpr uint32_t tab_fl = tab_out + 64u * 8u;                // 64 x u32: first pending piece
+    static constexpr int32_t max_pieces = (lc_budget<R>() + 15) / 16;     // 16-byte pieces per lane per chunk
+    static constexpr uint32_t own = tab_fl + 64u * 4u;                    // 64 x max_pieces x u16
+    static constexpr uint32_t total = own + ((64u * (uint32_t)max_pieces * 2u + 15u) & ~15u);
 };
 
 // page `idx` of the batch (its metadata; src may be read for the C == 0 case)
@@ -88,23 +91,50 @@ __device__ __forceinline__ LMeta lmeta(const tyche_batch_t &b, size_t idx) {
     return LMeta{r.src, r.dst, r.src_len, r.dst_cap};
 }
 
-// the window [ns, ns + 64) of the stream, zero outside [0, L)
+// the window [ns, ns + 64) of the stream (ns >= 0), zero from L on.  The loads
+// are issued unconditionally from clamped addresses and their results used only
+// in wstore, after the chunk's other work: a shift applied where a load is made
+// would wait for it (and for every load issued before it) right there.
 struct LWin {
     u128 c0, c1, c2, c3;
+    uint32_t sh;   // per piece (8 bits each): bytes to drop from the clamped load; >= 16: zero
 };
 __device__ __forceinline__ LWin wload(const uint8_t *__restrict__ in, int32_t ns, int32_t L) {
     LWin w;
-    w.c0 = chunk16z(in, ns, L);
-    w.c1 = chunk16z(in, ns + 16, L);
-    w.c2 = chunk16z(in, ns + 32, L);
-    w.c3 = chunk16z(in, ns + 48, L);
+    if (L >= 16) {
+        const int32_t top = L - 16;
+        const int32_t a0 = min(ns, top), a1 = min(ns + 16, top), a2 = min(ns + 32, top), a3 = min(ns + 48, top);
+        w.c0 = ld16(in + a0);
+        w.c1 = ld16(in + a1);
+        w.c2 = ld16(in + a2);
+        w.c3 = ld16(in + a3);
+        w.sh = (uint32_t)min(ns - a0, 16) | ((uint32_t)min(ns + 16 - a1, 16) << 8) |
+               ((uint32_t)min(ns + 32 - a2, 16) << 16) | ((uint32_t)min(ns + 48 - a3, 16) << 24);
+    } else {   // a stream shorter than one piece (rare): bytes, zero-padded
+        w.c0 = chunk16z(in, ns, L);
+        w.c1 = chunk16z(in, ns + 16, L);
+        w.c2 = chunk16z(in, ns + 32, L);
+        w.c3 = chunk16z(in, ns + 48, L);
+        w.sh = 0;
+    }
     return w;
 }
+__device__ __forceinline__ u128 wshift(u128 v, uint32_t k) {
+    k &= 0xFFu;
+    return k >= 16u ? (u128)0 : (k == 0u ? v : v >> (8u * k));
+}
 __device__ __forceinline__ void wstore(uint8_t *w16, const LWin &w) {
-    lds16(w16, w.c0);
-    lds16(w16 + 16, w.c1);
-    lds16(w16 + 32, w.c2);
-    lds16(w16 + 48, w.c3);
+    if (w.sh == 0) {
+        lds16(w16, w.c0);
+        lds16(w16 + 16, w.c1);
+        lds16(w16 + 32, w.c2);
+        lds16(w16 + 48, w.c3);
+    } else {
+        lds16(w16, wshift(w.c0, w.sh));
+        lds16(w16 + 16, wshift(w.c1, w.sh >> 8));
+        lds16(w16 + 32, wshift(w.c2, w.sh >> 16));
+        lds16(w16 + 48, wshift(w.c3, w.sh >> 24));
+    }
 }
 
 // starts the lane on page idx or a later one of its stride (pages with an
@@ -139,16 +169,28 @@ __device__ bool lpage_start(const tyche_batch_t &b, uint32_t in_cap, uint32_t ou
     return false;
 }
 
+// 32 bytes every lane without a far source reads instead (one line for the whole wave)
+__device__ __attribute__((aligned(64))) uint8_t g_lc_pad[64];
+
+// a record slot's far source: [src, src + 16) and, for a part over 16 bytes, [src + 16, src + 32)
+// of the page's output; the pad for lanes without one
+__device__ __forceinline__ void far_load(const LPage &P, bool far, int32_t src, uint32_t rec, u128 &f0, u128 &f1) {
+    if (TYCHE_ABLATE & 1024) far = false;   // timing only: no far loads (wrong output)
+    const bool two = far && ((rec >> 10) & 63u) > 16u;
+    f0 = ld16(far ? P.out + src : g_lc_pad);
+    f1 = ld16(two ? P.out + src + 16 : g_lc_pad + 16);
+}
+
 template <int32_t R>
-__global__ __launch_bounds__(64) void lz4_decode_lc_kernel(tyche_batch_t b, uint32_t in_cap, uint32_t out_cap) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void lz4_decode_lc_kernel(tyche_batch_t b, uint32_t in_cap, uint32_t out_cap) {
     typedef LCL<R> Lay;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t lane = threadIdx.x;
-    uint8_t *ring = smem + Lay::ring + lane * (uint32_t)Lay::rs;
-    uint8_t *w16 = smem + Lay::win + lane * (uint32_t)kLWS + 16;   // window byte 0
+    uint8_t *ring = smem + Lay::ring + lane * (uint32_t)R;
+    uint8_t *w16 = smem + Lay::win + lane * (uint32_t)kLWS;   // window byte 0
     uint64_t *tab_out = (uint64_t *)(smem + Lay::tab_out);
     uint32_t *tab_fl = (uint32_t *)(smem + Lay::tab_fl);
-    uint32_t *own = (uint32_t *)(smem + Lay::own);
+    uint16_t *own = (uint16_t *)(smem + Lay::own);
     const size_t G = (size_t)gridDim.x * 64u;
 
     LPage P;
@@ -167,38 +209,30 @@ __global__ __launch_bounds__(64) void lz4_decode_lc_kernel(tyche_batch_t b, uint
 #pragma unroll
         for (int32_t t = 0; t < kLC; t++) {
             rec[t] = 0;
-            farv[2 * t] = farv[2 * t + 1] = 0;
+            bool far = false;
+            int32_t src = 0;
             if (go) {
-                bool far = false;
-                int32_t src = 0;
                 const int32_t k = parse_fast<R>(P, w16, op0, rec[t], far, src);
                 if (k == 1) {
                     nrec = t + 1;
-                    // the source lies below fl (stage 4 of an earlier chunk wrote it): lc_budget
-                    if (far) {
-                        farv[2 * t] = ld16(P.out + src);
-                        farv[2 * t + 1] = ld16(P.out + src + 16);
-                    }
                 } else {
                     go = false;
                     need_gen = (k == 2 || t == 0) ? 1 : 0;   // the chunk's first record always makes progress
                     if (k == 0 && t != 0) st = kLCut;
                 }
             }
+            // the far source (below fl: stage 4 of an earlier chunk wrote it, lc_budget), loaded
+            // outside any branch so the registers are only waited for in stage 3
+            far_load(P, far, src, rec[t], farv[2 * t], farv[2 * t + 1]);
         }
         // one record of the general path (parse_slot) for the lanes that stopped on it
         rec[kLC] = 0;
-        farv[2 * kLC] = farv[2 * kLC + 1] = 0;
-        if (__builtin_amdgcn_ballot_w64(need_gen != 0) != 0 && need_gen) {
+        {
             bool far = false;
             int32_t src = 0;
-            if (parse_slot<R>(P, w16, op0, nrec == 0, st, rv, rec[kLC], far, src)) {
-                gen = true;
-                if (far) {
-                    farv[2 * kLC] = ld16(P.out + src);
-                    farv[2 * kLC + 1] = ld16(P.out + src + 16);
-                }
-            }
+            if (__builtin_amdgcn_ballot_w64(need_gen != 0) != 0 && need_gen)
+                gen = parse_slot<R>(P, w16, op0, nrec == 0, st, rv, rec[kLC], far, src);
+            far_load(P, far && gen, src, rec[kLC], farv[2 * kLC], farv[2 * kLC + 1]);
         }
         LPROF_MARK(1);
         LPROF_ADD(8, __builtin_amdgcn_ballot_w64(need_gen != 0) != 0);
@@ -222,27 +256,25 @@ __global__ __launch_bounds__(64) void lz4_decode_lc_kernel(tyche_batch_t b, uint
         }
 
         LPROF_MARK(3);
-        // ---- stage 4: the finished lines of all 64 pages, four lanes per line
-        const int32_t lend = !live ? 0 : (ended && rv < 0) ? P.fl : (P.op & ~63);
-        const int32_t nl = live ? (lend - P.fl) >> 6 : 0;
+        // ---- stage 4: the finished 16-byte pieces of all 64 pages, one per lane and store
+        // instruction (a page's pieces on neighbouring lanes: whole lines per few lanes)
+        const int32_t lend = !live ? 0 : (ended && rv < 0) ? P.fl : (P.op & ~15);
+        const int32_t nl = live ? (lend - P.fl) >> 4 : 0;
         const int32_t incl = wave_incl_sum(nl);
         const int32_t total = (int32_t)rdlane((uint32_t)incl, 63);
         if (total > 0) {
             tab_out[lane] = (uint64_t)(uintptr_t)P.out;
             tab_fl[lane] = (uint32_t)P.fl;
-            for (int32_t k = 0; k < nl; k++) own[incl - nl + k] = lane | ((uint32_t)k << 8);
+            for (int32_t k = 0; k < nl; k++) own[incl - nl + k] = (uint16_t)(lane | ((uint32_t)k << 6));
             asm volatile("" ::: "memory");
-            const uint32_t j = lane & 3u, q = lane >> 2;
-            for (int32_t g0 = 0; g0 < total; g0 += 16) {
-                const int32_t g = g0 + (int32_t)q;
-                if (g < total) {
-                    const uint32_t e = own[g];
-                    const uint32_t L2 = e & 63u, k = e >> 8;
-                    uint8_t *o = (uint8_t *)(uintptr_t)tab_out[L2];
-                    const int32_t f = (int32_t)tab_fl[L2] + 64 * (int32_t)k + 16 * (int32_t)j;
-                    const u128 v = lds16(smem + Lay::ring + L2 * (uint32_t)Lay::rs + (f & (R - 1)));
-                    st16f(o + f, v);
-                }
+            for (int32_t g = (int32_t)lane; g < total; g += 64) {
+                const uint32_t e = own[g];
+                const uint32_t L2 = e & 63u, k = e >> 6;
+                uint8_t *o = (uint8_t *)(uintptr_t)tab_out[L2];
+                const int32_t f = (int32_t)tab_fl[L2] + 16 * (int32_t)k;
+                const u128 v = lds16(smem + Lay::ring + L2 * (uint32_t)R + (f & (R - 1)));
+                if (!(TYCHE_ABLATE & 2048)) st16f(o + f, v);
+                else if (v == (u128)0x1234567) o[0] = 1;   // timing only: keeps the LDS read
             }
             asm volatile("" ::: "memory");
         }
@@ -289,9 +321,9 @@ extern "C" int tyche_debug_lc_profile(unsigned long long *host16, int reset) {
 
 hipError_t launch_lz4_decode_lc(const tyche_batch_t &b, uint32_t in_cap, uint32_t out_cap, hipStream_t s) {
     if (b.count == 0) return hipSuccess;
-    const long r = knob("LZ4_LC_RING", 256);
-    const void *k = r == 512 ? (const void *)lz4_decode_lc_kernel<512> : (const void *)lz4_decode_lc_kernel<256>;
-    const size_t lds = r == 512 ? LCL<512>::total : LCL<256>::total;
+    const long r = knob("LZ4_LC_RING", 128);
+    const void *k = r == 256 ? (const void *)lz4_decode_lc_kernel<256> : (const void *)lz4_decode_lc_kernel<128>;
+    const size_t lds = r == 256 ? LCL<256>::total : LCL<128>::total;
     const size_t ncu = prepare_launch(k);
     size_t waves = waves_per_cu(k, lds);
     const long env_waves = knob("LZ4_LC_WAVES", 0);

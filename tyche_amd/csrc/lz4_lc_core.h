@@ -19,9 +19,9 @@
 #define LC_BARRIER() asm volatile("" ::: "memory")
 #endif
 
-constexpr int32_t kLC = 8;           // record slots per chunk (unrolled)
+constexpr int32_t kLC = 7;           // record slots per chunk (unrolled)
 constexpr int32_t kLW = 64;          // window bytes
-constexpr int32_t kLWS = kLW + 32;   // + 16 B slack either side
+constexpr int32_t kLWS = kLW;   // window stride: reads past a window's end land in the next (unused bytes)
 
 // 16 bytes at byte position p of an 8-aligned LDS buffer (no wrap), as lo : hi
 LC_FN void get16(const uint8_t *base, int32_t p, uint64_t &lo, uint64_t &hi) {
@@ -66,7 +66,7 @@ struct LPage {
     size_t idx;
     int32_t ip;       // next stream byte the parse reads (a token, or the offset after a literal run)
     int32_t op;       // output bytes emitted into records
-    int32_t fl;       // output bytes in HBM (a multiple of 64 until the page ends)
+    int32_t fl;       // output bytes in HBM (a multiple of 16 until the page ends)
     int32_t wb;       // stream position of window byte 0 (a multiple of 16)
     uint64_t tail;
     int32_t lp, lrem;     // literal run in progress: stream position, bytes left
@@ -77,12 +77,19 @@ struct LPage {
 
 enum : int32_t { kLParse = 0, kLCut = 1, kLEnd = 2 };
 
-// Output bytes one chunk may emit.  A far match part reads its source from HBM
-// in stage 1 (two 16-byte loads from src): src + 32 <= op0 + budget - (R - 31) + 32
-// must stay below the flushed position fl >= op0 - 63, so budget <= R - 127;
-// 9 more bytes of margin.
+// Ring arithmetic (stage 4 flushes whole 16-byte pieces, so at a chunk's start
+// the bytes in HBM reach fl >= op0 - 15; a record part at output position d has
+// written at most up to d + 23 before it reads its source: the qwords of put16):
+//  * a near source [d - off, d - off + 16) is still in the ring of R bytes while
+//    off <= R - 24 (lc_near): larger offsets are far, read from HBM in stage 1;
+//  * a far source's used bytes end at d + n2 - off <= op0 + budget - (R - 23),
+//    below fl when budget <= R - 39; the chunk's writes (up to op0 + budget + 23)
+//    must not reach the unflushed bytes [fl, op0) a ring turn later: the same
+//    bound.  So budget = R - 40.
 template <int32_t R>
-constexpr int32_t lc_budget() { return R - 136; }
+constexpr int32_t lc_near() { return R - 24; }
+template <int32_t R>
+constexpr int32_t lc_budget() { return R - 40; }
 
 // record: literal part window position (6 bits) and length (<= 15), match part
 // length (<= 32), offset (16 bits)
@@ -150,7 +157,7 @@ LC_FN int32_t parse_fast(LPage &P, const uint8_t *w16, int32_t op0, uint32_t &re
         k = 2;
     if (k == 1) {
         const int32_t moff = isA ? P.moff : off;
-        far = n2 > 0 && moff > R - 32;
+        far = n2 > 0 && moff > lc_near<R>();
         src = P.op + n1 - moff;
         rec = lc_rec(n1 > 0 ? (isB ? P.lp - P.wb : x + 1) : 0, n1, n2, moff);
         P.op += n1 + n2;
@@ -201,17 +208,17 @@ LC_FN bool parse_slot(LPage &P, const uint8_t *w16, int32_t op0, bool deep, int3
             st = kLCut;
             return false;
         }
-        if (P.op + lit > P.C - kMfLimit || ip + pos + lit > P.L - 8) {
-            if (ip + pos + lit != P.L || P.op + lit > P.C) {
-                rv = -(ip + pos) - 1;
-                st = kLEnd;
-                return false;
-            }
-            P.term = 1;   // the last literal run (lz4.c:1155-1163)
-        } else {
-            P.hdr = 1;
-            P.mtok = (int32_t)(token & 15u);
+        const bool last = P.op + lit > P.C - kMfLimit || ip + pos + lit > P.L - 8;   // the last literal run
+        if (last && (ip + pos + lit != P.L || P.op + lit > P.C)) {                   // (lz4.c:1155-1163)
+            rv = -(ip + pos) - 1;
+            st = kLEnd;
+            return false;
         }
+        // both fields written on both paths: a store of 1 to one or the other through a selected
+        // address would put the lane state in scratch memory
+        P.term = last ? 1 : 0;
+        P.hdr = last ? 0 : 1;
+        P.mtok = (int32_t)(token & 15u);
         P.lp = ip + pos;
         P.lrem = lit;
         P.ip = ip + pos + lit;
@@ -280,7 +287,7 @@ LC_FN bool parse_slot(LPage &P, const uint8_t *w16, int32_t op0, bool deep, int3
         st = kLCut;
         return false;
     }
-    far = n2 > 0 && P.moff > R - 32;
+    far = n2 > 0 && P.moff > lc_near<R>();
     src = P.op + n1 - P.moff;
     // window position of the literal part (0 without one: a match continuation's lp may lie before the window)
     rec = lc_rec(n1 > 0 ? P.lp - P.wb : 0, n1, n2, P.moff);
@@ -296,8 +303,8 @@ LC_FN bool parse_slot(LPage &P, const uint8_t *w16, int32_t op0, bool deep, int3
 }
 
 // Stage 3: the chunk's records into the ring, from output position d on.
-// farv[2t], farv[2t + 1] hold the 32 source bytes of record t's match part when
-// that part is far.
+// farv[2t], farv[2t + 1] hold the source bytes of record t's match part when that
+// part is far (the second only when it is longer than 16 bytes).
 // Slots 0..kLC-1 hold the fast path's records (the first nrec of them), slot
 // kLC the general path's one (when gen).
 template <int32_t R>
@@ -316,7 +323,7 @@ LC_FN void copy_records(uint8_t *ring, const uint8_t *w16, int32_t d, uint64_t &
                 d += n1;
             }
             if (n2 > 0) {
-                const bool far = off > R - 32;
+                const bool far = off > lc_near<R>();
                 const int32_t h1 = min(n2, 16);
                 uint64_t lo, hi;
                 if (far) {
