@@ -21,7 +21,20 @@ using std::min;
 #define BF_FN static inline
 #define BF_ALIGNBYTE(a, b, c) ((uint32_t)(((((uint64_t)(a)) << 32) | (uint64_t)(b)) >> (8u * ((c) & 3u))))
 #define LC_FN static inline
+#define LC_Q(base, k) ((base) + ((uint32_t)(k) << 3))   // plain arrays (the kernel interleaves lanes)
 #define LC_RCP(x) (1.0f / (x))
+static inline uint32_t lc_perm_host(uint32_t hi, uint32_t lo, uint32_t sel) {   // v_perm_b32
+    const uint64_t v = ((uint64_t)hi << 32) | lo;
+    uint32_t d = 0;
+    for (int t = 0; t < 4; t++) {
+        const uint32_t x = (sel >> (8 * t)) & 0xFFu;
+        const uint32_t b = x < 8 ? (uint32_t)((v >> (8 * x)) & 0xFFu) : (x == 12 ? 0u : 0xFFu);
+        d |= b << (8 * t);
+    }
+    return d;
+}
+#define LC_PERM(hi, lo, sel) lc_perm_host((hi), (lo), (sel))
+static inline void lc_lut_load(const uint32_t *lut, int32_t c, uint32_t *ent) { memcpy(ent, lut + 12 * c, 48); }
 #define LC_BARRIER() \
     do {             \
     } while (0)
@@ -65,6 +78,12 @@ static void fetch_far(const LPage &P, uint32_t rec, int32_t src, u128 *f) {
     f[1] = n2 > 16 ? ld16(b + 16) : 0;
 }
 
+static uint32_t g_lut[17 * kLutStride];
+static bool g_lut_ready = [] {
+    for (int32_t c = 0; c <= 16; c++) lc_lut_entry(c, g_lut + kLutStride * c);
+    return true;
+}();
+
 template <int32_t R>
 static int lc_decode(const uint8_t *in, int32_t L, uint8_t *out, int32_t C) {
     if (C == 0) return (L == 1 && in[0] == 0) ? 0 : -1;
@@ -90,6 +109,8 @@ static int lc_decode(const uint8_t *in, int32_t L, uint8_t *out, int32_t C) {
         uint32_t rec[kLC + 1];
         u128 farv[2 * kLC + 2];
         bool go = true, gen = false;
+        uint64_t wq[4];
+        lc_wread(w16, lc_x0(P), wq);
         int32_t need_gen = 0;
         for (int32_t t = 0; t < kLC; t++) {
             rec[t] = 0;
@@ -97,7 +118,7 @@ static int lc_decode(const uint8_t *in, int32_t L, uint8_t *out, int32_t C) {
             if (go) {
                 bool far = false;
                 int32_t src = 0;
-                const int32_t k = getenv("LC_SLOW") ? 2 : parse_fast<R>(P, w16, op0, rec[t], far, src);
+                const int32_t k = getenv("LC_SLOW") ? 2 : parse_fast<R>(P, w16, op0, rec[t], far, src, wq);
                 if (k == 1) {
                     nrec = t + 1;
                     if (far) fetch_far(P, rec[t], src, farv + 2 * t);
@@ -113,10 +134,12 @@ static int lc_decode(const uint8_t *in, int32_t L, uint8_t *out, int32_t C) {
         if (need_gen) {
             bool far = false;
             int32_t src = 0;
-            if (parse_slot<R>(P, w16, op0, nrec == 0, st, rv, rec[kLC], far, src)) {
-                gen = true;
-                if (far) fetch_far(P, rec[kLC], src, farv + 2 * kLC);
+            gen = parse_slot<R>(P, w16, op0, false, st, rv, rec[kLC], far, src);
+            if (!gen && nrec == 0 && st == kLCut) {   // no progress: the deep retry, as the kernel
+                st = kLParse;
+                gen = parse_slot<R>(P, w16, op0, true, st, rv, rec[kLC], far, src);
             }
+            if (gen && far) fetch_far(P, rec[kLC], src, farv + 2 * kLC);
         }
         const bool ended = st == kLEnd;
         const int32_t nwb = (P.lrem > 0 ? P.lp : P.ip) & ~15;
@@ -139,7 +162,7 @@ static int lc_decode(const uint8_t *in, int32_t L, uint8_t *out, int32_t C) {
             }
         }
         uint64_t tail = P.tail;
-        copy_records<R>(ring, w16, op0, tail, rec, farv, nrec, gen);
+        copy_records<R>(ring, w16, op0, tail, rec, farv, nrec, gen, g_lut);
         P.tail = tail;
         const int32_t lend = (ended && rv < 0) ? P.fl : (P.op & ~15);
         for (int32_t f = P.fl; f + 16 <= lend; f += 16) memcpy(out + f, ring + (f & (R - 1)), 16);

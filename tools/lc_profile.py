@@ -13,8 +13,9 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from tyche_amd import _lib, codec  # noqa: E402
 
-NAMES = {1: "stage1_parse", 2: "window_issue", 3: "stage3_copy", 4: "stage4_flush", 5: "page_switch",
-         7: "loop_top_window_store"}
+NAMES = {1: "parse_slots_0_1", 2: "store_drain_wait", 3: "parse_slots_2up+far_issue", 4: "general_slot",
+         5: "window_issue", 6: "copy(far_wait)", 7: "window_wait+store", 8: "flush", 10: "tails+page_switch",
+         9: "loop_top"}
 
 
 def main():
@@ -36,8 +37,9 @@ def main():
     v = list(buf)
     tot = sum(v[k] for k in NAMES)
     chunks = max(v[0], 1)
-    print(f"pages {n}  wave-chunks {v[0]} ({v[0] * 64 / n:.0f} per page-lane)  lanes with records per chunk "
-          f"{v[8] / chunks:.1f}  lines flushed per chunk {v[9] / chunks:.1f}  page ends per chunk {v[10] / chunks:.2f}")
+    print(f"pages {n}  wave-chunks {v[0]} ({v[0] * 64 / n:.0f} per page-lane)  general slot taken in "
+          f"{100.0 * v[12] / chunks:.1f} % of chunks  pieces flushed per chunk {v[13] / chunks:.1f}  page ends per chunk "
+          f"{v[14] / chunks:.2f}")
     for k, name in NAMES.items():
         print(f"  {name:20s} {100.0 * v[k] / max(tot, 1):5.1f} %   {v[k] / chunks:8.0f} cycles per wave-chunk")
 

@@ -46,29 +46,55 @@
 namespace tyche {
 
 // Optional stage profile (diagnostic build only: -DTYCHE_PROFILE, tools/lc_profile.py):
-// shader cycles per stage summed over waves by lane 0, and event counts.
+// shader cycles per stage and event counts, summed per wave in scalar registers and added to
+// g_lcprof once when the wave ends (an atomic per stamp would itself sit in vmcnt and be
+// waited for by the stage that follows).
 #ifdef TYCHE_PROFILE
 __device__ unsigned long long g_lcprof[16];
-#define LPROF_DECL unsigned long long _pt = clock64();
-#define LPROF_MARK(k)                                                          \
-    do {                                                                       \
-        unsigned long long _n = clock64();                                     \
-        if (lane == 0) atomicAdd(&g_lcprof[k], _n - _pt);                      \
-        _pt = _n;                                                              \
+#define LPROF_DECL                                  \
+    unsigned long long _pt = clock64(), _acc[16]; \
+    for (int _k = 0; _k < 16; _k++) _acc[_k] = 0;
+#define LPROF_MARK(k)                  \
+    do {                               \
+        unsigned long long _n = clock64(); \
+        _acc[k] += _n - _pt;           \
+        _pt = _n;                      \
     } while (0)
-#define LPROF_ADD(k, v) do { if (lane == 0) atomicAdd(&g_lcprof[k], (unsigned long long)(v)); } while (0)
+#define LPROF_ADD(k, v) do { _acc[k] += (unsigned long long)(v); } while (0)
+#define LPROF_END                                                              \
+    do {                                                                       \
+        if (lane == 0)                                                         \
+            for (int _k = 0; _k < 16; _k++) atomicAdd(&g_lcprof[_k], _acc[_k]); \
+    } while (0)
 #else
 #define LPROF_DECL
 #define LPROF_MARK(k) do { } while (0)
 #define LPROF_ADD(k, v) do { } while (0)
+#define LPROF_END do { } while (0)
 #endif
 
 namespace {
 
+// the match-copy table entry of class c (lz4_lc_core.h): 9 u32 of a 48-byte LDS entry
+__device__ __forceinline__ void lc_lut_load(const uint32_t *lut, int32_t c, uint32_t *ent) {
+    const uint8_t *p = (const uint8_t *)lut + 48 * c;
+    const uint64_t a = lq(p), b = lq(p + 8), x = lq(p + 16), y = lq(p + 24);
+    ent[0] = (uint32_t)a;
+    ent[1] = (uint32_t)(a >> 32);
+    ent[2] = (uint32_t)b;
+    ent[3] = (uint32_t)(b >> 32);
+    ent[4] = (uint32_t)x;
+    ent[5] = (uint32_t)(x >> 32);
+    ent[6] = (uint32_t)y;
+    ent[7] = (uint32_t)(y >> 32);
+    ent[8] = ld32(p + 32);
+}
+
 #include "lz4_lc_core.h"
 
-// LDS of one wave: the 64 windows first (a parse read may run up to 32 bytes past
-// its window, into the next one or the rings), the 64 rings, the flush tables.
+// LDS of one wave: the 64 windows first (8 rows of 64 interleaved qwords; a parse
+// read may run up to 4 rows past them, into the rings), the 64 rings (R / 8 rows),
+// the flush tables.
 template <int32_t R>
 struct LCL {
     static constexpr uint32_t win = 0;
@@ -77,7 +103,8 @@ struct LCL {
     static constexpr uint32_t tab_fl = tab_out + 64u * 8u;                // 64 x u32: first pending piece
     static constexpr int32_t max_pieces = (lc_budget<R>() + 15) / 16;     // 16-byte pieces per lane per chunk
     static constexpr uint32_t own = tab_fl + 64u * 4u;                    // 64 x max_pieces x u16
-    static constexpr uint32_t total = own + ((64u * (uint32_t)max_pieces * 2u + 15u) & ~15u);
+    static constexpr uint32_t lut = own + ((64u * (uint32_t)max_pieces * 2u + 15u) & ~15u);   // match-copy table
+    static constexpr uint32_t total = lut + (uint32_t)kLutBytes;
 };
 
 // page `idx` of the batch (its metadata; src may be read for the C == 0 case)
@@ -123,19 +150,31 @@ __device__ __forceinline__ u128 wshift(u128 v, uint32_t k) {
     k &= 0xFFu;
     return k >= 16u ? (u128)0 : (k == 0u ? v : v >> (8u * k));
 }
+// 16-byte piece j of a lane's window / a ring piece at qword k (even), in the interleaved layout
+__device__ __forceinline__ void lc_put_piece(uint8_t *base, int32_t k, u128 v) {
+    lq(LC_Q(base, k), (uint64_t)v);
+    lq(LC_Q(base, k + 1), (uint64_t)(v >> 64));
+}
+__device__ __forceinline__ u128 lc_get_piece(const uint8_t *base, int32_t k) {
+    return (u128)lq(LC_Q(base, k)) | ((u128)lq(LC_Q(base, k + 1)) << 64);
+}
 __device__ __forceinline__ void wstore(uint8_t *w16, const LWin &w) {
     if (w.sh == 0) {
-        lds16(w16, w.c0);
-        lds16(w16 + 16, w.c1);
-        lds16(w16 + 32, w.c2);
-        lds16(w16 + 48, w.c3);
+        lc_put_piece(w16, 0, w.c0);
+        lc_put_piece(w16, 2, w.c1);
+        lc_put_piece(w16, 4, w.c2);
+        lc_put_piece(w16, 6, w.c3);
     } else {
-        lds16(w16, wshift(w.c0, w.sh));
-        lds16(w16 + 16, wshift(w.c1, w.sh >> 8));
-        lds16(w16 + 32, wshift(w.c2, w.sh >> 16));
-        lds16(w16 + 48, wshift(w.c3, w.sh >> 24));
+        lc_put_piece(w16, 0, wshift(w.c0, w.sh));
+        lc_put_piece(w16, 2, wshift(w.c1, w.sh >> 8));
+        lc_put_piece(w16, 4, wshift(w.c2, w.sh >> 16));
+        lc_put_piece(w16, 6, wshift(w.c3, w.sh >> 24));
     }
 }
+
+// s_waitcnt vmcnt(0) (expcnt, lgkmcnt not waited), as a builtin so the compiler's own wait
+// placement knows of it
+constexpr int kVmDrain = 0x0F70;
 
 // starts the lane on page idx or a later one of its stride (pages with an
 // immediate result -- empty capacity, empty stream, over the launch's sizing --
@@ -162,6 +201,9 @@ __device__ bool lpage_start(const tyche_batch_t &b, uint32_t in_cap, uint32_t ou
             P.tail = 0;
             P.lp = P.lrem = P.moff = P.mrem = P.mtok = P.hdr = P.term = 0;
             wstore(w16, wload(P.in, 0, P.L));
+            // every metadata load done here, where this path waits anyway: a load still in flight
+            // at the loop's back edge would make the compiler drain all stores at the loop's top
+            __builtin_amdgcn_s_waitcnt(kVmDrain);
             return true;
         }
         b.results[idx] = rv;
@@ -182,23 +224,29 @@ __device__ __forceinline__ void far_load(const LPage &P, bool far, int32_t src, 
 }
 
 template <int32_t R>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void lz4_decode_lc_kernel(tyche_batch_t b, uint32_t in_cap, uint32_t out_cap) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void lz4_decode_lc_kernel(tyche_batch_t b, uint32_t in_cap, uint32_t out_cap) {
     typedef LCL<R> Lay;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t lane = threadIdx.x;
-    uint8_t *ring = smem + Lay::ring + lane * (uint32_t)R;
-    uint8_t *w16 = smem + Lay::win + lane * (uint32_t)kLWS;   // window byte 0
+    uint8_t *ring = smem + Lay::ring + lane * 8u;   // qword-interleaved (LC_Q)
+    uint8_t *w16 = smem + Lay::win + lane * 8u;     // window byte 0, interleaved likewise
     uint64_t *tab_out = (uint64_t *)(smem + Lay::tab_out);
     uint32_t *tab_fl = (uint32_t *)(smem + Lay::tab_fl);
     uint16_t *own = (uint16_t *)(smem + Lay::own);
+    const uint32_t *lut = (const uint32_t *)(smem + Lay::lut);
     const size_t G = (size_t)gridDim.x * 64u;
+    if (lane <= 16) {   // the match-copy table, one entry per lane (the wave's later LDS reads see it)
+        uint32_t ent[kLutStride];
+        lc_lut_entry((int32_t)lane, ent);
+        for (int32_t j = 0; j < kLutStride; j++) ld32(smem + Lay::lut + 48u * lane + 4u * (uint32_t)j, ent[j]);
+    }
 
     LPage P;
     bool live = lpage_start(b, in_cap, out_cap, (size_t)blockIdx.x * 64u + lane, G, P, w16);
     LPROF_DECL
     while (__builtin_amdgcn_ballot_w64(live) != 0) {
         LPROF_ADD(0, 1);
-        LPROF_MARK(7);
+        LPROF_MARK(9);   // loop back edge and top
         // ---- stage 1: records into registers; far sources loaded as they are found
         const int32_t op0 = P.op;
         int32_t st = live ? kLParse : kLCut, rv = 0, nrec = 0;
@@ -206,13 +254,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void lz
         u128 farv[2 * kLC + 2];
         bool go = live, gen = false;
         int32_t need_gen = 0;
+        uint64_t wq[4];   // the next slot's window qwords (parse_fast)
+        lc_wread(w16, lc_x0(P), wq);
+        bool far0 = false, far1 = false;
+        int32_t src0 = 0, src1 = 0;
 #pragma unroll
         for (int32_t t = 0; t < kLC; t++) {
             rec[t] = 0;
             bool far = false;
             int32_t src = 0;
             if (go) {
-                const int32_t k = parse_fast<R>(P, w16, op0, rec[t], far, src);
+                const int32_t k = parse_fast<R>(P, w16, op0, rec[t], far, src, wq);
                 if (k == 1) {
                     nrec = t + 1;
                 } else {
@@ -221,21 +273,46 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void lz
                     if (k == 0 && t != 0) st = kLCut;
                 }
             }
-            // the far source (below fl: stage 4 of an earlier chunk wrote it, lc_budget), loaded
-            // outside any branch so the registers are only waited for in stage 3
-            far_load(P, far, src, rec[t], farv[2 * t], farv[2 * t + 1]);
+            // The far sources lie below fl: stage 4 of an earlier chunk stored them, on other
+            // lanes -- the last chunk's stores must have completed before the first one is read.
+            // They drain during the parse of slots 0 and 1; then the loads go out, outside any
+            // branch, so their registers are only waited for in stage 3.
+            if (t == 0) {
+                far0 = far;
+                src0 = src;
+            } else if (t == 1) {
+                far1 = far;
+                src1 = src;
+                LPROF_MARK(1);   // slots 0, 1
+                __builtin_amdgcn_s_waitcnt(kVmDrain);
+                LPROF_MARK(2);   // the store drain
+                asm volatile("" ::: "memory");
+                far_load(P, far0, src0, rec[0], farv[0], farv[1]);
+                far_load(P, far1, src1, rec[1], farv[2], farv[3]);
+            } else {
+                far_load(P, far, src, rec[t], farv[2 * t], farv[2 * t + 1]);
+            }
         }
-        // one record of the general path (parse_slot) for the lanes that stopped on it
+        LPROF_MARK(3);   // slots 2.. and their far loads
+        // one record of the general path (parse_slot) for the lanes that stopped on it; a lane
+        // whose chunk made no progress (a length field longer than the window) takes it again
+        // reading the stream straight from HBM, in its own rarely taken branch (window bytes and
+        // HBM bytes in one code path would make every LDS byte read wait for the far loads)
         rec[kLC] = 0;
         {
             bool far = false;
             int32_t src = 0;
             if (__builtin_amdgcn_ballot_w64(need_gen != 0) != 0 && need_gen)
-                gen = parse_slot<R>(P, w16, op0, nrec == 0, st, rv, rec[kLC], far, src);
+                gen = parse_slot<R>(P, w16, op0, false, st, rv, rec[kLC], far, src);
+            const bool deep = need_gen && !gen && nrec == 0 && st == kLCut;
+            if (__builtin_amdgcn_ballot_w64(deep) != 0 && deep) {
+                st = kLParse;
+                gen = parse_slot<R>(P, w16, op0, true, st, rv, rec[kLC], far, src);
+            }
             far_load(P, far && gen, src, rec[kLC], farv[2 * kLC], farv[2 * kLC + 1]);
         }
-        LPROF_MARK(1);
-        LPROF_ADD(8, __builtin_amdgcn_ballot_w64(need_gen != 0) != 0);
+        LPROF_MARK(4);   // the general slot
+        LPROF_ADD(12, __builtin_amdgcn_ballot_w64(need_gen != 0) != 0);
         // ---- the next window (the lane's next chunk), loaded behind the far sources
         const bool ended = live && st == kLEnd;
         const int32_t nwb = (P.lrem > 0 ? P.lp : P.ip) & ~15;   // the next stream byte the parse needs
@@ -247,15 +324,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void lz
             gen = false;
         }
 
-        LPROF_MARK(2);
+        LPROF_MARK(5);   // window issue
         // ---- stage 3: copy the records into the ring (aligned qwords only)
         if (live) {
             uint64_t tail = P.tail;
-            copy_records<R>(ring, w16, op0, tail, rec, farv, nrec, gen);
+            copy_records<R>(ring, w16, op0, tail, rec, farv, nrec, gen, lut);
             P.tail = tail;
         }
+        LPROF_MARK(6);   // copy (far-load wait included)
 
-        LPROF_MARK(3);
+        // the next window into LDS now, before stage 4 issues its stores: this wait covers
+        // loads only, and the stores drain during the next chunk's parse
+        if (live && !ended) {
+            P.wb = nwb;
+            wstore(w16, nw);
+        }
+        LPROF_MARK(7);   // window wait and store
         // ---- stage 4: the finished 16-byte pieces of all 64 pages, one per lane and store
         // instruction (a page's pieces on neighbouring lanes: whole lines per few lanes)
         const int32_t lend = !live ? 0 : (ended && rv < 0) ? P.fl : (P.op & ~15);
@@ -263,32 +347,58 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void lz
         const int32_t incl = wave_incl_sum(nl);
         const int32_t total = (int32_t)rdlane((uint32_t)incl, 63);
         if (total > 0) {
+            // piece g of the wave (g = lane + 64 * it) belongs to the lane own[g] names; the
+            // iterations' LDS reads are issued phase by phase (table entry, page, ring piece) so
+            // the whole flush waits three LDS round trips, not three per iteration
+            constexpr int32_t MP = Lay::max_pieces;
             tab_out[lane] = (uint64_t)(uintptr_t)P.out;
             tab_fl[lane] = (uint32_t)P.fl;
-            for (int32_t k = 0; k < nl; k++) own[incl - nl + k] = (uint16_t)(lane | ((uint32_t)k << 6));
+#pragma unroll
+            for (int32_t k = 0; k < MP; k++)
+                if (k < nl) own[incl - nl + k] = (uint16_t)(lane | ((uint32_t)k << 6));
             asm volatile("" ::: "memory");
-            for (int32_t g = (int32_t)lane; g < total; g += 64) {
-                const uint32_t e = own[g];
-                const uint32_t L2 = e & 63u, k = e >> 6;
-                uint8_t *o = (uint8_t *)(uintptr_t)tab_out[L2];
-                const int32_t f = (int32_t)tab_fl[L2] + 16 * (int32_t)k;
-                const u128 v = lds16(smem + Lay::ring + L2 * (uint32_t)R + (f & (R - 1)));
-                if (!(TYCHE_ABLATE & 2048)) st16f(o + f, v);
-                else if (v == (u128)0x1234567) o[0] = 1;   // timing only: keeps the LDS read
+            const int32_t iters = (total + 63) >> 6;   // wave-uniform
+            uint32_t e[MP];
+#pragma unroll
+            for (int32_t it = 0; it < MP; it++) e[it] = it < iters ? (uint32_t)own[lane + 64 * it] : 0u;
+            uint64_t o[MP];
+            int32_t f[MP];
+#pragma unroll
+            for (int32_t it = 0; it < MP; it++) {
+                o[it] = 0;
+                f[it] = 0;
+                if (it < iters) {
+                    const uint32_t L2 = e[it] & 63u;
+                    o[it] = tab_out[L2];
+                    f[it] = (int32_t)tab_fl[L2] + 16 * (int32_t)(e[it] >> 6);
+                }
+            }
+            u128 v[MP];
+#pragma unroll
+            for (int32_t it = 0; it < MP; it++)
+                v[it] = it < iters ? lc_get_piece(smem + Lay::ring + (e[it] & 63u) * 8u, (f[it] >> 3) & (R / 8 - 1))
+                                   : (u128)0;
+#pragma unroll
+            for (int32_t it = 0; it < MP; it++) {
+                if ((int32_t)lane + 64 * it < total) {
+                    uint8_t *dst = (uint8_t *)(uintptr_t)o[it] + f[it];
+                    if (!(TYCHE_ABLATE & 2048)) st16f(dst, v[it]);
+                    else if (v[it] == (u128)0x1234567) dst[0] = 1;   // timing only: keeps the LDS read
+                }
             }
             asm volatile("" ::: "memory");
         }
         if (live) P.fl = lend > P.fl ? lend : P.fl;
-        LPROF_MARK(4);
-        LPROF_ADD(9, total);
-        LPROF_ADD(10, __builtin_popcountll(__builtin_amdgcn_ballot_w64(ended)));
+        LPROF_MARK(8);   // flush
+        LPROF_ADD(13, total);
+        LPROF_ADD(14, __builtin_popcountll(__builtin_amdgcn_ballot_w64(ended)));
 
-        // ---- stage 5: the page's last bytes; the next page; the next window
+        // ---- stage 5: the page's last bytes; the next page
         if (ended) {
             if (rv >= 0) {
                 // bytes [fl, op): whole 16-byte pieces, then single bytes
                 for (int32_t a = P.fl; a < P.op; a += 16) {
-                    const u128 v = lds16(ring + (a & (R - 1)));
+                    const u128 v = lc_get_piece(ring, (a >> 3) & (R / 8 - 1));
                     if (a + 16 <= P.op) {
                         st16(P.out + a, v);
                     } else {
@@ -298,13 +408,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void lz
             }
             b.results[P.idx] = rv;
             live = lpage_start(b, in_cap, out_cap, P.idx + G, G, P, w16);
-            LPROF_MARK(5);
-        } else if (live) {
-            P.wb = nwb;
-            wstore(w16, nw);
         }
+        LPROF_MARK(10);   // stage 5: tails, page switch (uniform position: the stamps stay scalar)
         asm volatile("" ::: "memory");
     }
+    LPROF_END;
 }
 
 }  // namespace

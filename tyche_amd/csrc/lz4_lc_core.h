@@ -18,15 +18,65 @@
 #ifndef LC_BARRIER
 #define LC_BARRIER() asm volatile("" ::: "memory")
 #endif
+// Qword k of a lane's LDS buffer (ring or window) given the lane's base.  The
+// kernel interleaves the 64 lanes' buffers qword by qword (qword k of lane L at
+// (64 k + L) * 8): a wave-wide qword access then maps lane L to bank pair 2L
+// whatever the positions (lanes 0-31 and 32-63 in separate cycles), where
+// lane-contiguous buffers collide at random.  The host emulator's buffers are
+// plain arrays.
+#ifndef LC_Q
+#define LC_Q(base, k) ((base) + ((uint32_t)(k) << 9))
+#endif
+#ifndef LC_PERM
+#define LC_PERM(hi, lo, sel) __builtin_amdgcn_perm((hi), (lo), (sel))   // v_perm_b32
+#endif
+
+// The match-copy table, one entry per offset class c = min(off, 16): the
+// v_perm_b32 selectors that turn the 16 bytes at d - off (of which only the
+// first off are the match's when off < 16) into the match's first 16 bytes,
+// byte i = byte (i mod off) -- dword j = perm(s1, s0, sel[j]) | perm(s3, s2,
+// sel[4 + j]), selector 0x0C giving a zero byte -- and e = the smallest multiple
+// of off that is >= 16 (the second half's source distance).  Class 16 is the
+// identity (no overlap); class 0 (offset 0: a malformed stream the reference
+// accepts, undefined bytes) gives zeros.
+constexpr int32_t kLutStride = 12;   // u32 per entry: 8 selectors, e, 3 unused (16-byte aligned entries)
+constexpr int32_t kLutBytes = 17 * kLutStride * 4;
+LC_FN void lc_lut_entry(int32_t c, uint32_t *ent) {
+    for (int32_t j = 0; j < 4; j++) {
+        uint32_t a = 0, b = 0;
+        for (int32_t t = 0; t < 4; t++) {
+            const int32_t i = 4 * j + t;
+            const int32_t idx = c == 0 ? -1 : (c >= 16 ? i : i % c);
+            const uint32_t sa = idx >= 0 && idx < 8 ? (uint32_t)idx : 0x0Cu;
+            const uint32_t sb = idx >= 8 ? (uint32_t)(idx - 8) : 0x0Cu;
+            a |= sa << (8 * t);
+            b |= sb << (8 * t);
+        }
+        ent[j] = a;
+        ent[4 + j] = b;
+    }
+    ent[8] = (uint32_t)(c >= 16 ? 16 : (c > 0 ? c * ((16 + c - 1) / c) : 16));
+    ent[9] = ent[10] = ent[11] = 0;
+}
+// 16 bytes lo : hi rearranged by an entry's selectors
+LC_FN void lc_lut_apply(const uint32_t *sel, uint64_t &lo, uint64_t &hi) {
+    const uint32_t s0 = (uint32_t)lo, s1 = (uint32_t)(lo >> 32), s2 = (uint32_t)hi, s3 = (uint32_t)(hi >> 32);
+    const uint32_t d0 = LC_PERM(s1, s0, sel[0]) | LC_PERM(s3, s2, sel[4]);
+    const uint32_t d1 = LC_PERM(s1, s0, sel[1]) | LC_PERM(s3, s2, sel[5]);
+    const uint32_t d2 = LC_PERM(s1, s0, sel[2]) | LC_PERM(s3, s2, sel[6]);
+    const uint32_t d3 = LC_PERM(s1, s0, sel[3]) | LC_PERM(s3, s2, sel[7]);
+    lo = (uint64_t)d0 | ((uint64_t)d1 << 32);
+    hi = (uint64_t)d2 | ((uint64_t)d3 << 32);
+}
 
 constexpr int32_t kLC = 7;           // record slots per chunk (unrolled)
 constexpr int32_t kLW = 64;          // window bytes
-constexpr int32_t kLWS = kLW;   // window stride: reads past a window's end land in the next (unused bytes)
+constexpr int32_t kLWS = kLW;   // window bytes per lane in LDS (reads past the end land in later rows: unused bytes)
 
-// 16 bytes at byte position p of an 8-aligned LDS buffer (no wrap), as lo : hi
+// 16 bytes at byte position p >= 0 of a lane's window (no wrap), as lo : hi
 LC_FN void get16(const uint8_t *base, int32_t p, uint64_t &lo, uint64_t &hi) {
-    const int32_t a = p & ~7;
-    const uint64_t q0 = lq(base + a), q1 = lq(base + a + 8), q2 = lq(base + a + 16);
+    const int32_t k = p >> 3;
+    const uint64_t q0 = lq(LC_Q(base, k)), q1 = lq(LC_Q(base, k + 1)), q2 = lq(LC_Q(base, k + 2));
     const uint32_t s = (uint32_t)p & 7u;
     lo = funnel8(q0, q1, s);
     hi = funnel8(q1, q2, s);
@@ -34,9 +84,9 @@ LC_FN void get16(const uint8_t *base, int32_t p, uint64_t &lo, uint64_t &hi) {
 // the same from a ring of R bytes (page position p >= -8; wraps)
 template <int32_t R>
 LC_FN void ring16(const uint8_t *ring, int32_t p, uint64_t &lo, uint64_t &hi) {
-    const int32_t a = p & ~7;
-    const uint64_t q0 = lq(ring + (a & (R - 1))), q1 = lq(ring + ((a + 8) & (R - 1))),
-                   q2 = lq(ring + ((a + 16) & (R - 1)));
+    constexpr int32_t m = R / 8 - 1;
+    const int32_t k = p >> 3;   // (arithmetic shift: p >= -8 wraps correctly)
+    const uint64_t q0 = lq(LC_Q(ring, k & m)), q1 = lq(LC_Q(ring, (k + 1) & m)), q2 = lq(LC_Q(ring, (k + 2) & m));
     const uint32_t s = (uint32_t)p & 7u;
     lo = funnel8(q0, q1, s);
     hi = funnel8(q1, q2, s);
@@ -52,9 +102,11 @@ LC_FN uint64_t put16(uint8_t *ring, int32_t d, uint64_t tail, uint64_t lo, uint6
     const uint64_t o0 = keep_low(tail, lo << (8u * s), s);
     const uint64_t o1 = s ? (lo >> (64u - 8u * s)) | (hi << (8u * s)) : hi;
     const uint64_t o2 = s ? hi >> (64u - 8u * s) : 0ull;
-    lq(ring + (q0 & (R - 1)), o0);
-    lq(ring + ((q0 + 8) & (R - 1)), o1);
-    lq(ring + ((q0 + 16) & (R - 1)), o2);
+    constexpr int32_t m = R / 8 - 1;
+    const int32_t kq = q0 >> 3;
+    lq(LC_Q(ring, kq & m), o0);
+    lq(LC_Q(ring, (kq + 1) & m), o1);
+    lq(LC_Q(ring, (kq + 2) & m), o2);
     const uint32_t k = (s + (uint32_t)n) >> 3;
     return k == 0 ? o0 : (k == 1 ? o1 : o2);
 }
@@ -114,8 +166,26 @@ LC_FN uint64_t win8(uint64_t q0, uint64_t q1, uint64_t q2, uint64_t q3, uint32_t
 // path (parse_slot: the end of a long literal run and its header, long fields,
 // the last literal run, any failing check -- repeated there in the reference's
 // order).
+// The window qwords q[0..3] at (x & ~7) are read by the caller for the first
+// slot and by the slot before for every other one: as soon as a slot knows the
+// length of its sequence it reads the next slot's, at the position the next
+// slot will have if this one emits its record (the only case in which the next
+// one runs), so the read's latency overlaps this slot's checks.
+LC_FN void lc_wread(const uint8_t *w16, int32_t x, uint64_t (&q)[4]) {
+    const int32_t k = x >> 3;
+    q[0] = lq(LC_Q(w16, k));
+    q[1] = lq(LC_Q(w16, k + 1));
+    q[2] = lq(LC_Q(w16, k + 2));
+    q[3] = lq(LC_Q(w16, k + 3));
+}
+// the window position of the chunk's first token (0 when the parse resumes inside a run)
+LC_FN int32_t lc_x0(const LPage &P) {
+    return (P.lrem == 0 && P.mrem == 0 && P.hdr == 0) ? min(P.ip - P.wb, kLW) : 0;
+}
+
 template <int32_t R>
-LC_FN int32_t parse_fast(LPage &P, const uint8_t *w16, int32_t op0, uint32_t &rec, bool &far, int32_t &src) {
+LC_FN int32_t parse_fast(LPage &P, const uint8_t *w16, int32_t op0, uint32_t &rec, bool &far, int32_t &src,
+                         uint64_t (&q)[4]) {
     const int32_t room = op0 + lc_budget<R>() - P.op;   // output bytes the chunk can still take
     // a: the next part of a match
     const bool isA = P.mrem != 0 && P.lrem == 0;   // (a budget cut can leave a header read before its run's last bytes)
@@ -126,15 +196,17 @@ LC_FN int32_t parse_fast(LPage &P, const uint8_t *w16, int32_t op0, uint32_t &re
     // c: a new sequence
     const bool fresh = P.lrem == 0 && P.mrem == 0 && P.hdr == 0;
     const int32_t x = fresh ? P.ip - P.wb : 0;   // 0 <= x <= kLW at a token (the window starts at or before it)
-    const int32_t a = x & ~7;
-    const uint64_t q0 = lq(w16 + a), q1 = lq(w16 + a + 8), q2 = lq(w16 + a + 16), q3 = lq(w16 + a + 24);
+    const uint64_t q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
     const uint32_t s = (uint32_t)x & 7u;
     const uint32_t token = (uint32_t)(win8(q0, q1, q2, q3, s) & 0xFFu);
     const int32_t lit = (int32_t)(token >> 4), mn = (int32_t)(token & 15u);
+    const int32_t need = 1 + lit + (mn == 15 ? 3 : 2);   // stream bytes of the sequence
+    // the next slot's window qwords: after this sequence, or (a continuation part) at ip; a
+    // position past the window (clamped) means the next slot cannot take a fresh sequence
+    lc_wread(w16, min(fresh ? x + need : P.ip - P.wb, kLW), q);
     const uint64_t h = win8(q0, q1, q2, q3, s + 1u + (uint32_t)(lit & 15));   // lit < 15 below: s + 1 + lit <= 22
     const int32_t off = (int32_t)(h & 0xFFFFu), ext = (int32_t)((h >> 16) & 0xFFu);
     const int32_t ml = mn == 15 ? 19 + ext : mn + kMinMatch;
-    const int32_t need = 1 + lit + (mn == 15 ? 3 : 2);   // stream bytes of the sequence
     const bool fitC = x + need <= kLW;
     const bool okC = lit != 15 && !(mn == 15 && ext == 255) &&
                      P.op + lit <= P.C - kMfLimit && P.ip + 1 + lit <= P.L - 8 &&   // not the last run (lz4.c:1147)
@@ -175,7 +247,10 @@ LC_FN int32_t parse_fast(LPage &P, const uint8_t *w16, int32_t op0, uint32_t &re
 // `deep`, the chunk's first record: an extension run longer than the window)
 // straight from HBM; `miss` reports a byte that neither provides
 LC_FN uint32_t lbyte(const LPage &P, const uint8_t *w16, int32_t p, bool deep, bool &miss) {
-    if (p < P.wb + kLW) return lb(w16 + (p - P.wb));
+    if (p < P.wb + kLW) {
+        const int32_t i = p - P.wb;
+        return lb(LC_Q(w16, i >> 3) + (i & 7));
+    }
     if (deep) return sbyte(P.in, p, P.L);
     miss = true;
     return 0;
@@ -309,59 +384,49 @@ LC_FN bool parse_slot(LPage &P, const uint8_t *w16, int32_t op0, bool deep, int3
 // kLC the general path's one (when gen).
 template <int32_t R>
 LC_FN void copy_records(uint8_t *ring, const uint8_t *w16, int32_t d, uint64_t &tail, const uint32_t *rec,
-                        const u128 *farv, int32_t nrec, bool gen) {
+                        const u128 *farv, int32_t nrec, bool gen, const uint32_t *lut) {
+    // the literal source of the record after the current one is read one record ahead (the
+    // window is not written here): each record then waits for its match source only
+    uint64_t llo, lhi;
+    get16(w16, (int32_t)(rec[0] & 63u), llo, lhi);
 #pragma unroll
     for (int32_t t = 0; t <= kLC; t++) {
-        if (t < kLC ? t < nrec : gen) {
-            const uint32_t r = rec[t];
-            const int32_t lpr = (int32_t)(r & 63u), n1 = (int32_t)((r >> 6) & 15u), n2 = (int32_t)((r >> 10) & 63u),
-                          off = (int32_t)(r >> 16);
-            if (n1 > 0) {
-                uint64_t lo, hi;
-                get16(w16, lpr, lo, hi);
-                tail = put16<R>(ring, d, tail, lo, hi, n1);
-                d += n1;
-            }
-            if (n2 > 0) {
-                const bool far = off > lc_near<R>();
-                const int32_t h1 = min(n2, 16);
-                uint64_t lo, hi;
-                if (far) {
-                    lo = (uint64_t)farv[2 * t];
-                    hi = (uint64_t)(farv[2 * t] >> 64);
-                } else {
-                    ring16<R>(ring, d - off, lo, hi);
-                    if (off < h1) {
-                        // the match overlaps itself: the off bytes below d repeat
-                        // (offset 0, a malformed stream the reference accepts: undefined bytes, zeros here)
-                        u128 p = 0;
-                        if (off > 0) {
-                            p = (((u128)hi << 64) | lo) & ((((u128)1) << (8 * off)) - 1);
-                            for (int32_t len = off; len < 16; len <<= 1) p |= p << (8 * len);
-                        }
-                        lo = (uint64_t)p;
-                        hi = (uint64_t)(p >> 64);
-                    }
-                }
-                tail = put16<R>(ring, d, tail, lo, hi, h1);
-                if (n2 > 16) {
-                    // bytes 16..n2: a plain copy from 16 bytes behind a multiple of the offset that
-                    // is >= 16 (the first half, just written, repeats with that period)
-                    if (far) {
-                        lo = (uint64_t)farv[2 * t + 1];
-                        hi = (uint64_t)(farv[2 * t + 1] >> 64);
-                    } else {
-                        // e = off * ceil(16 / off) <= off + 15: the smallest period multiple >= 16 (16/off
-                        // has a fraction >= 1/15 unless off divides 16, so +0.999 rounds up exactly)
-                        const int32_t e = off >= 16 ? off : (off > 0 ? off * (int32_t)(16.0f * LC_RCP((float)off) + 0.999f) : 16);
-                        LC_BARRIER();
-                        ring16<R>(ring, d + 16 - e, lo, hi);
-                    }
-                    tail = put16<R>(ring, d + 16, tail, lo, hi, n2 - 16);
-                }
-                d += n2;
-            }
-            LC_BARRIER();
+        const uint32_t r = rec[t];
+        const bool on = t < kLC ? t < nrec : gen;
+        const int32_t n1 = on ? (int32_t)((r >> 6) & 15u) : 0, n2 = on ? (int32_t)((r >> 10) & 63u) : 0,
+                      off = (int32_t)(r >> 16);
+        uint32_t ent[12];
+        lc_lut_load(lut, min(off, 16), ent);
+        if (n1 > 0) {
+            tail = put16<R>(ring, d, tail, llo, lhi, n1);
+            d += n1;
         }
+        if (t < kLC) get16(w16, (int32_t)(rec[t + 1] & 63u), llo, lhi);
+        if (n2 > 0) {
+            const bool far = off > lc_near<R>();
+            const int32_t h1 = min(n2, 16);
+            uint64_t lo, hi;
+            ring16<R>(ring, d - off, lo, hi);
+            if (far) {
+                lo = (uint64_t)farv[2 * t];
+                hi = (uint64_t)(farv[2 * t] >> 64);
+            }
+            lc_lut_apply(ent, lo, hi);   // the period-off pattern when the match overlaps itself
+            tail = put16<R>(ring, d, tail, lo, hi, h1);
+            if (n2 > 16) {
+                // bytes 16..n2: a plain copy from e bytes back, e the smallest multiple of the offset
+                // that is >= 16 (the first half, just written, repeats with that period)
+                const int32_t e = off >= 16 ? off : (int32_t)ent[8];
+                LC_BARRIER();
+                ring16<R>(ring, d + 16 - e, lo, hi);
+                if (far) {
+                    lo = (uint64_t)farv[2 * t + 1];
+                    hi = (uint64_t)(farv[2 * t + 1] >> 64);
+                }
+                tail = put16<R>(ring, d + 16, tail, lo, hi, n2 - 16);
+            }
+            d += n2;
+        }
+        LC_BARRIER();
     }
 }
