@@ -357,7 +357,7 @@ def test_decode_lane_kernels_all_rings(tc, oracle_mod, knobs, lb, ring):
     the default, at each ring size; 0: the round-2 ring kernel), selected in-process with
     tyche_set_knob and forced on every batch size (LZ4_LANE_MIN=0): the fixtures with their exact
     return values, and seeded corruptions against the restated LZ4_decompress_safe."""
-    knobs(LZ4_LANE_LB=lb, LZ4_LANE_RING=ring, LZ4_LANE_MIN=0)
+    knobs(LZ4_LC=0, LZ4_LANE_LB=lb, LZ4_LANE_RING=ring, LZ4_LANE_MIN=0)
     test_decode_lane_path_fixtures(tc, 1)
     rng = np.random.default_rng(1000 + ring + lb)
     pages = oracle_mod.pagegen(256, 16384, seed=9, first=ring, dist=0)

@@ -603,7 +603,9 @@ constexpr int kDefaultWin = 16;
 hipError_t launch_lz4_decode_lane(const tyche_batch_t &b, uint32_t in_cap, uint32_t out_cap, hipStream_t s) {
     if (b.count == 0) return hipSuccess;
     if (knob("LZ4_QUAD", 0) != 0) return launch_lz4_decode_quad(b, in_cap, out_cap, s);
-    if (knob("LZ4_LC", 0) != 0) return launch_lz4_decode_lc(b, in_cap, out_cap, s);
+    // round 4 default: the chunked lane decoder (lz4_decode_lc.hip; 24.1 ms per 1M x 16 KiB pages
+    // vs 32.7 for the line-buffered ring kernel below, which TYCHE_LZ4_LC=0 selects)
+    if (knob("LZ4_LC", 1) != 0) return launch_lz4_decode_lc(b, in_cap, out_cap, s);
     const long env_waves = knob("LZ4_LANE_WAVES", 0);
     // line-buffered stream (round 3, default): 128-byte rings, 10 waves per CU -- 32.7 vs 34.3 ms per
     // 1M x 16 KiB pages for the ring kernel's 256-byte rings (r03 lane timing; 160 / 192-byte rings

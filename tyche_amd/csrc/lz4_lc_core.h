@@ -69,7 +69,10 @@ LC_FN void lc_lut_apply(const uint32_t *sel, uint64_t &lo, uint64_t &hi) {
     hi = (uint64_t)d2 | ((uint64_t)d3 << 32);
 }
 
-constexpr int32_t kLC = 7;           // record slots per chunk (unrolled)
+#ifndef LC_SLOTS
+#define LC_SLOTS 7
+#endif
+constexpr int32_t kLC = LC_SLOTS;   // record slots per chunk (unrolled)
 constexpr int32_t kLW = 64;          // window bytes
 constexpr int32_t kLWS = kLW;   // window bytes per lane in LDS (reads past the end land in later rows: unused bytes)
 
