@@ -378,7 +378,7 @@ def test_decode_lane_kernels_all_rings(tc, oracle_mod, knobs, lb, ring):
             assert outs[i][:r] == want[:r], i
 
 
-@pytest.mark.parametrize("ring", [128, 256])
+@pytest.mark.parametrize("ring", [128, 192, 256])
 def test_decode_lc_kernel_variants(tc, oracle_mod, knobs, ring):
     """The chunked lane-per-page decoder (lz4_decode_lc.hip) at both ring sizes, forced on every
     batch size (LZ4_LC=1, LZ4_LANE_MIN=0): the fixtures with their exact return values, seeded

@@ -71,7 +71,7 @@ def _cases(O):
     return cases
 
 
-@pytest.mark.parametrize("ring", [128, 256])
+@pytest.mark.parametrize("ring", [128, 192, 256])
 def test_lc_algorithm_vs_oracle(emul, oracle_mod, ring):
     for k, (s, cap, defined) in enumerate(_cases(oracle_mod)):
         r, out = emul(s, cap, ring)

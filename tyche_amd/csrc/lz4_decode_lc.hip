@@ -211,16 +211,32 @@ __device__ bool lpage_start(const tyche_batch_t &b, uint32_t in_cap, uint32_t ou
     return false;
 }
 
-// 32 bytes every lane without a far source reads instead (one line for the whole wave)
+// 64 bytes of zeros: the window source of a lane with no page (its loads are issued anyway, so that
+// exactly four window loads follow the far loads: lc_far_wait)
 __device__ __attribute__((aligned(64))) uint8_t g_lc_pad[64];
 
-// a record slot's far source: [src, src + 16) and, for a part over 16 bytes, [src + 16, src + 32)
-// of the page's output; the pad for lanes without one
-__device__ __forceinline__ void far_load(const LPage &P, bool far, int32_t src, uint32_t rec, u128 &f0, u128 &f1) {
+// A record slot's far source: [src, src + 16) and, for a part over 16 bytes, [src + 16, src + 32)
+// of the page's output, loaded by the lanes that have one only.  The return path of the CU's
+// vector memory (TD) is this kernel's busiest unit (r04 PMC: busy 94 % of the cycles), and a
+// load costs it per active lane.  The loads are inline asm with the destination tied to its
+// zero-initialised register, so the branch joins without a copy (a compiler-visible load in a
+// branch is joined by a copy that waits for it right there, in the next slot); the compiler
+// does not see them, and lc_far_wait waits for them before stage 3.
+__device__ __forceinline__ void far_load(const LPage &P, bool far, int32_t src, uint32_t rec, u32x4 &f0, u32x4 &f1) {
     if (TYCHE_ABLATE & 1024) far = false;   // timing only: no far loads (wrong output)
-    const bool two = far && ((rec >> 10) & 63u) > 16u;
-    f0 = ld16(far ? P.out + src : g_lc_pad);
-    f1 = ld16(two ? P.out + src + 16 : g_lc_pad + 16);
+    if (far) {
+        const uint8_t *a = P.out + src;
+        asm volatile("global_load_dwordx4 %0, %1, off" : "+v"(f0) : "v"(a) : "memory");
+        if (((rec >> 10) & 63u) > 16u) asm volatile("global_load_dwordx4 %0, %1, off offset:16" : "+v"(f1) : "v"(a) : "memory");
+    }
+}
+// every far load done: all but the four window loads issued after them (vmcnt is in order); the
+// empty asm statements tie the registers to this point, so no use moves above the wait
+template <int32_t N>
+__device__ __forceinline__ void lc_far_wait(u32x4 (&fv)[N]) {
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+#pragma unroll
+    for (int32_t i = 0; i < N; i++) asm volatile("" : "+v"(fv[i]));
 }
 
 template <int32_t R>
@@ -251,7 +267,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void lz
         const int32_t op0 = P.op;
         int32_t st = live ? kLParse : kLCut, rv = 0, nrec = 0;
         uint32_t rec[kLC + 1];
-        u128 farv[2 * kLC + 2];
+        u32x4 fv[2 * kLC + 2];   // far sources (far_load)
+#pragma unroll
+        for (int32_t i = 0; i < 2 * kLC + 2; i++) fv[i] = u32x4{0u, 0u, 0u, 0u};
         bool go = live, gen = false;
         int32_t need_gen = 0;
         uint64_t wq[4];   // the next slot's window qwords (parse_fast)
@@ -287,10 +305,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void lz
                 __builtin_amdgcn_s_waitcnt(kVmDrain);
                 LPROF_MARK(2);   // the store drain
                 asm volatile("" ::: "memory");
-                far_load(P, far0, src0, rec[0], farv[0], farv[1]);
-                far_load(P, far1, src1, rec[1], farv[2], farv[3]);
+                far_load(P, far0, src0, rec[0], fv[0], fv[1]);
+                far_load(P, far1, src1, rec[1], fv[2], fv[3]);
             } else {
-                far_load(P, far, src, rec[t], farv[2 * t], farv[2 * t + 1]);
+                far_load(P, far, src, rec[t], fv[2 * t], fv[2 * t + 1]);
             }
         }
         LPROF_MARK(3);   // slots 2.. and their far loads
@@ -309,16 +327,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void lz
                 st = kLParse;
                 gen = parse_slot<R>(P, w16, op0, true, st, rv, rec[kLC], far, src);
             }
-            far_load(P, far && gen, src, rec[kLC], farv[2 * kLC], farv[2 * kLC + 1]);
+            far_load(P, far && gen, src, rec[kLC], fv[2 * kLC], fv[2 * kLC + 1]);
         }
         LPROF_MARK(4);   // the general slot
         LPROF_ADD(12, __builtin_amdgcn_ballot_w64(need_gen != 0) != 0);
         // ---- the next window (the lane's next chunk), loaded behind the far sources
         const bool ended = live && st == kLEnd;
         const int32_t nwb = (P.lrem > 0 ? P.lp : P.ip) & ~15;   // the next stream byte the parse needs
-        LWin nw;
-        nw.c0 = nw.c1 = nw.c2 = nw.c3 = 0;
-        if (live && !ended) nw = wload(P.in, nwb, P.L);
+        const bool wlive = live && !ended;   // (lanes without a next window load the pad)
+        const LWin nw = wload(wlive ? P.in : g_lc_pad, wlive ? nwb : 0, wlive ? P.L : 64);
         if (ended && rv < 0) {   // a malformed page: its output is not defined
             nrec = 0;
             gen = false;
@@ -326,7 +343,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void lz
 
         LPROF_MARK(5);   // window issue
         // ---- stage 3: copy the records into the ring (aligned qwords only)
+        lc_far_wait(fv);
         if (live) {
+            u128 farv[2 * kLC + 2];
+#pragma unroll
+            for (int32_t i = 0; i < 2 * kLC + 2; i++) farv[i] = __builtin_bit_cast(u128, fv[i]);
             uint64_t tail = P.tail;
             copy_records<R>(ring, w16, op0, tail, rec, farv, nrec, gen, lut);
             P.tail = tail;
@@ -337,7 +358,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void lz
         // loads only, and the stores drain during the next chunk's parse
         if (live && !ended) {
             P.wb = nwb;
-            wstore(w16, nw);
+            wstore(w16, nw);   // (the compiler waits for the window loads here)
         }
         LPROF_MARK(7);   // window wait and store
         // ---- stage 4: the finished 16-byte pieces of all 64 pages, one per lane and store
@@ -376,7 +397,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void lz
             u128 v[MP];
 #pragma unroll
             for (int32_t it = 0; it < MP; it++)
-                v[it] = it < iters ? lc_get_piece(smem + Lay::ring + (e[it] & 63u) * 8u, (f[it] >> 3) & (R / 8 - 1))
+                v[it] = it < iters ? lc_get_piece(smem + Lay::ring + (e[it] & 63u) * 8u, lc_row<R>(f[it] >> 3))
                                    : (u128)0;
 #pragma unroll
             for (int32_t it = 0; it < MP; it++) {
@@ -398,7 +419,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void lz
             if (rv >= 0) {
                 // bytes [fl, op): whole 16-byte pieces, then single bytes
                 for (int32_t a = P.fl; a < P.op; a += 16) {
-                    const u128 v = lc_get_piece(ring, (a >> 3) & (R / 8 - 1));
+                    const u128 v = lc_get_piece(ring, lc_row<R>(a >> 3));
                     if (a + 16 <= P.op) {
                         st16(P.out + a, v);
                     } else {
@@ -429,9 +450,11 @@ extern "C" int tyche_debug_lc_profile(unsigned long long *host16, int reset) {
 
 hipError_t launch_lz4_decode_lc(const tyche_batch_t &b, uint32_t in_cap, uint32_t out_cap, hipStream_t s) {
     if (b.count == 0) return hipSuccess;
-    const long r = knob("LZ4_LC_RING", 128);
-    const void *k = r == 256 ? (const void *)lz4_decode_lc_kernel<256> : (const void *)lz4_decode_lc_kernel<128>;
-    const size_t lds = r == 256 ? LCL<256>::total : LCL<128>::total;
+    const long r = knob("LZ4_LC_RING", 192);   // 192: 24.1 ms per 1M x 16 KiB pages, 128: 25.0, 256: 28.6
+    const void *k = r == 256   ? (const void *)lz4_decode_lc_kernel<256>
+                    : r == 192 ? (const void *)lz4_decode_lc_kernel<192>
+                               : (const void *)lz4_decode_lc_kernel<128>;
+    const size_t lds = r == 256 ? LCL<256>::total : r == 192 ? LCL<192>::total : LCL<128>::total;
     const size_t ncu = prepare_launch(k);
     size_t waves = waves_per_cu(k, lds);
     const long env_waves = knob("LZ4_LC_WAVES", 0);

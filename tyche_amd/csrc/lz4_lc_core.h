@@ -84,12 +84,29 @@ LC_FN void get16(const uint8_t *base, int32_t p, uint64_t &lo, uint64_t &hi) {
     lo = funnel8(q0, q1, s);
     hi = funnel8(q1, q2, s);
 }
+// Ring rows (qwords) of a lane: R / 8 of them, R a power of two or 192 (24 rows:
+// row = k mod 24 by an exact multiply-high division).  k >= -1 (positions >= -8).
+template <int32_t R>
+LC_FN int32_t lc_row(int32_t k) {
+    constexpr int32_t rows = R / 8;
+    if constexpr ((rows & (rows - 1)) == 0) {
+        return k & (rows - 1);
+    } else {
+        static_assert(rows == 24, "ring rows: a power of two or 24");
+        const uint32_t u = (uint32_t)(k + rows);
+        const uint32_t q = (uint32_t)(((uint64_t)u * 0xAAAAAAABull) >> 36);   // u / 24
+        return (int32_t)(u - q * 24u);
+    }
+}
+template <int32_t R>
+LC_FN int32_t lc_row_next(int32_t r) { return r + 1 == R / 8 ? 0 : r + 1; }
+
 // the same from a ring of R bytes (page position p >= -8; wraps)
 template <int32_t R>
 LC_FN void ring16(const uint8_t *ring, int32_t p, uint64_t &lo, uint64_t &hi) {
-    constexpr int32_t m = R / 8 - 1;
-    const int32_t k = p >> 3;   // (arithmetic shift: p >= -8 wraps correctly)
-    const uint64_t q0 = lq(LC_Q(ring, k & m)), q1 = lq(LC_Q(ring, (k + 1) & m)), q2 = lq(LC_Q(ring, (k + 2) & m));
+    const int32_t r0 = lc_row<R>(p >> 3);   // (arithmetic shift: p >= -8 wraps correctly)
+    const int32_t r1 = lc_row_next<R>(r0), r2 = lc_row_next<R>(r1);
+    const uint64_t q0 = lq(LC_Q(ring, r0)), q1 = lq(LC_Q(ring, r1)), q2 = lq(LC_Q(ring, r2));
     const uint32_t s = (uint32_t)p & 7u;
     lo = funnel8(q0, q1, s);
     hi = funnel8(q1, q2, s);
@@ -105,11 +122,10 @@ LC_FN uint64_t put16(uint8_t *ring, int32_t d, uint64_t tail, uint64_t lo, uint6
     const uint64_t o0 = keep_low(tail, lo << (8u * s), s);
     const uint64_t o1 = s ? (lo >> (64u - 8u * s)) | (hi << (8u * s)) : hi;
     const uint64_t o2 = s ? hi >> (64u - 8u * s) : 0ull;
-    constexpr int32_t m = R / 8 - 1;
-    const int32_t kq = q0 >> 3;
-    lq(LC_Q(ring, kq & m), o0);
-    lq(LC_Q(ring, (kq + 1) & m), o1);
-    lq(LC_Q(ring, (kq + 2) & m), o2);
+    const int32_t r0 = lc_row<R>(q0 >> 3), r1 = lc_row_next<R>(r0), r2 = lc_row_next<R>(r1);
+    lq(LC_Q(ring, r0), o0);
+    lq(LC_Q(ring, r1), o1);
+    lq(LC_Q(ring, r2), o2);
     const uint32_t k = (s + (uint32_t)n) >> 3;
     return k == 0 ? o0 : (k == 1 ? o1 : o2);
 }
