@@ -1,5 +1,5 @@
 /* batched_stats.c -- linked into _app/tyche_batched only (TEST INFRASTRUCTURE):
- * at exit, prints the engine's restore-queue counters (launches and buffers
+ * at exit (and from quarantine.c's watchdog before its _exit), prints the engine's restore-queue counters (launches and buffers
  * served, tyche_restore_queue_stats) and the sweep batches (tyche_buffers_compress
  * calls and buffers) so the C1 batched test can see that the reference's own
  * callers drove batched GPU work. */
@@ -9,11 +9,11 @@
 
 void tyche_restore_queue_stats(uint64_t *batches, uint64_t *buffers);
 
-static void report(void) {
+void tyche_app_report(void) {
     uint64_t batches = 0, buffers = 0;
     tyche_restore_queue_stats(&batches, &buffers);
     fprintf(stderr, "tyche-restore-queue: batches %llu buffers %llu\n", (unsigned long long)batches,
             (unsigned long long)buffers);
 }
 
-__attribute__((constructor)) static void register_report(void) { atexit(report); }
+__attribute__((constructor)) static void register_report(void) { atexit(tyche_app_report); }

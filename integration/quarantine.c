@@ -49,7 +49,10 @@ static void on_fault(int sig) {
 
 // TYCHE_APP_WATCHDOG=<seconds>: if the process is still alive then, every
 // thread prints its backtrace (SIGUSR1 to each task) and the process exits
-// with status 3 -- names the frames a hung run is waiting in.
+// with status 3 -- names the frames a hung run is waiting in.  A binary that
+// defines tyche_app_report (batched_stats.c) has it called first: _exit runs
+// no atexit handlers.
+__attribute__((weak)) void tyche_app_report(void);
 static void on_dump(int sig) {
     (void)sig;
     char hdr[64];
@@ -77,6 +80,7 @@ static void *watchdog(void *arg) {
         closedir(d);
     }
     usleep(200000);
+    if (tyche_app_report) tyche_app_report();
     _exit(3);
     return NULL;
 }

@@ -1656,7 +1656,10 @@ struct RestoreQueue {
         }
     }
 };
-RestoreQueue g_rq;
+// never destroyed: a process may exit without tyche_restore_queue_stop (the reference app's
+// list__destroy can hang before it gets there), and destroying joinable dispatcher threads (or the
+// mutex they wait on) at exit would abort the process in std::terminate
+RestoreQueue &g_rq = *new RestoreQueue;
 }  // namespace
 
 int tyche_restore_queue_start(int max_batch, int max_wait_us) {
