@@ -115,6 +115,10 @@ void tyche_restore_queue_stop(void);
 int tyche_buffer_restore(Buffer *buf, int compressor_id);
 /* Launches and buffers served so far. */
 void tyche_restore_queue_stats(uint64_t *batches, uint64_t *buffers);
+/* Launches so far by batch size: counts[k] = launches of 2^k .. 2^(k+1)-1
+ * buffers (the last bucket takes every larger one); fills min(n, 11) buckets
+ * and returns that count. */
+int tyche_restore_queue_hist(uint64_t *counts, int n);
 
 /* ---- device-resident batch API ------------------------------------------- */
 /* Page i of the batch reads src + src_offsets[i] (or i*src_stride when

@@ -73,7 +73,7 @@ def test_plan_split_respects_minimum_part():
     assert all(b - a >= 4096 for a, b in zip(cuts[:-1], cuts[1:]))
 
 
-def _run_tool(args, env_extra=None, timeout=100):
+def _run_tool(args, env_extra=None, timeout=100, all_lines=False):
     exe = os.path.join(TOOLS, args[0])
     if not os.path.exists(exe):
         pytest.skip(f"{exe} not built")
@@ -84,7 +84,7 @@ def _run_tool(args, env_extra=None, timeout=100):
     out = p.stdout.decode()
     lines = [l for l in out.splitlines() if l.startswith("{")]
     assert p.returncode == 0 and lines, (p.returncode, out[-2000:], p.stderr.decode()[-2000:])
-    return json.loads(lines[-1])
+    return [json.loads(l) for l in lines] if all_lines else json.loads(lines[-1])
 
 
 @pytest.mark.gpu
@@ -114,6 +114,23 @@ def test_c5_live_cycle():
     assert r["restored_zlib"] > 0 and r["restored_lz4"] > 0, r    # pages swept during the run were restored again
     assert r["swept"] > 0 and r["sweeps"] > 0 and r["flushes"] >= r["sweeps"]
     assert r["queue_batches"] < r["restored"]                  # the queue coalesced concurrent restores
+
+
+@pytest.mark.gpu
+def test_c5_live_cycle_sustained():
+    """The live cycle held for 10 s of wall time (tools/cycle_live.c seconds mode): the sweeper runs
+    100+ sweeps against 64 restorers, pages cross zlib -> raw -> LZ4 -> raw many times, every page is
+    bit-exact at the end, every restore went through the queue, and the histograms (compressor-pool
+    call sizes, sweep flush sizes, restore launch sizes) account for every call, flush and launch."""
+    r, h = _run_tool(["cycle_live", 12000, 64, 600, 16, 10, 10], timeout=200, all_lines=True)
+    print(r, h)
+    assert r["run_s"] >= 10.0 and r["sweeps"] >= 100, r
+    assert r["mismatches"] == 0 and r["sweep_fails"] == 0, r
+    assert r["restored_lz4"] > r["restored_zlib"] > 0, r      # swept pages come back again and again
+    assert r["queue_buffers"] == r["restored"] and r["queue_batches"] < r["restored"], r
+    assert sum(h["restore_launch_sizes"]) == r["queue_batches"], h
+    assert sum(h["sweep_flush_sizes"]) == r["flushes"], h
+    assert sum(h["compress_call_sizes"]) >= r["flushes"], h   # a flush is split into calls of <= 250 victims
 
 
 @pytest.mark.gpu

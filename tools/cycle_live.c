@@ -31,7 +31,10 @@
  *   - afterwards every page is restored (if still compressed) and compared
  *     with a regenerated copy.
  *
- *   run: tools/bin/cycle_live [buffers] [restorers] [restores_per_thread] [compressors] [raw_budget_pct]
+ *   run: tools/bin/cycle_live [buffers] [restorers] [restores_per_thread] [compressors] [raw_budget_pct] [seconds]
+ *   seconds > 0: a sustained cycle -- the restorers search until that much wall time has passed
+ *   (restores_per_thread then only sets the minimum); the JSON line adds histograms of the
+ *   compressor pool's batch sizes, the sweeper's flush sizes and the restore queue's launches.
  *   The engine spreads work over every visible GPU (TYCHE_DEVICE_IDS=0,0 rehearses
  *   the fan-out on one).  Prints one JSON line.
  */
@@ -63,6 +66,15 @@ static volatile int64_t g_raw;             /* raw bytes resident (atomic) */
 static volatile long g_bad, g_hits, g_restored, g_restored_bytes, g_restored_zlib, g_restored_lz4;
 static volatile long g_swept, g_swept_bytes, g_comp_fails, g_sweeps, g_flushes;
 static volatile int g_done;
+static double g_deadline;                  /* > 0: restorers search until this time (sustained mode) */
+/* power-of-two histograms: compressor-pool call sizes and sweeper flush sizes */
+#define HB 11
+static volatile long g_comp_hist[HB], g_flush_hist[HB];
+static int hbucket(size_t k) {
+    int b = 0;
+    while ((k >>= 1) && b < HB - 1) b++;
+    return b;
+}
 
 static double now_s(void) {
     struct timespec t;
@@ -108,6 +120,7 @@ static void *compressor(void *arg) {
         while (k < COMP_BATCH && g_vict_next < g_vict_n) vict[k++] = g_victims[g_vict_next++];
         g_active++;
         pthread_mutex_unlock(&g_jobs_lock);
+        __sync_fetch_and_add(&g_comp_hist[hbucket(k)], 1);
         if (tyche_buffers_compress(vict, out, st, k, TYCHE_LZ4_COMPRESSOR_ID, 1) != TYCHE_E_OK)
             for (size_t j = 0; j < k; j++) st[j] = TYCHE_E_DEVICE;
         for (size_t j = 0; j < k; j++) {
@@ -142,6 +155,7 @@ static void clear_pending(size_t nv) {
     }
 }
 static void flush_victims(size_t nv) {
+    __sync_fetch_and_add(&g_flush_hist[hbucket(nv)], 1);
     pthread_mutex_lock(&g_jobs_lock);
     g_vict_n = nv;
     g_vict_next = 0;
@@ -204,7 +218,9 @@ static void *restorer(void *arg) {
     /* each restorer makes g_restores searches, and more (up to 8x) until the run has restored
      * MIN_LZ4_RESTORES pages that the sweeper compressed during it: a short run's searches can
      * otherwise all end before the cold pages the sweeps hit come back */
-    for (long k = 0; k < g_restores || (g_restored_lz4 < MIN_LZ4_RESTORES && k < 8 * g_restores); k++) {
+    for (long k = 0; k < g_restores || (g_deadline > 0 ? now_s() < g_deadline
+                                                        : (g_restored_lz4 < MIN_LZ4_RESTORES && k < 8 * g_restores));
+         k++) {
         const uint64_t r = splitmix(&rng);
         const size_t id = (r % 100u) < 80u ? (size_t)((r >> 8) % hot) : hot + (size_t)((r >> 8) % (g_n - hot ? g_n - hot : 1));
         if (id >= g_n) continue;
@@ -247,6 +263,7 @@ int main(int argc, char **argv) {
     g_restores = argc > 3 ? atol(argv[3]) : 4000;
     const int ncomp = argc > 4 ? atoi(argv[4]) : 16;
     const int budget_pct = argc > 5 ? atoi(argv[5]) : 25;
+    const double seconds = argc > 6 ? atof(argv[6]) : 0.0;
     if (tyche_device_ready() != 1) {
         fprintf(stderr, "no gfx950 device: %s\n", tyche_last_error());
         return 2;
@@ -293,6 +310,7 @@ int main(int argc, char **argv) {
     const int nc = ncomp < 1 ? 1 : ncomp < 256 ? ncomp : 256;
     const int nt = nr < 1 ? 1 : nr < 1024 ? nr : 1024;
     const double t0 = now_s();
+    if (seconds > 0) g_deadline = t0 + seconds;
     for (int t = 0; t < nc; t++) pthread_create(&cth[t], NULL, compressor, NULL);
     pthread_create(&sth, NULL, sweeper, NULL);
     for (int t = 0; t < nt; t++) pthread_create(&rth[t], NULL, restorer, (void *)(uintptr_t)t);
@@ -305,8 +323,9 @@ int main(int argc, char **argv) {
     pthread_mutex_unlock(&g_jobs_lock);
     for (int t = 0; t < nc; t++) pthread_join(cth[t], NULL);
     tyche_restore_queue_stop();
-    uint64_t batches = 0, served = 0;
+    uint64_t batches = 0, served = 0, qhist[HB] = {0};
     tyche_restore_queue_stats(&batches, &served);
+    tyche_restore_queue_hist(qhist, HB);
 
     /* ---- verify every page */
     size_t still = 0;
@@ -332,6 +351,15 @@ int main(int argc, char **argv) {
            g_restored_zlib, g_restored_lz4, g_restored_bytes / 1073741824.0 / run, g_swept,
            g_swept_bytes / 1073741824.0 / run, g_sweeps, g_flushes, g_comp_fails, (unsigned long long)batches,
            (unsigned long long)served, g_bad, still);
+    if (seconds > 0) {   /* the histograms, bucket k = sizes 2^k .. 2^(k+1)-1, as a second JSON line */
+        printf("{\"hist_buckets\": \"2^k..2^(k+1)-1\", \"compress_call_sizes\": [");
+        for (int i = 0; i < HB; i++) printf("%s%ld", i ? ", " : "", g_comp_hist[i]);
+        printf("], \"sweep_flush_sizes\": [");
+        for (int i = 0; i < HB; i++) printf("%s%ld", i ? ", " : "", g_flush_hist[i]);
+        printf("], \"restore_launch_sizes\": [");
+        for (int i = 0; i < HB; i++) printf("%s%llu", i ? ", " : "", (unsigned long long)qhist[i]);
+        printf("]}\n");
+    }
     for (size_t i = 0; i < g_n; i++) buffer__destroy(g_bufs[i], true);
     return (g_bad || g_comp_fails) ? 1 : 0;
 }

@@ -114,6 +114,7 @@ SIGNATURES = {
     "tyche_restore_queue_stop": (None, []),
     "tyche_buffer_restore": (ctypes.c_int, [_BufP, ctypes.c_int]),
     "tyche_restore_queue_stats": (None, [ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
+    "tyche_restore_queue_hist": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]),
     "tyche_device_count": (ctypes.c_int, []),
     "tyche_set_device": (ctypes.c_int, [ctypes.c_int]),
     "tyche_active_devices": (ctypes.c_int, []),

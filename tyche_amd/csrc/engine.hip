@@ -1597,6 +1597,7 @@ int buffer__decompress(Buffer *buf, int compressor_id) {
 // oversubscribe the queues (0.85 / 0.70), batches only get smaller and run
 // behind each other (profiles/r02_restore_dispatch.jsonl).
 namespace {
+constexpr int kQueueHistBuckets = 11;
 struct RestoreReq {
     Buffer *buf;
     int status;
@@ -1610,6 +1611,7 @@ struct RestoreQueue {
     bool running = false, stop = false;
     int max_batch = 1024, max_wait_us = 50, device = -1;
     uint64_t batches = 0, buffers = 0;
+    uint64_t hist[kQueueHistBuckets] = {};   // launches by batch size (power-of-two buckets)
     std::vector<std::thread> th;
     void loop(int codec) {
         (void)tyche_set_device(device);
@@ -1646,6 +1648,7 @@ struct RestoreQueue {
                 std::lock_guard<std::mutex> g(mu);
                 batches++;
                 buffers += take.size();
+                hist[std::min(kQueueHistBuckets - 1, 31 - __builtin_clz((unsigned)take.size()))]++;
                 for (size_t i = 0; i < take.size(); i++) {
                     take[i]->status = st[i];
                     take[i]->done = true;
@@ -1713,6 +1716,14 @@ void tyche_restore_queue_stats(uint64_t *batches, uint64_t *buffers) {
     std::lock_guard<std::mutex> g(g_rq.mu);
     if (batches) *batches = g_rq.batches;
     if (buffers) *buffers = g_rq.buffers;
+}
+
+int tyche_restore_queue_hist(uint64_t *counts, int n) {
+    if (!counts || n <= 0) return 0;
+    std::lock_guard<std::mutex> g(g_rq.mu);
+    const int k = std::min(n, kQueueHistBuckets);
+    for (int i = 0; i < k; i++) counts[i] = g_rq.hist[i];
+    return k;
 }
 
 // ---------------------------------------------------------- synthetic input
