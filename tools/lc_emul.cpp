@@ -164,7 +164,7 @@ static int lc_decode(const uint8_t *in, int32_t L, uint8_t *out, int32_t C) {
         uint64_t tail = P.tail;
         copy_records<R>(ring, w16, op0, tail, rec, farv, nrec, gen, g_lut);
         P.tail = tail;
-        const int32_t lend = (ended && rv < 0) ? P.fl : (P.op & ~15);
+        const int32_t lend = (ended && rv < 0) ? P.fl : (P.op & ~(kLcLine - 1));
         for (int32_t f = P.fl; f + 16 <= lend; f += 16) memcpy(out + f, ring + 8 * lc_row<R>(f >> 3), 16);
         P.fl = lend > P.fl ? lend : P.fl;
         if (ended) {
@@ -183,5 +183,8 @@ static int lc_decode(const uint8_t *in, int32_t L, uint8_t *out, int32_t C) {
 }
 
 extern "C" int lc_emul_decode(const uint8_t *in, int L, uint8_t *out, int C, int R) {
+#if LC_LINE == 64
+    if (R == 128) R = 192;   // (64-byte lines need R >= 192)
+#endif
     return R == 256 ? lc_decode<256>(in, L, out, C) : R == 192 ? lc_decode<192>(in, L, out, C) : lc_decode<128>(in, L, out, C);
 }

@@ -97,11 +97,12 @@ __device__ __forceinline__ void lc_lut_load(const uint32_t *lut, int32_t c, uint
 // the flush tables.
 template <int32_t R>
 struct LCL {
+    static_assert(lc_ring_ok<R>(), "ring too small for the flush granule (lc_budget)");
     static constexpr uint32_t win = 0;
     static constexpr uint32_t ring = 64u * kLWS;
     static constexpr uint32_t tab_out = ring + 64u * (uint32_t)R;         // 64 x u64: page output pointers
     static constexpr uint32_t tab_fl = tab_out + 64u * 8u;                // 64 x u32: first pending piece
-    static constexpr int32_t max_pieces = (lc_budget<R>() + 15) / 16;     // 16-byte pieces per lane per chunk
+    static constexpr int32_t max_pieces = (lc_budget<R>() + kLcLine - 1) / 16 + 1;   // 16-byte pieces per lane per chunk
     static constexpr uint32_t own = tab_fl + 64u * 4u;                    // 64 x max_pieces x u16
     static constexpr uint32_t lut = own + ((64u * (uint32_t)max_pieces * 2u + 15u) & ~15u);   // match-copy table
     static constexpr uint32_t total = lut + (uint32_t)kLutBytes;
@@ -363,7 +364,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void lz
         LPROF_MARK(7);   // window wait and store
         // ---- stage 4: the finished 16-byte pieces of all 64 pages, one per lane and store
         // instruction (a page's pieces on neighbouring lanes: whole lines per few lanes)
-        const int32_t lend = !live ? 0 : (ended && rv < 0) ? P.fl : (P.op & ~15);
+        const int32_t lend = !live ? 0 : (ended && rv < 0) ? P.fl : (P.op & ~(kLcLine - 1));
         const int32_t nl = live ? (lend - P.fl) >> 4 : 0;
         const int32_t incl = wave_incl_sum(nl);
         const int32_t total = (int32_t)rdlane((uint32_t)incl, 63);
@@ -451,10 +452,15 @@ extern "C" int tyche_debug_lc_profile(unsigned long long *host16, int reset) {
 hipError_t launch_lz4_decode_lc(const tyche_batch_t &b, uint32_t in_cap, uint32_t out_cap, hipStream_t s) {
     if (b.count == 0) return hipSuccess;
     const long r = knob("LZ4_LC_RING", 192);   // 192: 24.1 ms per 1M x 16 KiB pages, 128: 25.0, 256: 28.6
+#if LC_LINE == 16
     const void *k = r == 256   ? (const void *)lz4_decode_lc_kernel<256>
                     : r == 192 ? (const void *)lz4_decode_lc_kernel<192>
                                : (const void *)lz4_decode_lc_kernel<128>;
     const size_t lds = r == 256 ? LCL<256>::total : r == 192 ? LCL<192>::total : LCL<128>::total;
+#else   // 64-byte lines need R >= 192 (lc_ring_ok)
+    const void *k = r == 256 ? (const void *)lz4_decode_lc_kernel<256> : (const void *)lz4_decode_lc_kernel<192>;
+    const size_t lds = r == 256 ? LCL<256>::total : LCL<192>::total;
+#endif
     const size_t ncu = prepare_launch(k);
     size_t waves = waves_per_cu(k, lds);
     const long env_waves = knob("LZ4_LC_WAVES", 0);

@@ -184,16 +184,21 @@ __device__ bool emit_records(const uint2 *rec, uint32_t n, uint32_t anchor, cons
 // 1 KiB ring, 256-byte dword flushes 79.3-79.4; 2 KiB, 512-byte 8-byte flushes 78.1; 2 KiB, 1 KiB
 // 16-byte flushes 78.2; 1 KiB, 512-byte flushes 80.2 (more batches overflow the ring).  A wave-wide
 // copy of all long literal runs at once (instead of one run after another) ran 80.5.
+// Round 4: 512-byte rings with dword flushes -- a 3-wave page's LDS drops from 30.5 to 26 KiB (6 pages per
+// CU instead of 5) and, with the 5-waves-per-SIMD register budget (TYCHE_ENC_WPE), encode 77.5 -> 72.2 ms
+// (8-byte flushes with the 512-byte ring: 74.7; without the register budget: 79.0); a sink whose bytes
+// would overflow the ring takes emit_records, whose fields then span the records and the ring.
 #ifndef TYCHE_LZ4_RING
-#define TYCHE_LZ4_RING 2048
+#define TYCHE_LZ4_RING 512
 #endif
 #ifndef TYCHE_LZ4_FLUSH_VEC
-#define TYCHE_LZ4_FLUSH_VEC 2
+#define TYCHE_LZ4_FLUSH_VEC 1
 #endif
 constexpr uint32_t kOutRing = TYCHE_LZ4_RING;        // bytes; head is always a multiple of kFlushStep
 constexpr uint32_t kFlushVec = TYCHE_LZ4_FLUSH_VEC;  // dwords per lane per flush step (1, 2 or 4)
 constexpr uint32_t kFlushStep = 4u * kWave * kFlushVec;
-static_assert(kOutRing >= 1024 && kOutRing % kFlushStep == 0 && (kOutRing & (kOutRing - 1)) == 0, "ring");
+static_assert(kOutRing >= 512 && kOutRing % kFlushStep == 0 && (kOutRing & (kOutRing - 1)) == 0, "ring");
+static_assert(kOutRing + 64u * 8u >= 1024u, "emit_records' fields fit the records and the ring");
 typedef uint32_t u32x2_ua __attribute__((ext_vector_type(2), aligned(1)));
 typedef __attribute__((address_space(1))) u32x2_ua g_u32x2_ua;
 typedef uint32_t u32x4_uaf __attribute__((ext_vector_type(4), aligned(1)));
@@ -285,7 +290,11 @@ __device__ __forceinline__ bool emit_staged(const uint2 *rec, uint32_t n, uint32
     if (op + r.pend + et > cap) return false;
     if (r.pend + et > kOutRing) {
         out_flush_all(ring, r, dst, op, lane);
-        return emit_records(rec, n, anchor, in, dst, op, cap, map, (uint4 *)ring, lane);
+        // emit_records' 64 packed fields (1 KiB): the ring, or for a ring under 1 KiB the records
+        // before it and the ring (every layout puts the 64 records right before the ring; they are
+        // read into registers before the fields are written)
+        uint4 *fld = (uint4 *)(kOutRing >= 1024 ? ring : ring + kOutRing - 1024u);
+        return emit_records(rec, n, anchor, in, dst, op, cap, map, fld, lane);
     }
     SINK_PHASE(11);
     constexpr uint32_t m = kOutRing - 1;
@@ -665,7 +674,15 @@ template <uint32_t kNW>
 constexpr uint32_t split_prefetch() { return (16384u / 16u + kNW * kWave - 1u) / (kNW * kWave); }   // 16 KiB per page
 
 template <uint32_t kNW>
-__global__ __launch_bounds__(kNW * 64) void lz4_encode_splitn_kernel(tyche_batch_t b, uint32_t in_cap, unsigned *ctr,
+#ifndef TYCHE_ENC_WPE
+#define TYCHE_ENC_WPE 5   // amdgpu_waves_per_eu register budget of the split kernels (4 waves: 87 VGPRs, no spills; 0: none)
+#endif
+#if TYCHE_ENC_WPE > 0
+#define TYCHE_ENC_WPE_ATTR __attribute__((amdgpu_waves_per_eu(TYCHE_ENC_WPE)))
+#else
+#define TYCHE_ENC_WPE_ATTR
+#endif
+__global__ __launch_bounds__(kNW * 64) TYCHE_ENC_WPE_ATTR void lz4_encode_splitn_kernel(tyche_batch_t b, uint32_t in_cap, unsigned *ctr,
                                                                      uint8_t *ws, uint32_t ws_stride, uint32_t seed,
                                                                      uint32_t p0) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -921,11 +938,13 @@ hipError_t launch_lz4_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream_
     if (in_cap > 65535u) return hipErrorInvalidValue;    // 16-bit positions (byU16 regime)
     // TYCHE_LZ4_ENC=1: the one-wave kernel for every batch (A/B timing)
     const bool one_wave = knob("LZ4_ENC", 0) == 1;
-    // waves per page of the split encoders (2: the two-wave kernel; default 3 since round 3: 79.4 vs
-    // 85.0 ms per 1M x 16 KiB pages at ratio 2.6193 vs 2.6204, with part 0 taking 27/64 of the page
-    // and the later parts seeded with the 10,240 positions before them -- A/B of seeds 4,096-16,384
-    // and part-0 shares 21-29/64 in DESIGN.md §3.2)
-    const long nw = knob("LZ4_ENC_WAVES", 3);
+    // waves per page of the split encoders (2: the two-wave kernel; 3 in round 3: 79.4 vs 85.0 ms per
+    // 1M x 16 KiB pages at ratio 2.6193 vs 2.6204, part 0 taking 27/64 of the page and the later parts
+    // seeded with the 10,240 positions before them).  Round 4: 512-byte output rings and a 5-waves-
+    // per-SIMD register budget (18-20 waves per CU instead of 15) -- three waves 72.2 ms at 2.6188,
+    // four (default) 70.5 at 2.6184 with 9,216 seeds and part 0 22/64 (seeds 8,192-12,288 x shares
+    // 18-24/64: 69.5-72.9 ms at 2.6158-2.6184, profiles/r04_lz4_encode_occupancy.log)
+    const long nw = knob("LZ4_ENC_WAVES", 4);
     // TYCHE_LZ4_SPLIT_MIN: the smallest in_cap that takes a split kernel.  8 KiB pages split into
     // three parts too since round 3 (256K x 8 KiB pages, ms per 1M: one wave per page 70.6 -- it holds
     // 168 VGPRs, 12 waves per CU --, three waves 41.5 at ratio 2.525 vs 2.528, four 37.9 at 2.519);
@@ -944,10 +963,11 @@ hipError_t launch_lz4_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream_
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, (int)T, lds) != hipSuccess || per_cu < 1) per_cu = 1;
         const size_t grid = std::min<size_t>(b.count, ncu * (size_t)per_cu);
         const uint32_t pws = nw == 8 ? part_scratch<8>(in_cap) : nw == 4 ? part_scratch<4>(in_cap) : part_scratch<3>(in_cap);
-        uint32_t seed = (uint32_t)std::max(0L, knob("LZ4_ENC_SEED", nw == 3 ? 10240L : (long)kSeed)) & ~(kWave - 1u);   // positions seeded before a part
+        uint32_t seed = (uint32_t)std::max(0L, knob("LZ4_ENC_SEED", nw == 3 ? 10240L : nw == 4 ? 9216L : (long)kSeed)) &
+                        ~(kWave - 1u);   // positions seeded before a part
         // part 0's share of the page in 64ths (0: equal parts); at least 1/kNW, so the later parts fit
         // their scratch (part_scratch: a 1/kNW part)
-        uint32_t p0 = (uint32_t)std::max(0L, knob("LZ4_ENC_P0", nw == 3 ? 27L : 0L));
+        uint32_t p0 = (uint32_t)std::max(0L, knob("LZ4_ENC_P0", nw == 3 ? 27L : nw == 4 ? 22L : 0L));
         if (p0) p0 = std::min<uint32_t>(std::max<uint32_t>(p0, (64u + (uint32_t)nw - 1u) / (uint32_t)nw), 48u);
         const uint32_t ws_stride = (uint32_t)(nw - 1) * pws;
         ScratchLease ws(s, grid * (size_t)ws_stride);

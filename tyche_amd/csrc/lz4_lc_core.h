@@ -156,11 +156,22 @@ enum : int32_t { kLParse = 0, kLCut = 1, kLEnd = 2 };
 //  * a far source's used bytes end at d + n2 - off <= op0 + budget - (R - 23),
 //    below fl when budget <= R - 39; the chunk's writes (up to op0 + budget + 23)
 //    must not reach the unflushed bytes [fl, op0) a ring turn later: the same
-//    bound.  So budget = R - 40.
+//    bound.  So budget = R - 40 (R - 24 - the flush granule, below).
+// Flushing whole 64-byte lines instead (LC_LINE 64) leaves up to 63 bytes
+// unflushed: budget = R - 23 - 64 = R - 87 by the same two bounds, and every
+// flushed line leaves whole (fewer, full-line HBM writes).
+#ifndef LC_LINE
+#define LC_LINE 16
+#endif
+constexpr int32_t kLcLine = LC_LINE;   // flush granule: 16 or 64 bytes
+static_assert(kLcLine == 16 || kLcLine == 64, "flush granule");
 template <int32_t R>
 constexpr int32_t lc_near() { return R - 24; }
 template <int32_t R>
-constexpr int32_t lc_budget() { return R - 40; }
+constexpr int32_t lc_budget() { return R - 24 - kLcLine; }
+// a chunk's first record (<= 15 literal + 32 match bytes) must always fit
+template <int32_t R>
+constexpr bool lc_ring_ok() { return lc_budget<R>() >= 47; }
 
 // record: literal part window position (6 bits) and length (<= 15), match part
 // length (<= 32), offset (16 bits)
