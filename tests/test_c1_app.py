@@ -24,6 +24,7 @@ import hashlib
 import os
 import re
 import subprocess
+import time
 
 import numpy as np
 import pytest
@@ -232,15 +233,21 @@ def test_reference_app_device_failure(sample_dir):
       site sees comp_length == 0 and just clears the flag (list.c:568-587), leaving a raw page with no
       data, and the next rewrite of it faults in memcpy -- the page is lost.
     * The one-line change (tyche_fixed, built from list.c with line 1052 as INTEGRATION.md gives it):
-      the victim stays raw and intact; three runs end without a fault (in the reference's own
-      copy-on-write or sweep wedges at worst, no thread inside the engine) and pages compress."""
+      the victim stays raw and intact; runs (up to three, until one has compressed pages) end without
+      a fault (in the reference's own copy-on-write or sweep wedges at worst, no thread inside the
+      engine) and pages compress."""
     _need(APP_Q)
     _need(APP_FIXED)
     fault = {"TYCHE_FAIL_COMPRESS_EVERY": "2"}
     args = ["-c", "lz4", "-p", str(sample_dir / "16k"), "-w", "1", "-d", "3", "-m", "512000", "-f", "20", "-U", "50"]
     crashes, runs = [], []
-    for _ in range(6):   # the reference's list code is racy: a run may wedge before it rewrites a lost page
-        env = dict(os.environ, TYCHE_APP_WATCHDOG="15", TYCHE_LOG_ERRORS="1", TYCHE_FAIL_COMPRESS_EVERY="1")
+    # The reference's list code is racy: a run may wedge in its own sweep before it rewrites a lost
+    # page (2 of 3 box runs did, tools/c1_fail_probe.py), while a run that reaches one faults within
+    # a second.  -d 3 ends a healthy run in ~3 s, so an 8 s watchdog only cuts wedged runs short and
+    # the test gets many tries inside its time limit.
+    t_end = time.monotonic() + 75
+    while len(runs) < 12 and time.monotonic() < t_end:
+        env = dict(os.environ, TYCHE_APP_WATCHDOG="8", TYCHE_LOG_ERRORS="1", TYCHE_FAIL_COMPRESS_EVERY="1")
         p = subprocess.run([APP_Q] + args, stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=90, env=env)
         err = p.stderr.decode(errors="replace")
         runs.append(p.returncode)
@@ -250,7 +257,9 @@ def test_reference_app_device_failure(sample_dir):
             assert "manager__spawn_worker" in bt, bt[-3000:]   # the rewrite's memcpy of the NULL page (manager.c:358)
             crashes.append(p.returncode)
             break
-        assert p.returncode == 3, (p.returncode, err[-3000:])   # otherwise only the watchdog may end it
+        assert p.returncode in (0, 3), (p.returncode, err[-3000:])   # a clean end or the watchdog, nothing else
+        if p.returncode == 0:
+            continue                                  # ran its 3 s without rewriting a lost page
         # a watchdog exit: one of the reference's own wedges (copy-on-write or sweep scan), never a thread
         # inside the engine; it may come before the first sweep, so before any injected failure
         dump = err[err.find("--- thread"):]
@@ -267,6 +276,8 @@ def test_reference_app_device_failure(sample_dir):
         rec = _bench_attempt(APP_FIXED, "lz4", sample_dir, extra_env=dict(fault, TYCHE_LOG_ERRORS="0"),
                              extra_args=("-U", "50"))
         attempts.append(rec)
+        if rec["comps"] > 0:
+            break
     summary = [(a["rc"], a["kind"], a["comps"], a["rests"]) for a in attempts]
     print(f"fixed caller: attempts (rc, kind, compressions, restorations): {summary}")
     assert any(a["comps"] > 0 for a in attempts), summary   # failures leave pages raw; the others compress
