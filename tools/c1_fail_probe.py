@@ -41,7 +41,7 @@ def main():
     app = os.path.join(ROOT, "integration", "_app", "tyche_q")
     args = ["-c", "lz4", "-p", os.path.join(root, "16k"), "-w", "1", "-d", "3", "-m", "512000", "-f", "20",
             "-U", "50"] + extra
-    env = dict(os.environ, TYCHE_APP_WATCHDOG="15", TYCHE_LOG_ERRORS="1", TYCHE_FAIL_COMPRESS_EVERY="1")
+    env = dict(os.environ, TYCHE_APP_WATCHDOG=os.environ.get("WD", "15"), TYCHE_LOG_ERRORS="1", TYCHE_FAIL_COMPRESS_EVERY="1")
     for i in range(runs):
         t0 = time.time()
         p = subprocess.run([app] + args, stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=90, env=env)
@@ -51,9 +51,9 @@ def main():
         with open(os.path.join(out, f"run{i}.out"), "wb") as f:
             f.write(p.stdout)
         err = p.stderr.decode(errors="replace")
-        print(json.dumps({"run": i, "rc": p.returncode, "s": round(dt, 1),
+        print(json.dumps({"args": extra, "run": i, "rc": p.returncode, "s": round(dt, 1),
                           "engine_errors": err.count("tyche-engine:")}), flush=True)
-        if p.returncode == -11:
+        if p.returncode == -11 and os.environ.get("ALL") != "1":
             break
 
 
