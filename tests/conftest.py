@@ -12,6 +12,17 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU; runs the HIP kernels through the C ABI")
+    config.addinivalue_line("markers", "legacy: superseded decoders, only in the A/B library build (test_legacy_decoders.py)")
+
+
+def pytest_collection_modifyitems(config, items):
+    """Legacy-decoder tests run only against the library that contains those kernels."""
+    if "legacy" in os.environ.get("TYCHE_CODEC_LIB", ""):
+        return
+    keep = [it for it in items if it.get_closest_marker("legacy") is None]
+    if len(keep) != len(items):
+        config.hook.pytest_deselected(items=[it for it in items if it.get_closest_marker("legacy") is not None])
+        items[:] = keep
 
 
 def load_golden(name: str):

@@ -130,7 +130,9 @@ def _bench_attempt(app, codec, sample_dir, extra_env=None, extra_args=(), worker
     rest = re.search(r"Restorations\s*:\s*([\d,]+) restorations", out)
     if comp and rest:
         rec["comps"], rec["rests"] = int(comp.group(1).replace(",", "")), int(rest.group(1).replace(",", ""))
+        rec["rests_exact"] = True
     else:
+        rec["rests_exact"] = False
         status = re.findall(r"([\d.,]+)(\S?) Comps \(([\d.,]+)(\S?) Res\)", err)
         scale = {"": 1, "K": 1e3, "M": 1e6, "B": 1e9}
         rec["comps"] = float(status[-1][0].replace(",", "")) * scale.get(status[-1][1], 1) if status else 0
@@ -191,7 +193,10 @@ def test_reference_app_batched_run(sample_dir, codec):
     restore goes through the engine's restore queue (list.c:572, started at list.c:169).  Pages
     are compressed and restored through those calls, and every restore the app made was served by
     the queue (its counters, printed at exit or by the watchdog before a wedged run's exit: queue
-    buffers == restorations, batches <= buffers).  Every run is checked as in the unbatched test.
+    buffers == restorations when the app printed its results block -- list.c:578-584 counts a
+    restoration only after the call returned, and every call is one queued buffer --, buffers >= the
+    last status line's rounded count on a wedged run, whose status line precedes the watchdog's
+    counters; batches <= buffers).  Every run is checked as in the unbatched test.
 
     Coalescing (batches < buffers) needs restores that overlap in time; the reference's list code
     wedges long before its workers restore that often -- 4 to 16 workers on 20 or 256
@@ -211,6 +216,10 @@ def test_reference_app_batched_run(sample_dir, codec):
     for a in attempts:   # the counters are printed on every exit path
         assert a.get("queue_buffers") is not None, summary
         assert a["queue_batches"] <= a["queue_buffers"], summary
+        if a["rests_exact"]:
+            assert a["queue_buffers"] == a["rests"], summary
+        else:   # the status line rounds (e.g. 1.2K): its count is at most ~5 % above the true one
+            assert a["queue_buffers"] >= int(a["rests"] * 0.95), summary
     last = attempts[-1]
     assert last["comps"] > 0 and last["rests"] > 0, summary
     assert last["queue_buffers"] >= 1, summary

@@ -351,33 +351,6 @@ def test_decode_lane_path_fixtures(tc, target):
             assert hashlib.sha256(outs[j]).digest() == want_dig[i], (j, i)
 
 
-@pytest.mark.parametrize("lb,ring", [(1, 128), (1, 160), (1, 192), (1, 256), (0, 256), (0, 128)])
-def test_decode_lane_kernels_all_rings(tc, oracle_mod, knobs, lb, ring):
-    """Every lane-per-page kernel variant (LZ4_LANE_LB=1: the stream through a per-lane line buffer,
-    the default, at each ring size; 0: the round-2 ring kernel), selected in-process with
-    tyche_set_knob and forced on every batch size (LZ4_LANE_MIN=0): the fixtures with their exact
-    return values, and seeded corruptions against the restated LZ4_decompress_safe."""
-    knobs(LZ4_LC=0, LZ4_LANE_LB=lb, LZ4_LANE_RING=ring, LZ4_LANE_MIN=0)
-    test_decode_lane_path_fixtures(tc, 1)
-    rng = np.random.default_rng(1000 + ring + lb)
-    pages = oracle_mod.pagegen(256, 16384, seed=9, first=ring, dist=0)
-    streams, caps = [], []
-    for i in range(256):
-        c = bytearray(oracle_mod.lz4_compress(pages[i].tobytes()))
-        if i % 4 == 1:
-            c[int(rng.integers(0, len(c)))] ^= 1 << int(rng.integers(0, 8))
-        elif i % 4 == 2:
-            c = c[: int(rng.integers(1, len(c)))]
-        streams.append(bytes(c))
-        caps.append(16384 if i % 4 != 3 else int(rng.integers(100, 16384)))
-    rv, outs = ragged_decode(tc, streams, caps)
-    for i in range(256):
-        r, want = oracle_mod.lz4_decompress(streams[i], caps[i])
-        assert rv[i] == r, (i, rv[i], r)
-        if r > 0 and i % 4 in (0, 3):   # untouched streams (a flipped one may hold an offset-0 match: undefined bytes)
-            assert outs[i][:r] == want[:r], i
-
-
 @pytest.mark.parametrize("ring", [128, 192, 256])
 def test_decode_lc_kernel_variants(tc, oracle_mod, knobs, ring):
     """The chunked lane-per-page decoder (lz4_decode_lc.hip) at both ring sizes, forced on every
@@ -408,35 +381,6 @@ def test_decode_lc_kernel_variants(tc, oracle_mod, knobs, ring):
         test_decode_jump_path_page_kinds(tc, oracle_mod, plen, 300)
     test_decode_token_list_near_output(tc, oracle_mod, 6000, 16384, True)
     test_decode_token_list_near_output(tc, oracle_mod, 20000, 65535, True)
-
-
-@pytest.mark.parametrize("ring,far", [(1024, 8), (1024, 6), (512, 8), (512, 6), (2048, 8)])
-def test_decode_quad_kernel_variants(tc, oracle_mod, knobs, ring, far):
-    """The quad-per-page chunked decoder (lz4_decode_quad.hip) at every ring / far-entry size,
-    forced on every batch size (LZ4_QUAD=1, LZ4_LANE_MIN=0): the fixtures with their exact return
-    values, seeded corruptions against the restated LZ4_decompress_safe, and pages built for its
-    slow path (incompressible, long literal runs, long and self-overlapping matches)."""
-    knobs(LZ4_QUAD=1, LZ4_QUAD_RING=ring, LZ4_QUAD_FAR=far, LZ4_LANE_MIN=0)
-    test_decode_lane_path_fixtures(tc, 1)
-    rng = np.random.default_rng(2000 + ring + far)
-    pages = oracle_mod.pagegen(256, 16384, seed=11, first=ring + far, dist=0)
-    streams, caps = [], []
-    for i in range(256):
-        c = bytearray(oracle_mod.lz4_compress(pages[i].tobytes()))
-        if i % 4 == 1:
-            c[int(rng.integers(0, len(c)))] ^= 1 << int(rng.integers(0, 8))
-        elif i % 4 == 2:
-            c = c[: int(rng.integers(1, len(c)))]
-        streams.append(bytes(c))
-        caps.append(16384 if i % 4 != 3 else int(rng.integers(100, 16384)))
-    rv, outs = ragged_decode(tc, streams, caps)
-    for i in range(256):
-        r, want = oracle_mod.lz4_decompress(streams[i], caps[i])
-        assert rv[i] == r, (i, rv[i], r)
-        if r > 0 and i % 4 in (0, 3):
-            assert outs[i][:r] == want[:r], i
-    for plen in (8192, 16384, 32768):
-        test_decode_jump_path_page_kinds(tc, oracle_mod, plen, 300)
 
 
 @pytest.mark.parametrize("dist", [0, 1, 2, 3, 4, 5])
@@ -558,3 +502,24 @@ def test_c2_full_size_round_trip(tc):
     assert 2.55 < ratio < 2.7, ratio
     del pages, comp, out
     torch.cuda.empty_cache()
+
+
+def test_scratch_oom_recovered(tc, knobs, oracle_mod):
+    """A scratch lease whose first hipMalloc fails (SCRATCH_OOM_SEQ: an oversized real request, so
+    the HIP error slot is set exactly as by an out-of-memory) frees the idle pool, retries and
+    succeeds; the launch that follows must not report the recovered failure (engine.hip
+    ScratchLease: the error slot is cleared), and the split encoder's output still round-trips."""
+    n, plen = 2048, 16384
+    pages = tc.pagegen(n, plen, dist=0, device=DEV)
+    for seq in (1, 2):   # each new value forces one failure
+        knobs(SCRATCH_OOM_SEQ=seq)
+        comp, clen = tc.compress_pages(pages)   # raises on a non-zero engine status
+        out, rv = tc.decompress_pages(comp, clen, plen)
+        torch.cuda.synchronize()
+        assert bool((clen > 0).all()) and bool((rv == plen).all())
+        assert torch.equal(out, pages)
+    ch, lh = comp[:4].cpu().numpy(), clen[:4].cpu().numpy()
+    host = pages[:4].cpu().numpy()
+    for i in range(4):
+        r, dec = oracle_mod.lz4_decompress(ch[i, :lh[i]].tobytes(), plen)
+        assert r == plen and dec == host[i].tobytes()

@@ -14,7 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 BUILD = os.path.join(HERE, "..", "build", "tyche_amd")
 LIB = os.path.join(HERE, "libtyche_codec.so")
-SOURCES = ["engine.hip", "lz4_decode.hip", "lz4_decode_lane.hip", "lz4_decode_quad.hip", "lz4_decode_lc.hip", "lz4_encode.hip", "zlib_inflate.hip", "zstd_decode.hip", "zstd_encode.hip", "zlib_deflate.hip", "pagegen.hip",
+SOURCES = ["engine.hip", "lz4_decode.hip", "lz4_decode_lane.hip", "lz4_decode_lc.hip", "lz4_encode.hip", "zlib_inflate.hip", "zstd_decode.hip", "zstd_encode.hip", "zlib_deflate.hip", "pagegen.hip",
            "errno_guard.hip"]   # errno_guard last: its constructor runs after the code-object registrations
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
@@ -24,6 +24,9 @@ FLAGS = ["--offload-arch=" + ARCH, "-O3", "-fPIC", "-std=c++17", "-Wall", "-Wno-
 # load/store vectorizer would fuse neighbouring dwords into ds_read_b64/b128 at
 # 4-byte-aligned addresses, which the LDS replays at ~64 cycles per instruction.
 # Without it, pairs still become ds_read2_b32 (4-byte alignment suffices).
+# superseded large-batch LZ4 decoders (round-2/3 lane kernels, the round-4 quad kernel): only in the
+# A/B build, libtyche_codec_legacy_decoders.so (build(legacy=True)), never in the product library
+LEGACY_SOURCES = ["lz4_decode_quad.hip"]
 NO_LSV = ["-mllvm", "-amdgpu-load-store-vectorizer=false"]
 SOURCE_FLAGS = {"lz4_encode.hip": NO_LSV, "zstd_encode.hip": NO_LSV, "zlib_deflate.hip": NO_LSV, "zstd_decode.hip": NO_LSV}
 
@@ -50,9 +53,11 @@ def _newer(target: str, deps: list[str]) -> bool:
 
 
 def build(force: bool = False, verbose: bool = False, profile: bool = False, ablate: int = 0,
-          eablate: int = 0, defines: tuple = ()) -> str:
+          eablate: int = 0, defines: tuple = (), legacy: bool = False) -> str:
     """profile=True builds the diagnostic variant (per-phase cycle stamps, -DTYCHE_PROFILE)
     as libtyche_codec_prof.so; it is never loaded by the product path."""
+    if legacy:
+        defines = tuple(defines) + ("TYCHE_LEGACY_DECODERS",)
     tag = ("_prof" if profile else "") + (f"_abl{ablate}" if ablate else "") + (f"_eabl{eablate}" if eablate else "") + \
         "".join("_" + d.replace("TYCHE_", "").replace("=", "").lower() for d in defines)   # A/B variant libraries
     build_dir = BUILD + tag
@@ -64,7 +69,8 @@ def build(force: bool = False, verbose: bool = False, profile: bool = False, abl
     headers.append(os.path.join(HERE, "..", "include", "tyche_codec.h"))
     objs = []
     jobs = []
-    for src in SOURCES:
+    sources = SOURCES[:-1] + (LEGACY_SOURCES if legacy else []) + SOURCES[-1:]   # errno_guard stays last
+    for src in sources:
         s = os.path.join(CSRC, src)
         o = os.path.join(build_dir, src.replace(".hip", ".o"))
         objs.append(o)
@@ -111,4 +117,4 @@ if __name__ == "__main__":
     abl = [int(a.split("=")[1]) for a in sys.argv if a.startswith("--ablate=")]
     eabl = [int(a.split("=")[1]) for a in sys.argv if a.startswith("--eablate=")]
     print(build(force="--force" in sys.argv, verbose=True, profile="--profile" in sys.argv,
-                ablate=abl[0] if abl else 0, eablate=eabl[0] if eabl else 0))
+                ablate=abl[0] if abl else 0, eablate=eabl[0] if eabl else 0, legacy="--legacy" in sys.argv))

@@ -56,7 +56,7 @@ struct CounterPool {
     size_t cursor = 0;
     unsigned *junk = nullptr;   // shared by launches whose grid covers all their pages
 };
-CounterPool g_counters[kMaxDevices];
+CounterPool *const g_counters = new CounterPool[kMaxDevices];   // never destroyed (restore dispatchers may run at exit)
 constexpr size_t kCounterBlock = 64;
 }  // namespace
 
@@ -126,7 +126,7 @@ struct ScratchPool {
     std::mutex mu;
     std::vector<Entry> e;
 };
-ScratchPool g_scratch[kMaxDevices];
+ScratchPool *const g_scratch = new ScratchPool[kMaxDevices];   // never destroyed (restore dispatchers may run at exit)
 }  // namespace
 
 // Leases are sized by the request (1 MiB granules) and reused best-fit, never
@@ -182,44 +182,67 @@ tyche::ScratchLease::ScratchLease(hipStream_t s, size_t bytes) : s_(s) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return;
     ScratchPool &P = g_scratch[dev];
-    std::vector<ScratchPool::Entry> victims;   // trimmed under the lock, freed after it
-    {
-        std::lock_guard<std::mutex> g(P.mu);
-        const size_t want = (std::max<size_t>(bytes, 1) + 0xFFFFF) & ~size_t(0xFFFFF);
-        size_t take = P.e.size();
-        for (size_t i = 0; i < P.e.size(); i++) {   // best fit among idle entries of at most 4x the request
-            ScratchPool::Entry &x = P.e[i];
-            if (x.state == 1 || x.bytes < want || x.bytes / 4 > want) continue;
-            if (!entry_idle(x)) continue;
-            if (take == P.e.size() || x.bytes < P.e[take].bytes) take = i;
-        }
-        if (take == P.e.size()) {
-            victims = pool_trim(P, kPoolKeep > want ? kPoolKeep - want : 0);
-            ScratchPool::Entry x{nullptr, want, nullptr, 0};
-            if (hipMalloc(&x.p, x.bytes) != hipSuccess) {
-                // out of memory: every idle entry goes, now (under the lock: this lease needs it)
-                free_entries(victims);
-                victims = pool_trim(P, 0);
-                free_entries(victims);
-                victims.clear();
-                if (hipMalloc(&x.p, x.bytes) != hipSuccess) return;
+    const size_t want = (std::max<size_t>(bytes, 1) + 0xFFFFF) & ~size_t(0xFFFFF);
+    // test hook: each new value of the SCRATCH_OOM_SEQ knob makes one lease skip the pool and see its
+    // first hipMalloc fail (a real, oversized request: the HIP error slot is set as by a real OOM)
+    static std::atomic<long> oom_seq{0};
+    const long seq = knob("SCRATCH_OOM_SEQ", 0);
+    const bool force_oom = seq != 0 && oom_seq.exchange(seq) != seq;
+    auto lease = [&](size_t i) {
+        P.e[i].state = 1;
+        dev_ = dev;
+        idx_ = (int)i;
+        p_ = P.e[i].p;
+    };
+    // best fit among idle entries of at most 4x the request; without one, the pool is trimmed and
+    // the victims freed (outside the lock: hipFree synchronises the device) BEFORE the new
+    // allocation, so device memory never holds both; then a second look (another thread may have
+    // released a fitting entry meanwhile) and only then hipMalloc
+    for (int pass = 0; pass < 2; pass++) {
+        std::vector<ScratchPool::Entry> victims;
+        {
+            std::lock_guard<std::mutex> g(P.mu);
+            size_t take = P.e.size();
+            for (size_t i = 0; i < P.e.size(); i++) {
+                ScratchPool::Entry &x = P.e[i];
+                if (x.state == 1 || x.bytes < want || x.bytes / 4 > want) continue;
+                if (!entry_idle(x)) continue;
+                if (take == P.e.size() || x.bytes < P.e[take].bytes) take = i;
             }
-            if (hipEventCreateWithFlags(&x.ev, hipEventDisableTiming) != hipSuccess) {
-                (void)hipFree(x.p);
-                x.p = nullptr;
-            } else {
-                P.e.push_back(x);
-                take = P.e.size() - 1;   // pool_trim may have erased entries: the new one is the last
+            if (take < P.e.size() && !force_oom) {
+                lease(take);
+                return;
             }
+            if (pass == 0) victims = pool_trim(P, kPoolKeep > want ? kPoolKeep - want : 0);
         }
-        if (take < P.e.size()) {
-            P.e[take].state = 1;
-            dev_ = dev;
-            idx_ = (int)take;
-            p_ = P.e[take].p;
+        if (victims.empty()) break;
+        free_entries(victims);
+    }
+    ScratchPool::Entry x{nullptr, want, nullptr, 0};
+    if ((force_oom ? hipMalloc(&x.p, size_t(1) << 62) : hipMalloc(&x.p, x.bytes)) != hipSuccess) {
+        // out of memory: every idle entry goes, then one more try.  The failed call's error stays in
+        // the thread's HIP error slot, where the launch helpers' hipGetLastError() would report a
+        // recovered allocation as a failed launch: clear it.
+        (void)hipGetLastError();
+        std::vector<ScratchPool::Entry> all;
+        {
+            std::lock_guard<std::mutex> g(P.mu);
+            all = pool_trim(P, 0);
+        }
+        free_entries(all);
+        if (hipMalloc(&x.p, x.bytes) != hipSuccess) {
+            (void)hipGetLastError();   // reported by get() == nullptr: the caller's own error path
+            return;
         }
     }
-    free_entries(victims);
+    if (hipEventCreateWithFlags(&x.ev, hipEventDisableTiming) != hipSuccess) {
+        (void)hipFree(x.p);
+        (void)hipGetLastError();
+        return;
+    }
+    std::lock_guard<std::mutex> g(P.mu);
+    P.e.push_back(x);
+    lease(P.e.size() - 1);
 }
 
 tyche::ScratchLease::~ScratchLease() {
@@ -240,8 +263,8 @@ tyche::ScratchLease::~ScratchLease() {
 }
 
 size_t tyche::prepare_launch(const void *kernel) {
-    static std::mutex mu;
-    static std::set<std::pair<int, const void *>> raised;
+    static std::mutex &mu = *new std::mutex;   // never destroyed, like the pools (dispatchers at exit)
+    static auto &raised = *new std::set<std::pair<int, const void *>>;
     static int cus[kMaxDevices] = {0};
     int dev = 0;
     (void)hipGetDevice(&dev);
@@ -330,7 +353,7 @@ struct DeviceSet {
     std::string why;   // empty when ids is non-empty
 };
 const DeviceSet &device_set() {
-    static DeviceSet ds = [] {
+    static DeviceSet &ds = *new DeviceSet([] {
         DeviceSet d;
         int n = 0;
         if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
@@ -355,7 +378,7 @@ const DeviceSet &device_set() {
         }
         if (d.ids.empty()) d.why = "no gfx950 device; libtyche_codec.so carries gfx950 code only";
         return d;
-    }();
+    }());   // never destroyed, like the pools
     return ds;
 }
 
@@ -517,7 +540,7 @@ struct CtxPool {
     std::vector<HostCtx *> all, idle;
     std::vector<int> busy;   // leased contexts per hardware-queue group
 };
-CtxPool g_ctx[kMaxDevices];
+CtxPool *const g_ctx = new CtxPool[kMaxDevices];   // never destroyed (restore dispatchers may run at exit)
 
 // HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default), in
 // creation order; kernels of streams that share a queue run one after the

@@ -43,6 +43,10 @@
 
 namespace tyche {
 
+// The round-2/3 lane kernels below (ring, line-buffered ring, ring-less) are superseded by the
+// chunked decoder (lz4_decode_lc.hip) and are compiled only into the A/B build
+// (-DTYCHE_LEGACY_DECODERS: _build.build(legacy=True), tests/test_legacy_decoders.py).
+#ifdef TYCHE_LEGACY_DECODERS
 namespace {
 
 // 32-byte stream window at ip, zero past L (windowN<16> below is the default
@@ -574,6 +578,7 @@ __global__ __launch_bounds__(64) void lz4_decode_lane_kernel(tyche_batch_t b, ui
 }
 
 }  // namespace
+#endif   // TYCHE_LEGACY_DECODERS
 
 // Threshold and residency (env, for A/B timing): TYCHE_LZ4_LANE_MIN pages per
 // batch (default kLaneMin) switch the batch to this kernel, TYCHE_LZ4_LANE_WAVES
@@ -602,6 +607,9 @@ constexpr int kDefaultWin = 16;
 
 hipError_t launch_lz4_decode_lane(const tyche_batch_t &b, uint32_t in_cap, uint32_t out_cap, hipStream_t s) {
     if (b.count == 0) return hipSuccess;
+#ifndef TYCHE_LEGACY_DECODERS
+    return launch_lz4_decode_lc(b, in_cap, out_cap, s);
+#else
     if (knob("LZ4_QUAD", 0) != 0) return launch_lz4_decode_quad(b, in_cap, out_cap, s);
     // round 4 default: the chunked lane decoder (lz4_decode_lc.hip; 24.1 ms per 1M x 16 KiB pages
     // vs 32.7 for the line-buffered ring kernel below, which TYCHE_LZ4_LC=0 selects)
@@ -660,6 +668,7 @@ hipError_t launch_lz4_decode_lane(const tyche_batch_t &b, uint32_t in_cap, uint3
     if (!ctr.get()) return hipErrorOutOfMemory;
     hipLaunchKernelGGL(lz4_decode_lane_kernel, dim3((unsigned)grid), dim3(64), 0, s, b, in_cap, out_cap, ctr.get());
     return hipGetLastError();
+#endif   // TYCHE_LEGACY_DECODERS
 }
 
 }  // namespace tyche

@@ -386,7 +386,10 @@ __device__ int32_t encode_page(const uint8_t *in, uint32_t L, uint16_t *table, u
     auto sink = [&](const uint2 *rr, uint32_t n, uint32_t anchor) -> bool {
         if ((TYCHE_LZ4_STAGED != 0) & ((TYCHE_LZ4_SINK_CALL & 1) != 0)) return emit_staged_call(rr, n, anchor, in, dst, op, cap, ring, r, map, lane);
         if (TYCHE_LZ4_STAGED) return emit_staged(rr, n, anchor, in, dst, op, cap, ring, r, map, lane);
-        return emit_records(rr, n, anchor, in, dst, op, cap, map, fld, lane);
+        // emit_records' 1 KiB field area ends where the ring does (as in emit_staged's fallback):
+        // with a ring under 1 KiB it starts in the record array, never past the ring into the page
+        return emit_records(rr, n, anchor, in, dst, op, cap, map,
+                            (uint4 *)(kOutRing >= 1024 ? ring : ring + kOutRing - 1024u), lane);
     };
     const uint32_t anchor = lzp::parse_page(in, L, table, rec, lane, sink);
     if (anchor == 0xFFFFFFFFu) return 0;

@@ -652,6 +652,7 @@ hipError_t launch_zlib_deflate(const tyche_batch_t &b, uint32_t in_cap, hipStrea
     // last covers a match of >= 3 bytes)
     const uint32_t ws_stride = ((in_cap / 3u + 3u) * 8u + 255u) & ~255u;
     ScratchLease ws(s, grid * (size_t)ws_stride);
+    if (!ws.get()) return hipErrorOutOfMemory;   // the kernel writes its records there
     hipLaunchKernelGGL(zlib_deflate_kernel, dim3((unsigned)grid), dim3(kWave), lds, s, b, in_cap, ctr.get(),
                        (uint8_t *)ws.get(), ws_stride);
     return hipGetLastError();
