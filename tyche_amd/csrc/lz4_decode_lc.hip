@@ -240,8 +240,11 @@ __device__ __forceinline__ void lc_far_wait(u32x4 (&fv)[N]) {
     for (int32_t i = 0; i < N; i++) asm volatile("" : "+v"(fv[i]));
 }
 
+#ifndef LC_WPE
+#define LC_WPE 2   // register budget: waves per SIMD
+#endif
 template <int32_t R>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void lz4_decode_lc_kernel(tyche_batch_t b, uint32_t in_cap, uint32_t out_cap) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LC_WPE))) void lz4_decode_lc_kernel(tyche_batch_t b, uint32_t in_cap, uint32_t out_cap) {
     typedef LCL<R> Lay;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t lane = threadIdx.x;
@@ -345,7 +348,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void lz
         LPROF_MARK(5);   // window issue
         // ---- stage 3: copy the records into the ring (aligned qwords only)
         lc_far_wait(fv);
-        if (live) {
+        if (TYCHE_ABLATE & 8192) {   // timing only: four more window-sized loads per chunk, waited for
+            const LWin xw = wload(wlive ? P.in : g_lc_pad, wlive ? min(nwb + 64, max(P.L - 64, 0)) : 0, wlive ? P.L : 64);
+            __builtin_amdgcn_s_waitcnt(kVmDrain);
+            if (xw.c0 == (u128)0x123457 && xw.c3 == (u128)1) P.tail ^= 1;
+        }
+        if (live && !(TYCHE_ABLATE & 4096)) {   // (4096, timing only: no copy stage)
             u128 farv[2 * kLC + 2];
 #pragma unroll
             for (int32_t i = 0; i < 2 * kLC + 2; i++) farv[i] = __builtin_bit_cast(u128, fv[i]);
