@@ -923,7 +923,7 @@ int run_host_batch(int dev, size_t n, const void *const *src, const uint32_t *sr
     bool fstop = false;
     int frc = TYCHE_E_OK;
     std::string ferr;
-    std::thread fth;
+    std::vector<std::thread> fth;
     auto finish_async = [&](Slot &S) -> int {   // helper thread: sync, scatter, then free the slot
         hipError_t fe;
         {
@@ -949,22 +949,30 @@ int run_host_batch(int dev, size_t n, const void *const *src, const uint32_t *sr
         g_hprof[kHpChunks]++;
         return TYCHE_E_OK;
     };
-    if (async) {
-        fth = std::thread([&] {
+    // Round 5: HOST_FINISHERS helpers (default 2), each taking the next queued slot: one helper
+    // alternated waiting for a slot and scattering it, so a chunk's scatter never overlapped the
+    // next chunk's wait (r04_host_probe.jsonl: a 13.2 ms decompress call = 7.0 ms of waits + 6.7 ms
+    // of scatter, serially).  Chunks go to disjoint destinations, so their scatters may run in any
+    // order, on the shared copy pool.
+    const int nfin = async ? (int)std::min(4L, std::max(1L, knob("HOST_FINISHERS", 2))) : 0;
+    for (int h = 0; h < nfin; h++) {
+        fth.emplace_back([&] {
             for (;;) {
                 int idx;
                 {
                     std::unique_lock<std::mutex> g(fm);
-                    fcv.wait(g, [&] { return !fq.empty() || fstop; });
-                    if (fq.empty()) return;
+                    fcv.wait(g, [&] { return !fq.empty() || fstop || frc != TYCHE_E_OK; });
+                    if (fq.empty() || frc != TYCHE_E_OK) return;
                     idx = fq.front();
                     fq.erase(fq.begin());
                 }
                 const int r = finish_async(c.slot[idx]);
                 std::lock_guard<std::mutex> g(fm);
                 if (r) {
-                    frc = r;
-                    ferr = t_error;   // the helper's thread-local message
+                    if (frc == TYCHE_E_OK) {
+                        frc = r;
+                        ferr = t_error;   // the helper's thread-local message
+                    }
                     fcv.notify_all();
                     return;
                 }
@@ -974,13 +982,14 @@ int run_host_batch(int dev, size_t n, const void *const *src, const uint32_t *sr
         });
     }
     auto stop_helper = [&] {
-        if (!fth.joinable()) return;
+        if (fth.empty()) return;
         {
             std::lock_guard<std::mutex> g(fm);
             fstop = true;
         }
         fcv.notify_all();
-        fth.join();
+        for (auto &t : fth) t.join();
+        fth.clear();
     };
     struct HelperJoin {   // every return path stops the helper (bail() does so before draining the streams)
         std::function<void()> f;
