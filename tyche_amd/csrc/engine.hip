@@ -824,10 +824,11 @@ int run_host_batch(int dev, size_t n, const void *const *src, const uint32_t *sr
         const uint8_t *hout = (const uint8_t *)S.h_out.p;
         const size_t f0 = S.first;
         std::atomic<uint64_t> moved{0};
+        const bool no_copy = (knob("HOST_DIAG", 0) & 1) != 0;   // diagnostic: results only, no page bytes
         pool.run(k, [&](size_t j) {
             const int32_t r = m_res[j];
             results[f0 + j] = r;
-            if (r > 0 && (uint32_t)r <= dst_cap[f0 + j]) {
+            if (r > 0 && (uint32_t)r <= dst_cap[f0 + j] && !no_copy) {
                 copy_nt(dst[f0 + j], hout + m_doff[j], (size_t)r);
                 moved.fetch_add((uint64_t)r, std::memory_order_relaxed);
             }
@@ -937,10 +938,11 @@ int run_host_batch(int dev, size_t n, const void *const *src, const uint32_t *sr
         const uint8_t *hout = (const uint8_t *)S.h_out.p;
         const size_t f0 = S.first;
         std::atomic<uint64_t> moved{0};
+        const bool no_copy = (knob("HOST_DIAG", 0) & 1) != 0;   // diagnostic: results only, no page bytes
         pool.run(k, [&](size_t j) {
             const int32_t r = m_res[j];
             results[f0 + j] = r;
-            if (r > 0 && (uint32_t)r <= dst_cap[f0 + j]) {
+            if (r > 0 && (uint32_t)r <= dst_cap[f0 + j] && !no_copy) {
                 copy_nt(dst[f0 + j], hout + m_doff[j], (size_t)r);
                 moved.fetch_add((uint64_t)r, std::memory_order_relaxed);
             }
@@ -949,12 +951,12 @@ int run_host_batch(int dev, size_t n, const void *const *src, const uint32_t *sr
         g_hprof[kHpChunks]++;
         return TYCHE_E_OK;
     };
-    // Round 5: HOST_FINISHERS helpers (default 2), each taking the next queued slot: one helper
-    // alternated waiting for a slot and scattering it, so a chunk's scatter never overlapped the
-    // next chunk's wait (r04_host_probe.jsonl: a 13.2 ms decompress call = 7.0 ms of waits + 6.7 ms
-    // of scatter, serially).  Chunks go to disjoint destinations, so their scatters may run in any
-    // order, on the shared copy pool.
-    const int nfin = async ? (int)std::min(4L, std::max(1L, knob("HOST_FINISHERS", 2))) : 0;
+    // HOST_FINISHERS helpers (default 1), each taking the next queued slot (chunks go to disjoint
+    // destinations, so their scatters may run in any order, on the shared copy pool).  Round 5: a
+    // second and third helper, so that one chunk's scatter overlaps the next one's wait, did not
+    // move decompress (32K pages, best of 5 interleaved: 34.2 / 33.7 / 31.7 GiB/s for 1 / 2 / 3,
+    // profiles/r05_host_probe.jsonl).
+    const int nfin = async ? (int)std::min(4L, std::max(1L, knob("HOST_FINISHERS", 1))) : 0;
     for (int h = 0; h < nfin; h++) {
         fth.emplace_back([&] {
             for (;;) {
