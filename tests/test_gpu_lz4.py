@@ -486,6 +486,74 @@ def test_decode_jump_path_page_kinds(tc, oracle_mod, plen, n):
         assert r == plen and dec == host[i].tobytes(), i
 
 
+def short_sequence_stream(rng, plen):
+    """A valid LZ4 block made almost entirely of 3-byte sequences (no literals, 4..18-byte matches
+    at random offsets): the token chain runs in phase with period 3 for the whole page, the case
+    that defeats token walks started at fixed segment offsets."""
+    first = 24
+    s = bytearray([0xF0 | 0, first - 15]) + bytearray(rng.integers(0, 256, first, dtype=np.uint8).tobytes())
+    s += int(rng.integers(1, first + 1)).to_bytes(2, "little")
+    out = first + 4
+    while out < plen - 40:
+        code = int(rng.integers(0, 15))
+        s.append(code)
+        s += int(rng.integers(1, min(out, 65535) + 1)).to_bytes(2, "little")
+        out += code + 4
+    lit = plen - out
+    ext = lit - 15
+    s.append(0xF0)
+    while ext >= 255:
+        s.append(255)
+        ext -= 255
+    s.append(ext)
+    s += bytearray(rng.integers(0, 256, lit, dtype=np.uint8).tobytes())
+    return bytes(s)
+
+
+@pytest.mark.parametrize("kernel", ["solo", "jump"])
+def test_decode_small_batch_kernels(tc, oracle_mod, knobs, kernel):
+    """The small-batch LZ4 decoders side by side: the single-page decoder (round 5, the default
+    for batches of <= 4,096 pages) and the jump decoder (LZ4_SOLO_MAX=0).  The reference fixtures
+    with their exact return values at 1 and 20 pages, seeded corruptions (bit flips, truncations,
+    reduced capacities) against the restated LZ4_decompress_safe, crafted pages of back-to-back
+    3-byte sequences (with and without corruptions), and every page kind at 8, 16 and 32 KiB."""
+    if kernel == "jump":
+        knobs(LZ4_SOLO_MAX=0)
+    test_decode_lane_path_fixtures(tc, 1)
+    test_decode_lane_path_fixtures(tc, 20)
+    rng = np.random.default_rng(4000 + len(kernel))
+    pages = oracle_mod.pagegen(300, 16384, seed=17, first=len(kernel), dist=0)
+    streams, caps = [], []
+    for i in range(300):
+        c = bytearray(oracle_mod.lz4_compress(pages[i].tobytes()))
+        if i % 4 == 1:
+            c[int(rng.integers(0, len(c)))] ^= 1 << int(rng.integers(0, 8))
+        elif i % 4 == 2:
+            c = c[: int(rng.integers(1, len(c)))]
+        streams.append(bytes(c))
+        caps.append(16384 if i % 4 != 3 else int(rng.integers(100, 16384)))
+    rv, outs = ragged_decode(tc, streams, caps)
+    for i in range(300):
+        r, want = oracle_mod.lz4_decompress(streams[i], caps[i])
+        assert rv[i] == r, (i, rv[i], r)
+        if r > 0 and i % 4 in (0, 3):
+            assert outs[i][:r] == want[:r], i
+    streams = [short_sequence_stream(rng, 16384) for _ in range(24)]
+    for i in range(8, 24, 2):
+        c = bytearray(streams[i])
+        c[int(rng.integers(0, len(c)))] ^= 1 << int(rng.integers(0, 8))
+        streams[i] = bytes(c)
+    for n in (1, 24):
+        rv, outs = ragged_decode(tc, streams[:n], [16384] * n)
+        for i in range(n):
+            r, want = oracle_mod.lz4_decompress(streams[i], 16384)
+            assert rv[i] == r, (i, rv[i], r)
+            assert r < 0 or outs[i][:r] == want[:r], i
+    for plen in (8192, 16384, 32768):
+        test_decode_jump_path_page_kinds(tc, oracle_mod, plen, 7)
+        test_decode_jump_path_page_kinds(tc, oracle_mod, plen, 300)
+
+
 def test_c2_full_size_round_trip(tc):
     """BASELINE configs[1] at its full size on one GPU: 1,048,576 x 16 KiB synthetic pages
     (16 GiB) LZ4-compressed and decompressed through the lane decoder, every page bit-exact,

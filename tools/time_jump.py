@@ -1,4 +1,5 @@
-"""Diagnostic: LZ4 decode time of the jump decoder vs the wave decoder per batch size.
+"""Diagnostic: LZ4 decode time of the small-batch decoders per batch size (single-page decoder, jump
+decoder at 1,024 / 512 threads, wave decoder; MODES selects).
 
     python tools/time_jump.py            # prints one JSON line per (decoder, page_len, batch)
 Each decoder runs in a child process (TYCHE_LZ4_JUMP_MAX is read once per process):
@@ -73,8 +74,12 @@ def main():
         print(r.stdout.strip() or r.stderr.strip()[-1500:], flush=True)
     if os.environ.get("LZ4", "1") == "0":
         return
-    for mode, jmax, wide in (("jump", "32767", "1"), ("jump512", "32767", "0"), ("wave", "0", "1")):
-        env = dict(os.environ, MODE=mode, TYCHE_LZ4_JUMP_MAX=jmax, TYCHE_LZ4_JUMP_WIDE=wide)
+    modes = os.environ.get("MODES", "solo,jump,jump512,wave").split(",")
+    table = {"solo": ("4096", "32767", "1"), "jump": ("0", "32767", "1"), "jump512": ("0", "32767", "0"),
+             "wave": ("0", "0", "1")}
+    for mode in modes:
+        smax, jmax, wide = table[mode]
+        env = dict(os.environ, MODE=mode, TYCHE_LZ4_SOLO_MAX=smax, TYCHE_LZ4_JUMP_MAX=jmax, TYCHE_LZ4_JUMP_WIDE=wide)
         r = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=600)
         print(r.stdout.strip() or r.stderr.strip()[-1500:], flush=True)
 

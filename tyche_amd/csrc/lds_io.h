@@ -6,6 +6,7 @@
 namespace tyche {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 // LDS accesses at any byte address: gfx950 runs in unaligned DS mode, so a
 // 32-bit access through an align(1) type is a single ds_read_b32 / ds_write_b32

@@ -1234,6 +1234,413 @@ __global__ __launch_bounds__(kJumpThreads) void lz4_decode_jump_kernel(tyche_bat
     }
 }
 
+// ---------------------------------------------------------------------------
+// Round 5: the single-page decoder (the restore path's latency).  One 1,024-thread
+// workgroup per page; the jump kernel's cells and pointer jumping, with its two
+// slowest phases replaced (one 16 KiB page alone on a CU: token chain walked by one
+// wave while the others wait, then a run-start scan):
+//
+//  1. token chain by pointer doubling over stream positions.  Every position q
+//     gets J(q) = where the token after a token at q would start (next_token_w;
+//     a terminal or malformed token and the stream's end map to the sink L).
+//     Position 0 is marked; in each round every marked q marks J(q), then
+//     J <- J o J, so after k rounds every position at chain distance < 2^k from 0
+//     is marked; the rounds stop when J(0) is the sink.  Marks only grow and only
+//     land on chain positions, so a round needs no order among its threads.  The
+//     marked positions in position order are the token list (a block prefix sum
+//     of per-thread counts places them).  Every position costs the same: no walk
+//     can start out of phase (segment walks with stamps, tried first, stay out of
+//     phase through runs of 3-byte sequences and their bridges ran 100+ tokens);
+//  2. every thread takes consecutive tokens: decodes them (decode_seq_in), a
+//     block prefix sum of their output lengths gives their output offsets, the
+//     reference's checks run at those offsets (seq_check; atomicMin of the first
+//     failing token gives the exact -(consumed)-1), then the tokens before it fill
+//     their cells directly -- literals final (0x8000 | byte), match bytes pointing
+//     at the byte they copy (fill_match: d - off + j, or + j mod off when the match
+//     overlaps itself), runs over 16 bytes through the workgroup's list;
+//  3. pointer jumping, pack and store as in the jump kernel.
+
+constexpr uint32_t kSoloNpt = 8;      // positions per thread chunk
+constexpr uint32_t kSoloChunks = 3;   // chunks per thread: streams up to 3 * 8 * 1,024 - 1 bytes
+constexpr uint32_t kSoloGroups = 4;   // 8-cell groups per thread in the jump rounds: pages up to 32 KiB
+// next_token_w for the token byte t at p, without the offset and literal reads next_token_w's
+// decode_seq_in makes: only the length-extension bytes are read (lz4.c:1134-1143, 1165, 1172-1182)
+__device__ __forceinline__ uint32_t solo_next(const uint8_t *in, int32_t L, int32_t p, uint32_t t) {
+    int32_t q = p + 1, lit = (int32_t)(t >> 4);
+    if (lit == kRunMask) {
+        uint32_t b;
+        do {
+            b = in[q];
+            q++;
+            lit += (int32_t)b;
+        } while (q < L - kRunMask && b == 255);
+    }
+    if (q + lit > L - 8) return kEnd;   // terminal literal run
+    int32_t q2 = q + lit + 2;
+    if ((t & 15u) == 15u) {
+        uint32_t b;
+        do {
+            b = in[q2];
+            q2++;
+            if (q2 > L - kLastLiterals) return kEnd;   // overrun in the match length
+        } while (b == 255);
+    }
+    return (uint32_t)q2;
+}
+
+// LDS layout of the single-page decoder (host and device agree through this)
+struct SoloLay {
+    uint32_t stage, tok, scr;   // byte offsets in LDS
+    uint32_t jb, mark;          // byte offsets in scr: the second J buffer, the marks (token chain)
+    uint32_t rec, slot;         // byte offsets in scr: token records, 4-cell group covering table (cells)
+    uint32_t nslots, total;
+};
+__host__ __device__ inline uint32_t solo_up16(uint32_t x) { return (x + 15u) & ~15u; }
+__host__ __device__ inline SoloLay solo_layout(uint32_t in_cap, uint32_t out_cap) {
+    SoloLay l;
+    l.stage = 256u;   // 64 header words
+    l.tok = l.stage + solo_up16(in_cap + 16u + kPad);
+    const uint32_t max_tok = in_cap / 3u + 2u;   // a chain token consumes >= 3 bytes, but the last
+    l.scr = l.tok + solo_up16(2u * max_tok);
+    const uint32_t nodes = solo_up16(2u * (in_cap + 1u));   // u16 per position, + the sink
+    l.jb = nodes;
+    l.mark = 2u * nodes;
+    const uint32_t chain_bytes = 2u * nodes + solo_up16(in_cap + 4u);   // (marks read as 8-byte words)
+    const uint32_t cells_bytes = 2u * ((out_cap + 63u) & ~63u);
+    l.rec = cells_bytes;
+    l.slot = l.rec + 8u * (max_tok + 1u);
+    l.nslots = ((out_cap + 63u) & ~63u) / 4u;
+    l.total = l.scr + std::max(chain_bytes, l.slot + solo_up16(2u * l.nslots));
+    return l;
+}
+
+// exclusive prefix sum over the workgroup (every thread calls it; wsum: kT / 64 words)
+template <uint32_t kT>
+__device__ __forceinline__ uint32_t solo_excl_sum(uint32_t v, uint32_t *wsum, uint32_t tid, uint32_t &total) {
+    const uint32_t w = tid >> 6;
+    const uint32_t incl = (uint32_t)wave_incl_sum((int32_t)v);
+    if ((tid & 63u) == 63u) wsum[w] = incl;
+    __syncthreads();
+    uint32_t base = 0, tot = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kT / 64u; k++) {
+        const uint32_t x = wsum[k];
+        base += k < w ? x : 0u;
+        tot += x;
+    }
+    total = tot;
+    __syncthreads();   // wsum may be reused
+    return base + incl - v;
+}
+
+template <uint32_t kT>
+__global__ __launch_bounds__(kT) void lz4_decode_solo_kernel(tyche_batch_t b, uint32_t in_cap, uint32_t out_cap,
+                                                             SoloLay lay, unsigned *ctr) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1);
+    // words: [0] rv, [2] first failing (or the terminal) token, [5] claimed page, [6..8] jump round flags,
+    // [16..31] block-sum scratch
+    uint32_t *hw = (uint32_t *)smem;
+    int32_t &s_rv = *(int32_t *)&hw[0];
+    uint32_t *wsum = hw + 16;
+    uint8_t *stage = smem + lay.stage;
+    uint16_t *tok = (uint16_t *)(smem + lay.tok);
+    uint8_t *scr = smem + lay.scr;
+    uint16_t *ja0 = (uint16_t *)scr, *jb0 = (uint16_t *)(scr + lay.jb);   // J, double-buffered
+    uint8_t *mark = scr + lay.mark;
+    uint16_t *cells = (uint16_t *)scr;   // the same bytes once the token list is out
+    uint2 *rec = (uint2 *)(scr + lay.rec);
+    uint16_t *slot = (uint16_t *)(scr + lay.slot);
+    size_t page = blockIdx.x;
+    while (page < b.count) {
+        PROF_DECL
+        const PageRef p = batch_page(b, page);
+        const bool fits = p.src_len <= in_cap && p.dst_cap <= out_cap;
+        const uint32_t head = stage_in(p.src, fits ? p.src_len : 0u, stage, tid, kT);
+        const int32_t L = (int32_t)p.src_len, C = (int32_t)p.dst_cap;
+        if (tid == 0) {
+            hw[2] = 0xFFFFFFFFu;
+            hw[6] = 0;   // round 0's flag
+        }
+        uint8_t *in = stage + head;
+        const bool go = fits && C > 0 && L > 0;
+        __syncthreads();
+        if (fits && tid < kPad) in[L + tid] = 0;   // kPad zero bytes past the end
+        if (tid == 0)
+            s_rv = !fits ? kResultTooLarge : C == 0 ? ((L == 1 && in[0] == 0) ? 0 : -1) : L == 0 ? -1 : kJumpPending;
+        __syncthreads();
+        PROF_MARK(1);
+        if (go) {
+            // ---- 1. J(q) for every position, position 0 marked.  Thread t owns positions
+            // [8 (t nch + c), +8) for its nch chunks c and keeps their J values in registers (two per
+            // word), so a round reads only its marks (one 8-byte word) and the 8 J(J(q)) from LDS and
+            // writes one 16-byte word of J (and the marks it sets).
+            const uint32_t n = (uint32_t)L + 1u;   // positions + the sink
+            const uint32_t nch = (n + kSoloNpt * kT - 1u) / (kSoloNpt * kT);
+            uint32_t jr[kSoloChunks][4];
+            {
+                const uint32_t ib = (uint32_t)(uintptr_t)in & 3u;
+                const uint32_t *A = (const uint32_t *)(in - ib);
+#pragma unroll
+                for (uint32_t c = 0; c < kSoloChunks; c++) {
+                    const uint32_t base = (tid * nch + c) * kSoloNpt;
+                    if (c < nch && base < n) {
+                        const uint32_t qa = base + ib;
+                        const uint32_t w0 = A[qa >> 2], w1 = A[(qa >> 2) + 1], w2 = A[(qa >> 2) + 2];
+                        const uint32_t x0 = __builtin_amdgcn_alignbyte(w1, w0, qa & 3u);
+                        const uint32_t x1 = __builtin_amdgcn_alignbyte(w2, w1, qa & 3u);
+                        uint32_t nx[8];
+#pragma unroll
+                        for (uint32_t u = 0; u < 8u; u++) {
+                            const uint32_t q = base + u;
+                            const uint32_t t = ((u < 4u ? x0 : x1) >> (8u * (u & 3u))) & 0xFFu;
+                            nx[u] = q < (uint32_t)L ? min(solo_next(in, L, (int32_t)q, t), (uint32_t)L) : (uint32_t)L;
+                        }
+#pragma unroll
+                        for (uint32_t k = 0; k < 4u; k++) jr[c][k] = nx[2 * k] | nx[2 * k + 1] << 16;
+                        *(uint4 *)(ja0 + base) = make_uint4(jr[c][0], jr[c][1], jr[c][2], jr[c][3]);
+                        *(uint2 *)(mark + base) = make_uint2(base == 0 ? 1u : 0u, 0u);
+                    } else {
+#pragma unroll
+                        for (uint32_t k = 0; k < 4u; k++) jr[c][k] = 0;
+                    }
+                }
+            }
+            __syncthreads();
+            PROF_MARK(2);
+            // doubling rounds (at most 16: J^(2^16)(0) is the sink for any u16 position chain)
+            uint16_t *Ja = ja0, *Jb = jb0;
+            uint32_t lev = 0;
+            for (; lev < 17u && Ja[0] != (uint16_t)L; lev++) {
+#pragma unroll
+                for (uint32_t c = 0; c < kSoloChunks; c++) {
+                    const uint32_t base = (tid * nch + c) * kSoloNpt;
+                    if (c < nch && base < n) {
+                        const uint2 mw = *(const uint2 *)(mark + base);
+                        uint32_t jj[8];
+#pragma unroll
+                        for (uint32_t u = 0; u < 8u; u++) jj[u] = Ja[(jr[c][u >> 1] >> (16u * (u & 1u))) & 0xFFFFu];
+#pragma unroll
+                        for (uint32_t u = 0; u < 8u; u++)
+                            if ((((u < 4u ? mw.x : mw.y) >> (8u * (u & 3u))) & 1u) != 0u)
+                                mark[(jr[c][u >> 1] >> (16u * (u & 1u))) & 0xFFFFu] = 1;
+#pragma unroll
+                        for (uint32_t k = 0; k < 4u; k++) jr[c][k] = jj[2 * k] | jj[2 * k + 1] << 16;
+                        *(uint4 *)(Jb + base) = make_uint4(jr[c][0], jr[c][1], jr[c][2], jr[c][3]);
+                    }
+                }
+                __syncthreads();
+                uint16_t *x = Ja;
+                Ja = Jb;
+                Jb = x;
+            }
+            PROF_MARK(3);
+            PROF_ADD(11, lev);
+            // ---- the token list: the marked positions below L, in order (thread order = position order)
+            uint32_t cnt = 0;
+            uint64_t mk[kSoloChunks];
+#pragma unroll
+            for (uint32_t c = 0; c < kSoloChunks; c++) {
+                const uint32_t base = (tid * nch + c) * kSoloNpt;
+                mk[c] = 0;
+                if (c < nch && base < (uint32_t)L) {
+                    const uint64_t keep = (uint32_t)L - base >= 8u ? ~0ull : (1ull << (8u * ((uint32_t)L - base))) - 1ull;
+                    mk[c] = *(const uint64_t *)(mark + base) & keep & 0x0101010101010101ull;
+                    cnt += (uint32_t)__builtin_popcountll(mk[c]);
+                }
+            }
+            uint32_t ntok = 0;
+            uint32_t o = solo_excl_sum<kT>(cnt, wsum, tid, ntok);
+#pragma unroll
+            for (uint32_t c = 0; c < kSoloChunks; c++) {
+                const uint32_t base = (tid * nch + c) * kSoloNpt;
+#pragma unroll
+                for (uint32_t u = 0; u < 8u; u++)
+                    if ((mk[c] >> (8u * u)) & 1u) tok[o++] = (uint16_t)(base + u);
+            }
+            __syncthreads();   // marks read: the cells may take the bytes
+            PROF_MARK(4);
+            // ---- 2. decode, output offsets, checks and one record per token (its output offset o,
+            // literal count, literal start and match offset); the covering table gets, at slot
+            // ceil(o / 4), the token whose output holds the first cell of 4-cell group (o + 3) / 4
+            const uint32_t K = (ntok + kT - 1u) / kT;
+            const uint32_t t0 = min(tid * K, ntok), t1 = min(t0 + K, ntok);
+            for (uint32_t w = tid; w < lay.nslots; w += kT) slot[w] = 0;
+            uint32_t olen = 0;
+            for (uint32_t i = t0; i < t1; i++) {
+                const SeqIn sq = decode_seq_in(in, L, (int32_t)tok[i]);
+                olen += (uint32_t)(sq.in_term ? sq.lit : sq.lit + sq.ml);
+            }
+            uint32_t otot = 0;
+            const uint32_t obase = solo_excl_sum<kT>(olen, wsum, tid, otot);
+            int32_t ob = (int32_t)obase;
+            uint32_t my_first = 0xFFFFFFFFu;
+            int32_t my_rv = -1;
+            for (uint32_t i = t0; i < t1; i++) {
+                const SeqIn sq = decode_seq_in(in, L, (int32_t)tok[i]);
+                int32_t r;
+                const int32_t st = seq_check(sq, ob, L, C, r);
+                if (st) {
+                    my_first = i;
+                    my_rv = r;
+                    atomicMin(&hw[2], i);
+                }
+                if (st == 2) break;   // (a token that passes its own checks lies inside [0, C))
+                const int32_t e = ob + sq.lit + (st == 1 ? 0 : sq.ml);
+                rec[i] = make_uint2((uint32_t)ob | ((uint32_t)sq.lit << 16), (uint32_t)sq.ls | ((uint32_t)sq.off << 16));
+                const uint32_t s0 = ((uint32_t)ob + 3u) >> 2;
+                if (s0 < (((uint32_t)e + 3u) >> 2)) slot[s0] = (uint16_t)i;
+                if (st == 1) break;
+                ob = e;
+            }
+            __syncthreads();
+            if (my_first != 0xFFFFFFFFu && my_first == hw[2]) s_rv = my_rv;
+            if (hw[2] == 0xFFFFFFFFu && tid == 0) s_rv = -1;   // unreachable: the chain ends in a stop
+            __syncthreads();
+            PROF_MARK(5);
+        }
+        PROF_ADD(9, 1);
+        const int32_t rv = s_rv;
+        if (rv > 0) {
+            // ---- 3. cells, one per lane (consecutive lanes, consecutive cells): the token holding cell
+            // c is the covering token of its 4-cell group (the running maximum of the slots) or the next
+            // one (a token other than the last spans >= 4 cells); literal cells final (0x8000 | byte),
+            // match cells pointing at the byte they copy (d - off + ((c - d) mod off): the match's own
+            // earlier bytes when it overlaps itself), cells past rv final
+            const uint32_t n64 = ((uint32_t)rv + 63u) & ~63u;
+            const uint32_t ng4 = n64 / 4u, gpt = (ng4 + kT - 1u) / kT;   // groups per thread: <= 8
+            const uint32_t last = hw[2];   // the terminal token
+            {
+                uint32_t m = 0;
+                for (uint32_t u = 0; u < gpt; u++) {
+                    const uint32_t g = tid * gpt + u;
+                    if (g < ng4) m = max(m, (uint32_t)slot[g]);
+                }
+                const uint32_t w = tid >> 6;
+                const uint32_t incl = (uint32_t)wave_incl_max((int32_t)m);
+                if ((tid & 63u) == 63u) wsum[w] = incl;
+                uint32_t before = (uint32_t)__shfl_up((int32_t)incl, 1);
+                if ((tid & 63u) == 0u) before = 0;
+                __syncthreads();
+                for (uint32_t k = 0; k < w; k++) before = max(before, wsum[k]);
+                for (uint32_t u = 0; u < gpt; u++) {
+                    const uint32_t g = tid * gpt + u;
+                    if (g < ng4) {
+                        before = max(before, (uint32_t)slot[g]);
+                        slot[g] = (uint16_t)before;
+                    }
+                }
+                __syncthreads();
+            }
+            PROF_MARK(10);
+            for (uint32_t c0 = tid; c0 < n64; c0 += 4u * kT) {
+                uint32_t cc[4], kk[4];
+                uint2 r0[4], r1[4];
+#pragma unroll
+                for (uint32_t u = 0; u < 4u; u++) {
+                    cc[u] = c0 + u * kT;
+                    kk[u] = cc[u] < (uint32_t)rv ? (uint32_t)slot[cc[u] >> 2] : 0u;
+                }
+#pragma unroll
+                for (uint32_t u = 0; u < 4u; u++) {
+                    r0[u] = rec[kk[u]];
+                    r1[u] = rec[kk[u] < last ? kk[u] + 1u : kk[u]];
+                }
+                uint32_t lb[4];
+#pragma unroll
+                for (uint32_t u = 0; u < 4u; u++) {
+                    const uint2 r = kk[u] < last && cc[u] >= (r1[u].x & 0xFFFFu) ? r1[u] : r0[u];
+                    r0[u] = r;
+                    const uint32_t o = r.x & 0xFFFFu, d = o + (r.x >> 16);
+                    lb[u] = cc[u] < (uint32_t)rv && cc[u] < d ? (uint32_t)in[(r.y & 0xFFFFu) + cc[u] - o] : 0u;
+                }
+#pragma unroll
+                for (uint32_t u = 0; u < 4u; u++) {
+                    if (cc[u] >= n64) continue;
+                    const uint2 r = r0[u];
+                    const uint32_t o = r.x & 0xFFFFu, d = o + (r.x >> 16), off = r.y >> 16;
+                    uint32_t v = kLitFlag;
+                    if (cc[u] < (uint32_t)rv) {
+                        if (cc[u] < d) {
+                            v = kLitFlag | lb[u];
+                        } else if (off != 0) {
+                            const uint32_t j = cc[u] - d;
+                            v = d - off + (j < off ? j : mod_small(j, off));
+                        }
+                    }
+                    cells[cc[u]] = (uint16_t)v;
+                }
+            }
+            __syncthreads();
+            PROF_MARK(6);
+            // pointer jumping, 8 cells per group; each thread keeps its groups (tid + i kT) in registers
+            // across the rounds, so a round reads LDS only for its unresolved cells' targets and writes
+            // back only the groups that changed, and the last round's registers are packed and stored
+            u32x4 *c4 = (u32x4 *)cells;
+            const uint32_t ng = n64 / 8u;
+            uint32_t *flag = hw + 6;
+            const u32x4 fin = {0x80008000u, 0x80008000u, 0x80008000u, 0x80008000u};
+            u32x4 cv[kSoloGroups];
+#pragma unroll
+            for (uint32_t i = 0; i < kSoloGroups; i++) {
+                const uint32_t g = tid + i * kT;
+                cv[i] = g < ng ? c4[g] : fin;
+            }
+            for (uint32_t r = 0;; r++) {
+                if (tid == 0) flag[(r + 1) % 3] = 0;
+                uint32_t open = 0;
+#pragma unroll
+                for (uint32_t i = 0; i < kSoloGroups; i++) {
+                    u32x4 v = cv[i];
+                    if (((v.x & v.y & v.z & v.w) & 0x80008000u) != 0x80008000u) {
+                        v.x = jump_pair(cells, v.x, open);
+                        v.y = jump_pair(cells, v.y, open);
+                        v.z = jump_pair(cells, v.z, open);
+                        v.w = jump_pair(cells, v.w, open);
+                        c4[tid + i * kT] = v;
+                        cv[i] = v;
+                    }
+                }
+                if (open) atomicOr(&flag[r % 3], 1u);
+                __syncthreads();
+                if (flag[r % 3] == 0) {
+                    PROF_ADD(12, r + 1);
+                    break;
+                }
+            }
+            PROF_MARK(7);
+            // cells -> bytes, 8 per group
+            uint8_t *dst = p.dst;
+            const bool al = ((uintptr_t)dst & 7u) == 0;
+#pragma unroll
+            for (uint32_t i = 0; i < kSoloGroups; i++) {
+                const uint32_t g = tid + i * kT;
+                if (g >= ng) continue;
+                const u32x4 a = cv[i];
+                const uint32_t lo = __builtin_amdgcn_perm(a.y, a.x, 0x06040200u);
+                const uint32_t hi = __builtin_amdgcn_perm(a.w, a.z, 0x06040200u);
+                const uint32_t base = 8u * g;
+                if (al && base + 8u <= (uint32_t)rv) {
+                    __builtin_nontemporal_store(u32x2{lo, hi}, (u32x2 *)(dst + base));
+                } else if (base < (uint32_t)rv) {
+                    const uint32_t nb8 = min(8u, (uint32_t)rv - base);
+                    for (uint32_t j = 0; j < nb8; j++) dst[base + j] = (uint8_t)((j < 4u ? lo : hi) >> (8u * (j & 3u)));
+                }
+            }
+        }
+        PROF_MARK(8);
+        if (tid == 0) b.results[page] = rv;
+        if (ctr) {
+            if (tid == 0) hw[5] = atomicAdd(ctr, 1u) + gridDim.x;
+            __syncthreads();
+            page = hw[5];
+        } else {
+            page += gridDim.x;
+        }
+        __syncthreads();
+    }
+}
+
 }  // namespace
 
 // Batches below this many pages (TYCHE_LZ4_JUMP_MAX) take the jump decoder when
@@ -1273,13 +1680,46 @@ static hipError_t launch_lz4_decode_jump(const tyche_batch_t &b, uint32_t in_cap
     return hipGetLastError();
 }
 
+// Batches of at most this many pages (TYCHE_LZ4_SOLO_MAX; 0 turns it off) take the single-page
+// decoder when its LDS layout fits (pages <= 16 KiB and streams up to their bound; larger pages
+// take the jump decoder)
+constexpr long kSoloMax = 4096;
+static hipError_t launch_lz4_decode_solo(const tyche_batch_t &b, uint32_t in_cap, uint32_t out_cap, hipStream_t s,
+                                         bool &launched) {
+    launched = false;
+    const long smax = knob("LZ4_SOLO_MAX", kSoloMax);
+    if ((long)b.count > smax || out_cap > 32768u || in_cap >= kSoloChunks * kSoloNpt * 1024u) return hipSuccess;
+    constexpr uint32_t kT = 1024;
+    const SoloLay lay = solo_layout(in_cap, out_cap);
+    if (lay.total > 160u * 1024u) return hipSuccess;
+    const void *k = (const void *)lz4_decode_solo_kernel<kT>;
+    const size_t ncu = prepare_launch(k);
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, (int)kT, lay.total) != hipSuccess || per_cu < 1)
+        per_cu = 1;
+    const size_t grid = std::min<size_t>(b.count, ncu * (size_t)per_cu);
+    WorkCounter ctr(s, grid < b.count);
+    if (grid < b.count && !ctr.get()) return hipErrorOutOfMemory;
+    unsigned *cp = grid < b.count ? ctr.get() : nullptr;
+    void *args[] = {(void *)&b, &in_cap, &out_cap, (void *)&lay, &cp};
+    (void)hipLaunchKernel(k, dim3((unsigned)grid), dim3(kT), args, lay.total, s);
+    launched = true;
+    return hipGetLastError();
+}
+
 hipError_t launch_lz4_decode(const tyche_batch_t &b, uint32_t in_cap, uint32_t out_cap, hipStream_t s,
                              bool allow_lane) {
     if (b.count == 0) return hipSuccess;
     // large batches: one page per lane (lz4_decode_lane.hip); never into host memory (allow_lane
     // false): that decoder reads its flushed output back
     if (allow_lane && lz4_lane_decode_wanted(b.count, in_cap, out_cap)) return launch_lz4_decode_lane(b, in_cap, out_cap, s);
-    // small batches: workgroup per page, pointer-jumping match resolution
+    // small batches: workgroup per page, pointer-jumping match resolution -- the single-page decoder
+    // (round 5) when its layout fits, else the jump decoder
+    {
+        bool launched = false;
+        const hipError_t es = launch_lz4_decode_solo(b, in_cap, out_cap, s, launched);
+        if (launched || es != hipSuccess) return es;
+    }
     {
         bool launched = false;
         const hipError_t e = launch_lz4_decode_jump(b, in_cap, out_cap, s, launched);
