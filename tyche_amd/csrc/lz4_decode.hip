@@ -1288,6 +1288,47 @@ __device__ __forceinline__ uint32_t solo_next(const uint8_t *in, int32_t L, int3
     return (uint32_t)q2;
 }
 
+// decode_seq_in without the literal window (the single-page decoder reads literal bytes per cell):
+// token, length-extension bytes and the offset, the reads of lz4.c:1134-1143, 1165, 1172-1182
+__device__ __forceinline__ SeqIn solo_seq(const uint8_t *in, int32_t L, int32_t p) {
+    SeqIn s;
+    const uint32_t t = in[p];
+    int32_t q = p + 1;
+    s.lit = (int32_t)(t >> 4);
+    s.lit_win = false;
+    if (s.lit == kRunMask) {
+        uint32_t b;
+        do {
+            b = in[q];
+            q++;
+            s.lit += (int32_t)b;
+        } while (q < L - kRunMask && b == 255);
+    }
+    s.ls = q;
+    s.in_term = q + s.lit > L - 8;
+    s.off = 0;
+    s.ml = 0;
+    s.q2 = 0;
+    s.ml_err = false;
+    if (!s.in_term) {
+        s.off = (int32_t)lds_ld16(in + q + s.lit);
+        int32_t q2 = q + s.lit + 2;
+        int32_t ml = (int32_t)(t & 15u);
+        if (ml == 15) {
+            uint32_t b;
+            do {
+                b = in[q2];
+                q2++;
+                if (q2 > L - kLastLiterals) { s.ml_err = true; break; }
+                ml += (int32_t)b;
+            } while (b == 255);
+        }
+        s.ml = ml + kMinMatch;
+        s.q2 = q2;
+    }
+    return s;
+}
+
 // LDS layout of the single-page decoder (host and device agree through this)
 struct SoloLay {
     uint32_t stage, tok, scr;   // byte offsets in LDS
@@ -1335,7 +1376,7 @@ __device__ __forceinline__ uint32_t solo_excl_sum(uint32_t v, uint32_t *wsum, ui
 
 template <uint32_t kT>
 __global__ __launch_bounds__(kT) void lz4_decode_solo_kernel(tyche_batch_t b, uint32_t in_cap, uint32_t out_cap,
-                                                             SoloLay lay, unsigned *ctr) {
+                                                             SoloLay lay, unsigned *ctr, uint32_t sys_fence) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1);
     // words: [0] rv, [2] first failing (or the terminal) token, [5] claimed page, [6..8] jump round flags,
@@ -1419,7 +1460,10 @@ __global__ __launch_bounds__(kT) void lz4_decode_solo_kernel(tyche_batch_t b, ui
                         const uint2 mw = *(const uint2 *)(mark + base);
                         uint32_t jj[8];
 #pragma unroll
-                        for (uint32_t u = 0; u < 8u; u++) jj[u] = Ja[(jr[c][u >> 1] >> (16u * (u & 1u))) & 0xFFFFu];
+                        for (uint32_t u = 0; u < 8u; u++) {
+                            const uint32_t j = (jr[c][u >> 1] >> (16u * (u & 1u))) & 0xFFFFu;
+                            jj[u] = j == (uint32_t)L ? j : (uint32_t)Ja[j];   // (the sink maps to itself)
+                        }
 #pragma unroll
                         for (uint32_t u = 0; u < 8u; u++)
                             if ((((u < 4u ? mw.x : mw.y) >> (8u * (u & 3u))) & 1u) != 0u)
@@ -1468,7 +1512,7 @@ __global__ __launch_bounds__(kT) void lz4_decode_solo_kernel(tyche_batch_t b, ui
             for (uint32_t w = tid; w < lay.nslots; w += kT) slot[w] = 0;
             uint32_t olen = 0;
             for (uint32_t i = t0; i < t1; i++) {
-                const SeqIn sq = decode_seq_in(in, L, (int32_t)tok[i]);
+                const SeqIn sq = solo_seq(in, L, (int32_t)tok[i]);
                 olen += (uint32_t)(sq.in_term ? sq.lit : sq.lit + sq.ml);
             }
             uint32_t otot = 0;
@@ -1477,7 +1521,7 @@ __global__ __launch_bounds__(kT) void lz4_decode_solo_kernel(tyche_batch_t b, ui
             uint32_t my_first = 0xFFFFFFFFu;
             int32_t my_rv = -1;
             for (uint32_t i = t0; i < t1; i++) {
-                const SeqIn sq = decode_seq_in(in, L, (int32_t)tok[i]);
+                const SeqIn sq = solo_seq(in, L, (int32_t)tok[i]);
                 int32_t r;
                 const int32_t st = seq_check(sq, ob, L, C, r);
                 if (st) {
@@ -1533,42 +1577,49 @@ __global__ __launch_bounds__(kT) void lz4_decode_solo_kernel(tyche_batch_t b, ui
                 __syncthreads();
             }
             PROF_MARK(10);
-            for (uint32_t c0 = tid; c0 < n64; c0 += 4u * kT) {
-                uint32_t cc[4], kk[4];
+            // (each lane takes 4-cell groups tid + i kT: one covering-table read and two record reads per
+            // group, its 4 cells written as one 8-byte word)
+            for (uint32_t g0 = tid; g0 < ng4; g0 += 4u * kT) {
+                uint32_t gk[4];
                 uint2 r0[4], r1[4];
 #pragma unroll
                 for (uint32_t u = 0; u < 4u; u++) {
-                    cc[u] = c0 + u * kT;
-                    kk[u] = cc[u] < (uint32_t)rv ? (uint32_t)slot[cc[u] >> 2] : 0u;
+                    const uint32_t g = g0 + u * kT;
+                    gk[u] = g < ng4 && 4u * g < (uint32_t)rv ? (uint32_t)slot[g] : 0u;
                 }
 #pragma unroll
                 for (uint32_t u = 0; u < 4u; u++) {
-                    r0[u] = rec[kk[u]];
-                    r1[u] = rec[kk[u] < last ? kk[u] + 1u : kk[u]];
+                    r0[u] = rec[gk[u]];
+                    r1[u] = rec[gk[u] < last ? gk[u] + 1u : gk[u]];
                 }
-                uint32_t lb[4];
+                uint32_t lb[4][4];
 #pragma unroll
                 for (uint32_t u = 0; u < 4u; u++) {
-                    const uint2 r = kk[u] < last && cc[u] >= (r1[u].x & 0xFFFFu) ? r1[u] : r0[u];
-                    r0[u] = r;
-                    const uint32_t o = r.x & 0xFFFFu, d = o + (r.x >> 16);
-                    lb[u] = cc[u] < (uint32_t)rv && cc[u] < d ? (uint32_t)in[(r.y & 0xFFFFu) + cc[u] - o] : 0u;
-                }
+                    const uint32_t o1 = gk[u] < last ? (r1[u].x & 0xFFFFu) : 0xFFFFFFFFu;
 #pragma unroll
-                for (uint32_t u = 0; u < 4u; u++) {
-                    if (cc[u] >= n64) continue;
-                    const uint2 r = r0[u];
-                    const uint32_t o = r.x & 0xFFFFu, d = o + (r.x >> 16), off = r.y >> 16;
-                    uint32_t v = kLitFlag;
-                    if (cc[u] < (uint32_t)rv) {
-                        if (cc[u] < d) {
-                            v = kLitFlag | lb[u];
-                        } else if (off != 0) {
-                            const uint32_t j = cc[u] - d;
-                            v = d - off + (j < off ? j : mod_small(j, off));
-                        }
+                    for (uint32_t j = 0; j < 4u; j++) {
+                        const uint32_t c = 4u * (g0 + u * kT) + j;
+                        const uint2 r = c >= o1 ? r1[u] : r0[u];
+                        const uint32_t o = r.x & 0xFFFFu, d = o + (r.x >> 16);
+                        lb[u][j] = c < (uint32_t)rv && c < d ? (uint32_t)in[(r.y & 0xFFFFu) + c - o] : 0u;
                     }
-                    cells[cc[u]] = (uint16_t)v;
+                }
+#pragma unroll
+                for (uint32_t u = 0; u < 4u; u++) {
+                    const uint32_t g = g0 + u * kT;
+                    if (g >= ng4) continue;
+                    const uint32_t o1 = gk[u] < last ? (r1[u].x & 0xFFFFu) : 0xFFFFFFFFu;
+                    uint32_t v[4];
+#pragma unroll
+                    for (uint32_t j = 0; j < 4u; j++) {
+                        const uint32_t c = 4u * g + j;
+                        const uint2 r = c >= o1 ? r1[u] : r0[u];
+                        const uint32_t o = r.x & 0xFFFFu, d = o + (r.x >> 16), off = r.y >> 16;
+                        uint32_t jm = c - d;   // (wraps below d: a literal cell)
+                        if (c >= d && jm >= off && off != 0u) jm = mod_small(jm, off);   // overlapping match
+                        v[j] = c >= (uint32_t)rv ? kLitFlag : c < d ? kLitFlag | lb[u][j] : off == 0u ? kLitFlag : d - off + jm;
+                    }
+                    *(uint2 *)(cells + 4u * g) = make_uint2(v[0] | v[1] << 16, v[2] | v[3] << 16);
                 }
             }
             __syncthreads();
@@ -1629,6 +1680,10 @@ __global__ __launch_bounds__(kT) void lz4_decode_solo_kernel(tyche_batch_t b, ui
             }
         }
         PROF_MARK(8);
+        if (sys_fence) {   // output in host memory: every wave's page stores visible before the result
+            __threadfence_system();
+            __syncthreads();
+        }
         if (tid == 0) b.results[page] = rv;
         if (ctr) {
             if (tid == 0) hw[5] = atomicAdd(ctr, 1u) + gridDim.x;
@@ -1685,7 +1740,7 @@ static hipError_t launch_lz4_decode_jump(const tyche_batch_t &b, uint32_t in_cap
 // take the jump decoder)
 constexpr long kSoloMax = 4096;
 static hipError_t launch_lz4_decode_solo(const tyche_batch_t &b, uint32_t in_cap, uint32_t out_cap, hipStream_t s,
-                                         bool &launched) {
+                                         bool &launched, bool sys_fence) {
     launched = false;
     const long smax = knob("LZ4_SOLO_MAX", kSoloMax);
     if ((long)b.count > smax || out_cap > 32768u || in_cap >= kSoloChunks * kSoloNpt * 1024u) return hipSuccess;
@@ -1701,10 +1756,13 @@ static hipError_t launch_lz4_decode_solo(const tyche_batch_t &b, uint32_t in_cap
     WorkCounter ctr(s, grid < b.count);
     if (grid < b.count && !ctr.get()) return hipErrorOutOfMemory;
     unsigned *cp = grid < b.count ? ctr.get() : nullptr;
-    void *args[] = {(void *)&b, &in_cap, &out_cap, (void *)&lay, &cp};
+    uint32_t fence = sys_fence ? 1u : 0u;
+    void *args[] = {(void *)&b, &in_cap, &out_cap, (void *)&lay, &cp, &fence};
     (void)hipLaunchKernel(k, dim3((unsigned)grid), dim3(kT), args, lay.total, s);
     launched = true;
-    return hipGetLastError();
+    const hipError_t e = hipGetLastError();
+    if (e == hipSuccess && sys_fence) t_results_fenced = true;
+    return e;
 }
 
 hipError_t launch_lz4_decode(const tyche_batch_t &b, uint32_t in_cap, uint32_t out_cap, hipStream_t s,
@@ -1717,7 +1775,7 @@ hipError_t launch_lz4_decode(const tyche_batch_t &b, uint32_t in_cap, uint32_t o
     // (round 5) when its layout fits, else the jump decoder
     {
         bool launched = false;
-        const hipError_t es = launch_lz4_decode_solo(b, in_cap, out_cap, s, launched);
+        const hipError_t es = launch_lz4_decode_solo(b, in_cap, out_cap, s, launched, !allow_lane);
         if (launched || es != hipSuccess) return es;
     }
     {
