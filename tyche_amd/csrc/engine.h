@@ -13,13 +13,6 @@ namespace tyche {
 // results[i] value for a page that does not fit the launch's LDS sizing
 // (caller passed max_src_length / dst_capacity smaller than a page's sizes)
 constexpr int32_t kResultTooLarge = INT32_MIN;
-// Host-visible completion (the restore path's latency): a launcher whose kernel makes each page's
-// output visible at system scope before it writes that page's result sets t_results_fenced; the
-// zero-copy host path, whose results live in pinned host memory, then spins on the results (set
-// to kResultPending before the launch) instead of synchronizing the stream -- 5.9 vs 12.1 us for
-// an empty kernel (profiles/r05_launch_latency.jsonl).
-constexpr int32_t kResultPending = INT32_MIN + 3;
-extern thread_local bool t_results_fenced;
 
 // LZ4 block-format constants (lz4.c:264-281)
 constexpr int kMinMatch = 4;

@@ -305,10 +305,6 @@ long tyche::knob(const char *name, long dflt) {
     return e->second.first ? e->second.second : dflt;
 }
 
-namespace tyche {
-thread_local bool t_results_fenced = false;
-}
-
 namespace {
 
 // -1: the host API spreads work over every usable device (the default);
@@ -891,27 +887,9 @@ int run_host_batch(int dev, size_t n, const void *const *src, const uint32_t *sr
                 S.first = 0;
                 S.count = n;
                 S.busy = true;
-                for (size_t j = 0; j < n; j++) m_res[j] = kResultPending;
-                tyche::t_results_fenced = false;
                 if ((e = launch(b, S.stream, true)) != hipSuccess) return bail(fail("kernel launch", e));
                 S.busy = false;
-                bool seen = false;
-                if (tyche::t_results_fenced && knob("HOST_POLL", 0) != 0) {
-                    // the kernel publishes each page's bytes before its result: spin on the results, for
-                    // up to 20 ms (then the stream wait below, which also reports a failed kernel)
-                    HpClock hc(kHpWait);
-                    const auto t_end = std::chrono::steady_clock::now() + std::chrono::milliseconds(20);
-                    for (size_t j = 0;;) {
-                        while (j < n && ((volatile int32_t *)m_res)[j] != kResultPending) j++;
-                        if (j == n) {
-                            seen = true;
-                            break;
-                        }
-                        if (std::chrono::steady_clock::now() > t_end) break;
-                    }
-                    std::atomic_thread_fence(std::memory_order_acquire);
-                }
-                if (!seen && (e = hipStreamSynchronize(S.stream)) != hipSuccess) return bail(fail("hipStreamSynchronize", e));
+                if ((e = hipStreamSynchronize(S.stream)) != hipSuccess) return bail(fail("hipStreamSynchronize", e));
                 const uint8_t *hout = (const uint8_t *)S.h_out.p;
                 pool.run(n, [&](size_t j) {
                     const int32_t r = m_res[j];

@@ -1376,7 +1376,7 @@ __device__ __forceinline__ uint32_t solo_excl_sum(uint32_t v, uint32_t *wsum, ui
 
 template <uint32_t kT>
 __global__ __launch_bounds__(kT) void lz4_decode_solo_kernel(tyche_batch_t b, uint32_t in_cap, uint32_t out_cap,
-                                                             SoloLay lay, unsigned *ctr, uint32_t sys_fence) {
+                                                             SoloLay lay, unsigned *ctr) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1);
     // words: [0] rv, [2] first failing (or the terminal) token, [5] claimed page, [6..8] jump round flags,
@@ -1680,10 +1680,6 @@ __global__ __launch_bounds__(kT) void lz4_decode_solo_kernel(tyche_batch_t b, ui
             }
         }
         PROF_MARK(8);
-        if (sys_fence) {   // output in host memory: every wave's page stores visible before the result
-            __threadfence_system();
-            __syncthreads();
-        }
         if (tid == 0) b.results[page] = rv;
         if (ctr) {
             if (tid == 0) hw[5] = atomicAdd(ctr, 1u) + gridDim.x;
@@ -1740,7 +1736,7 @@ static hipError_t launch_lz4_decode_jump(const tyche_batch_t &b, uint32_t in_cap
 // take the jump decoder)
 constexpr long kSoloMax = 4096;
 static hipError_t launch_lz4_decode_solo(const tyche_batch_t &b, uint32_t in_cap, uint32_t out_cap, hipStream_t s,
-                                         bool &launched, bool sys_fence) {
+                                         bool &launched) {
     launched = false;
     const long smax = knob("LZ4_SOLO_MAX", kSoloMax);
     if ((long)b.count > smax || out_cap > 32768u || in_cap >= kSoloChunks * kSoloNpt * 1024u) return hipSuccess;
@@ -1756,13 +1752,10 @@ static hipError_t launch_lz4_decode_solo(const tyche_batch_t &b, uint32_t in_cap
     WorkCounter ctr(s, grid < b.count);
     if (grid < b.count && !ctr.get()) return hipErrorOutOfMemory;
     unsigned *cp = grid < b.count ? ctr.get() : nullptr;
-    uint32_t fence = sys_fence ? 1u : 0u;
-    void *args[] = {(void *)&b, &in_cap, &out_cap, (void *)&lay, &cp, &fence};
+    void *args[] = {(void *)&b, &in_cap, &out_cap, (void *)&lay, &cp};
     (void)hipLaunchKernel(k, dim3((unsigned)grid), dim3(kT), args, lay.total, s);
     launched = true;
-    const hipError_t e = hipGetLastError();
-    if (e == hipSuccess && sys_fence) t_results_fenced = true;
-    return e;
+    return hipGetLastError();
 }
 
 hipError_t launch_lz4_decode(const tyche_batch_t &b, uint32_t in_cap, uint32_t out_cap, hipStream_t s,
@@ -1775,7 +1768,7 @@ hipError_t launch_lz4_decode(const tyche_batch_t &b, uint32_t in_cap, uint32_t o
     // (round 5) when its layout fits, else the jump decoder
     {
         bool launched = false;
-        const hipError_t es = launch_lz4_decode_solo(b, in_cap, out_cap, s, launched, !allow_lane);
+        const hipError_t es = launch_lz4_decode_solo(b, in_cap, out_cap, s, launched);
         if (launched || es != hipSuccess) return es;
     }
     {
