@@ -510,15 +510,18 @@ def short_sequence_stream(rng, plen):
     return bytes(s)
 
 
-@pytest.mark.parametrize("kernel", ["solo", "jump"])
+@pytest.mark.parametrize("kernel", ["solo", "solo_lockstep", "jump"])
 def test_decode_small_batch_kernels(tc, oracle_mod, knobs, kernel):
     """The small-batch LZ4 decoders side by side: the single-page decoder (round 5, the default
-    for batches of <= 4,096 pages) and the jump decoder (LZ4_SOLO_MAX=0).  The reference fixtures
+    for batches of <= 4,096 pages), the same with its jump rounds handed to the lock-step loop
+    after one barrier-free round (LZ4_SOLO_ASYNC=1), and the jump decoder (LZ4_SOLO_MAX=0).  The reference fixtures
     with their exact return values at 1 and 20 pages, seeded corruptions (bit flips, truncations,
     reduced capacities) against the restated LZ4_decompress_safe, crafted pages of back-to-back
     3-byte sequences (with and without corruptions), and every page kind at 8, 16 and 32 KiB."""
     if kernel == "jump":
         knobs(LZ4_SOLO_MAX=0)
+    elif kernel == "solo_lockstep":
+        knobs(LZ4_SOLO_ASYNC=1)
     test_decode_lane_path_fixtures(tc, 1)
     test_decode_lane_path_fixtures(tc, 20)
     rng = np.random.default_rng(4000 + len(kernel))

@@ -11,6 +11,8 @@
 // There is no CPU codec in this library: if the HIP device or the gfx950 code
 // object is unavailable every codec entry point returns an error.
 #include <hip/hip_runtime.h>
+#include <linux/futex.h>
+#include <sys/syscall.h>
 #include <unistd.h>
 #include <pthread.h>
 #include <stdio.h>
@@ -1632,14 +1634,29 @@ int buffer__decompress(Buffer *buf, int compressor_id) {
 // behind each other (profiles/r02_restore_dispatch.jsonl).
 namespace {
 constexpr int kQueueHistBuckets = 11;
+// A restorer waits on its own request word (spin briefly, then futex), so a finished batch wakes
+// exactly its callers -- a shared condition variable woke every blocked restorer (64 in the C5
+// cycle) to re-take the queue mutex and find its request still pending.
 struct RestoreReq {
     Buffer *buf;
     int status;
-    bool done;
+    std::atomic<int> done{0};
+    void wait() {
+        for (int i = 0; i < 64; i++) {   // (a batch takes ~0.1 ms: spinning longer only takes CPU from the others)
+            if (done.load(std::memory_order_acquire)) return;
+            _mm_pause();
+        }
+        while (!done.load(std::memory_order_acquire))
+            syscall(SYS_futex, (int *)&done, FUTEX_WAIT_PRIVATE, 0, nullptr, nullptr, 0);
+    }
+    void wake() {
+        done.store(1, std::memory_order_release);
+        syscall(SYS_futex, (int *)&done, FUTEX_WAKE_PRIVATE, 1, nullptr, nullptr, 0);
+    }
 };
 struct RestoreQueue {
     std::mutex mu;
-    std::condition_variable cv, done_cv;
+    std::condition_variable cv;
     std::vector<RestoreReq *> q[4];   // by codec id (NO is restored by the caller)
     bool collecting[4] = {false, false, false, false};
     bool running = false, stop = false;
@@ -1683,13 +1700,12 @@ struct RestoreQueue {
                 batches++;
                 buffers += take.size();
                 hist[std::min(kQueueHistBuckets - 1, 31 - __builtin_clz((unsigned)take.size()))]++;
-                for (size_t i = 0; i < take.size(); i++) {
-                    take[i]->status = st[i];
-                    take[i]->done = true;
-                }
                 idle = cq.empty();
             }
-            done_cv.notify_all();
+            for (size_t i = 0; i < take.size(); i++) {
+                take[i]->status = st[i];
+                take[i]->wake();   // (the request lives on its caller's stack: not touched after this)
+            }
         }
     }
 };
@@ -1731,7 +1747,9 @@ void tyche_restore_queue_stop(void) {
 int tyche_buffer_restore(Buffer *buf, int compressor_id) {
     // NO and unknown ids need no GPU batch: the direct path gives the reference's answer
     if (compressor_id < 1 || compressor_id > 3) return buffer__decompress(buf, compressor_id);
-    RestoreReq r{buf, TYCHE_E_OK, false};
+    RestoreReq r;
+    r.buf = buf;
+    r.status = TYCHE_E_OK;
     {
         std::unique_lock<std::mutex> g(g_rq.mu);
         if (!g_rq.running || g_rq.stop) {
@@ -1741,8 +1759,7 @@ int tyche_buffer_restore(Buffer *buf, int compressor_id) {
         g_rq.q[compressor_id].push_back(&r);
     }
     g_rq.cv.notify_all();   // the collecting dispatcher, whichever it is
-    std::unique_lock<std::mutex> g(g_rq.mu);
-    g_rq.done_cv.wait(g, [&] { return r.done; });
+    r.wait();
     return r.status;
 }
 

@@ -1263,6 +1263,7 @@ __global__ __launch_bounds__(kJumpThreads) void lz4_decode_jump_kernel(tyche_bat
 constexpr uint32_t kSoloNpt = 8;      // positions per thread chunk
 constexpr uint32_t kSoloChunks = 3;   // chunks per thread: streams up to 3 * 8 * 1,024 - 1 bytes
 constexpr uint32_t kSoloGroups = 4;   // 8-cell groups per thread in the jump rounds: pages up to 32 KiB
+constexpr long kSoloAsyncRounds = 64;   // barrier-free jump rounds per thread before lock-step ones
 // next_token_w for the token byte t at p, without the offset and literal reads next_token_w's
 // decode_seq_in makes: only the length-extension bytes are read (lz4.c:1134-1143, 1165, 1172-1182)
 __device__ __forceinline__ uint32_t solo_next(const uint8_t *in, int32_t L, int32_t p, uint32_t t) {
@@ -1376,11 +1377,11 @@ __device__ __forceinline__ uint32_t solo_excl_sum(uint32_t v, uint32_t *wsum, ui
 
 template <uint32_t kT>
 __global__ __launch_bounds__(kT) void lz4_decode_solo_kernel(tyche_batch_t b, uint32_t in_cap, uint32_t out_cap,
-                                                             SoloLay lay, unsigned *ctr) {
+                                                             SoloLay lay, unsigned *ctr, uint32_t async_rounds) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1);
     // words: [0] rv, [2] first failing (or the terminal) token, [5] claimed page, [6..8] jump round flags,
-    // [16..31] block-sum scratch
+    // [10] barrier-free jump rounds gave up, [16..31] block-sum scratch
     uint32_t *hw = (uint32_t *)smem;
     int32_t &s_rv = *(int32_t *)&hw[0];
     uint32_t *wsum = hw + 16;
@@ -1401,7 +1402,8 @@ __global__ __launch_bounds__(kT) void lz4_decode_solo_kernel(tyche_batch_t b, ui
         const int32_t L = (int32_t)p.src_len, C = (int32_t)p.dst_cap;
         if (tid == 0) {
             hw[2] = 0xFFFFFFFFu;
-            hw[6] = 0;   // round 0's flag
+            hw[6] = 0;    // round 0's flag
+            hw[10] = 0;   // barrier-free jump rounds gave up
         }
         uint8_t *in = stage + head;
         const bool go = fits && C > 0 && L > 0;
@@ -1637,8 +1639,14 @@ __global__ __launch_bounds__(kT) void lz4_decode_solo_kernel(tyche_batch_t b, ui
                 const uint32_t g = tid + i * kT;
                 cv[i] = g < ng ? c4[g] : fin;
             }
-            for (uint32_t r = 0;; r++) {
-                if (tid == 0) flag[(r + 1) % 3] = 0;
+            // Rounds without barriers: a thread jumps its own cells until they are all final.  Reading a
+            // cell another thread is rewriting returns its old or its new value, both pointers further
+            // back along the same copy chain (or the final byte), and a pointer only ever moves back: each
+            // round strictly advances every open cell, so the loop ends; the others' jumps make it
+            // ~log2(depth) rounds as in lock-step.  A thread that runs async_rounds rounds (kSoloAsyncRounds;
+            // TYCHE_LZ4_SOLO_ASYNC, a test hook) leaves the rest to lock-step rounds.
+            uint32_t ar = 0;
+            for (;; ar++) {
                 uint32_t open = 0;
 #pragma unroll
                 for (uint32_t i = 0; i < kSoloGroups; i++) {
@@ -1652,11 +1660,33 @@ __global__ __launch_bounds__(kT) void lz4_decode_solo_kernel(tyche_batch_t b, ui
                         cv[i] = v;
                     }
                 }
-                if (open) atomicOr(&flag[r % 3], 1u);
-                __syncthreads();
-                if (flag[r % 3] == 0) {
-                    PROF_ADD(12, r + 1);
+                if (!open) break;
+                if (ar + 1 >= async_rounds) {
+                    atomicOr(&hw[10], 1u);
                     break;
+                }
+            }
+            PROF_ADD(12, ar + 1);
+            __syncthreads();
+            if (hw[10]) {
+                for (uint32_t r = 0;; r++) {
+                    if (tid == 0) flag[(r + 1) % 3] = 0;
+                    uint32_t open = 0;
+#pragma unroll
+                    for (uint32_t i = 0; i < kSoloGroups; i++) {
+                        u32x4 v = cv[i];
+                        if (((v.x & v.y & v.z & v.w) & 0x80008000u) != 0x80008000u) {
+                            v.x = jump_pair(cells, v.x, open);
+                            v.y = jump_pair(cells, v.y, open);
+                            v.z = jump_pair(cells, v.z, open);
+                            v.w = jump_pair(cells, v.w, open);
+                            c4[tid + i * kT] = v;
+                            cv[i] = v;
+                        }
+                    }
+                    if (open) atomicOr(&flag[r % 3], 1u);
+                    __syncthreads();
+                    if (flag[r % 3] == 0) break;
                 }
             }
             PROF_MARK(7);
@@ -1752,7 +1782,8 @@ static hipError_t launch_lz4_decode_solo(const tyche_batch_t &b, uint32_t in_cap
     WorkCounter ctr(s, grid < b.count);
     if (grid < b.count && !ctr.get()) return hipErrorOutOfMemory;
     unsigned *cp = grid < b.count ? ctr.get() : nullptr;
-    void *args[] = {(void *)&b, &in_cap, &out_cap, (void *)&lay, &cp};
+    uint32_t async_rounds = (uint32_t)std::max(1L, knob("LZ4_SOLO_ASYNC", kSoloAsyncRounds));
+    void *args[] = {(void *)&b, &in_cap, &out_cap, (void *)&lay, &cp, &async_rounds};
     (void)hipLaunchKernel(k, dim3((unsigned)grid), dim3(kT), args, lay.total, s);
     launched = true;
     return hipGetLastError();
