@@ -1624,14 +1624,14 @@ int buffer__decompress(Buffer *buf, int compressor_id) {
 // buffer__decompress status.  Per-buffer semantics are unchanged.
 //
 // Each codec has its own queue and dispatchers (TYCHE_RESTORE_DISPATCHERS per
-// codec, default one per device): a batch's latency is that of its slowest
-// page (~0.09 ms for a 16 KiB LZ4 page on the jump decoder, ~0.3 ms for zlib,
-// tools/latency.c), so LZ4 restores never wait behind a zlib batch.  A second
-// dispatcher per codec (4 batches in flight with two codecs, one per hardware
-// queue, GPU_MAX_HW_QUEUES) measured 1.70 vs 1.32 GiB/s of tools/cycle.c
-// restores on one box and 1.12-1.24 vs 1.32-1.36 on another; 3-4 per codec
-// oversubscribe the queues (0.85 / 0.70), batches only get smaller and run
-// behind each other (profiles/r02_restore_dispatch.jsonl).
+// codec, default two per device): a batch's latency is that of its slowest
+// page (~0.04 ms for a 16 KiB LZ4 page on the single-page decoder, ~0.3 ms for
+// zlib, tools/latency.c), so LZ4 restores never wait behind a zlib batch, and a
+// second dispatcher collects the next batch while one runs: 2.53 vs 2.06 GiB/s of
+// tools/cycle.c restores (round 5, r05_restore_dispatch.log; with the jump
+// decoder and a shared wake-up round 2 had measured 1.70 vs 1.32 on one box and
+// 1.12-1.24 vs 1.32-1.36 on another, r02_restore_dispatch.jsonl); 3-4 per codec
+// oversubscribed the hardware queues then.
 namespace {
 constexpr int kQueueHistBuckets = 11;
 // A restorer waits on its own request word (spin briefly, then futex), so a finished batch wakes
@@ -1724,7 +1724,7 @@ int tyche_restore_queue_start(int max_batch, int max_wait_us) {
     g_rq.stop = false;
     for (bool &c : g_rq.collecting) c = false;
     g_rq.running = true;
-    int k = (int)knob("RESTORE_DISPATCHERS", std::max(1, tyche_active_devices()));
+    int k = (int)knob("RESTORE_DISPATCHERS", 2 * std::max(1, tyche_active_devices()));
     k = std::max(1, std::min(k, 64));
     for (int codec = 1; codec <= 3; codec++)
         for (int i = 0; i < k; i++) g_rq.th.emplace_back([codec] { g_rq.loop(codec); });
