@@ -1264,28 +1264,42 @@ constexpr uint32_t kSoloNpt = 8;      // positions per thread chunk
 constexpr uint32_t kSoloChunks = 3;   // chunks per thread: streams up to 3 * 8 * 1,024 - 1 bytes
 constexpr uint32_t kSoloGroups = 4;   // 8-cell groups per thread in the jump rounds: pages up to 32 KiB
 constexpr long kSoloAsyncRounds = 64;   // barrier-free jump rounds per thread before lock-step ones
-// next_token_w for the token byte t at p, without the offset and literal reads next_token_w's
-// decode_seq_in makes: only the length-extension bytes are read (lz4.c:1134-1143, 1165, 1172-1182)
-__device__ __forceinline__ uint32_t solo_next(const uint8_t *in, int32_t L, int32_t p, uint32_t t) {
+// next_token_w for the token at p = base + u, and the token's output length (lit + ml, or lit for a
+// terminal literal run): the reads of lz4.c:1134-1143, 1165, 1172-1182 without the offset and the
+// literals.  x holds bytes base .. base+11: the token and its first literal-length byte (compile-time
+// indices -- a run-time index into x sends it to scratch memory); other length bytes come from LDS.
+__device__ __forceinline__ uint32_t solo_next(const uint8_t *in, int32_t L, int32_t p, uint32_t u,
+                                              const uint32_t (&x)[3], uint32_t &olen) {
+    const uint32_t t = (x[u >> 2] >> (8u * (u & 3u))) & 0xFFu;
     int32_t q = p + 1, lit = (int32_t)(t >> 4);
     if (lit == kRunMask) {
-        uint32_t b;
-        do {
+        uint32_t b = (x[(u + 1u) >> 2] >> (8u * ((u + 1u) & 3u))) & 0xFFu;
+        q++;
+        lit += (int32_t)b;
+        while (q < L - kRunMask && b == 255) {
             b = in[q];
             q++;
             lit += (int32_t)b;
-        } while (q < L - kRunMask && b == 255);
+        }
     }
-    if (q + lit > L - 8) return kEnd;   // terminal literal run
-    int32_t q2 = q + lit + 2;
-    if ((t & 15u) == 15u) {
+    if (q + lit > L - 8) {   // terminal literal run
+        olen = (uint32_t)lit;
+        return kEnd;
+    }
+    int32_t q2 = q + lit + 2, ml = (int32_t)(t & 15u);
+    if (ml == 15) {
         uint32_t b;
         do {
             b = in[q2];
             q2++;
-            if (q2 > L - kLastLiterals) return kEnd;   // overrun in the match length
+            if (q2 > L - kLastLiterals) {   // overrun in the match length
+                olen = 0;
+                return kEnd;
+            }
+            ml += (int32_t)b;
         } while (b == 255);
     }
+    olen = (uint32_t)(lit + ml + kMinMatch);
     return (uint32_t)q2;
 }
 
@@ -1332,27 +1346,27 @@ __device__ __forceinline__ SeqIn solo_seq(const uint8_t *in, int32_t L, int32_t 
 
 // LDS layout of the single-page decoder (host and device agree through this)
 struct SoloLay {
-    uint32_t stage, tok, scr;   // byte offsets in LDS
-    uint32_t jb, mark;          // byte offsets in scr: the second J buffer, the marks (token chain)
-    uint32_t rec, slot;         // byte offsets in scr: token records, 4-cell group covering table (cells)
+    uint32_t stage, scr;   // byte offsets in LDS
+    uint32_t jb, mark;     // byte offsets in scr: the second J buffer, the marks (token chain)
+    uint32_t rec, slot;    // byte offsets in scr: token records (after the cells), 4-cell group covering table
     uint32_t nslots, total;
 };
 __host__ __device__ inline uint32_t solo_up16(uint32_t x) { return (x + 15u) & ~15u; }
 __host__ __device__ inline SoloLay solo_layout(uint32_t in_cap, uint32_t out_cap) {
     SoloLay l;
     l.stage = 256u;   // 64 header words
-    l.tok = l.stage + solo_up16(in_cap + 16u + kPad);
+    l.scr = l.stage + solo_up16(in_cap + 16u + kPad);
     const uint32_t max_tok = in_cap / 3u + 2u;   // a chain token consumes >= 3 bytes, but the last
-    l.scr = l.tok + solo_up16(2u * max_tok);
     const uint32_t nodes = solo_up16(2u * (in_cap + 1u));   // u16 per position, + the sink
     l.jb = nodes;
     l.mark = 2u * nodes;
-    const uint32_t chain_bytes = 2u * nodes + solo_up16(in_cap + 4u);   // (marks read as 8-byte words)
+    const uint32_t chain_bytes = 2u * nodes + solo_up16(in_cap + 8u);   // (marks read as 8-byte words)
     const uint32_t cells_bytes = 2u * ((out_cap + 63u) & ~63u);
     l.rec = cells_bytes;
-    l.slot = l.rec + 8u * (max_tok + 1u);
+    // the covering table is zeroed while J is built: it overlaps neither J nor the marks
+    l.slot = std::max(chain_bytes, l.rec + 8u * (max_tok + 1u));
     l.nslots = ((out_cap + 63u) & ~63u) / 4u;
-    l.total = l.scr + std::max(chain_bytes, l.slot + solo_up16(2u * l.nslots));
+    l.total = l.scr + l.slot + solo_up16(2u * l.nslots);
     return l;
 }
 
@@ -1375,18 +1389,44 @@ __device__ __forceinline__ uint32_t solo_excl_sum(uint32_t v, uint32_t *wsum, ui
     return base + incl - v;
 }
 
+// the same over two values at once (wsum: 2 kT / 64 words)
+template <uint32_t kT>
+__device__ __forceinline__ uint2 solo_excl_sum2(uint32_t a, uint32_t b, uint32_t *wsum, uint32_t tid, uint32_t &ta,
+                                                uint32_t &tb) {
+    constexpr uint32_t kW = kT / 64u;
+    const uint32_t w = tid >> 6;
+    const uint32_t ia = (uint32_t)wave_incl_sum((int32_t)a), ibb = (uint32_t)wave_incl_sum((int32_t)b);
+    if ((tid & 63u) == 63u) {
+        wsum[w] = ia;
+        wsum[kW + w] = ibb;
+    }
+    __syncthreads();
+    uint32_t ba = 0, bb = 0, sa = 0, sb = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kW; k++) {
+        const uint32_t x = wsum[k], y = wsum[kW + k];
+        ba += k < w ? x : 0u;
+        bb += k < w ? y : 0u;
+        sa += x;
+        sb += y;
+    }
+    ta = sa;
+    tb = sb;
+    __syncthreads();   // wsum may be reused
+    return make_uint2(ba + ia - a, bb + ibb - b);
+}
+
 template <uint32_t kT>
 __global__ __launch_bounds__(kT) void lz4_decode_solo_kernel(tyche_batch_t b, uint32_t in_cap, uint32_t out_cap,
                                                              SoloLay lay, unsigned *ctr, uint32_t async_rounds) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1);
     // words: [0] rv, [2] first failing (or the terminal) token, [5] claimed page, [6..8] jump round flags,
-    // [10] barrier-free jump rounds gave up, [16..31] block-sum scratch
+    // [10] barrier-free jump rounds gave up, [16..47] block-sum scratch
     uint32_t *hw = (uint32_t *)smem;
     int32_t &s_rv = *(int32_t *)&hw[0];
     uint32_t *wsum = hw + 16;
     uint8_t *stage = smem + lay.stage;
-    uint16_t *tok = (uint16_t *)(smem + lay.tok);
     uint8_t *scr = smem + lay.scr;
     uint16_t *ja0 = (uint16_t *)scr, *jb0 = (uint16_t *)(scr + lay.jb);   // J, double-buffered
     uint8_t *mark = scr + lay.mark;
@@ -1417,37 +1457,44 @@ __global__ __launch_bounds__(kT) void lz4_decode_solo_kernel(tyche_batch_t b, ui
             // ---- 1. J(q) for every position, position 0 marked.  Thread t owns positions
             // [8 (t nch + c), +8) for its nch chunks c and keeps their J values in registers (two per
             // word), so a round reads only its marks (one 8-byte word) and the 8 J(J(q)) from LDS and
-            // writes one 16-byte word of J (and the marks it sets).
+            // writes one 16-byte word of J (and the marks it sets).  The output length of the token
+            // each position would start is kept too (the chain's offsets need no second parse).
             const uint32_t n = (uint32_t)L + 1u;   // positions + the sink
             const uint32_t nch = (n + kSoloNpt * kT - 1u) / (kSoloNpt * kT);
-            uint32_t jr[kSoloChunks][4];
+            uint32_t jr[kSoloChunks][4], ol[kSoloChunks][4];
             {
                 const uint32_t ib = (uint32_t)(uintptr_t)in & 3u;
                 const uint32_t *A = (const uint32_t *)(in - ib);
 #pragma unroll
                 for (uint32_t c = 0; c < kSoloChunks; c++) {
                     const uint32_t base = (tid * nch + c) * kSoloNpt;
+#pragma unroll
+                    for (uint32_t k = 0; k < 4u; k++) jr[c][k] = ol[c][k] = 0;
                     if (c < nch && base < n) {
+                        // bytes base .. base+11: the 8 tokens and their first literal-length bytes
                         const uint32_t qa = base + ib;
-                        const uint32_t w0 = A[qa >> 2], w1 = A[(qa >> 2) + 1], w2 = A[(qa >> 2) + 2];
-                        const uint32_t x0 = __builtin_amdgcn_alignbyte(w1, w0, qa & 3u);
-                        const uint32_t x1 = __builtin_amdgcn_alignbyte(w2, w1, qa & 3u);
-                        uint32_t nx[8];
+                        uint32_t w[4], x[3];
+#pragma unroll
+                        for (uint32_t k = 0; k < 4u; k++) w[k] = A[(qa >> 2) + k];
+#pragma unroll
+                        for (uint32_t k = 0; k < 3u; k++) x[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], qa & 3u);
+                        uint32_t nx[8], no[8];
 #pragma unroll
                         for (uint32_t u = 0; u < 8u; u++) {
                             const uint32_t q = base + u;
-                            const uint32_t t = ((u < 4u ? x0 : x1) >> (8u * (u & 3u))) & 0xFFu;
-                            nx[u] = q < (uint32_t)L ? min(solo_next(in, L, (int32_t)q, t), (uint32_t)L) : (uint32_t)L;
+                            no[u] = 0;
+                            nx[u] = q < (uint32_t)L ? min(solo_next(in, L, (int32_t)q, u, x, no[u]), (uint32_t)L) : (uint32_t)L;
                         }
 #pragma unroll
-                        for (uint32_t k = 0; k < 4u; k++) jr[c][k] = nx[2 * k] | nx[2 * k + 1] << 16;
+                        for (uint32_t k = 0; k < 4u; k++) {
+                            jr[c][k] = nx[2 * k] | nx[2 * k + 1] << 16;
+                            ol[c][k] = min(no[2 * k], 0xFFFFu) | min(no[2 * k + 1], 0xFFFFu) << 16;
+                        }
                         *(uint4 *)(ja0 + base) = make_uint4(jr[c][0], jr[c][1], jr[c][2], jr[c][3]);
                         *(uint2 *)(mark + base) = make_uint2(base == 0 ? 1u : 0u, 0u);
-                    } else {
-#pragma unroll
-                        for (uint32_t k = 0; k < 4u; k++) jr[c][k] = 0;
                     }
                 }
+                for (uint32_t w = tid; w < lay.nslots; w += kT) slot[w] = 0;   // (its own bytes)
             }
             __syncthreads();
             PROF_MARK(2);
@@ -1482,8 +1529,9 @@ __global__ __launch_bounds__(kT) void lz4_decode_solo_kernel(tyche_batch_t b, ui
             }
             PROF_MARK(3);
             PROF_ADD(11, lev);
-            // ---- the token list: the marked positions below L, in order (thread order = position order)
-            uint32_t cnt = 0;
+            // ---- the tokens: each thread's marked positions below L, in position (= chain) order; one
+            // scan of (tokens, output bytes) per thread gives its first token number and output offset
+            uint32_t cnt = 0, osum = 0;
             uint64_t mk[kSoloChunks];
 #pragma unroll
             for (uint32_t c = 0; c < kSoloChunks; c++) {
@@ -1493,51 +1541,49 @@ __global__ __launch_bounds__(kT) void lz4_decode_solo_kernel(tyche_batch_t b, ui
                     const uint64_t keep = (uint32_t)L - base >= 8u ? ~0ull : (1ull << (8u * ((uint32_t)L - base))) - 1ull;
                     mk[c] = *(const uint64_t *)(mark + base) & keep & 0x0101010101010101ull;
                     cnt += (uint32_t)__builtin_popcountll(mk[c]);
+#pragma unroll
+                    for (uint32_t u = 0; u < 8u; u++)
+                        if ((mk[c] >> (8u * u)) & 1u) osum += (ol[c][u >> 1] >> (16u * (u & 1u))) & 0xFFFFu;
                 }
             }
-            uint32_t ntok = 0;
-            uint32_t o = solo_excl_sum<kT>(cnt, wsum, tid, ntok);
-#pragma unroll
-            for (uint32_t c = 0; c < kSoloChunks; c++) {
-                const uint32_t base = (tid * nch + c) * kSoloNpt;
-#pragma unroll
-                for (uint32_t u = 0; u < 8u; u++)
-                    if ((mk[c] >> (8u * u)) & 1u) tok[o++] = (uint16_t)(base + u);
-            }
-            __syncthreads();   // marks read: the cells may take the bytes
+            uint32_t ntok = 0, otot = 0;
+            const uint2 ex = solo_excl_sum2<kT>(cnt, osum, wsum, tid, ntok, otot);   // (marks read: J's bytes are free)
             PROF_MARK(4);
-            // ---- 2. decode, output offsets, checks and one record per token (its output offset o,
-            // literal count, literal start and match offset); the covering table gets, at slot
+            // ---- 2. per token: decode, the reference's checks at its output offset, a record (output
+            // offset, literal count, literal start, match offset); the covering table gets, at slot
             // ceil(o / 4), the token whose output holds the first cell of 4-cell group (o + 3) / 4
-            const uint32_t K = (ntok + kT - 1u) / kT;
-            const uint32_t t0 = min(tid * K, ntok), t1 = min(t0 + K, ntok);
-            for (uint32_t w = tid; w < lay.nslots; w += kT) slot[w] = 0;
-            uint32_t olen = 0;
-            for (uint32_t i = t0; i < t1; i++) {
-                const SeqIn sq = solo_seq(in, L, (int32_t)tok[i]);
-                olen += (uint32_t)(sq.in_term ? sq.lit : sq.lit + sq.ml);
-            }
-            uint32_t otot = 0;
-            const uint32_t obase = solo_excl_sum<kT>(olen, wsum, tid, otot);
-            int32_t ob = (int32_t)obase;
             uint32_t my_first = 0xFFFFFFFFu;
             int32_t my_rv = -1;
-            for (uint32_t i = t0; i < t1; i++) {
-                const SeqIn sq = solo_seq(in, L, (int32_t)tok[i]);
-                int32_t r;
-                const int32_t st = seq_check(sq, ob, L, C, r);
-                if (st) {
-                    my_first = i;
-                    my_rv = r;
-                    atomicMin(&hw[2], i);
-                }
-                if (st == 2) break;   // (a token that passes its own checks lies inside [0, C))
-                const int32_t e = ob + sq.lit + (st == 1 ? 0 : sq.ml);
-                rec[i] = make_uint2((uint32_t)ob | ((uint32_t)sq.lit << 16), (uint32_t)sq.ls | ((uint32_t)sq.off << 16));
-                const uint32_t s0 = ((uint32_t)ob + 3u) >> 2;
-                if (s0 < (((uint32_t)e + 3u) >> 2)) slot[s0] = (uint16_t)i;
-                if (st == 1) break;
-                ob = e;
+            {
+                uint32_t i = ex.x;
+                int32_t ob = (int32_t)ex.y;
+                bool stop = false;
+                auto chunk = [&](uint64_t m, uint32_t base) {
+                    while (m && !stop) {
+                        const uint32_t u = (uint32_t)__builtin_ctzll(m) >> 3;
+                        m &= m - 1ull;
+                        const SeqIn sq = solo_seq(in, L, (int32_t)(base + u));
+                        int32_t r;
+                        const int32_t st = seq_check(sq, ob, L, C, r);
+                        if (st) {
+                            my_first = i;
+                            my_rv = r;
+                            atomicMin(&hw[2], i);
+                            stop = true;
+                        }
+                        if (st != 2) {   // (a token that passes its own checks lies inside [0, C))
+                            const int32_t e = ob + sq.lit + (st == 1 ? 0 : sq.ml);
+                            rec[i] = make_uint2((uint32_t)ob | ((uint32_t)sq.lit << 16), (uint32_t)sq.ls | ((uint32_t)sq.off << 16));
+                            const uint32_t s0 = ((uint32_t)ob + 3u) >> 2;
+                            if (s0 < (((uint32_t)e + 3u) >> 2)) slot[s0] = (uint16_t)i;
+                            ob = e;
+                        }
+                        i++;
+                    }
+                };
+                chunk(mk[0], tid * nch * kSoloNpt);
+                if (nch > 1u) chunk(mk[1], (tid * nch + 1u) * kSoloNpt);
+                if (nch > 2u) chunk(mk[2], (tid * nch + 2u) * kSoloNpt);
             }
             __syncthreads();
             if (my_first != 0xFFFFFFFFu && my_first == hw[2]) s_rv = my_rv;
