@@ -871,9 +871,12 @@ int run_host_batch(int dev, size_t n, const void *const *src, const uint32_t *sr
                     dof += up16(dst_cap[j]);
                 }
                 uint8_t *hin = (uint8_t *)S.h_in.p;
-                pool.run(n, [&](size_t j) {
-                    if (m_slen[j]) copy_nt(hin + m_soff[j], src[j], m_slen[j]);
-                });
+                {
+                    HpClock hc(kHpGather);
+                    pool.run(n, [&](size_t j) {
+                        if (m_slen[j]) copy_nt(hin + m_soff[j], src[j], m_slen[j]);
+                    });
+                }
                 uint8_t *dm = (uint8_t *)S.h_meta.dp;
                 tyche_batch_t b{};
                 b.count = n;
@@ -889,10 +892,17 @@ int run_host_batch(int dev, size_t n, const void *const *src, const uint32_t *sr
                 S.first = 0;
                 S.count = n;
                 S.busy = true;
-                if ((e = launch(b, S.stream, true)) != hipSuccess) return bail(fail("kernel launch", e));
+                {
+                    HpClock hc(kHpEnqueue);
+                    if ((e = launch(b, S.stream, true)) != hipSuccess) return bail(fail("kernel launch", e));
+                }
                 S.busy = false;
-                if ((e = hipStreamSynchronize(S.stream)) != hipSuccess) return bail(fail("hipStreamSynchronize", e));
+                {
+                    HpClock hc(kHpWait);
+                    if ((e = hipStreamSynchronize(S.stream)) != hipSuccess) return bail(fail("hipStreamSynchronize", e));
+                }
                 const uint8_t *hout = (const uint8_t *)S.h_out.p;
+                HpClock hc(kHpScatter);
                 pool.run(n, [&](size_t j) {
                     const int32_t r = m_res[j];
                     results[j] = r;

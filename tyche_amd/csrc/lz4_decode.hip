@@ -1821,8 +1821,9 @@ static hipError_t launch_lz4_decode_solo(const tyche_batch_t &b, uint32_t in_cap
     if (lay.total > 160u * 1024u) return hipSuccess;
     const void *k = (const void *)lz4_decode_solo_kernel<kT>;
     const size_t ncu = prepare_launch(k);
-    int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, (int)kT, lay.total) != hipSuccess || per_cu < 1)
+    int per_cu = 1;   // (batches up to one page per CU -- the restore path's -- skip the occupancy query)
+    if (b.count > ncu &&
+        (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, (int)kT, lay.total) != hipSuccess || per_cu < 1))
         per_cu = 1;
     const size_t grid = std::min<size_t>(b.count, ncu * (size_t)per_cu);
     WorkCounter ctr(s, grid < b.count);
