@@ -294,17 +294,51 @@ KnobTable &knob_table() {
 }
 }  // namespace
 
-long tyche::knob(const char *name, long dflt) {
+namespace {
+// Knobs are read on every launch (a restore reads ~10).  The table's lookups (mutex, string maps) cost
+// ~0.1-0.3 us each, so each thread keeps what it read, keyed by the name's address (the call sites
+// pass literals), until tyche_set_knob / tyche_clear_knob bump the generation.
+std::atomic<uint64_t> g_knob_gen{1};
+struct KnobSeen {
+    const char *name;
+    uint64_t gen;
+    bool present;
+    long value;
+};
+constexpr int kKnobCache = 64;
+thread_local KnobSeen t_knobs[kKnobCache];
+bool knob_slow(const char *name, long &value) {
     KnobTable &T = knob_table();
     std::lock_guard<std::mutex> g(T.mu);
     const auto o = T.over.find(name);
-    if (o != T.over.end()) return o->second;
+    if (o != T.over.end()) {
+        value = o->second;
+        return true;
+    }
     auto e = T.env.find(name);
     if (e == T.env.end()) {
         const char *v = getenv((std::string("TYCHE_") + name).c_str());
         e = T.env.emplace(name, std::make_pair(v != nullptr && *v, v ? strtol(v, nullptr, 10) : 0L)).first;
     }
-    return e->second.first ? e->second.second : dflt;
+    value = e->second.second;
+    return e->second.first;
+}
+}  // namespace
+
+long tyche::knob(const char *name, long dflt) {
+    const uint64_t gen = g_knob_gen.load(std::memory_order_acquire);
+    const uint32_t h = (uint32_t)(((uintptr_t)name * 0x9E3779B97F4A7C15ull) >> 58);   // 6 bits
+    for (int k = 0; k < 4; k++) {   // a short probe; a miss just takes the table
+        KnobSeen &c = t_knobs[(h + (uint32_t)k) % kKnobCache];
+        if (c.name == name && c.gen == gen) return c.present ? c.value : dflt;
+        if (c.name == nullptr || c.gen != gen || k == 3) {
+            long v = 0;
+            const bool present = knob_slow(name, v);
+            c = KnobSeen{name, gen, present, v};
+            return present ? v : dflt;
+        }
+    }
+    return dflt;   // (unreachable)
 }
 
 namespace {
@@ -1242,6 +1276,7 @@ int tyche_set_knob(const char *name, long value) {
     KnobTable &T = knob_table();
     std::lock_guard<std::mutex> g(T.mu);
     T.over[name] = value;
+    g_knob_gen.fetch_add(1, std::memory_order_acq_rel);
     return TYCHE_E_OK;
 }
 
@@ -1250,6 +1285,7 @@ int tyche_clear_knob(const char *name) {
     KnobTable &T = knob_table();
     std::lock_guard<std::mutex> g(T.mu);
     T.over.erase(name);
+    g_knob_gen.fetch_add(1, std::memory_order_acq_rel);
     return TYCHE_E_OK;
 }
 
