@@ -31,8 +31,11 @@
 // 2^10 hash slots (2 KB): the wave's LDS (page 16.4 KB + table + records) drops
 // to 20 KB, one 512-byte granule under 160 KB / 8, so 8 waves per CU instead of
 // 7: 127.7 -> 111.6 ms per 1M pages for ratio 2.635 -> 2.621 (reference 2.647)
+#ifndef TYCHE_LZ4_HASH_LOG
+#define TYCHE_LZ4_HASH_LOG 10
+#endif
 #ifndef TYCHE_HASH_LOG
-#define TYCHE_HASH_LOG 10
+#define TYCHE_HASH_LOG TYCHE_LZ4_HASH_LOG
 #endif
 
 #include <algorithm>
