@@ -1251,14 +1251,19 @@ __global__ __launch_bounds__(kJumpThreads) void lz4_decode_jump_kernel(tyche_bat
 //     of per-thread counts places them).  Every position costs the same: no walk
 //     can start out of phase (segment walks with stamps, tried first, stay out of
 //     phase through runs of 3-byte sequences and their bridges ran 100+ tokens);
-//  2. every thread takes consecutive tokens: decodes them (decode_seq_in), a
-//     block prefix sum of their output lengths gives their output offsets, the
-//     reference's checks run at those offsets (seq_check; atomicMin of the first
-//     failing token gives the exact -(consumed)-1), then the tokens before it fill
-//     their cells directly -- literals final (0x8000 | byte), match bytes pointing
-//     at the byte they copy (fill_match: d - off + j, or + j mod off when the match
-//     overlaps itself), runs over 16 bytes through the workgroup's list;
-//  3. pointer jumping, pack and store as in the jump kernel.
+//  2. one block scan of (marked positions, their output lengths -- kept with J) per
+//     thread gives each token its number and output offset; each thread decodes its
+//     own tokens once (solo_seq), runs the reference's checks at those offsets
+//     (seq_check; atomicMin of the first failing token gives the exact
+//     -(consumed)-1) and writes a record per token (output offset, literal count,
+//     literal start, match offset) and, at slot ceil(o / 4), its number into the
+//     covering table, whose running maximum then names the token that holds the
+//     first cell of every 4-cell group;
+//  3. cells, a 4-cell group per lane and step: literals final (0x8000 | byte),
+//     match bytes pointing at the byte they copy (d - off + ((c - d) mod off));
+//  4. pointer jumping without barriers, each thread's 16 cells in registers until
+//     they are all final (lock-step rounds for a thread that runs async_rounds of
+//     them), then packed to bytes and stored.
 
 constexpr uint32_t kSoloNpt = 8;      // positions per thread chunk
 constexpr uint32_t kSoloChunks = 3;   // chunks per thread: streams up to 3 * 8 * 1,024 - 1 bytes
