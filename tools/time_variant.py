@@ -22,6 +22,12 @@ mx = int(clen.max())
 out, rv = codec.decompress_pages(comp, clen, plen, compressor_id=cid, max_comp_len=mx)
 torch.cuda.synchronize()
 ok = bool((rv == plen).all()) and torch.equal(out, pages)
+# digest of the first 4,096 compressed pages (bytes past each page's length masked): variants that
+# must produce the same streams print the same digest
+import hashlib
+k = min(n, 4096)
+mask = torch.arange(comp.shape[1], device=comp.device)[None, :] < clen[:k, None].to(torch.int64)
+dig = hashlib.sha1((comp[:k] * mask).cpu().numpy().tobytes() + clen[:k].cpu().numpy().tobytes()).hexdigest()[:12]
 def t(fn, reps=3):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     best = 1e9
@@ -31,7 +37,7 @@ def t(fn, reps=3):
 d = t(lambda: codec.decompress_pages(comp, clen, plen, compressor_id=cid, out=out, rv=rv, max_comp_len=mx))
 c = t(lambda: codec.compress_pages(pages, compressor_id=cid, out=comp, out_len=clen))
 print(f"{os.path.basename(os.environ['TYCHE_CODEC_LIB'])}: compress {c * (1 << 20) / n:8.1f} ms/1M  "
-      f"decompress {d * (1 << 20) / n:8.1f} ms/1M  ratio {n * plen / float(clen.to(torch.int64).sum()):.3f}  correct={ok}")
+      f"decompress {d * (1 << 20) / n:8.1f} ms/1M  ratio {n * plen / float(clen.to(torch.int64).sum()):.4f}  correct={ok}  streams {dig}")
 '''
 
 

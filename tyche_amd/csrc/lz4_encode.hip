@@ -37,6 +37,9 @@
 #ifndef TYCHE_HASH_LOG
 #define TYCHE_HASH_LOG TYCHE_LZ4_HASH_LOG
 #endif
+#ifndef TYCHE_LANE_ADDR
+#define TYCHE_LANE_ADDR 1   // lz_parse.h: block windows from per-lane LDS addresses (every page has LDS in front)
+#endif
 
 #include <algorithm>
 #include <cstdlib>
@@ -451,6 +454,33 @@ struct SplitHdr {
     uint32_t pad[6];
 };
 static_assert(sizeof(SplitHdr) == 64, "split header");
+// Inserts the positions of blocks [from, to) (multiples of 64) into the table in
+// block order, as parse_page would have (later blocks overwrite earlier ones).
+// Four blocks' words are read before their inserts, so one LDS round trip covers
+// four blocks, and each lane addresses its words from a base fixed for the page.
+__device__ __forceinline__ void seed_table(const uint8_t *in, uint16_t *table, uint32_t from, uint32_t to,
+                                           uint32_t lane) {
+    const uint32_t ib = (uint32_t)(uintptr_t)in & 3u;
+    const uint32_t la = lzp::lds_addr(in - ib) + ((lane + ib) & ~3u), ls = (lane + ib) & 3u;
+    uint32_t blk = from;
+    for (; blk + 4u * kWave <= to; blk += 4u * kWave) {
+        const lzp::lds_u32_t *P = (const lzp::lds_u32_t *)(uintptr_t)(la + blk);
+        uint32_t w[4];
+#pragma unroll
+        for (uint32_t u = 0; u < 4u; u++) w[u] = lzp::word_at(P[16u * u], P[16u * u + 1u], ls);
+#pragma unroll
+        for (uint32_t u = 0; u < 4u; u++) {
+            table[lzp::hash4(w[u])] = (uint16_t)(blk + kWave * u + lane);
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+    for (; blk < to; blk += kWave) {
+        const lzp::lds_u32_t *P = (const lzp::lds_u32_t *)(uintptr_t)(la + blk);
+        table[lzp::hash4(lzp::word_at(P[0], P[1], ls))] = (uint16_t)(blk + lane);
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
 // per-wave region: table | map (256) | records (512) | fields / output ring (1 KiB)
 constexpr size_t kWaveRegion = kHashSize * sizeof(uint16_t) + 4 * kWave + kWave * sizeof(uint2) + kOutRing;
 constexpr size_t kSplitStage = sizeof(SplitHdr) + 2 * kWaveRegion;
@@ -545,14 +575,7 @@ __global__ __launch_bounds__(128, 3) void lz4_encode_split_kernel(tyche_batch_t 
                 hdr->next2_hi = (uint32_t)(nx >> 32);
             }
         } else if (split) {
-            // the positions of A's half, in block order (later blocks overwrite earlier ones)
-            const uint32_t ib = (uint32_t)(uintptr_t)in & 3u;
-            const uint32_t *A = (const uint32_t *)(in - ib);
-            for (uint32_t blk = 0; blk < H; blk += kWave) {
-                const uint32_t pos = blk + lane;
-                table[lzp::hash4(lzp::lds_word(A, pos + ib))] = (uint16_t)pos;
-                __builtin_amdgcn_wave_barrier();
-            }
+            seed_table(in, table, 0u, H, lane);   // the positions of A's half
             uint32_t op = 0;
             OutRing r{0u, 0u};
             bool first = true;
@@ -755,14 +778,7 @@ __global__ __launch_bounds__(kNW * 64) TYCHE_ENC_WPE_ATTR void lz4_encode_splitn
             // 51; 77.8 vs 78.0 ms per 1M x 16 KiB pages): part 0 writes to dst within its capacity,
             // later parts seed their table, hold back their first record and write to their scratch
             if (wave > 0) {
-                // the positions before the part, in block order (later blocks overwrite earlier ones)
-                const uint32_t ib = (uint32_t)(uintptr_t)in & 3u;
-                const uint32_t *A = (const uint32_t *)(in - ib);
-                for (uint32_t blk = b0 > seed ? b0 - seed : 0u; blk < b0; blk += kWave) {
-                    const uint32_t pos = blk + lane;
-                    table[lzp::hash4(lzp::lds_word(A, pos + ib))] = (uint16_t)pos;
-                    __builtin_amdgcn_wave_barrier();
-                }
+                seed_table(in, table, b0 > seed ? b0 - seed : 0u, b0, lane);   // the positions before the part
                 if (lane == 0) hdr->has_first[wave] = 0;
             }
             uint8_t *odst = wave == 0 ? p.dst : scratch;

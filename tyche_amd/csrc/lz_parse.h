@@ -102,6 +102,45 @@ __device__ __forceinline__ Window lds_window(const uint32_t *A, uint32_t q) {
     return r;
 }
 
+// LDS byte address of a pointer into LDS, and a dword pointer from one: the LZ4
+// encoder addresses a lane's windows from a per-lane base fixed for the page
+// (TYCHE_LANE_ADDR below), so a block's window costs one add and one min
+// instead of the nine address instructions of lds_window's general form.
+typedef const __attribute__((address_space(3))) uint32_t lds_u32_t;
+__device__ __forceinline__ uint32_t lds_addr(const void *p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t *)p;
+}
+// the window of lds_window from the LDS byte address a of the dword before the
+// one holding q (q's byte shift s = q & 3)
+__device__ __forceinline__ Window lds_window_at(uint32_t a, uint32_t s) {
+    const lds_u32_t *P = (const lds_u32_t *)(uintptr_t)a;
+    uint32_t d[7];
+#pragma unroll
+    for (int j = 0; j < 7; j++) d[j] = P[j];
+    Window r;
+    r.back = word_at(d[0], d[1], s);
+    r.w0 = word_at(d[1], d[2], s);
+#pragma unroll
+    for (int k = 0; k < 4; k++) r.fw[k] = word_at(d[k + 2], d[k + 3], s);
+    return r;
+}
+
+// v_ffbl_b32: the lowest set bit, 0xFFFFFFFF for 0 (cttz without the zero select)
+__device__ __forceinline__ uint32_t ffbl_raw(uint32_t x) {
+    uint32_t r;
+    asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+// MINMATCH + the equal leading bytes of the forward probe words a, b (4 + kProbe when all
+// are equal): the first set bit of the 128-bit difference from one min over per-word bit
+// positions (0xFFFFFFFF stays above every real one), 15 instructions instead of 24
+__device__ __forceinline__ uint32_t probe_len(const uint32_t (&a)[kProbeWords], const uint32_t (&b)[kProbeWords]) {
+    static_assert(kProbeWords == 4, "four probe words");
+    const uint32_t t0 = ffbl_raw(a[0] ^ b[0]), t1 = ffbl_raw(a[1] ^ b[1]) | 32u, t2 = ffbl_raw(a[2] ^ b[2]) | 64u,
+                   t3 = ffbl_raw(a[3] ^ b[3]) | 96u;
+    return 4u + (min(min(t0, t1), min(min(t2, t3), 128u)) >> 3);
+}
+
 // equal bytes at a and b going forward, a stopping before `limit` (whole wave,
 // 256 bytes per step); a, b, limit are positions, ib = (in & 3)
 __device__ inline uint32_t wave_extend(const uint8_t *in, const uint32_t *A, uint32_t ib, uint32_t a, uint32_t b,
@@ -215,6 +254,14 @@ __device__ __forceinline__ uint32_t bucket_of(uint32_t v, uint32_t v2 = 0, uint3
 // 650 -- the LDS latency it hides is not what bounds the parse, and its 6 VGPRs cost.  Off.
 #define TYCHE_PW_PREFETCH 0
 #endif
+#ifndef TYCHE_LANE_ADDR
+// 1 (the LZ4 encoder): parse_page's block windows from per-lane LDS addresses (lds_window_at).
+// Lanes past mflimit read the words at mflimit's dword with their own shift (unused values, and
+// their inserts into the table are followed by no lookup); a lane below position 4 reads the
+// dword before the page (unused: such positions take no backward extension), so the page must
+// have LDS in front of it.
+#define TYCHE_LANE_ADDR 0
+#endif
 #ifndef TYCHE_HASH_BYTES
 #define TYCHE_HASH_BYTES 5   // kRepCand (zstd): bytes hashed -- zstd level 1 hashes searchLength bytes
 #endif
@@ -239,6 +286,11 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
     bool done = false;
     Window pwn{};                       // TYCHE_PW_PREFETCH: the next block's window, loaded ahead
     uint32_t pwn_blk = 0xFFFFFFFFu;     // the block it belongs to (none yet)
+    constexpr bool kLaneAddr = TYCHE_LANE_ADDR && kWays == 1 && !kRepCand && !TYCHE_PW_PREFETCH;
+    const uint32_t abase = rfl(lds_addr(A));
+    const uint32_t la = abase + ((lane + ib) & ~3u) - 4u;              // this lane's window at block 0
+    const uint32_t la_max = abase + ((mflimit + ib) & ~3u) - 4u;       // mflimit's window
+    const uint32_t lsh = (lane + ib) & 3u;                             // (blocks are 64-aligned)
     PHASE_INIT();
     for (; !done && blk <= mflimit; blk = max(blk + kWave, cursor & ~(kWave - 1))) {
         const uint32_t pos = blk + lane;
@@ -248,7 +300,8 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
         // then insert this block's positions.  Every lane takes part, branch-free:
         // lanes past mflimit only exist in the last block, and no lookup follows
         // their inserts.
-        const Window pw = (TYCHE_PW_PREFETCH && pwn_blk == blk) ? pwn : lds_window(A, (live ? pos : mflimit) + ib);
+        const Window pw = kLaneAddr ? lds_window_at(min(la + blk, la_max), lsh)
+                          : (TYCHE_PW_PREFETCH && pwn_blk == blk) ? pwn : lds_window(A, (live ? pos : mflimit) + ib);
         const uint32_t v = pw.w0;
         constexpr uint32_t vm = kMin3 ? 0xFFFFFFu : 0xFFFFFFFFu;   // the bytes a candidate must match
         uint32_t cands[kWays];
@@ -304,16 +357,11 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
         // to kProbe bytes) and backward probe (up to 4 bytes).  A candidate is a
         // position <= mflimit, so the window stays inside the page's zero pad.
         uint32_t cand = cands[0];
-        Window cw = lds_window(A, cand + ib);
+        Window cw = kLaneAddr ? lds_window_at(abase - 4u + ((cand + ib) & ~3u), (cand + ib) & 3u) : lds_window(A, cand + ib);
         // deflate (kMin3): a candidate beyond the 32 KiB window cannot be coded; rejecting it here
         // lets a nearer bucket entry win (pages over 32 KiB)
         bool ok = live & (cand < pos) & (!kMin3 || pos - cand <= 32768u) & (((cw.w0 ^ v) & vm) == 0u);
-        uint32_t n = 4u + kProbe;
-#pragma unroll
-        for (int k = (int)kProbeWords - 1; k >= 0; k--) {
-            const uint32_t x = pw.fw[k] ^ cw.fw[k];
-            if (x) n = 4u + 4u * (uint32_t)k + ((uint32_t)__builtin_ctz(x) >> 3);
-        }
+        uint32_t n = probe_len(pw.fw, cw.fw);
         if (kMin3 && cw.w0 != v) n = 3u;
 #pragma unroll
         for (int w = 1; w < kWays; w++) {
@@ -321,12 +369,7 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
             const uint32_t cw2 = cands[w];
             const Window ww = lds_window(A, cw2 + ib);
             const bool okw = live & (cw2 < pos) & (!kMin3 || pos - cw2 <= 32768u) & (((ww.w0 ^ v) & vm) == 0u);
-            uint32_t nw = 4u + kProbe;
-#pragma unroll
-            for (int k = (int)kProbeWords - 1; k >= 0; k--) {
-                const uint32_t x = pw.fw[k] ^ ww.fw[k];
-                if (x) nw = 4u + 4u * (uint32_t)k + ((uint32_t)__builtin_ctz(x) >> 3);
-            }
+            uint32_t nw = probe_len(pw.fw, ww.fw);
             if (kMin3 && ww.w0 != v) nw = 3u;
             if (okw && (!ok || nw > n)) {
                 cand = cw2;
@@ -369,12 +412,7 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
             const uint32_t rc = pos >= R ? pos - R : 0u;
             const Window rw = lds_window(A, min(rc, mflimit) + ib);
             rok = live & (pos >= R) & (((rw.w0 ^ v) & vm) == 0u);
-            uint32_t rn = 4u + kProbe;
-#pragma unroll
-            for (int k = (int)kProbeWords - 1; k >= 0; k--) {
-                const uint32_t x = pw.fw[k] ^ rw.fw[k];
-                if (x) rn = 4u + 4u * (uint32_t)k + ((uint32_t)__builtin_ctz(x) >> 3);
-            }
+            uint32_t rn = probe_len(pw.fw, rw.fw);
             if (kMin3 && rw.w0 != v) rn = 3u;
 #ifndef TYCHE_REP_SLACK
 // a repeat candidate wins when at most this many bytes shorter than the hash candidate: a repeat
@@ -390,12 +428,7 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
 #define TYCHE_REP2 1
 #endif
             const bool rok2 = TYCHE_REP2 && live & (pos >= R2) & (((rw2.w0 ^ v) & vm) == 0u) & (R2 != R);
-            uint32_t rn2 = 4u + kProbe;
-#pragma unroll
-            for (int k = (int)kProbeWords - 1; k >= 0; k--) {
-                const uint32_t x = pw.fw[k] ^ rw2.fw[k];
-                if (x) rn2 = 4u + 4u * (uint32_t)k + ((uint32_t)__builtin_ctz(x) >> 3);
-            }
+            uint32_t rn2 = probe_len(pw.fw, rw2.fw);
             if (kMin3 && rw2.w0 != v) rn2 = 3u;
             if (rok && (!ok || rn + TYCHE_REP_SLACK >= n)) {
                 cand = rc;
