@@ -131,6 +131,12 @@ __device__ __forceinline__ uint32_t ffbl_raw(uint32_t x) {
     asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(x));
     return r;
 }
+// v_ffbh_u32: the leading zeros, 0xFFFFFFFF for 0
+__device__ __forceinline__ uint32_t ffbh_raw(uint32_t x) {
+    uint32_t r;
+    asm("v_ffbh_u32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
 // MINMATCH + the equal leading bytes of the forward probe words a, b (4 + kProbe when all
 // are equal): the first set bit of the 128-bit difference from one min over per-word bit
 // positions (0xFFFFFFFF stays above every real one), 15 instructions instead of 24
@@ -361,7 +367,10 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
         // deflate (kMin3): a candidate beyond the 32 KiB window cannot be coded; rejecting it here
         // lets a nearer bucket entry win (pages over 32 KiB)
         bool ok = live & (cand < pos) & (!kMin3 || pos - cand <= 32768u) & (((cw.w0 ^ v) & vm) == 0u);
-        uint32_t n = probe_len(pw.fw, cw.fw);
+        // one hash candidate and nothing else (LZ4): the probe waits until a match is known to
+        // start at or after the cursor (kLateProbe), otherwise the candidates compare lengths here
+        constexpr bool kLateProbe = kWays == 1 && !kRepCand && !kMin3;
+        uint32_t n = kLateProbe ? 0u : probe_len(pw.fw, cw.fw);
         if (kMin3 && cw.w0 != v) n = 3u;
 #pragma unroll
         for (int w = 1; w < kWays; w++) {
@@ -444,12 +453,26 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
             }
             rok |= rok2;
         }
-        const uint32_t xb = pw.back ^ cw.back;
-        const uint32_t e = min(matchlimit, pos + kMinMatch + kProbe);
-        n = min(n, e - pos);
-        uint32_t len = (TYCHE_EABLATE & 2) ? 4u : n;
-        const bool capped = !(TYCHE_EABLATE & 2) && pos + n == e && e < matchlimit;
-        const uint32_t back = (TYCHE_EABLATE & 2) || pos < 4 || cand < 4 ? 0u : xb ? (__builtin_clz(xb) >> 3) : 4u;
+        // match length within the probe limit and matchlimit; capped: it reached the probe limit
+        // before matchlimit (its end is not known yet).  n <= kMinMatch + kProbe, so
+        // min(n, min(matchlimit, pos + 20) - pos) is min(n, matchlimit - pos) (for lanes past
+        // matchlimit both wrap to n; their values are never used)
+        uint32_t len = 0, back = 0;
+        bool capped = false;
+        auto lengths = [&]() {
+            if (kLateProbe) n = probe_len(pw.fw, cw.fw);
+            n = min(n, matchlimit - pos);
+            len = (TYCHE_EABLATE & 2) ? 4u : n;
+            capped = !(TYCHE_EABLATE & 2) && n == kMinMatch + kProbe &&
+                     (int32_t)pos < (int32_t)matchlimit - (int32_t)(kMinMatch + kProbe);
+            // backward extension: the equal bytes before both positions, up to 4 (a selected match
+            // has cand < pos, so cand < 4 covers pos < 4); v_ffbh_u32 gives 0xFFFFFFFF for equal
+            // words (the asm result computed unconditionally: inline asm is never speculated, so
+            // inside the select it would become a branch)
+            const uint32_t bx = min(ffbh_raw(pw.back ^ cw.back), 32u) >> 3;
+            back = (TYCHE_EABLATE & 2) || cand < 4 ? 0u : bx;
+        };
+        if (!kLateProbe) lengths();
         // ---- greedy parse of this block.  Every lane first finds the next match
         // lane at or after its own match's end (64: none in this block; 128: the
         // match reached the probe limit, end not known yet), so the walk from the
@@ -470,12 +493,13 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
         }
         PHASE(0);
         PHASE_COUNT(8);
-        const uint32_t at = cursor > blk ? cursor - blk : 0u;
+        // (a signed max on the scalar unit: an unsigned saturating subtract goes to a vector ALU)
+        const uint32_t at = (uint32_t)max((int32_t)(cursor - blk), 0);
         const uint64_t rem = mall & (~0ull << at);
         if (rem == 0) continue;                                // no match starts at or after it
         PHASE_COUNT(10);
-        const uint32_t endp = pos + len;
-        const uint32_t rl = endp - blk;
+        if (kLateProbe) lengths();
+        const uint32_t rl = lane + len;                        // the match's end, from blk
         const uint64_t after = rl < kWave ? mall & (~0ull << rl) : 0ull;
         const uint32_t nxt = (capped && !(TYCHE_EABLATE & 8)) ? 2u * kWave
                            : after ? (uint32_t)__builtin_ctzll(after) : kWave;
@@ -500,12 +524,12 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
                 li = rdlane(nxt, li);
             } while (li < kWave);
             if (li == kWave) {
-                end = rdlane(endp, at_li);
+                end = blk + at_li + rdlane(len, at_li);
                 break;
             }
             // reached the probe limit: extend with the whole wave, then look for
             // the next match after the extended end
-            const uint32_t mp = blk + at_li, mc = rdlane(cand, at_li), ln0 = rdlane(endp, at_li) - mp;
+            const uint32_t mp = blk + at_li, mc = rdlane(cand, at_li), ln0 = rdlane(len, at_li);
             PHASE(1);
             const uint32_t ln = ln0 + wave_extend(in, A, ib, mp + ln0, mc + ln0, matchlimit, lane);
             PHASE(5);
@@ -522,7 +546,7 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
         PHASE(1);
         // ---- append this block's records (stream order)
         const bool is_sel = (sel >> lane) & 1ull;
-        const uint32_t rank = nacc + (uint32_t)__popcll(sel & ((1ull << lane) - 1ull));
+        const uint32_t rank = nacc + __builtin_amdgcn_mbcnt_hi((uint32_t)(sel >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sel, 0u));
         if (is_sel) rec[rank] = make_uint2(pos | (cand << 16), len | (back << 16));
         nacc += (uint32_t)__popcll(sel);
         // a block adds at most 16 records (each covers >= 4 positions; 22 of >= 3)
