@@ -985,11 +985,13 @@ hipError_t launch_lz4_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream_
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, (int)T, lds) != hipSuccess || per_cu < 1) per_cu = 1;
         const size_t grid = std::min<size_t>(b.count, ncu * (size_t)per_cu);
         const uint32_t pws = nw == 8 ? part_scratch<8>(in_cap) : nw == 4 ? part_scratch<4>(in_cap) : part_scratch<3>(in_cap);
-        uint32_t seed = (uint32_t)std::max(0L, knob("LZ4_ENC_SEED", nw == 3 ? 10240L : nw == 4 ? 9216L : (long)kSeed)) &
+        uint32_t seed = (uint32_t)std::max(0L, knob("LZ4_ENC_SEED", nw == 3 ? 10240L : nw == 4 ? 8192L : (long)kSeed)) &
                         ~(kWave - 1u);   // positions seeded before a part
         // part 0's share of the page in 64ths (0: equal parts); at least 1/kNW, so the later parts fit
         // their scratch (part_scratch: a 1/kNW part)
-        uint32_t p0 = (uint32_t)std::max(0L, knob("LZ4_ENC_P0", nw == 3 ? 27L : nw == 4 ? 22L : 0L));
+        // Round 5, after the parse's instruction diet made seeding cheaper (profiles/r05_knob_enc*.log,
+        // 256K pages): part 0 19/64 and 8,192 seeds 63.6 ms at ratio 2.6175 (22/64 and 9,216: 65.0 at 2.6189)
+        uint32_t p0 = (uint32_t)std::max(0L, knob("LZ4_ENC_P0", nw == 3 ? 27L : nw == 4 ? 19L : 0L));
         if (p0) p0 = std::min<uint32_t>(std::max<uint32_t>(p0, (64u + (uint32_t)nw - 1u) / (uint32_t)nw), 48u);
         const uint32_t ws_stride = (uint32_t)(nw - 1) * pws;
         ScratchLease ws(s, grid * (size_t)ws_stride);
