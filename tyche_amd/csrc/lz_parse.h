@@ -261,12 +261,12 @@ __device__ __forceinline__ uint32_t bucket_of(uint32_t v, uint32_t v2 = 0, uint3
 #define TYCHE_PW_PREFETCH 0
 #endif
 #ifndef TYCHE_LANE_ADDR
-// 1 (the LZ4 encoder): parse_page's block windows from per-lane LDS addresses (lds_window_at).
-// Lanes past mflimit read the words at mflimit's dword with their own shift (unused values, and
-// their inserts into the table are followed by no lookup); a lane below position 4 reads the
-// dword before the page (unused: such positions take no backward extension), so the page must
-// have LDS in front of it.
-#define TYCHE_LANE_ADDR 0
+// 1: parse_page's windows from LDS addresses (lds_window_at): a lane's own window from a base
+// fixed for the page, candidates' from the page's base.  Lanes past mflimit read mflimit's dword
+// (the LZ4 encoder with their own shift: unused values, inserts that no lookup follows); a window
+// below position 4 reads the dword before the page (unused: such positions and candidates take no
+// backward extension), so every caller keeps LDS in front of the page.
+#define TYCHE_LANE_ADDR 1
 #endif
 #ifndef TYCHE_HASH_BYTES
 #define TYCHE_HASH_BYTES 5   // kRepCand (zstd): bytes hashed -- zstd level 1 hashes searchLength bytes
@@ -292,11 +292,17 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
     bool done = false;
     Window pwn{};                       // TYCHE_PW_PREFETCH: the next block's window, loaded ahead
     uint32_t pwn_blk = 0xFFFFFFFFu;     // the block it belongs to (none yet)
-    constexpr bool kLaneAddr = TYCHE_LANE_ADDR && kWays == 1 && !kRepCand && !TYCHE_PW_PREFETCH;
+    constexpr bool kLaneAddr = TYCHE_LANE_ADDR && !TYCHE_PW_PREFETCH;
     const uint32_t abase = rfl(lds_addr(A));
     const uint32_t la = abase + ((lane + ib) & ~3u) - 4u;              // this lane's window at block 0
     const uint32_t la_max = abase + ((mflimit + ib) & ~3u) - 4u;       // mflimit's window
     const uint32_t lsh = (lane + ib) & 3u;                             // (blocks are 64-aligned)
+    // lanes past mflimit read mflimit's window exactly (its shift too) where their table inserts
+    // can be followed by lookups: a zstd part's warm-up parse shares its table with the part
+    constexpr bool kExactDead = kWays > 1 || kRepCand || kMin3;
+    const uint32_t msh = (mflimit + ib) & 3u;
+    // a candidate's window (a position <= mflimit) from its LDS address
+    auto win_at = [&](uint32_t x) { return lds_window_at(abase - 4u + ((x + ib) & ~3u), (x + ib) & 3u); };
     PHASE_INIT();
     for (; !done && blk <= mflimit; blk = max(blk + kWave, cursor & ~(kWave - 1))) {
         const uint32_t pos = blk + lane;
@@ -306,7 +312,7 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
         // then insert this block's positions.  Every lane takes part, branch-free:
         // lanes past mflimit only exist in the last block, and no lookup follows
         // their inserts.
-        const Window pw = kLaneAddr ? lds_window_at(min(la + blk, la_max), lsh)
+        const Window pw = kLaneAddr ? lds_window_at(min(la + blk, la_max), kExactDead && !live ? msh : lsh)
                           : (TYCHE_PW_PREFETCH && pwn_blk == blk) ? pwn : lds_window(A, (live ? pos : mflimit) + ib);
         const uint32_t v = pw.w0;
         constexpr uint32_t vm = kMin3 ? 0xFFFFFFu : 0xFFFFFFFFu;   // the bytes a candidate must match
@@ -363,7 +369,7 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
         // to kProbe bytes) and backward probe (up to 4 bytes).  A candidate is a
         // position <= mflimit, so the window stays inside the page's zero pad.
         uint32_t cand = cands[0];
-        Window cw = kLaneAddr ? lds_window_at(abase - 4u + ((cand + ib) & ~3u), (cand + ib) & 3u) : lds_window(A, cand + ib);
+        Window cw = kLaneAddr ? win_at(cand) : lds_window(A, cand + ib);
         // deflate (kMin3): a candidate beyond the 32 KiB window cannot be coded; rejecting it here
         // lets a nearer bucket entry win (pages over 32 KiB)
         bool ok = live & (cand < pos) & (!kMin3 || pos - cand <= 32768u) & (((cw.w0 ^ v) & vm) == 0u);
@@ -376,7 +382,7 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
         for (int w = 1; w < kWays; w++) {
             // older bucket entries: taken only when strictly longer
             const uint32_t cw2 = cands[w];
-            const Window ww = lds_window(A, cw2 + ib);
+            const Window ww = kLaneAddr ? win_at(cw2) : lds_window(A, cw2 + ib);
             const bool okw = live & (cw2 < pos) & (!kMin3 || pos - cw2 <= 32768u) & (((ww.w0 ^ v) & vm) == 0u);
             uint32_t nw = probe_len(pw.fw, ww.fw);
             if (kMin3 && ww.w0 != v) nw = 3u;
@@ -419,7 +425,7 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
         if (kRepCand) {
             // the repeat-offset candidate (consecutive windows: cheap loads)
             const uint32_t rc = pos >= R ? pos - R : 0u;
-            const Window rw = lds_window(A, min(rc, mflimit) + ib);
+            const Window rw = kLaneAddr ? win_at(min(rc, mflimit)) : lds_window(A, min(rc, mflimit) + ib);
             rok = live & (pos >= R) & (((rw.w0 ^ v) & vm) == 0u);
             uint32_t rn = probe_len(pw.fw, rw.fw);
             if (kMin3 && rw.w0 != v) rn = 3u;
@@ -432,7 +438,7 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
 #endif
             // repeat offset 2 (the other offset of two alternating ones)
             const uint32_t rc2 = pos >= R2 ? pos - R2 : 0u;
-            const Window rw2 = lds_window(A, min(rc2, mflimit) + ib);
+            const Window rw2 = kLaneAddr ? win_at(min(rc2, mflimit)) : lds_window(A, min(rc2, mflimit) + ib);
 #ifndef TYCHE_REP2
 #define TYCHE_REP2 1
 #endif
