@@ -1090,18 +1090,31 @@ __global__ __launch_bounds__(kNW * 64) void zstd_parse_split_kernel(tyche_batch_
             uint32_t rep[2] = {1u, 4u};
             if (wave > 0) {   // seed: the positions before the part, block order, as the parse inserts them
                 const uint32_t ib = (uint32_t)(uintptr_t)in & 3u;
-                const uint32_t *A = (const uint32_t *)(in - ib);
                 uint32_t *T = (uint32_t *)table;
                 const uint32_t wstart = b0 > kZWarm ? b0 - kZWarm : 0u;
-                for (uint32_t blk = wstart > seed ? wstart - seed : 0u; blk < wstart; blk += kWave) {
-                    const uint32_t pos = blk + lane;
-                    const uint32_t h = lzp::bucket_of<kZWays>(lzp::lds_word(A, pos + ib), lzp::lds_word(A, pos + 4u + ib),
-                                                              TYCHE_HASH_BYTES);
+                // four blocks' words and hashes at once (one LDS round trip for their windows, from
+                // this lane's base address), then each block's bucket update in block order
+                const uint32_t la = lzp::lds_addr(in - ib) + ((lane + ib) & ~3u), ls = (lane + ib) & 3u;
+                auto hash_at = [&](uint32_t blk) {
+                    const lzp::lds_u32_t *P = (const lzp::lds_u32_t *)(uintptr_t)(la + blk);
+                    const uint32_t d0 = P[0], d1 = P[1], d2 = P[2];
+                    return lzp::bucket_of<kZWays>(lzp::word_at(d0, d1, ls), lzp::word_at(d1, d2, ls), TYCHE_HASH_BYTES);
+                };
+                auto insert = [&](uint32_t h, uint32_t pos) {
                     const uint32_t bk = T[h];
                     __builtin_amdgcn_wave_barrier();
                     T[h] = pos | (bk << 16);
                     __builtin_amdgcn_wave_barrier();
+                };
+                uint32_t blk = wstart > seed ? wstart - seed : 0u;
+                for (; blk + 4u * kWave <= wstart; blk += 4u * kWave) {
+                    uint32_t h[4];
+#pragma unroll
+                    for (uint32_t u = 0; u < 4u; u++) h[u] = hash_at(blk + kWave * u);
+#pragma unroll
+                    for (uint32_t u = 0; u < 4u; u++) insert(h[u], blk + kWave * u + lane);
                 }
+                for (; blk < wstart; blk += kWave) insert(hash_at(blk), blk + lane);
                 // warm-up: parse the kZWarm bytes before the part, sequences dropped, for the repeat
                 // offsets the part's parse starts from (a cold {1, 4} cost the 4-wave split 1.7 % of
                 // ratio; tools/parse_sim.c zsplit: 4.999 -> 5.069 of 5.100)
