@@ -23,6 +23,8 @@ using std::min;
 #define LC_FN static inline
 #define LC_Q(base, k) ((base) + ((uint32_t)(k) << 3))   // plain arrays (the kernel interleaves lanes)
 #define LC_RCP(x) (1.0f / (x))
+#define LC_UMUL24(a, b) ((uint32_t)(a) * (uint32_t)(b))
+#define LC_MUL24(a, b) ((int32_t)(a) * (int32_t)(b))
 static inline uint32_t lc_perm_host(uint32_t hi, uint32_t lo, uint32_t sel) {   // v_perm_b32
     const uint64_t v = ((uint64_t)hi << 32) | lo;
     uint32_t d = 0;

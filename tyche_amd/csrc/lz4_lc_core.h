@@ -30,6 +30,10 @@
 #ifndef LC_PERM
 #define LC_PERM(hi, lo, sel) __builtin_amdgcn_perm((hi), (lo), (sel))   // v_perm_b32
 #endif
+#ifndef LC_UMUL24
+#define LC_UMUL24(a, b) __umul24((a), (b))   // v_mul_u32_u24 (full rate; v_mul_hi_u32 is not)
+#define LC_MUL24(a, b) __mul24((a), (b))     // v_mul_i32_i24 / v_mad_i32_i24
+#endif
 
 // The match-copy table, one entry per offset class c = min(off, 16): the
 // v_perm_b32 selectors that turn the 16 bytes at d - off (of which only the
@@ -93,9 +97,11 @@ LC_FN int32_t lc_row(int32_t k) {
         return k & (rows - 1);
     } else {
         static_assert(rows == 24, "ring rows: a power of two or 24");
+        // u / 24 = (u * 43691) >> 20 exactly for u < 2^16 (the error u * 3.2e-7 stays under 1/24
+        // there; u <= 65535 / 8 + 25), with 24-bit multiplies
         const uint32_t u = (uint32_t)(k + rows);
-        const uint32_t q = (uint32_t)(((uint64_t)u * 0xAAAAAAABull) >> 36);   // u / 24
-        return (int32_t)(u - q * 24u);
+        const uint32_t q = LC_UMUL24(u, 43691u) >> 20;
+        return (int32_t)u + LC_MUL24((int32_t)q, -24);
     }
 }
 template <int32_t R>
