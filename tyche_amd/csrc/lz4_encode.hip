@@ -278,18 +278,17 @@ __device__ __forceinline__ bool emit_staged(const uint2 *rec, uint32_t n, uint32
     const uint2 rp = rec[lane > 0 && is_sel ? lane - 1 : 0];
     const uint32_t pos = rc.x & 0xFFFFu, cand = rc.x >> 16, len = rc.y & 0xFFFFu, back = rc.y >> 16;
     const uint32_t prev_end = lane == 0 ? anchor : (rp.x & 0xFFFFu) + (rp.y & 0xFFFFu);
-    uint32_t lit = 0, lext = 0, lstart = 0, off = 0, mc = 0, mext = 0, token = 0, enc = 0;
-    if (is_sel) {
-        const uint32_t k = min(min(back, pos - prev_end), cand);   // catch-up (lz4.c:549)
-        lstart = prev_end;
-        lit = pos - k - prev_end;
-        lext = lit >= 15 ? (lit - 15) / 255 + 1 : 0;
-        off = pos - cand;
-        mc = len + k - kMinMatch;
-        mext = mc >= 15 ? (mc - 15) / 255 + 1 : 0;
-        token = (min(lit, 15u) << 4) | min(mc, 15u);
-        enc = 1 + lext + lit + 2 + mext;
-    }
+    // branch-free: lanes past n compute values from record 0 that are never stored (enc 0; lit 0
+    // keeps them out of the long-run loop); a branch around these costs more exec-mask work
+    const uint32_t k = min(min(back, pos - prev_end), cand);   // catch-up (lz4.c:549)
+    const uint32_t lstart = prev_end;
+    const uint32_t lit = is_sel ? pos - k - prev_end : 0u;
+    const uint32_t lext = lit >= 15 ? (lit - 15) / 255 + 1 : 0;
+    const uint32_t off = pos - cand;
+    const uint32_t mc = len + k - kMinMatch;
+    const uint32_t mext = mc >= 15 ? (mc - 15) / 255 + 1 : 0;
+    const uint32_t token = (min(lit, 15u) << 4) | min(mc, 15u);
+    const uint32_t enc = is_sel ? 1 + lext + lit + 2 + mext : 0u;
     const int32_t incl = wave_incl_sum((int32_t)enc);
     const uint32_t eo = (uint32_t)incl - enc;
     const uint32_t et = rdlane((uint32_t)incl, 63);
@@ -325,9 +324,13 @@ __device__ __forceinline__ bool emit_staged(const uint2 *rec, uint32_t n, uint32
         const uint32_t q0 = lstart + ib, i0 = q0 >> 2, sh = q0 & 3u;
         const uint32_t d0 = A[i0], d1 = A[i0 + 1], d2 = A[i0 + 2];
         const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, sh), w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+        // byte t >= ls goes to a dummy byte (the owner map, unused here): selects instead of eight
+        // exec-mask branches
 #pragma unroll
-        for (uint32_t t = 0; t < 8; t++)
-            if (t < ls) ring[(q_lit + t) & m] = (uint8_t)((t < 4 ? w0 : w1) >> (8 * (t & 3u)));
+        for (uint32_t t = 0; t < 8; t++) {
+            uint8_t *bp = t < ls ? ring + ((q_lit + t) & m) : map;
+            *bp = (uint8_t)((t < 4 ? w0 : w1) >> (8 * (t & 3u)));
+        }
 #else
         for (uint32_t t = 0; t < ls; t++) ring[(q_lit + t) & m] = in[lstart + t];
 #endif
