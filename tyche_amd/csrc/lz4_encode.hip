@@ -465,6 +465,8 @@ __device__ __forceinline__ void seed_table(const uint8_t *in, uint16_t *table, u
                                            uint32_t lane) {
     const uint32_t ib = (uint32_t)(uintptr_t)in & 3u;
     const uint32_t la = lzp::lds_addr(in - ib) + ((lane + ib) & ~3u), ls = (lane + ib) & 3u;
+    const uint32_t tbase = rfl(lzp::lds_addr(table));
+    auto slot = [&](uint32_t w) { return (lzp::lds_u16_t *)(uintptr_t)lzp::slot_addr(tbase, lzp::hash4(w)); };
     uint32_t blk = from;
     for (; blk + 4u * kWave <= to; blk += 4u * kWave) {
         const lzp::lds_u32_t *P = (const lzp::lds_u32_t *)(uintptr_t)(la + blk);
@@ -473,13 +475,13 @@ __device__ __forceinline__ void seed_table(const uint8_t *in, uint16_t *table, u
         for (uint32_t u = 0; u < 4u; u++) w[u] = lzp::word_at(P[16u * u], P[16u * u + 1u], ls);
 #pragma unroll
         for (uint32_t u = 0; u < 4u; u++) {
-            table[lzp::hash4(w[u])] = (uint16_t)(blk + kWave * u + lane);
+            *slot(w[u]) = (uint16_t)(blk + kWave * u + lane);
             __builtin_amdgcn_wave_barrier();
         }
     }
     for (; blk < to; blk += kWave) {
         const lzp::lds_u32_t *P = (const lzp::lds_u32_t *)(uintptr_t)(la + blk);
-        table[lzp::hash4(lzp::word_at(P[0], P[1], ls))] = (uint16_t)(blk + lane);
+        *slot(lzp::word_at(P[0], P[1], ls)) = (uint16_t)(blk + lane);
         __builtin_amdgcn_wave_barrier();
     }
 }

@@ -125,6 +125,15 @@ __device__ __forceinline__ Window lds_window_at(uint32_t a, uint32_t s) {
     return r;
 }
 
+// LDS byte address of 16-bit table slot h: one v_lshl_add_u32 (the compiler's own form of
+// base + 2 * (x >> 22) is a shift, a mask and an add)
+typedef __attribute__((address_space(3))) uint16_t lds_u16_t;
+__device__ __forceinline__ uint32_t slot_addr(uint32_t tbase, uint32_t h) {
+    uint32_t a;
+    asm("v_lshl_add_u32 %0, %1, 1, %2" : "=v"(a) : "v"(h), "s"(tbase));
+    return a;
+}
+
 // v_ffbl_b32: the lowest set bit, 0xFFFFFFFF for 0 (cttz without the zero select)
 __device__ __forceinline__ uint32_t ffbl_raw(uint32_t x) {
     uint32_t r;
@@ -297,6 +306,7 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
     const uint32_t la = abase + ((lane + ib) & ~3u) - 4u;              // this lane's window at block 0
     const uint32_t la_max = abase + ((mflimit + ib) & ~3u) - 4u;       // mflimit's window
     const uint32_t lsh = (lane + ib) & 3u;                             // (blocks are 64-aligned)
+    const uint32_t tbase = rfl(lds_addr(table));
     // lanes past mflimit read mflimit's window exactly (its shift too) where their table inserts
     // can be followed by lookups: a zstd part's warm-up parse shares its table with the part
     constexpr bool kExactDead = kWays > 1 || kRepCand || kMin3;
@@ -322,9 +332,16 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
                                    ? (uint32_t)(((((uint64_t)(pw.fw[0] & (TYCHE_HASH_BYTES == 5 ? 0xFFu : 0xFFFFu)) << 32) | v) *
                                                  0xCF1BBCDCB7A56463ull) >> (64 - kHashLog))
                                    : hash4(v);
-            cands[0] = table[h];
-            __builtin_amdgcn_wave_barrier();
-            table[h] = (uint16_t)pos;
+            if (kLaneAddr && !kRepCand) {
+                lds_u16_t *slot = (lds_u16_t *)(uintptr_t)slot_addr(tbase, h);
+                cands[0] = *slot;
+                __builtin_amdgcn_wave_barrier();
+                *slot = (uint16_t)pos;
+            } else {
+                cands[0] = table[h];
+                __builtin_amdgcn_wave_barrier();
+                table[h] = (uint16_t)pos;
+            }
         } else if (kWays == 2) {
             uint32_t *T = (uint32_t *)table;
             const uint32_t h = kRepCand ? bucket_of<kWays>(v, pw.fw[0], TYCHE_HASH_BYTES)
@@ -485,7 +502,13 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
         // parse position is one v_readlane per selected match.  The parse
         // position is always inside the block (blk >= cursor & ~63), and no mask
         // bit lies past mflimit, so a match ending there ends the walk.
-        uint64_t mall = (TYCHE_EABLATE & 4) ? 0ull : __ballot(ok);
+        // (the single-candidate parse ballots its three conditions separately: each compare's lane
+        // mask goes straight into the scalar AND, where a ballot of the combined bool is turned into
+        // a 0/1 vector value and compared back)
+        uint64_t mall = (TYCHE_EABLATE & 4) ? 0ull
+                      : kLateProbe ? __builtin_amdgcn_ballot_w64(live) & __builtin_amdgcn_ballot_w64(cand < pos) &
+                                         __builtin_amdgcn_ballot_w64(((cw.w0 ^ v) & vm) == 0u)
+                                   : __ballot(ok);
 #ifndef TYCHE_REP_NEXT
 #define TYCHE_REP_NEXT 1
 #endif
