@@ -492,8 +492,12 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
             // has cand < pos, so cand < 4 covers pos < 4); v_ffbh_u32 gives 0xFFFFFFFF for equal
             // words (the asm result computed unconditionally: inline asm is never speculated, so
             // inside the select it would become a branch)
-            const uint32_t bx = min(ffbh_raw(pw.back ^ cw.back), 32u) >> 3;
-            back = (TYCHE_EABLATE & 2) || cand < 4 ? 0u : bx;
+            // (kLateProbe, the LZ4 encoder: its sink computes the extension for the selected matches
+            // only, from the page; the record carries 0)
+            if (!kLateProbe) {
+                const uint32_t bx = min(ffbh_raw(pw.back ^ cw.back), 32u) >> 3;
+                back = (TYCHE_EABLATE & 2) || cand < 4 ? 0u : bx;
+            }
         };
         if (!kLateProbe) lengths();
         // ---- greedy parse of this block.  Every lane first finds the next match
