@@ -58,18 +58,6 @@ constexpr uint32_t kPad = 64;
 constexpr uint32_t kPrefetchVec = 16;    // 16-byte vectors per lane prefetched for the next page (16 KiB; 8 or 4
                                           // take the one-wave kernel to 132 / 119 VGPRs: 70.6 / 70.9 ms per 1M x 8 KiB)
 
-// Backward extension of the match at pos from cand (lz4.c:549's catch-up, up to 4 bytes): the
-// equal bytes before both, 0 when cand < 4 (a match has cand < pos).  The parse leaves it to the
-// sinks (lz_parse.h kLateProbe): ~50 selected matches per sink call instead of every lane of
-// every block.
-__device__ __forceinline__ uint32_t back_len(const uint8_t *in, uint32_t pos, uint32_t cand) {
-    const uint32_t ib = (uint32_t)(uintptr_t)in & 3u;
-    const uint32_t *A = (const uint32_t *)(in - ib);
-    const uint32_t a = lzp::lds_word(A, max(pos, 4u) - 4u + ib), b = lzp::lds_word(A, max(cand, 4u) - 4u + ib);
-    const uint32_t x = min(lzp::ffbh_raw(a ^ b), 32u) >> 3;   // (v_ffbh_u32: 0xFFFFFFFF for equal words)
-    return cand < 4u ? 0u : x;
-}
-
 // a sequence's encoding: token, literal-length bytes, literals, offset, match-length bytes
 struct SeqFields {
     uint32_t lit, lext, anchor, off, mc, token, total;
@@ -109,7 +97,7 @@ __device__ bool emit_records(const uint2 *rec, uint32_t n, uint32_t anchor, cons
     const bool is_sel = lane < n;
     const uint2 r = rec[is_sel ? lane : 0];
     const uint2 rp = rec[lane > 0 && is_sel ? lane - 1 : 0];
-    const uint32_t pos = r.x & 0xFFFFu, cand = r.x >> 16, len = r.y & 0xFFFFu, back = back_len(in, pos, cand);
+    const uint32_t pos = r.x & 0xFFFFu, cand = r.x >> 16, len = r.y & 0xFFFFu, back = lzp::back_at(in, pos, cand);
     const uint32_t prev_end = lane == 0 ? anchor : (rp.x & 0xFFFFu) + (rp.y & 0xFFFFu);
     SeqFields f{};
     uint32_t enc = 0;
@@ -288,7 +276,7 @@ __device__ __forceinline__ bool emit_staged(const uint2 *rec, uint32_t n, uint32
     const bool is_sel = lane < n;
     const uint2 rc = rec[is_sel ? lane : 0];
     const uint2 rp = rec[lane > 0 && is_sel ? lane - 1 : 0];
-    const uint32_t pos = rc.x & 0xFFFFu, cand = rc.x >> 16, len = rc.y & 0xFFFFu, back = back_len(in, pos, cand);
+    const uint32_t pos = rc.x & 0xFFFFu, cand = rc.x >> 16, len = rc.y & 0xFFFFu, back = lzp::back_at(in, pos, cand);
     const uint32_t prev_end = lane == 0 ? anchor : (rp.x & 0xFFFFu) + (rp.y & 0xFFFFu);
     // branch-free: lanes past n compute values from record 0 that are never stored (enc 0; lit 0
     // keeps them out of the long-run loop); a branch around these costs more exec-mask work

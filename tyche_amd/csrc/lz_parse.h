@@ -179,17 +179,31 @@ __device__ inline uint32_t wave_extend(const uint8_t *in, const uint32_t *A, uin
     }
 }
 
+// Backward extension of the match at pos from cand (lz4.c:549's catch-up, up to 4 bytes): the
+// equal bytes before both, 0 when cand < 4 (a match has cand < pos).  Parses whose records leave
+// it to the sink (parse_page's kSinkBack) compute it there for the ~50 selected matches of a call
+// instead of for every lane of every block.
+__device__ __forceinline__ uint32_t back_at(const uint8_t *in, uint32_t pos, uint32_t cand) {
+    const uint32_t ib = (uint32_t)(uintptr_t)in & 3u;
+    const uint32_t *A = (const uint32_t *)(in - ib);
+    const uint32_t a = lds_word(A, max(pos, 4u) - 4u + ib), b = lds_word(A, max(cand, 4u) - 4u + ib);
+    const uint32_t x = min(ffbh_raw(a ^ b), 32u) >> 3;   // (v_ffbh_u32: 0xFFFFFFFF for equal words)
+    return cand < 4u ? 0u : x;
+}
+
 // A record: x = pos | cand << 16, y = len | back << 16 (match at pos from cand,
-// len bytes forward, up to `back` bytes of backward extension available).
+// len bytes forward, up to `back` bytes of backward extension available; with
+// `in` given, the back field is not used and the extension comes from the page).
 // The literal run before a record starts at the previous record's end (or the
 // anchor); the catch-up actually taken is min(back, pos - prev_end, cand).
 __device__ __forceinline__ void decode_record(const uint2 *rec, uint32_t n, uint32_t anchor, uint32_t lane,
                                               uint32_t &lit_start, uint32_t &lit_len, uint32_t &match_len,
-                                              uint32_t &offset) {
+                                              uint32_t &offset, const uint8_t *in = nullptr) {
     const bool is_sel = lane < n;
     const uint2 r = rec[is_sel ? lane : 0];
     const uint2 rp = rec[lane > 0 && is_sel ? lane - 1 : 0];
-    const uint32_t pos = r.x & 0xFFFFu, cand = r.x >> 16, len = r.y & 0xFFFFu, back = r.y >> 16;
+    const uint32_t pos = r.x & 0xFFFFu, cand = r.x >> 16, len = r.y & 0xFFFFu;
+    const uint32_t back = in ? back_at(in, pos, cand) : r.y >> 16;
     const uint32_t prev_end = lane == 0 ? anchor : (rp.x & 0xFFFFu) + (rp.y & 0xFFFFu);
     const uint32_t k = min(min(back, pos - prev_end), cand);
     lit_start = prev_end;
@@ -276,6 +290,9 @@ __device__ __forceinline__ uint32_t bucket_of(uint32_t v, uint32_t v2 = 0, uint3
 // below position 4 reads the dword before the page (unused: such positions and candidates take no
 // backward extension), so every caller keeps LDS in front of the page.
 #define TYCHE_LANE_ADDR 1
+#endif
+#ifndef TYCHE_SINK_BACK
+#define TYCHE_SINK_BACK 1   // zstd: backward extension computed by the sinks (decode_record with `in`)
 #endif
 #ifndef TYCHE_HASH_BYTES
 #define TYCHE_HASH_BYTES 5   // kRepCand (zstd): bytes hashed -- zstd level 1 hashes searchLength bytes
@@ -393,6 +410,9 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
         // one hash candidate and nothing else (LZ4): the probe waits until a match is known to
         // start at or after the cursor (kLateProbe), otherwise the candidates compare lengths here
         constexpr bool kLateProbe = kWays == 1 && !kRepCand && !kMin3;
+        // the LZ4 encoder and the zstd encoder (TYCHE_SINK_BACK) take the backward extension in
+        // their sinks; not deflate, whose distance-4 candidate takes none by construction
+        constexpr bool kSinkBack = kLateProbe || (TYCHE_SINK_BACK && kRepCand && !kMin3);
         uint32_t n = kLateProbe ? 0u : probe_len(pw.fw, cw.fw);
         if (kMin3 && cw.w0 != v) n = 3u;
 #pragma unroll
@@ -492,9 +512,9 @@ __device__ inline uint32_t parse_page(const uint8_t *in, uint32_t L, uint16_t *t
             // has cand < pos, so cand < 4 covers pos < 4); v_ffbh_u32 gives 0xFFFFFFFF for equal
             // words (the asm result computed unconditionally: inline asm is never speculated, so
             // inside the select it would become a branch)
-            // (kLateProbe, the LZ4 encoder: its sink computes the extension for the selected matches
-            // only, from the page; the record carries 0)
-            if (!kLateProbe) {
+            // (kSinkBack: the sink computes the extension for the selected matches only, from the
+            // page -- back_at; the record carries 0)
+            if (!kSinkBack) {
                 const uint32_t bx = min(ffbh_raw(pw.back ^ cw.back), 32u) >> 3;
                 back = (TYCHE_EABLATE & 2) || cand < 4 ? 0u : bx;
             }

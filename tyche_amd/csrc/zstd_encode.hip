@@ -727,7 +727,7 @@ __device__ __forceinline__ int32_t encode_page(const uint8_t *in, uint32_t L, ui
     e.logcap = logcap;
     auto sink = [&](const uint2 *r, uint32_t n, uint32_t anchor) -> bool {
         uint32_t ls, ll, ml, off;
-        lzp::decode_record(r, n, anchor, lane, ls, ll, ml, off);
+        lzp::decode_record(r, n, anchor, lane, ls, ll, ml, off, TYCHE_SINK_BACK ? in : nullptr);
         if (lane < n) seq[e.nseq + lane] = make_uint2(ll | (off << 16), ml);
         e.nseq += n;
         const uint2 lastr = r[n - 1];
@@ -766,7 +766,7 @@ static_assert(kZBlk >= kWave && (65536u / 4u + kZBlk - 1u) / kZBlk + 1u <= kMaxB
 // parse(sink) runs the parse over the page and returns its last anchor.
 template <typename Parse>
 __device__ __forceinline__ int32_t parse_to_area_with(uint32_t L, uint8_t *area, uint32_t rec_cap, uint32_t lane,
-                                                      Parse &&parse) {
+                                                      Parse &&parse, const uint8_t *sink_in) {
     uint2 *S = area_seq(area, rec_cap);
     uint32_t nseq = 0, bseq = 0, bstart = 0, cursor = 0, npb = 0;
     auto put_pblk = [&](uint32_t bend) {
@@ -781,7 +781,7 @@ __device__ __forceinline__ int32_t parse_to_area_with(uint32_t L, uint8_t *area,
     };
     auto sink = [&](const uint2 *r, uint32_t n, uint32_t anchor) -> bool {
         uint32_t ls, ll, ml, off;
-        lzp::decode_record(r, n, anchor, lane, ls, ll, ml, off);
+        lzp::decode_record(r, n, anchor, lane, ls, ll, ml, off, sink_in);   // (sink_in: lz_parse.h back_at)
         if (nseq + n > rec_cap) return false;
         if (lane < n) S[nseq + lane] = make_uint2(ll | (off << 16), ml);
         nseq += n;
@@ -805,9 +805,9 @@ __device__ __forceinline__ int32_t parse_to_area_with(uint32_t L, uint8_t *area,
 template <int kW>
 __device__ __forceinline__ int32_t parse_to_area(const uint8_t *in, uint32_t L, uint16_t *table, uint2 *rec,
                                                  uint8_t *area, uint32_t rec_cap, uint32_t lane) {
-    return parse_to_area_with(L, area, rec_cap, lane, [&](auto &sink) {
-        return lzp::parse_page<true, false, kW>(in, L, table, rec, lane, sink);
-    });
+    return parse_to_area_with(
+        L, area, rec_cap, lane, [&](auto &sink) { return lzp::parse_page<true, false, kW>(in, L, table, rec, lane, sink); },
+        TYCHE_SINK_BACK ? in : nullptr);
 }
 
 // Pass A2: frame header and every block of the page from the area (the page
@@ -980,7 +980,7 @@ __global__ __launch_bounds__(128) void zstd_parse_pipe_kernel(tyche_batch_t b, s
             if (wave == 1) {
                 rv = parse_to_area_with(L, ws + page * ws_page, rec_cap, lane, [&](auto &sink) {
                     return lzp::parse_page_piped(in, L, table, rec, slots, &hdr->flag, 1u, lane, sink);
-                });
+                }, nullptr);   // (the piped parse's records carry their extension)
             } else {
                 auto none = [](const uint2 *, uint32_t, uint32_t) -> bool { return true; };
                 (void)lzp::parse_page_piped(in, L, table, rec, slots, &hdr->flag, 0u, lane, none);
@@ -1124,7 +1124,7 @@ __global__ __launch_bounds__(kNW * 64) void zstd_parse_split_kernel(tyche_batch_
             uint32_t nseq = 0;
             auto sink = [&](const uint2 *r, uint32_t n, uint32_t anchor) -> bool {
                 uint32_t ls, ll, ml, off;
-                lzp::decode_record(r, n, anchor, lane, ls, ll, ml, off);
+                lzp::decode_record(r, n, anchor, lane, ls, ll, ml, off, TYCHE_SINK_BACK ? in : nullptr);
                 if (nseq + n > slice) return false;
                 if (lane < n) W[nseq + lane] = make_uint2(ll | (off << 16), ml);
                 nseq += n;
