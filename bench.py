@@ -179,22 +179,42 @@ def e2e_host(pages_dev: torch.Tensor, n: int) -> dict:
     slen = u32(*([plen] * n))
     ccap = u32(*([cap] * n))
     i32p = ctypes.POINTER(ctypes.c_int32)
+    prof = (ctypes.c_uint64 * 8)()
+
+    def stage_clocks():   # the engine's host-stage clocks since the last read (tyche_host_profile)
+        lib.tyche_host_profile(prof, 8)
+        return [int(x) for x in prof]
+    reps = 3
     best_c = best_d = float("inf")
-    for _ in range(3):
+    acc = {"compress": [0] * 8, "decompress": [0] * 8}
+    stage_clocks()
+    for _ in range(reps):
         t0 = time.perf_counter()
         _lib.check(lib.tyche_compress_host(1, 1, n, src_p, slen, comp_p, ccap, res.ctypes.data_as(i32p)),
                    "tyche_compress_host")
         t1 = time.perf_counter()
+        acc["compress"] = [a + b for a, b in zip(acc["compress"], stage_clocks())]
         clen = u32(*[int(x) for x in res])
         _lib.check(lib.tyche_decompress_host(1, n, comp_p, clen, out_p, slen, rv.ctypes.data_as(i32p)),
                    "tyche_decompress_host")
         t2 = time.perf_counter()
+        acc["decompress"] = [a + b for a, b in zip(acc["decompress"], stage_clocks())]
         best_c, best_d = min(best_c, t1 - t0), min(best_d, t2 - t1)
     assert (rv == plen).all() and np.array_equal(out, host), "host-path round trip failed"
     nbytes = n * plen
     res = {"pages": n, "compress_gib_s": round(nbytes / best_c / GIB, 3),
            "decompress_gib_s": round(nbytes / best_d / GIB, 3),
-           "combined_gib_s": round(nbytes / (best_c + best_d) / GIB, 3)}
+           "combined_gib_s": round(nbytes / (best_c + best_d) / GIB, 3),
+           "wall_ms": {"compress": round(best_c * 1e3, 3), "decompress": round(best_d * 1e3, 3)}}
+    # where a call's time goes (engine.hip run_host_batch), ms per call averaged over the reps and summed
+    # over the threads that ran each stage: waiting for a slot's stream (H2D + kernel + D2H not yet
+    # overlapped), scattering results into the callers' buffers, gathering inputs into pinned memory,
+    # enqueuing copies and kernels; plus the bytes gathered / scattered and the chunks per call
+    res["stages_ms_per_call"] = {
+        d: {"wait": round(v[0] / reps / 1e6, 3), "scatter": round(v[1] / reps / 1e6, 3),
+            "gather": round(v[2] / reps / 1e6, 3), "enqueue": round(v[3] / reps / 1e6, 3),
+            "gather_mib": round(v[4] / reps / 2 ** 20, 2), "scatter_mib": round(v[5] / reps / 2 ** 20, 2),
+            "chunks": round(v[6] / reps, 2)} for d, v in acc.items()}
     link = pcie_probe(pages_dev.device, nbytes)
     res["link_probe"] = link
     # the ceiling each direction could reach if only the link moved bytes: compress sends the pages

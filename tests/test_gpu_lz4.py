@@ -101,6 +101,20 @@ def test_decode_malformed_exact_return(tc):
             assert hashlib.sha256(outs[i]).digest() == g["digest"][i].tobytes(), i
 
 
+# device bytes / reference bytes per (page size, distribution), measured (r06_ratio_probe.jsonl);
+# dist 3 is the all-zero page (~50 B per page, a few bytes of which are the excess)
+LZ4_PIN = {(8192, 0): 1.0155, (8192, 1): 1.0226, (8192, 2): 0.9820, (8192, 3): 1.2326, (8192, 4): 1.0000,
+           (8192, 5): 1.0114, (16384, 0): 1.0116, (16384, 1): 1.0296, (16384, 2): 0.9520, (16384, 3): 1.1067,
+           (16384, 4): 1.0000, (16384, 5): 1.0084, (32768, 0): 1.0235, (32768, 1): 1.0411, (32768, 2): 0.9413,
+           (32768, 3): 1.0863, (32768, 4): 1.0000, (32768, 5): 1.0114}
+
+
+def ratio_bound(pins, plen, dist):
+    """Allowed device/reference byte ratio: the pinned measurement + 0.5 % (1.03 or less everywhere
+    but the cases the pin table shows above it)."""
+    return pins[(plen, dist)] + 0.005
+
+
 @pytest.mark.parametrize("dist", [0, 1, 2, 3, 4, 5])
 @pytest.mark.parametrize("plen", [8192, 16384, 32768])
 def test_encode_roundtrip_oracle(tc, oracle_mod, dist, plen):
@@ -123,8 +137,11 @@ def test_encode_roundtrip_oracle(tc, oracle_mod, dist, plen):
         if O.have_ref():
             r2, dec2 = O.ref_lz4_decompress(stream, plen)
             assert r2 == plen and dec2 == host[i].tobytes()
-    # ratio within a few percent of LZ4 1.7.5 on the same pages
-    assert sum(lh) <= 1.10 * sum(ref_sizes) + 64 * n
+    # ratio pinned against LZ4 1.7.5 on the same pages: the measured device/reference bytes + 0.5 %
+    # (<= 1.03 but for 16/32 KiB dist 1 and the all-zero pages, where the device parse's 2^10 hash
+    # slots against the reference's 2^13 cost more), so a 0.5 % ratio regression fails here
+    # (tools/ratio_probe.py, profiles/r06_ratio_probe.jsonl)
+    assert sum(lh) <= ratio_bound(LZ4_PIN, plen, dist) * sum(ref_sizes), (sum(lh), sum(ref_sizes))
 
 
 def _literal_run_pages(n, plen, seed):
@@ -570,7 +587,8 @@ def test_c2_full_size_round_trip(tc):
     assert bool((rv == plen).all())
     assert torch.equal(out, pages)
     ratio = n * plen / float(clen.to(torch.int64).sum())
-    assert 2.55 < ratio < 2.7, ratio
+    # pinned: the bench pages' ratio is 2.6175 (r05/r06 bench lines; LZ4 1.7.5 gets 2.647)
+    assert 2.61 <= ratio < 2.7, ratio
     del pages, comp, out
     torch.cuda.empty_cache()
 

@@ -223,6 +223,15 @@ def _check_zlib_streams(O, comp, clen, host):
     return total
 
 
+# device bytes / reference (zlib 1.2.8 compress2 level 1) bytes per (page size, distribution),
+# measured (tools/ratio_probe.py, profiles/r06_ratio_probe.jsonl).  Above 1 only on dist 2 (a
+# text-like page the device's one dynamic block per page codes worse than deflate_fast's blocks)
+ZLIB_PIN = {(8192, 0): 0.9921, (8192, 1): 0.9632, (8192, 2): 1.2535, (8192, 3): 0.5424, (8192, 4): 1.0000,
+            (8192, 5): 0.9652, (16384, 0): 0.9702, (16384, 1): 0.9591, (16384, 2): 1.2939, (16384, 3): 0.4211,
+            (16384, 4): 1.0000, (16384, 5): 0.9551, (32768, 0): 1.0160, (32768, 1): 0.9608, (32768, 2): 1.2880,
+            (32768, 3): 0.3374, (32768, 4): 0.9998, (32768, 5): 0.9490}
+
+
 @pytest.mark.parametrize("dist", [0, 1, 2, 3, 4, 5])
 @pytest.mark.parametrize("plen", [8192, 16384, 32768])
 def test_deflate_roundtrip_reference(tc, oracle_mod, dist, plen):
@@ -234,9 +243,13 @@ def test_deflate_roundtrip_reference(tc, oracle_mod, dist, plen):
     out, rv = tc.decompress_pages(comp, clen, plen, compressor_id=ZLIB)
     torch.cuda.synchronize()
     assert torch.equal(out, pages) and bool((rv == plen).all())
-    total = _check_zlib_streams(oracle_mod, comp, clen, pages.cpu().numpy())
+    host = pages.cpu().numpy()
+    total = _check_zlib_streams(oracle_mod, comp, clen, host)
     if dist in (0, 1):
         assert total < 0.6 * n * plen
+    if oracle_mod.have_ref():   # ratio pinned within 0.5 % of the measured device/reference bytes
+        ref = sum(len(oracle_mod.ref_zlib_compress(host[i].tobytes())) for i in range(n))
+        assert total <= (ZLIB_PIN[(plen, dist)] + 0.005) * ref, (total, ref)
 
 
 @pytest.mark.parametrize("n", [0, 1, 2, 12, 13, 100, 258, 259, 260, 1000, 4095, 40000, 65535])

@@ -239,11 +239,21 @@ def _check_frames(O, comp, clen, host, plen):
     return int(lh.sum())
 
 
+# device bytes / reference (zstd 1.1.2 level 1) bytes per (page size, distribution), measured with
+# the multi-pass encoder these tests force on every batch (and the bench runs at 1M pages;
+# tools/ratio_probe.py, profiles/r06_ratio_probe.jsonl); dist 3 = all-zero pages (~20 B per frame)
+ZSTD_PIN = {(8192, 0): 1.0076, (8192, 1): 1.0040, (8192, 2): 1.0397, (8192, 3): 1.2105, (8192, 4): 1.0000,
+            (8192, 5): 0.9611, (16384, 0): 1.0009, (16384, 1): 1.0024, (16384, 2): 0.9970, (16384, 3): 1.2105,
+            (16384, 4): 1.0000, (16384, 5): 0.9690, (32768, 0): 1.0022, (32768, 1): 1.0023, (32768, 2): 0.9735,
+            (32768, 3): 1.7895, (32768, 4): 1.0000, (32768, 5): 0.9894}
+
+
 @pytest.mark.parametrize("dist", [0, 1, 2, 3, 4, 5])
 @pytest.mark.parametrize("plen", [8192, 16384, 32768])
-def test_encode_roundtrip_reference_decoder(tc, oracle_mod, dist, plen):
+def test_encode_roundtrip_reference_decoder(tc, oracle_mod, dist, plen, pin=True):
     """Every device-encoded frame decodes with the reference's ZSTD_decompress (oracle/_ref) and
-    the restatement, back to the page; the device decoder round-trips it too."""
+    the restatement, back to the page; the device decoder round-trips it too.  With the default
+    encoder (pin) the frames' bytes stay within 0.5 % of the pinned device/reference ratio."""
     O = oracle_mod
     n = 32
     pages = tc.pagegen(n, plen, seed=777, first=plen + dist * 100, dist=dist, device=DEV)
@@ -251,9 +261,13 @@ def test_encode_roundtrip_reference_decoder(tc, oracle_mod, dist, plen):
     out, rv = tc.decompress_pages(comp, clen, plen, compressor_id=ZSTD)
     torch.cuda.synchronize()
     assert torch.equal(out, pages) and bool((rv == plen).all())
-    total = _check_frames(O, comp, clen, pages.cpu().numpy(), plen)
+    host = pages.cpu().numpy()
+    total = _check_frames(O, comp, clen, host, plen)
     if dist in (0, 1):   # compressible database pages: the frame is well below the page
         assert total < 0.6 * n * plen
+    if pin and O.have_ref():
+        ref = sum(len(O.ref_zstd_compress(host[i].tobytes())) for i in range(n))
+        assert total <= (ZSTD_PIN[(plen, dist)] + 0.005) * ref, (total, ref)
 
 
 @pytest.mark.parametrize("n", [0, 1, 5, 12, 13, 64, 255, 256, 300, 4095, 65535])
@@ -697,7 +711,7 @@ def test_zstd_encode_fused_kernel_and_chunked_split(tc, oracle_mod, knobs, mode)
     knobs(**ENCODE_MODES[mode])
     for dist in (0, 3):
         for plen in (8192, 32768):
-            test_encode_roundtrip_reference_decoder(tc, oracle_mod, dist, plen)
+            test_encode_roundtrip_reference_decoder(tc, oracle_mod, dist, plen, pin=False)
     test_encode_multiblock_and_incompressible(tc, oracle_mod)
     test_encode_tight_capacity(tc, oracle_mod, 16)
 
@@ -714,6 +728,7 @@ def test_c3_full_size_round_trip(tc):
     assert bool((rv == plen).all())
     assert torch.equal(out, pages)
     ratio = n * plen / float(clen.to(torch.int64).sum())
-    assert ratio > 4.8, ratio
+    # pinned: 4.921 on the bench pages (r05 bench line; zstd 1.1.2 level 1 gets 4.915)
+    assert ratio > 4.91, ratio
     del pages, comp, out
     torch.cuda.empty_cache()

@@ -30,8 +30,11 @@ for _ in range(3):
     c0.record(); codec.compress_pages(pages, out=comp, out_len=clen); c1.record()
     torch.cuda.synchronize(); bc = min(bc, c0.elapsed_time(c1))
 ratio = n * plen / float(clen.to(torch.int64).sum())
+import hashlib
+ch, lh = comp[:2048].cpu().numpy(), clen[:2048].cpu().numpy()
+dig = hashlib.sha1(b"".join(ch[i, :lh[i]].tobytes() for i in range(len(lh)))).hexdigest()[:12]
 print(f"{os.environ['TYCHE_CODEC_LIB']}: max_comp {mx} ratio {ratio:.4f} decode {best * (1 << 20) / n:8.2f} ms/1M pages  "
-      f"({n * plen / best / 1e6 / 1.073741824:7.1f} GiB/s)  encode {bc * (1 << 20) / n:8.2f} ms/1M  correct={ok}")
+      f"({n * plen / best / 1e6 / 1.073741824:7.1f} GiB/s)  encode {bc * (1 << 20) / n:8.2f} ms/1M  correct={ok}  streams {dig}")
 '''
 
 

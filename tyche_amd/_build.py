@@ -26,7 +26,7 @@ FLAGS = ["--offload-arch=" + ARCH, "-O3", "-fPIC", "-std=c++17", "-Wall", "-Wno-
 # Without it, pairs still become ds_read2_b32 (4-byte alignment suffices).
 # superseded large-batch LZ4 decoders (round-2/3 lane kernels, the round-4 quad kernel): only in the
 # A/B build, libtyche_codec_legacy_decoders.so (build(legacy=True)), never in the product library
-LEGACY_SOURCES = ["lz4_decode_quad.hip"]
+LEGACY_SOURCES = ["legacy/lz4_decode_lane_legacy.hip", "legacy/lz4_decode_quad.hip"]
 NO_LSV = ["-mllvm", "-amdgpu-load-store-vectorizer=false"]
 SOURCE_FLAGS = {"lz4_encode.hip": NO_LSV, "zstd_encode.hip": NO_LSV, "zlib_deflate.hip": NO_LSV, "zstd_decode.hip": NO_LSV}
 
@@ -65,14 +65,14 @@ def build(force: bool = False, verbose: bool = False, profile: bool = False, abl
     flags = FLAGS + (["-DTYCHE_PROFILE"] if profile else []) + ([f"-DTYCHE_ABLATE={ablate}"] if ablate else []) + \
         ([f"-DTYCHE_EABLATE={eablate}"] if eablate else []) + ["-D" + d for d in defines]
     os.makedirs(build_dir, exist_ok=True)
-    headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+    headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]   # (legacy/ has none)
     headers.append(os.path.join(HERE, "..", "include", "tyche_codec.h"))
     objs = []
     jobs = []
     sources = SOURCES[:-1] + (LEGACY_SOURCES if legacy else []) + SOURCES[-1:]   # errno_guard stays last
     for src in sources:
         s = os.path.join(CSRC, src)
-        o = os.path.join(build_dir, src.replace(".hip", ".o"))
+        o = os.path.join(build_dir, src.replace("/", "_").replace(".hip", ".o"))
         objs.append(o)
         if force or not _newer(o, [s] + headers):
             jobs.append([HIPCC] + flags + SOURCE_FLAGS.get(src, []) + ["-c", s, "-o", o])

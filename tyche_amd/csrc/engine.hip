@@ -342,6 +342,20 @@ long tyche::knob(const char *name, long dflt) {
 }
 
 namespace {
+// Diagnostic builds only (-DTYCHE_PROFILE, libtyche_codec_prof.so): TYCHE_HOST_DIAG bit 0 makes the
+// host batch report the results without copying the page bytes out (prices the scatter copies).  The
+// product library has no such switch, so a stray setting can never report success without the data
+// (ADVICE r05).
+bool host_diag_no_copy() {
+#ifdef TYCHE_PROFILE
+    return (tyche::knob("HOST_DIAG", 0) & 1) != 0;
+#else
+    return false;
+#endif
+}
+}  // namespace
+
+namespace {
 
 // -1: the host API spreads work over every usable device (the default);
 // >= 0: tyche_set_device pinned the calling thread to that device
@@ -860,7 +874,7 @@ int run_host_batch(int dev, size_t n, const void *const *src, const uint32_t *sr
         const uint8_t *hout = (const uint8_t *)S.h_out.p;
         const size_t f0 = S.first;
         std::atomic<uint64_t> moved{0};
-        const bool no_copy = (knob("HOST_DIAG", 0) & 1) != 0;   // diagnostic: results only, no page bytes
+        const bool no_copy = host_diag_no_copy();
         pool.run(k, [&](size_t j) {
             const int32_t r = m_res[j];
             results[f0 + j] = r;
@@ -984,7 +998,7 @@ int run_host_batch(int dev, size_t n, const void *const *src, const uint32_t *sr
         const uint8_t *hout = (const uint8_t *)S.h_out.p;
         const size_t f0 = S.first;
         std::atomic<uint64_t> moved{0};
-        const bool no_copy = (knob("HOST_DIAG", 0) & 1) != 0;   // diagnostic: results only, no page bytes
+        const bool no_copy = host_diag_no_copy();
         pool.run(k, [&](size_t j) {
             const int32_t r = m_res[j];
             results[f0 + j] = r;
@@ -1683,23 +1697,30 @@ constexpr int kQueueHistBuckets = 11;
 // A restorer waits on its own request word (spin briefly, then futex), so a finished batch wakes
 // exactly its callers -- a shared condition variable woke every blocked restorer (64 in the C5
 // cycle) to re-take the queue mutex and find its request still pending.
+// A request lives on its caller's stack; the futex word it is woken through does not: it is the
+// caller's thread_local word (reset on entry), so the FUTEX_WAKE that follows the store -- which
+// the waiter may already have seen and returned on -- still lands on a live word of that thread,
+// never on a reused stack frame.  A wake that finds no waiter is a no-op, and every
+// waiter re-checks its word in a loop, so a late wake is harmless.
 struct RestoreReq {
     Buffer *buf;
     int status;
-    std::atomic<int> done{0};
+    std::atomic<int> *done;
     void wait() {
         for (int i = 0; i < 64; i++) {   // (a batch takes ~0.1 ms: spinning longer only takes CPU from the others)
-            if (done.load(std::memory_order_acquire)) return;
+            if (done->load(std::memory_order_acquire)) return;
             _mm_pause();
         }
-        while (!done.load(std::memory_order_acquire))
-            syscall(SYS_futex, (int *)&done, FUTEX_WAIT_PRIVATE, 0, nullptr, nullptr, 0);
+        while (!done->load(std::memory_order_acquire))
+            syscall(SYS_futex, (int *)done, FUTEX_WAIT_PRIVATE, 0, nullptr, nullptr, 0);
     }
     void wake() {
-        done.store(1, std::memory_order_release);
-        syscall(SYS_futex, (int *)&done, FUTEX_WAKE_PRIVATE, 1, nullptr, nullptr, 0);
+        std::atomic<int> *w = done;   // read before the store: the request may be gone after it
+        w->store(1, std::memory_order_release);
+        syscall(SYS_futex, (int *)w, FUTEX_WAKE_PRIVATE, 1, nullptr, nullptr, 0);
     }
 };
+thread_local std::atomic<int> t_restore_word{0};
 struct RestoreQueue {
     std::mutex mu;
     std::condition_variable cv;
@@ -1796,6 +1817,8 @@ int tyche_buffer_restore(Buffer *buf, int compressor_id) {
     RestoreReq r;
     r.buf = buf;
     r.status = TYCHE_E_OK;
+    t_restore_word.store(0, std::memory_order_relaxed);
+    r.done = &t_restore_word;
     {
         std::unique_lock<std::mutex> g(g_rq.mu);
         if (!g_rq.running || g_rq.stop) {

@@ -27,30 +27,14 @@ __device__ __forceinline__ u128 ld16(const uint8_t *p) {
     u32x4 v = *(const g_u32x4_ua *)(uintptr_t)p;
     return __builtin_bit_cast(u128, v);
 }
-// Cache-policy experiments (-DTYCHE_ABLATE, tools/time_decode.py over
-// libtyche_codec_ablN.so; LZ4 lane decoder only): 16 = non-temporal stream loads,
-// 32 = non-temporal line flushes, 128 = no line flushes, 256 = parse only,
-// 512 = ring LDS accesses forced to 16-byte alignment (wrong output, the parse is untouched: prices
-// the per-lane replays of byte-unaligned ds_read/ds_write_b128).
-#ifndef TYCHE_ABLATE
-#define TYCHE_ABLATE 0
-#endif
-__device__ __forceinline__ u128 ld16s(const uint8_t *p) {
-    if (TYCHE_ABLATE & 16) return __builtin_bit_cast(u128, __builtin_nontemporal_load((const g_u32x4_ua *)(uintptr_t)p));
-    return ld16(p);
-}
+// (round-1/2 cache-policy experiments on the lane decoder, r01-r02 logs: non-temporal stream
+// loads and line flushes were slower; the default policy stays)
+__device__ __forceinline__ u128 ld16s(const uint8_t *p) { return ld16(p); }
 __device__ __forceinline__ uint64_t ld8(const uint8_t *p) { return *(const g_u64_ua *)(uintptr_t)p; }
 __device__ __forceinline__ void st16(uint8_t *p, u128 v) {
     *(g_u32x4_ua *)(uintptr_t)p = __builtin_bit_cast(u32x4, v);
 }
-__device__ __forceinline__ void st16f(uint8_t *p, u128 v) {
-    if (TYCHE_ABLATE & (128 | 256)) return;
-    if (TYCHE_ABLATE & 32) {
-        __builtin_nontemporal_store(__builtin_bit_cast(u32x4, v), (g_u32x4_ua *)(uintptr_t)p);
-        return;
-    }
-    st16(p, v);
-}
+__device__ __forceinline__ void st16f(uint8_t *p, u128 v) { st16(p, v); }
 __device__ __forceinline__ uint32_t ld1(const uint8_t *p) { return *(const g_u8 *)(uintptr_t)p; }
 __device__ __forceinline__ void st1(uint8_t *p, uint32_t v) { *(g_u8 *)(uintptr_t)p = (uint8_t)v; }
 
@@ -74,14 +58,11 @@ __device__ __forceinline__ void lds16(uint8_t *p, u128 v) {
 // the ring's end mirror its first 16)
 template <int32_t kRing>
 __device__ __forceinline__ u128 ring_rd(uint8_t *rb, int32_t x) {
-    if (TYCHE_ABLATE & 512) return lds16(rb + ((int32_t)((uint32_t)x % (uint32_t)kRing) & ~15));   // timing only: aligned
     return lds16(rb + ((int32_t)((uint32_t)x % (uint32_t)kRing)));
 }
 template <int32_t kRing>
 __device__ __forceinline__ void ring_wr(uint8_t *rb, int32_t x, u128 v) {
-    if (TYCHE_ABLATE & 256) return;
-    int32_t q = (int32_t)((uint32_t)x % (uint32_t)kRing);
-    if (TYCHE_ABLATE & 512) q &= ~15;   // timing only: 16-byte aligned LDS stores (wrong output)
+    const int32_t q = (int32_t)((uint32_t)x % (uint32_t)kRing);
     lds16(rb + q, v);
     if (q + 16 > kRing) lds16(rb + q - kRing, v);   // wrapped part, to the ring's start
     if (q < 16) lds16(rb + q + kRing, v);           // mirror of the start, past the end

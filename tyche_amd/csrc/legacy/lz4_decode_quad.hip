@@ -45,10 +45,10 @@
 // decoders); on error the page's destination holds partial output.
 #include <hip/hip_runtime.h>
 
-#include "engine.h"
-#include "lane_ring.h"
-#include "lds_io.h"
-#include "lds_qword.h"
+#include "../engine.h"
+#include "../lane_ring.h"
+#include "../lds_io.h"
+#include "../lds_qword.h"
 
 namespace tyche {
 

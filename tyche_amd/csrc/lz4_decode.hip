@@ -1057,11 +1057,21 @@ __device__ __forceinline__ void jump_scan(uint16_t *cells, uint32_t n64, uint32_
     }
 }
 
-// one round's update of 2 cells packed in a dword; `open` gathers the cells still unresolved afterwards
+// one round's update of 2 cells packed in a dword; `open` gathers the cells still unresolved afterwards.
+// kRacy: the barrier-free rounds of the single-page decoder, where other threads rewrite the cells
+// being read -- volatile loads, so that no compiler may cache, merge or move them (the hardware
+// returns the old or the new value, and the algorithm accepts either: ADVICE r05)
+template <bool kRacy = false>
 __device__ __forceinline__ uint32_t jump_pair(const uint16_t *cells, uint32_t w, uint32_t &open) {
     uint32_t lo = w & 0xFFFFu, hi = w >> 16;
-    if (!(lo & kLitFlag)) lo = cells[lo];
-    if (!(hi & kLitFlag)) hi = cells[hi];
+    if constexpr (kRacy) {
+        const volatile uint16_t *vc = cells;
+        if (!(lo & kLitFlag)) lo = vc[lo];
+        if (!(hi & kLitFlag)) hi = vc[hi];
+    } else {
+        if (!(lo & kLitFlag)) lo = cells[lo];
+        if (!(hi & kLitFlag)) hi = cells[hi];
+    }
     open |= ~(lo & hi) & kLitFlag;
     return lo | (hi << 16);
 }
@@ -1703,10 +1713,10 @@ __global__ __launch_bounds__(kT) void lz4_decode_solo_kernel(tyche_batch_t b, ui
                 for (uint32_t i = 0; i < kSoloGroups; i++) {
                     u32x4 v = cv[i];
                     if (((v.x & v.y & v.z & v.w) & 0x80008000u) != 0x80008000u) {
-                        v.x = jump_pair(cells, v.x, open);
-                        v.y = jump_pair(cells, v.y, open);
-                        v.z = jump_pair(cells, v.z, open);
-                        v.w = jump_pair(cells, v.w, open);
+                        v.x = jump_pair<true>(cells, v.x, open);
+                        v.y = jump_pair<true>(cells, v.y, open);
+                        v.z = jump_pair<true>(cells, v.z, open);
+                        v.w = jump_pair<true>(cells, v.w, open);
                         c4[tid + i * kT] = v;
                         cv[i] = v;
                     }

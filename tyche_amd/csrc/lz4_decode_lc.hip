@@ -45,6 +45,15 @@
 
 namespace tyche {
 
+// Timing-only ablation builds (-DTYCHE_ABLATE=mask: _build.build(ablate=mask), tools/time_variant.py;
+// their outputs are wrong, the product build has mask 0 and none of these branches):
+//   1024 no far loads | 2048 no flush stores | 4096 no copy stage | 8192 four extra window loads per chunk
+#if defined(TYCHE_ABLATE) && TYCHE_ABLATE
+#define LC_ABLATE(bit) ((TYCHE_ABLATE & (bit)) != 0)
+#else
+#define LC_ABLATE(bit) false
+#endif
+
 // Optional stage profile (diagnostic build only: -DTYCHE_PROFILE, tools/lc_profile.py):
 // shader cycles per stage and event counts, summed per wave in scalar registers and added to
 // g_lcprof once when the wave ends (an atomic per stamp would itself sit in vmcnt and be
@@ -224,7 +233,7 @@ __device__ __attribute__((aligned(64))) uint8_t g_lc_pad[64];
 // branch is joined by a copy that waits for it right there, in the next slot); the compiler
 // does not see them, and lc_far_wait waits for them before stage 3.
 __device__ __forceinline__ void far_load(const LPage &P, bool far, int32_t src, uint32_t rec, u32x4 &f0, u32x4 &f1) {
-    if (TYCHE_ABLATE & 1024) far = false;   // timing only: no far loads (wrong output)
+    if (LC_ABLATE(1024)) far = false;
     if (far) {
         const uint8_t *a = P.out + src;
         asm volatile("global_load_dwordx4 %0, %1, off" : "+v"(f0) : "v"(a) : "memory");
@@ -348,12 +357,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LC_WPE))) vo
         LPROF_MARK(5);   // window issue
         // ---- stage 3: copy the records into the ring (aligned qwords only)
         lc_far_wait(fv);
-        if (TYCHE_ABLATE & 8192) {   // timing only: four more window-sized loads per chunk, waited for
+        if (LC_ABLATE(8192)) {
             const LWin xw = wload(wlive ? P.in : g_lc_pad, wlive ? min(nwb + 64, max(P.L - 64, 0)) : 0, wlive ? P.L : 64);
             __builtin_amdgcn_s_waitcnt(kVmDrain);
             if (xw.c0 == (u128)0x123457 && xw.c3 == (u128)1) P.tail ^= 1;
         }
-        if (live && !(TYCHE_ABLATE & 4096)) {   // (4096, timing only: no copy stage)
+        if (live && !LC_ABLATE(4096)) {
             u128 farv[2 * kLC + 2];
 #pragma unroll
             for (int32_t i = 0; i < 2 * kLC + 2; i++) farv[i] = __builtin_bit_cast(u128, fv[i]);
@@ -412,8 +421,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LC_WPE))) vo
             for (int32_t it = 0; it < MP; it++) {
                 if ((int32_t)lane + 64 * it < total) {
                     uint8_t *dst = (uint8_t *)(uintptr_t)o[it] + f[it];
-                    if (!(TYCHE_ABLATE & 2048)) st16f(dst, v[it]);
-                    else if (v[it] == (u128)0x1234567) dst[0] = 1;   // timing only: keeps the LDS read
+                    if (!LC_ABLATE(2048)) st16f(dst, v[it]);
+                    else if (v[it] == (u128)0x1234567) dst[0] = 1;   // (keeps the LDS read)
                 }
             }
             asm volatile("" ::: "memory");

@@ -224,13 +224,13 @@ LC_FN int32_t parse_fast(LPage &P, const uint8_t *w16, int32_t op0, uint32_t &re
                          uint64_t (&q)[4]) {
     const int32_t room = op0 + lc_budget<R>() - P.op;   // output bytes the chunk can still take
     // a: the next part of a match
-    const bool isA = P.mrem != 0 && P.lrem == 0;   // (a budget cut can leave a header read before its run's last bytes)
+    const bool isA = (P.mrem != 0) & (P.lrem == 0);   // (a budget cut can leave a header read before its run's last bytes)
     const int32_t nA = min(P.mrem, 32);
     // b: the next part of a literal run that goes on after it
     const int32_t nB = min(min(P.lrem, 15), P.wb + kLW - P.lp);
-    const bool isB = P.lrem != 0 && nB < P.lrem;   // nB <= 0: the run continues past the window
+    const bool isB = (P.lrem != 0) & (nB < P.lrem);   // nB <= 0: the run continues past the window
     // c: a new sequence
-    const bool fresh = P.lrem == 0 && P.mrem == 0 && P.hdr == 0;
+    const bool fresh = (P.lrem == 0) & (P.mrem == 0) & (P.hdr == 0);
     const int32_t x = fresh ? P.ip - P.wb : 0;   // 0 <= x <= kLW at a token (the window starts at or before it)
     const uint64_t q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
     const uint32_t s = (uint32_t)x & 7u;
@@ -243,41 +243,37 @@ LC_FN int32_t parse_fast(LPage &P, const uint8_t *w16, int32_t op0, uint32_t &re
     const uint64_t h = win8(q0, q1, q2, q3, s + 1u + (uint32_t)(lit & 15));   // lit < 15 below: s + 1 + lit <= 22
     const int32_t off = (int32_t)(h & 0xFFFFu), ext = (int32_t)((h >> 16) & 0xFFu);
     const int32_t ml = mn == 15 ? 19 + ext : mn + kMinMatch;
+    // Every condition below is combined with bitwise & / | on bools and every update is a select:
+    // short-circuit && / if chains compile to exec-mask branches (s_and_saveexec / s_cbranch_execz
+    // per term) that all 64 lanes walk anyway, since some lane almost always takes each side.
     const bool fitC = x + need <= kLW;
-    const bool okC = lit != 15 && !(mn == 15 && ext == 255) &&
-                     P.op + lit <= P.C - kMfLimit && P.ip + 1 + lit <= P.L - 8 &&   // not the last run (lz4.c:1147)
-                     off <= P.op + lit &&                                             // lz4.c:1168
-                     !(mn == 15 && P.ip + need > P.L - kLastLiterals) &&              // lz4.c:1176
-                     P.op + lit + ml <= P.C - kLastLiterals &&                        // lz4.c:1225
-                     ml <= 32;
+    const bool okC = (lit != 15) & !((mn == 15) & (ext == 255)) &
+                     (P.op + lit <= P.C - kMfLimit) & (P.ip + 1 + lit <= P.L - 8) &   // not the last run (lz4.c:1147)
+                     (off <= P.op + lit) &                                              // lz4.c:1168
+                     !((mn == 15) & (P.ip + need > P.L - kLastLiterals)) &              // lz4.c:1176
+                     (P.op + lit + ml <= P.C - kLastLiterals) &                         // lz4.c:1225
+                     (ml <= 32);
     const int32_t n1 = isA ? 0 : (isB ? nB : lit);
     const int32_t n2 = isA ? nA : (isB ? 0 : ml);
-    int32_t k;
-    if (isA || isB)
-        k = n1 + n2 <= room ? 1 : 0;
-    else if (P.lrem != 0 && nB <= 0)
-        k = 0;
-    else if (fresh && !fitC)
-        k = 0;
-    else if (fresh && okC)
-        k = n1 + n2 <= room ? 1 : 0;
-    else
-        k = 2;
-    if (k == 1) {
-        const int32_t moff = isA ? P.moff : off;
-        far = n2 > 0 && moff > lc_near<R>();
-        src = P.op + n1 - moff;
-        rec = lc_rec(n1 > 0 ? (isB ? P.lp - P.wb : x + 1) : 0, n1, n2, moff);
-        P.op += n1 + n2;
-        if (isA) P.mrem -= n2;
-        if (isB) {
-            P.lp += n1;
-            P.lrem -= n1;
-        }
-        if (fresh) P.ip += need;
-    }
+    const bool fits = n1 + n2 <= room;
+    // k: 1 the record is emitted; 0 the chunk stops here (window or budget); 2 the general path
+    const bool cont = isA | isB;
+    const bool stop = !cont & (((P.lrem != 0) & (nB <= 0)) | (fresh & !fitC));
+    const bool fast = cont | (fresh & okC);
+    const int32_t k = stop ? 0 : (fast ? (fits ? 1 : 0) : 2);
+    const bool emit = (k == 1);
+    const int32_t moff = isA ? P.moff : off;
+    far = emit & (n2 > 0) & (moff > lc_near<R>());
+    src = emit ? P.op + n1 - moff : src;
+    rec = emit ? lc_rec(n1 > 0 ? (isB ? P.lp - P.wb : x + 1) : 0, n1, n2, moff) : rec;
+    P.op += emit ? n1 + n2 : 0;
+    P.mrem -= (emit & isA) ? n2 : 0;
+    P.lp += (emit & isB) ? n1 : 0;
+    P.lrem -= (emit & isB) ? n1 : 0;
+    P.ip += (emit & fresh) ? need : 0;
     return k;
 }
+
 
 // byte p of the stream: from the window when it lies there, else (only when
 // `deep`, the chunk's first record: an extension run longer than the window)

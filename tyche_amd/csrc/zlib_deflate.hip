@@ -41,6 +41,11 @@
 #ifndef TYCHE_ZLIB_MIN3
 #define TYCHE_ZLIB_MIN3 1
 #endif
+// The sinks' page pointer for decode_record: the parse leaves the backward extension to its sinks
+// (lz_parse.h kSinkBack) without 3-byte matches -- one-way, or repeat candidates -- so A/B builds of
+// those (TYCHE_ZLIB_MIN3=0 with TYCHE_ZLIB_WAYS=1 or TYCHE_ZLIB_REP=1) hand the page over and keep
+// the catch-up; the default parse keeps the extension in its records
+#define ZLIB_SINK_IN(in) ((!TYCHE_ZLIB_MIN3 && ((TYCHE_ZLIB_WAYS == 1 && !TYCHE_ZLIB_REP) || (TYCHE_SINK_BACK && TYCHE_ZLIB_REP))) ? (in) : nullptr)
 #ifndef TYCHE_ZLIB_WAYS
 #define TYCHE_ZLIB_WAYS 8   // candidates per hash bucket (lz_parse.h kWays; 4 before round 3)
 #endif
@@ -284,7 +289,7 @@ __device__ int32_t encode_fixed1(const uint8_t *in, uint32_t L, uint32_t adler, 
     if (ok) {
         auto sink = [&](const uint2 *r, uint32_t n, uint32_t anc) -> bool {
             uint32_t ls, ll, ml, off;
-            lzp::decode_record(r, n, anc, lane, ls, ll, ml, off);
+            lzp::decode_record(r, n, anc, lane, ls, ll, ml, off, ZLIB_SINK_IN(in));
             if (off > 32768u) { ll += ml; ml = 0; }     // beyond the deflate window: literals
             return code_runs(o, in, n, ls, ll, ml, off, map, lane);
         };
@@ -376,7 +381,7 @@ __device__ int32_t encode_page(const uint8_t *in, uint32_t L, uint16_t *table, u
     auto sink = [&](const uint2 *r, uint32_t n, uint32_t anc) -> bool {
         if (nrec + n > room) return false;
         uint32_t ls, ll, ml, off;
-        lzp::decode_record(r, n, anc, lane, ls, ll, ml, off);
+        lzp::decode_record(r, n, anc, lane, ls, ll, ml, off, ZLIB_SINK_IN(in));
         if (off > 32768u) { ll += ml; ml = 0; off = 1; }     // beyond the deflate window: literals
         if (lane < n) recs[-1 - (int32_t)(nrec + lane)] = make_uint2(ls | (ll << 16), ml | (off << 16));
         nrec += n;
