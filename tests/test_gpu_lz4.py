@@ -368,9 +368,9 @@ def test_decode_lane_path_fixtures(tc, target):
             assert hashlib.sha256(outs[j]).digest() == want_dig[i], (j, i)
 
 
-@pytest.mark.parametrize("ring", [128, 192, 256])
+@pytest.mark.parametrize("ring", [128, 160, 192, 256])
 def test_decode_lc_kernel_variants(tc, oracle_mod, knobs, ring):
-    """The chunked lane-per-page decoder (lz4_decode_lc.hip) at both ring sizes, forced on every
+    """The chunked lane-per-page decoder (lz4_decode_lc.hip) at every ring size, forced on every
     batch size (LZ4_LC=1, LZ4_LANE_MIN=0): the fixtures with their exact return values, seeded
     corruptions against the restated LZ4_decompress_safe, and the page kinds that exercise its
     split records (incompressible pages: literal runs longer than a window; zero and short-period

@@ -19,12 +19,17 @@ SRC = os.path.join(ROOT, "tools", "lc_emul.cpp")
 CORE = [os.path.join(ROOT, "tyche_amd", "csrc", f) for f in ("lz4_lc_core.h", "byte_funnel.h")]
 
 
-@pytest.fixture(scope="module")
-def emul():
-    if not os.path.exists(LIB) or any(os.path.getmtime(f) > os.path.getmtime(LIB) for f in [SRC] + CORE):
-        os.makedirs(os.path.dirname(LIB), exist_ok=True)
-        subprocess.check_call(["g++", "-O2", "-shared", "-fPIC", "-o", LIB, SRC])
-    lib = ctypes.CDLL(LIB)
+@pytest.fixture(scope="module", params=[0, 1], ids=["far32", "far16"])
+def emul(request):
+    """The emulator built as each kernel build is: far match parts of up to 32 bytes (two far
+    registers per record slot) or, LC_FAR16=1 (the default), of up to 16 bytes (one register;
+    longer far matches continue in the next record)."""
+    far16 = request.param
+    lib_path = LIB.replace(".so", "_f%d.so" % far16)
+    if not os.path.exists(lib_path) or any(os.path.getmtime(f) > os.path.getmtime(lib_path) for f in [SRC] + CORE):
+        os.makedirs(os.path.dirname(lib_path), exist_ok=True)
+        subprocess.check_call(["g++", "-O2", "-shared", "-fPIC", "-DLC_FAR16=%d" % far16, "-o", lib_path, SRC])
+    lib = ctypes.CDLL(lib_path)
 
     def dec(s, cap, ring):
         buf = (ctypes.c_uint8 * max(len(s), 1)).from_buffer_copy(s if s else b"\0")
@@ -71,7 +76,7 @@ def _cases(O):
     return cases
 
 
-@pytest.mark.parametrize("ring", [128, 192, 256])
+@pytest.mark.parametrize("ring", [128, 160, 192, 256])
 def test_lc_algorithm_vs_oracle(emul, oracle_mod, ring):
     for k, (s, cap, defined) in enumerate(_cases(oracle_mod)):
         r, out = emul(s, cap, ring)

@@ -66,6 +66,14 @@ static inline u128 chunk16z(const uint8_t *in, int32_t a, int32_t L) {
 #include "../tyche_amd/csrc/byte_funnel.h"
 #include "../tyche_amd/csrc/lz4_lc_core.h"
 
+// the window at nwb (the kernel's wload / wstore)
+static void wfill(uint8_t *w16, const uint8_t *in, int32_t L, int32_t nwb) {
+    for (int32_t k = 0; k < kLW; k += 16) {
+        const u128 v = chunk16z(in, nwb + k, L);
+        memcpy(w16 + k, &v, 16);
+    }
+}
+
 // a far match part's source: its n2 used bytes must be in HBM already (lc_budget); the
 // kernel's loads may run past them (bytes it does not use), the emulator's stop there
 static void fetch_far(const LPage &P, uint32_t rec, int32_t src, u128 *f) {
@@ -77,7 +85,7 @@ static void fetch_far(const LPage &P, uint32_t rec, int32_t src, u128 *f) {
     uint8_t b[32] = {0};
     memcpy(b, P.out + src, (size_t)n2);
     f[0] = ld16(b);
-    f[1] = n2 > 16 ? ld16(b + 16) : 0;
+    if (kFarPer == 2) f[1] = n2 > 16 ? ld16(b + 16) : 0;
 }
 
 static uint32_t g_lut[17 * kLutStride];
@@ -91,7 +99,7 @@ static int lc_decode(const uint8_t *in, int32_t L, uint8_t *out, int32_t C) {
     if (C == 0) return (L == 1 && in[0] == 0) ? 0 : -1;
     if (L <= 0) return -1;
     alignas(16) uint8_t ring[R];
-    alignas(16) uint8_t win[kLWS + 64];   // reads run up to 32 bytes past the window's end
+    alignas(16) uint8_t win[kLWS + 64];   // reads run up to 32 bytes past the window's (mirror) rows
     uint8_t *w16 = win + 16;
     memset(ring, 0xA5, sizeof(ring));
     memset(win, 0x5A, sizeof(win));
@@ -101,29 +109,26 @@ static int lc_decode(const uint8_t *in, int32_t L, uint8_t *out, int32_t C) {
     P.out = out;
     P.L = L;
     P.C = C;
-    for (int32_t k = 0; k < kLW; k += 16) {
-        const u128 v = chunk16z(in, k, L);
-        memcpy(w16 + k, &v, 16);
-    }
+    wfill(w16, in, L, 0);
     for (long chunk = 0; chunk < 100000000; chunk++) {
         const int32_t op0 = P.op;
         int32_t st = kLParse, rv = 0, nrec = 0;
         uint32_t rec[kLC + 1];
-        u128 farv[2 * kLC + 2];
+        u128 farv[2 * kLC + 2];   // (kFarPer per slot are used)
         bool go = true, gen = false;
         uint64_t wq[4];
         lc_wread(w16, lc_x0(P), wq);
         int32_t need_gen = 0;
         for (int32_t t = 0; t < kLC; t++) {
             rec[t] = 0;
-            farv[2 * t] = farv[2 * t + 1] = 0;
+            farv[kFarPer * t] = farv[kFarPer * t + kFarPer - 1] = 0;
             if (go) {
                 bool far = false;
                 int32_t src = 0;
                 const int32_t k = getenv("LC_SLOW") ? 2 : parse_fast<R>(P, w16, op0, rec[t], far, src, wq);
                 if (k == 1) {
                     nrec = t + 1;
-                    if (far) fetch_far(P, rec[t], src, farv + 2 * t);
+                    if (far) fetch_far(P, rec[t], src, farv + kFarPer * t);
                 } else {
                     go = false;
                     need_gen = (k == 2 || t == 0) ? 1 : 0;
@@ -132,7 +137,7 @@ static int lc_decode(const uint8_t *in, int32_t L, uint8_t *out, int32_t C) {
             }
         }
         rec[kLC] = 0;
-        farv[2 * kLC] = farv[2 * kLC + 1] = 0;
+        farv[kFarPer * kLC] = farv[kFarPer * kLC + kFarPer - 1] = 0;
         if (need_gen) {
             bool far = false;
             int32_t src = 0;
@@ -141,7 +146,7 @@ static int lc_decode(const uint8_t *in, int32_t L, uint8_t *out, int32_t C) {
                 st = kLParse;
                 gen = parse_slot<R>(P, w16, op0, true, st, rv, rec[kLC], far, src);
             }
-            if (gen && far) fetch_far(P, rec[kLC], src, farv + 2 * kLC);
+            if (gen && far) fetch_far(P, rec[kLC], src, farv + kFarPer * kLC);
         }
         const bool ended = st == kLEnd;
         const int32_t nwb = (P.lrem > 0 ? P.lp : P.ip) & ~15;
@@ -174,11 +179,8 @@ static int lc_decode(const uint8_t *in, int32_t L, uint8_t *out, int32_t C) {
                 for (int32_t a = P.fl; a < P.op; a++) out[a] = ring[8 * lc_row<R>(a >> 3) + (a & 7)];
             return rv;
         }
+        wfill(w16, in, L, nwb);
         P.wb = nwb;
-        for (int32_t k = 0; k < kLW; k += 16) {
-            const u128 v = chunk16z(in, nwb + k, L);
-            memcpy(w16 + k, &v, 16);
-        }
     }
     fprintf(stderr, "lc_emul: no end\n");
     abort();
@@ -188,5 +190,8 @@ extern "C" int lc_emul_decode(const uint8_t *in, int L, uint8_t *out, int C, int
 #if LC_LINE == 64
     if (R == 128) R = 192;   // (64-byte lines need R >= 192)
 #endif
-    return R == 256 ? lc_decode<256>(in, L, out, C) : R == 192 ? lc_decode<192>(in, L, out, C) : lc_decode<128>(in, L, out, C);
+    return R == 256   ? lc_decode<256>(in, L, out, C)
+           : R == 192 ? lc_decode<192>(in, L, out, C)
+           : R == 160 ? lc_decode<160>(in, L, out, C)
+                      : lc_decode<128>(in, L, out, C);
 }

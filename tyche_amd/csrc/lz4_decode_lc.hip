@@ -232,12 +232,14 @@ __device__ __attribute__((aligned(64))) uint8_t g_lc_pad[64];
 // zero-initialised register, so the branch joins without a copy (a compiler-visible load in a
 // branch is joined by a copy that waits for it right there, in the next slot); the compiler
 // does not see them, and lc_far_wait waits for them before stage 3.
-__device__ __forceinline__ void far_load(const LPage &P, bool far, int32_t src, uint32_t rec, u32x4 &f0, u32x4 &f1) {
+template <int32_t N>
+__device__ __forceinline__ void far_load(const LPage &P, bool far, int32_t src, uint32_t rec, u32x4 (&fv)[N], int32_t t) {
     if (LC_ABLATE(1024)) far = false;
     if (far) {
         const uint8_t *a = P.out + src;
-        asm volatile("global_load_dwordx4 %0, %1, off" : "+v"(f0) : "v"(a) : "memory");
-        if (((rec >> 10) & 63u) > 16u) asm volatile("global_load_dwordx4 %0, %1, off offset:16" : "+v"(f1) : "v"(a) : "memory");
+        asm volatile("global_load_dwordx4 %0, %1, off" : "+v"(fv[kFarPer * t]) : "v"(a) : "memory");
+        if (kFarPer == 2 && ((rec >> 10) & 63u) > 16u)
+            asm volatile("global_load_dwordx4 %0, %1, off offset:16" : "+v"(fv[kFarPer * t + (kFarPer - 1)]) : "v"(a) : "memory");
     }
 }
 // every far load done: all but the four window loads issued after them (vmcnt is in order); the
@@ -280,9 +282,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LC_WPE))) vo
         const int32_t op0 = P.op;
         int32_t st = live ? kLParse : kLCut, rv = 0, nrec = 0;
         uint32_t rec[kLC + 1];
-        u32x4 fv[2 * kLC + 2];   // far sources (far_load)
+        u32x4 fv[kFarPer * (kLC + 1)];   // far sources (far_load)
 #pragma unroll
-        for (int32_t i = 0; i < 2 * kLC + 2; i++) fv[i] = u32x4{0u, 0u, 0u, 0u};
+        for (int32_t i = 0; i < kFarPer * (kLC + 1); i++) fv[i] = u32x4{0u, 0u, 0u, 0u};
         bool go = live, gen = false;
         int32_t need_gen = 0;
         uint64_t wq[4];   // the next slot's window qwords (parse_fast)
@@ -318,10 +320,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LC_WPE))) vo
                 __builtin_amdgcn_s_waitcnt(kVmDrain);
                 LPROF_MARK(2);   // the store drain
                 asm volatile("" ::: "memory");
-                far_load(P, far0, src0, rec[0], fv[0], fv[1]);
-                far_load(P, far1, src1, rec[1], fv[2], fv[3]);
+                far_load(P, far0, src0, rec[0], fv, 0);
+                far_load(P, far1, src1, rec[1], fv, 1);
             } else {
-                far_load(P, far, src, rec[t], fv[2 * t], fv[2 * t + 1]);
+                far_load(P, far, src, rec[t], fv, t);
             }
         }
         LPROF_MARK(3);   // slots 2.. and their far loads
@@ -340,7 +342,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LC_WPE))) vo
                 st = kLParse;
                 gen = parse_slot<R>(P, w16, op0, true, st, rv, rec[kLC], far, src);
             }
-            far_load(P, far && gen, src, rec[kLC], fv[2 * kLC], fv[2 * kLC + 1]);
+            far_load(P, far && gen, src, rec[kLC], fv, kLC);
         }
         LPROF_MARK(4);   // the general slot
         LPROF_ADD(12, __builtin_amdgcn_ballot_w64(need_gen != 0) != 0);
@@ -363,9 +365,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LC_WPE))) vo
             if (xw.c0 == (u128)0x123457 && xw.c3 == (u128)1) P.tail ^= 1;
         }
         if (live && !LC_ABLATE(4096)) {
-            u128 farv[2 * kLC + 2];
+            u128 farv[kFarPer * (kLC + 1)];
 #pragma unroll
-            for (int32_t i = 0; i < 2 * kLC + 2; i++) farv[i] = __builtin_bit_cast(u128, fv[i]);
+            for (int32_t i = 0; i < kFarPer * (kLC + 1); i++) farv[i] = __builtin_bit_cast(u128, fv[i]);
             uint64_t tail = P.tail;
             copy_records<R>(ring, w16, op0, tail, rec, farv, nrec, gen, lut);
             P.tail = tail;
@@ -468,19 +470,26 @@ extern "C" int tyche_debug_lc_profile(unsigned long long *host16, int reset) {
 
 hipError_t launch_lz4_decode_lc(const tyche_batch_t &b, uint32_t in_cap, uint32_t out_cap, hipStream_t s) {
     if (b.count == 0) return hipSuccess;
-    const long r = knob("LZ4_LC_RING", 192);   // 192: 24.1 ms per 1M x 16 KiB pages, 128: 25.0, 256: 28.6
+    // R = 160 (20 qword rows, 17.1 KiB of LDS per wave, 8 waves per CU): 24.07 / 24.37 ms per 1M x 16 KiB
+    // pages with / without LC_FAR16, 192: 24.22 / 24.46, 128: 28.9 / 25.1 (11 waves per CU with LC_FAR16:
+    // more waves in flight made it slower), 256: 28.6 (round 4) -- profiles/r06_ring_ab.log, r06_far16.log
+    const long r = knob("LZ4_LC_RING", 160);
 #if LC_LINE == 16
     const void *k = r == 256   ? (const void *)lz4_decode_lc_kernel<256>
                     : r == 192 ? (const void *)lz4_decode_lc_kernel<192>
+                    : r == 160 ? (const void *)lz4_decode_lc_kernel<160>
                                : (const void *)lz4_decode_lc_kernel<128>;
-    const size_t lds = r == 256 ? LCL<256>::total : r == 192 ? LCL<192>::total : LCL<128>::total;
+    const size_t lds = r == 256   ? LCL<256>::total
+                       : r == 192 ? LCL<192>::total
+                       : r == 160 ? LCL<160>::total
+                                  : LCL<128>::total;
 #else   // 64-byte lines need R >= 192 (lc_ring_ok)
     const void *k = r == 256 ? (const void *)lz4_decode_lc_kernel<256> : (const void *)lz4_decode_lc_kernel<192>;
     const size_t lds = r == 256 ? LCL<256>::total : LCL<192>::total;
 #endif
     const size_t ncu = prepare_launch(k);
     size_t waves = waves_per_cu(k, lds);
-    const long env_waves = knob("LZ4_LC_WAVES", 0);
+    const long env_waves = knob("LZ4_LC_WAVES", 8);   // (LC_FAR16's 154 VGPRs would allow 9 at R = 160: slower)
     if (env_waves > 0) waves = std::min<size_t>(waves, (size_t)env_waves);
     const size_t grid = std::min<size_t>((b.count + 63) / 64, ncu * waves);
     void *args[] = {(void *)&b, &in_cap, &out_cap};

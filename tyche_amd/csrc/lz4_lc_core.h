@@ -73,11 +73,20 @@ LC_FN void lc_lut_apply(const uint32_t *sel, uint64_t &lo, uint64_t &hi) {
     hi = (uint64_t)d2 | ((uint64_t)d3 << 32);
 }
 
+// LC_FAR16 1: a far match part (source out of the ring, loaded from HBM into registers) takes at
+// most 16 bytes, so a record slot needs one 16-byte far register instead of two (32 VGPRs fewer
+// per wave); longer far matches continue in the next record
+#ifndef LC_FAR16
+#define LC_FAR16 1   // round 6: 24.07 vs 24.37 ms per 1M x 16 KiB pages at R = 160 (profiles/r06_ring_ab.log)
+#endif
+constexpr int32_t kFarPer = LC_FAR16 ? 1 : 2;   // 16-byte far registers per record slot
 #ifndef LC_SLOTS
 #define LC_SLOTS 7
 #endif
 constexpr int32_t kLC = LC_SLOTS;   // record slots per chunk (unrolled)
 constexpr int32_t kLW = 64;          // window bytes
+// (round 6 tried the window as a ring of rows refilled with only its missing 16-byte pieces, about
+// 2 of 4 per chunk: slower, 24.8-24.9 vs 24.3-24.4 ms, profiles/r06_wring_ab.log)
 constexpr int32_t kLWS = kLW;   // window bytes per lane in LDS (reads past the end land in later rows: unused bytes)
 
 // 16 bytes at byte position p >= 0 of a lane's window (no wrap), as lo : hi
@@ -88,20 +97,25 @@ LC_FN void get16(const uint8_t *base, int32_t p, uint64_t &lo, uint64_t &hi) {
     lo = funnel8(q0, q1, s);
     hi = funnel8(q1, q2, s);
 }
-// Ring rows (qwords) of a lane: R / 8 of them, R a power of two or 192 (24 rows:
-// row = k mod 24 by an exact multiply-high division).  k >= -1 (positions >= -8).
+// Ring rows (qwords) of a lane: R / 8 of them, R a power of two, 160 or 192 (20 / 24 rows:
+// row = k mod 20 / 24 by an exact multiply-high division).  k >= -1 (positions >= -8).
 template <int32_t R>
 LC_FN int32_t lc_row(int32_t k) {
     constexpr int32_t rows = R / 8;
     if constexpr ((rows & (rows - 1)) == 0) {
         return k & (rows - 1);
-    } else {
-        static_assert(rows == 24, "ring rows: a power of two or 24");
+    } else if constexpr (rows == 24) {
         // u / 24 = (u * 43691) >> 20 exactly for u < 2^16 (the error u * 3.2e-7 stays under 1/24
         // there; u <= 65535 / 8 + 25), with 24-bit multiplies
         const uint32_t u = (uint32_t)(k + rows);
         const uint32_t q = LC_UMUL24(u, 43691u) >> 20;
         return (int32_t)u + LC_MUL24((int32_t)q, -24);
+    } else {
+        static_assert(rows == 20, "ring rows: a power of two, 20 or 24");
+        // u / 20 = (u * 3277) >> 16 exactly for u < 2^14 (error u * 3.1e-6 < 1/20; u <= 65535 / 8 + 21)
+        const uint32_t u = (uint32_t)(k + rows);
+        const uint32_t q = LC_UMUL24(u, 3277u) >> 16;
+        return (int32_t)u + LC_MUL24((int32_t)q, -20);
     }
 }
 template <int32_t R>
@@ -253,8 +267,10 @@ LC_FN int32_t parse_fast(LPage &P, const uint8_t *w16, int32_t op0, uint32_t &re
                      !((mn == 15) & (P.ip + need > P.L - kLastLiterals)) &              // lz4.c:1176
                      (P.op + lit + ml <= P.C - kLastLiterals) &                         // lz4.c:1225
                      (ml <= 32);
+    const int32_t moff = isA ? P.moff : off;
     const int32_t n1 = isA ? 0 : (isB ? nB : lit);
-    const int32_t n2 = isA ? nA : (isB ? 0 : ml);
+    const int32_t n2f = isA ? nA : (isB ? 0 : ml);
+    const int32_t n2 = (LC_FAR16 && moff > lc_near<R>()) ? min(n2f, 16) : n2f;   // (LC_FAR16: far parts <= 16)
     const bool fits = n1 + n2 <= room;
     // k: 1 the record is emitted; 0 the chunk stops here (window or budget); 2 the general path
     const bool cont = isA | isB;
@@ -262,7 +278,6 @@ LC_FN int32_t parse_fast(LPage &P, const uint8_t *w16, int32_t op0, uint32_t &re
     const bool fast = cont | (fresh & okC);
     const int32_t k = stop ? 0 : (fast ? (fits ? 1 : 0) : 2);
     const bool emit = (k == 1);
-    const int32_t moff = isA ? P.moff : off;
     far = emit & (n2 > 0) & (moff > lc_near<R>());
     src = emit ? P.op + n1 - moff : src;
     rec = emit ? lc_rec(n1 > 0 ? (isB ? P.lp - P.wb : x + 1) : 0, n1, n2, moff) : rec;
@@ -271,6 +286,10 @@ LC_FN int32_t parse_fast(LPage &P, const uint8_t *w16, int32_t op0, uint32_t &re
     P.lp += (emit & isB) ? n1 : 0;
     P.lrem -= (emit & isB) ? n1 : 0;
     P.ip += (emit & fresh) ? need : 0;
+    if (LC_FAR16) {   // a new sequence's far match cut at 16 bytes: the rest is a match in progress
+        P.mrem += (emit & fresh) ? ml - n2 : 0;
+        P.moff = (emit & fresh) ? off : P.moff;
+    }
     return k;
 }
 
@@ -380,7 +399,7 @@ LC_FN bool parse_slot(LPage &P, const uint8_t *w16, int32_t op0, bool deep, int3
         miss = false;
     }
     // 4. match bytes of this record (after the whole literal run)
-    const int32_t n2 = (P.lrem == n1 && P.hdr == 0) ? min(P.mrem, 32) : 0;
+    const int32_t n2 = (P.lrem == n1 && P.hdr == 0) ? min(P.mrem, (LC_FAR16 && P.moff > lc_near<R>()) ? 16 : 32) : 0;
     if (P.term && P.lrem == 0) {   // an empty last literal run (a stream the reference accepts)
         rv = P.op;
         st = kLEnd;
@@ -410,8 +429,8 @@ LC_FN bool parse_slot(LPage &P, const uint8_t *w16, int32_t op0, bool deep, int3
 }
 
 // Stage 3: the chunk's records into the ring, from output position d on.
-// farv[2t], farv[2t + 1] hold the source bytes of record t's match part when that
-// part is far (the second only when it is longer than 16 bytes).
+// farv[kFarPer t] (and farv[2t + 1] when kFarPer is 2) hold the source bytes of record t's match
+// part when that part is far (the second only when it is longer than 16 bytes).
 // Slots 0..kLC-1 hold the fast path's records (the first nrec of them), slot
 // kLC the general path's one (when gen).
 template <int32_t R>
@@ -440,8 +459,8 @@ LC_FN void copy_records(uint8_t *ring, const uint8_t *w16, int32_t d, uint64_t &
             uint64_t lo, hi;
             ring16<R>(ring, d - off, lo, hi);
             if (far) {
-                lo = (uint64_t)farv[2 * t];
-                hi = (uint64_t)(farv[2 * t] >> 64);
+                lo = (uint64_t)farv[kFarPer * t];
+                hi = (uint64_t)(farv[kFarPer * t] >> 64);
             }
             lc_lut_apply(ent, lo, hi);   // the period-off pattern when the match overlaps itself
             tail = put16<R>(ring, d, tail, lo, hi, h1);
@@ -451,9 +470,9 @@ LC_FN void copy_records(uint8_t *ring, const uint8_t *w16, int32_t d, uint64_t &
                 const int32_t e = off >= 16 ? off : (int32_t)ent[8];
                 LC_BARRIER();
                 ring16<R>(ring, d + 16 - e, lo, hi);
-                if (far) {
-                    lo = (uint64_t)farv[2 * t + 1];
-                    hi = (uint64_t)(farv[2 * t + 1] >> 64);
+                if (far && kFarPer == 2) {
+                    lo = (uint64_t)farv[kFarPer * t + (kFarPer - 1)];
+                    hi = (uint64_t)(farv[kFarPer * t + (kFarPer - 1)] >> 64);
                 }
                 tail = put16<R>(ring, d + 16, tail, lo, hi, n2 - 16);
             }
