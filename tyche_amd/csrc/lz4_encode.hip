@@ -382,97 +382,6 @@ __device__ __forceinline__ bool emit_sink_n(const uint2 *rec, uint32_t n, uint32
     return emit_staged(rec, n, anchor, in, dst, op, cap, ring, r, map, lane);
 }
 
-// ---- The N-wave kernels' sink with the output ring in the record array (TYCHE_ENC_SHARED_RING).
-//
-// The encoder is latency-bound at the 5 pages (20 waves) per CU its LDS allows: 5 / 4 / 3 resident
-// pages per CU run 59.8 / 67.5 / 82.1 ms per 1M x 16 KiB pages (profiles/r06_enc_occ.log, ~165 / p +
-// 27 ms).  A wave's region was table 2 KiB | owner map 256 B | 64 records 512 B | ring 512 B.  Here a
-// call's records are read into registers first, the same 512 bytes then take the call's sequences,
-// and the call ends with all of them flushed -- nothing stays in the ring between calls, so the parse
-// may append its next records there.  A batch whose encoding exceeds 512 bytes (long literal runs)
-// goes straight to HBM with byte stores, lane by lane, and long runs wave-wide.  2,576 B per wave:
-// 26.9 KiB per 16 KiB page, 6 pages (24 waves) per CU.
-#ifndef TYCHE_ENC_SHARED_RING
-#define TYCHE_ENC_SHARED_RING 0
-#endif
-constexpr uint32_t kSharedRing = 64u * sizeof(uint2);   // the record array's bytes
-__device__ __forceinline__ bool emit_shared(const uint2 *rec, uint32_t n, uint32_t anchor, const uint8_t *in, uint8_t *dst,
-                                            uint32_t &op, uint32_t cap, uint8_t *ring, uint8_t *dummy, uint32_t lane) {
-    const bool is_sel = lane < n;
-    const uint2 rc = rec[is_sel ? lane : 0];
-    const uint2 rp = rec[lane > 0 && is_sel ? lane - 1 : 0];
-    const uint32_t pos = rc.x & 0xFFFFu, cand = rc.x >> 16, len = rc.y & 0xFFFFu, back = lzp::back_at(in, pos, cand);
-    const uint32_t prev_end = lane == 0 ? anchor : (rp.x & 0xFFFFu) + (rp.y & 0xFFFFu);
-    const uint32_t k = min(min(back, pos - prev_end), cand);   // catch-up (lz4.c:549)
-    const uint32_t lstart = prev_end;
-    const uint32_t lit = is_sel ? pos - k - prev_end : 0u;
-    const uint32_t lext = lit >= 15 ? (lit - 15) / 255 + 1 : 0;
-    const uint32_t off = pos - cand;
-    const uint32_t mc = len + k - kMinMatch;
-    const uint32_t mext = mc >= 15 ? (mc - 15) / 255 + 1 : 0;
-    const uint32_t token = (min(lit, 15u) << 4) | min(mc, 15u);
-    const uint32_t enc = is_sel ? 1 + lext + lit + 2 + mext : 0u;
-    const int32_t incl = wave_incl_sum((int32_t)enc);
-    const uint32_t eo = (uint32_t)incl - enc;
-    const uint32_t et = rdlane((uint32_t)incl, 63);
-    if (op + et > cap) return false;
-    // every lane's record reads are issued before the first ring byte store (LDS keeps a wave's
-    // operations in order; this keeps the compiler from moving a store above a read)
-    asm volatile("" ::: "memory");
-    const bool direct = et > kSharedRing;   // wave-uniform
-    uint8_t *base = direct ? dst + op : ring;
-    const uint32_t q_lit = eo + 1 + lext;
-    if (is_sel) {
-        uint32_t q = eo;
-        base[q] = (uint8_t)token;
-        q++;
-        for (uint32_t t = 0; t < lext; t++) base[q + t] = (uint8_t)(t + 1 == lext ? (lit - 15) % 255 : 255);
-        const uint32_t ls = min(lit, kLitLane);
-        // the run's first 8 bytes from three aligned dwords of the staged page (64 zero bytes of padding)
-        static_assert(kLitLane == 8, "two gathered dwords");
-        const uint32_t ib = (uint32_t)(uintptr_t)in & 3u;
-        const uint32_t *A = (const uint32_t *)(in - ib);
-        const uint32_t q0 = lstart + ib, i0 = q0 >> 2, sh = q0 & 3u;
-        const uint32_t d0 = A[i0], d1 = A[i0 + 1], d2 = A[i0 + 2];
-        const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, sh), w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
-        if (!direct) {
-#pragma unroll
-            for (uint32_t t = 0; t < 8; t++) {
-                uint8_t *bp = t < ls ? ring + q_lit + t : dummy;
-                *bp = (uint8_t)((t < 4 ? w0 : w1) >> (8 * (t & 3u)));
-            }
-        } else {
-            for (uint32_t t = 0; t < ls; t++) base[q_lit + t] = (uint8_t)((t < 4 ? w0 : w1) >> (8 * (t & 3u)));
-        }
-        q = q_lit + lit;
-        base[q] = (uint8_t)off;
-        base[q + 1] = (uint8_t)(off >> 8);
-        q += 2;
-        for (uint32_t t = 0; t < mext; t++) base[q + t] = (uint8_t)(t + 1 == mext ? (mc - 15) % 255 : 255);
-    }
-    uint64_t longm = __ballot(is_sel && lit > kLitLane);
-    while (longm) {
-        const uint32_t kk = (uint32_t)__builtin_ctzll(longm);
-        longm &= longm - 1;
-        const uint32_t kl = rdlane(lit, kk) - kLitLane, kq = rdlane(q_lit, kk) + kLitLane, ks = rdlane(lstart, kk) + kLitLane;
-        for (uint32_t i = lane; i < kl; i += kWave) base[kq + i] = in[ks + i];
-    }
-    __builtin_amdgcn_wave_barrier();
-    if (!direct) {   // the whole batch to dst + op, a dword per lane and step
-        for (uint32_t j = 4u * lane; j < et; j += 4u * kWave) {
-            const uint32_t w = *(const uint32_t *)(ring + j);
-            if (j + 4u <= et) {
-                store_u32_unaligned(dst + op + j, w);
-            } else {
-                for (uint32_t t = 0; j + t < et; t++) dst[op + j + t] = (uint8_t)(w >> (8 * t));
-            }
-        }
-    }
-    op += et;
-    __builtin_amdgcn_wave_barrier();   // the flush's ring reads before the parse's next record writes
-    return true;
-}
-
 // Encodes one page held in LDS into dst (global, capacity cap).  Returns the
 // compressed size, or 0 if it does not fit in cap.
 __device__ int32_t encode_page(const uint8_t *in, uint32_t L, uint16_t *table, uint8_t *map, uint2 *rec,
@@ -789,10 +698,8 @@ struct SplitHdrN {
 };
 template <uint32_t kNW>
 constexpr size_t split_hdr_bytes() { return (sizeof(SplitHdrN<kNW>) + 63) & ~(size_t)63; }
-// per-wave region of the N-wave kernels: table | records (= output ring) | dummy byte target
-constexpr size_t kWaveRegionN = TYCHE_ENC_SHARED_RING ? kHashSize * sizeof(uint16_t) + kWave * sizeof(uint2) + 16u : kWaveRegion;
 template <uint32_t kNW>
-constexpr size_t split_stage_off() { return split_hdr_bytes<kNW>() + kNW * kWaveRegionN; }
+constexpr size_t split_stage_off() { return split_hdr_bytes<kNW>() + kNW * kWaveRegion; }
 template <uint32_t kNW>
 __host__ __device__ constexpr uint32_t part_scratch(uint32_t in_cap) {   // a part's worst-case stream, 256-aligned
     return (lz4_bound(in_cap / kNW + 2u * kWave) + 64u + 255u) & ~255u;
@@ -801,9 +708,6 @@ template <uint32_t kNW>
 constexpr uint32_t split_prefetch() { return (16384u / 16u + kNW * kWave - 1u) / (kNW * kWave); }   // 16 KiB per page
 
 template <uint32_t kNW>
-#ifndef TYCHE_ENC_PF
-#define TYCHE_ENC_PF 1
-#endif
 #ifndef TYCHE_ENC_WPE
 #define TYCHE_ENC_WPE 5   // amdgpu_waves_per_eu register budget of the split kernels (4 waves: 87 VGPRs, no spills; 0: none)
 #endif
@@ -817,24 +721,16 @@ __global__ __launch_bounds__(kNW * 64) TYCHE_ENC_WPE_ATTR void lz4_encode_splitn
                                                                      uint32_t p0) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr uint32_t kT = kNW * kWave;                 // threads per page
-    // 16-byte vectors per thread of the next page held in registers across the parse (TYCHE_ENC_PF=0:
-    // none -- the next page is staged straight from HBM after the page barrier, 16 VGPRs fewer)
-    constexpr uint32_t kPf = TYCHE_ENC_PF ? split_prefetch<kNW>() : 0u;
+    constexpr uint32_t kPf = split_prefetch<kNW>();       // 16-byte vectors per thread prefetched
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const uint32_t wave = rfl(tid >> 6);
     SplitHdrN<kNW> *hdr = (SplitHdrN<kNW> *)smem;
-    uint8_t *region = smem + split_hdr_bytes<kNW>() + wave * kWaveRegionN;
+    uint8_t *region = smem + split_hdr_bytes<kNW>() + wave * kWaveRegion;
     uint16_t *table = (uint16_t *)region;
-#if TYCHE_ENC_SHARED_RING
-    uint2 *rec = (uint2 *)(region + kHashSize * sizeof(uint16_t));
-    uint8_t *map = (uint8_t *)(rec + kWave);   // (the dummy byte target)
-    uint8_t *ring = (uint8_t *)rec;
-#else
     uint8_t *map = region + kHashSize * sizeof(uint16_t);
     uint2 *rec = (uint2 *)(map + 4 * kWave);
     uint4 *fld = (uint4 *)(rec + kWave);
     uint8_t *ring = (uint8_t *)fld;
-#endif
     uint8_t *stage = smem + split_stage_off<kNW>();
     const uint32_t part_ws = part_scratch<kNW>(in_cap);
     uint8_t *scratch = ws + (size_t)blockIdx.x * ws_stride + (size_t)(wave ? wave - 1u : 0u) * part_ws;
@@ -854,7 +750,7 @@ __global__ __launch_bounds__(kNW * 64) TYCHE_ENC_WPE_ATTR void lz4_encode_splitn
         __syncthreads();
         const size_t next = (size_t)rfl(hdr->next_lo) | ((size_t)rfl(hdr->next_hi) << 32);
         PageRef pn;
-        u32x4 pf[kPf > 0 ? kPf : 1];
+        u32x4 pf[kPf];
         uint32_t nhead = 0, nvec = 0;
         if (next < b.count) {
             pn = batch_page(b, next);
@@ -909,11 +805,7 @@ __global__ __launch_bounds__(kNW * 64) TYCHE_ENC_WPE_ATTR void lz4_encode_splitn
                     a2 = (rr[0].x & 0xFFFFu) + (rr[0].y & 0xFFFFu);
                     if (n2 == 0) return true;
                 }
-#if TYCHE_ENC_SHARED_RING
-                return emit_shared(r2, n2, a2, in, odst, op, ocap, ring, map, lane);
-#else
                 return emit_sink_n(r2, n2, a2, in, odst, op, ocap, ring, r, map, lane);
-#endif
             };
             const uint32_t cur = lzp::parse_page(in, Lp, table, rec, lane, sink, b0);
             if (wave == 0) {
@@ -954,11 +846,7 @@ __global__ __launch_bounds__(kNW * 64) TYCHE_ENC_WPE_ATTR void lz4_encode_splitn
                     }
                     if (lane == 0) rec[0] = hdr->first[w];
                     __builtin_amdgcn_wave_barrier();
-#if TYCHE_ENC_SHARED_RING
-                    ok = emit_shared(rec, 1, cur, in, p.dst, op, p.dst_cap, ring, map, lane);
-#else
                     ok = emit_sink_n(rec, 1, cur, in, p.dst, op, p.dst_cap, ring, r, map, lane);
-#endif
                     if (ok) out_flush_all(ring, r, p.dst, op, lane);
                     if (lane == 0) hdr->seg[w] = op;
                     op += rfl(hdr->len[w]);
@@ -991,18 +879,14 @@ __global__ __launch_bounds__(kNW * 64) TYCHE_ENC_WPE_ATTR void lz4_encode_splitn
         p = pn;
         head = nhead;
         if (p.src_len <= in_cap && p.src_len > 0) {
-            if (kPf == 0) {
-                (void)stage_in(p.src, p.src_len, stage, tid, kT);   // (4 loads in flight per thread)
-            } else {
-                u32x4 *l = (u32x4 *)stage;
+            u32x4 *l = (u32x4 *)stage;
 #pragma unroll
-                for (uint32_t k = 0; k < kPf; k++) {
-                    const uint32_t v = tid + k * kT;
-                    if (v < nvec) l[v] = pf[k];
-                }
-                const u32x4 *g = (const u32x4 *)((uintptr_t)p.src - nhead);
-                for (uint32_t v = tid + kPf * kT; v < nvec; v += kT) l[v] = gload_nt(g + v);
+            for (uint32_t k = 0; k < kPf; k++) {
+                const uint32_t v = tid + k * kT;
+                if (v < nvec) l[v] = pf[k];
             }
+            const u32x4 *g = (const u32x4 *)((uintptr_t)p.src - nhead);
+            for (uint32_t v = tid + kPf * kT; v < nvec; v += kT) l[v] = gload_nt(g + v);
         }
         if (tid == 0) {
             hdr->next_lo = hdr->next2_lo;
