@@ -470,10 +470,13 @@ extern "C" int tyche_debug_lc_profile(unsigned long long *host16, int reset) {
 
 hipError_t launch_lz4_decode_lc(const tyche_batch_t &b, uint32_t in_cap, uint32_t out_cap, hipStream_t s) {
     if (b.count == 0) return hipSuccess;
-    // R = 160 (20 qword rows, 17.1 KiB of LDS per wave, 8 waves per CU): 24.07 / 24.37 ms per 1M x 16 KiB
-    // pages with / without LC_FAR16, 192: 24.22 / 24.46, 128: 28.9 / 25.1 (11 waves per CU with LC_FAR16:
-    // more waves in flight made it slower), 256: 28.6 (round 4) -- profiles/r06_ring_ab.log, r06_far16.log
-    const long r = knob("LZ4_LC_RING", 160);
+    // R = 192 (24 qword rows, 18.9 KiB of LDS per wave, 8 waves per CU).  Round 6, ms per 1M x 16 KiB pages
+    // with / without LC_FAR16: at 256K pages per launch R = 160 24.07 / 24.37, 192 24.22 / 24.46, 128
+    // 28.9 / 25.1 (11 waves per CU with LC_FAR16: more waves in flight made it slower; 256: 28.6 in round
+    // 4) -- r06_ring_ab.log, r06_far16.log; at the bench's 1M pages 160 and 192 tie (23.8-24.1 either
+    // way, r06_1m_ab.log), while 192 reads less (57 vs 60 KB per page) and decodes the C4 shard's 8 KiB
+    // pages faster (12.0 vs 13.0 ms per 1M)
+    const long r = knob("LZ4_LC_RING", 192);
 #if LC_LINE == 16
     const void *k = r == 256   ? (const void *)lz4_decode_lc_kernel<256>
                     : r == 192 ? (const void *)lz4_decode_lc_kernel<192>
@@ -489,7 +492,7 @@ hipError_t launch_lz4_decode_lc(const tyche_batch_t &b, uint32_t in_cap, uint32_
 #endif
     const size_t ncu = prepare_launch(k);
     size_t waves = waves_per_cu(k, lds);
-    const long env_waves = knob("LZ4_LC_WAVES", 8);   // (LC_FAR16's 154 VGPRs would allow 9 at R = 160: slower)
+    const long env_waves = knob("LZ4_LC_WAVES", 8);   // (LC_FAR16's 154 VGPRs would allow more at R = 128 / 160: slower)
     if (env_waves > 0) waves = std::min<size_t>(waves, (size_t)env_waves);
     const size_t grid = std::min<size_t>((b.count + 63) / 64, ncu * waves);
     void *args[] = {(void *)&b, &in_cap, &out_cap};

@@ -77,7 +77,7 @@ LC_FN void lc_lut_apply(const uint32_t *sel, uint64_t &lo, uint64_t &hi) {
 // most 16 bytes, so a record slot needs one 16-byte far register instead of two (32 VGPRs fewer
 // per wave); longer far matches continue in the next record
 #ifndef LC_FAR16
-#define LC_FAR16 1   // round 6: 24.07 vs 24.37 ms per 1M x 16 KiB pages at R = 160 (profiles/r06_ring_ab.log)
+#define LC_FAR16 1   // round 6: 182 -> 154 VGPRs, 1 % faster at 256K pages, equal at 1M (profiles/r06_*ab.log)
 #endif
 constexpr int32_t kFarPer = LC_FAR16 ? 1 : 2;   // 16-byte far registers per record slot
 #ifndef LC_SLOTS
