@@ -109,6 +109,17 @@ def cpu_baseline(codec: str, n: int, page_len: int, threads: int, seed: int, rep
             "compress_gib_s": r["compress_gib_s"], "decompress_gib_s": r["decompress_gib_s"], "ratio": r["ratio"]}
 
 
+def pages_equal(out, pages, rv, plen: int) -> bool:
+    """Every page decoded to its full length and bit-exact, compared in 1 GiB slices: torch.equal
+    over the whole 16 GiB would allocate a 16 GiB temporary, and on a fresh allocation of that size
+    the next memory-bound kernel ran ~23 % slower (profiles/r06_steps*.jsonl)."""
+    step = max(1, (1 << 30) // plen)
+    ok = bool((rv == plen).all().item())
+    for a in range(0, out.shape[0], step):
+        ok = ok and torch.equal(out[a:a + step], pages[a:a + step])
+    return ok
+
+
 def measure_codec(cid: int, name: str, n: int, plen: int, steps: int, warmup: int, dev, seed: int, first: int,
                   dist: int) -> dict:
     """Device-resident compress+decompress of n resident pages with codec `cid` (HIP events on the stream)."""
@@ -125,8 +136,6 @@ def measure_codec(cid: int, name: str, n: int, plen: int, steps: int, warmup: in
         codec.compress_pages(pages, compressor_id=cid, out=comp, out_len=clen)
         codec.decompress_pages(comp, clen, plen, compressor_id=cid, out=out, rv=rv, max_comp_len=mx)
     torch.cuda.synchronize()
-    if not (bool((rv == plen).all().item()) and bool((clen > 0).all().item()) and torch.equal(out, pages)):
-        raise SystemExit(f"{name}: round trip failed on the benchmark pages")
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -138,6 +147,9 @@ def measure_codec(cid: int, name: str, n: int, plen: int, steps: int, warmup: in
         ev[k][2].record()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
+    # the last timed step's output, after the timed region
+    if not (bool((clen > 0).all().item()) and pages_equal(out, pages, rv, plen)):
+        raise SystemExit(f"{name}: round trip failed on the benchmark pages")
     c_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / steps
     d_ms = sum(e[1].elapsed_time(e[2]) for e in ev) / steps
     nbytes = n * plen
@@ -305,9 +317,6 @@ def run_c4(args, info, dev):
     for _ in range(max(args.warmup, 1)):
         codec.decompress_pages(comp, clen, plen, out=out, rv=rv, max_comp_len=mx)
     torch.cuda.synchronize()
-    if not (bool((rv == plen).all().item()) and torch.equal(out, pages)):
-        raise SystemExit("C4: round trip failed")
-    del pages
     comp_bytes = int(clen.to(torch.int64).sum().item())
     events = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(args.steps)]
     runner.barrier(info)
@@ -320,6 +329,9 @@ def run_c4(args, info, dev):
     torch.cuda.synchronize()
     runner.barrier(info)
     elapsed = runner.max_over_ranks(info, time.perf_counter() - t0)
+    if not pages_equal(out, pages, rv, plen):   # the last timed step's output, after the timed region
+        raise SystemExit("C4: round trip failed")
+    del pages
     d_ms = sum(e[0].elapsed_time(e[1]) for e in events) / args.steps
     total = runner.sum_over_ranks(info, float(n))
     algo = n * plen + comp_bytes
@@ -381,16 +393,14 @@ def main():
         if ev is not None:
             ev[2].record()
 
-    # warm-up, then a full-size correctness property: every page round-trips bit-exactly
+    # warm-up (the timed steps' output is checked after the timed region: every page round-trips
+    # bit-exactly)
     step()
     torch.cuda.synchronize()
     max_comp = int(clen.max().item())
     for _ in range(max(args.warmup - 1, 0)):
         step(max_comp=max_comp)
     torch.cuda.synchronize()
-    ok = bool((rv == plen).all().item()) and bool((clen > 0).all().item()) and torch.equal(out, pages)
-    if not ok:
-        raise SystemExit("round trip failed on the benchmark pages")
     comp_bytes = int(clen.to(torch.int64).sum().item())
 
     events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
@@ -403,6 +413,8 @@ def main():
     runner.barrier(info)
     t1 = time.perf_counter()
     elapsed = runner.max_over_ranks(info, t1 - t0)
+    if not (bool((clen > 0).all().item()) and pages_equal(out, pages, rv, plen)):
+        raise SystemExit("round trip failed on the benchmark pages")
 
     c_ms = sum(e[0].elapsed_time(e[1]) for e in events) / args.steps
     d_ms = sum(e[1].elapsed_time(e[2]) for e in events) / args.steps
