@@ -110,9 +110,8 @@ def cpu_baseline(codec: str, n: int, page_len: int, threads: int, seed: int, rep
 
 
 def pages_equal(out, pages, rv, plen: int) -> bool:
-    """Every page decoded to its full length and bit-exact, compared in 1 GiB slices: torch.equal
-    over the whole 16 GiB would allocate a 16 GiB temporary, and on a fresh allocation of that size
-    the next memory-bound kernel ran ~23 % slower (profiles/r06_steps*.jsonl)."""
+    """Every page decoded to its full length and bit-exact, compared in 1 GiB slices (torch.equal
+    over the whole tensors would take a 16 GiB temporary).  Runs after the timed region."""
     step = max(1, (1 << 30) // plen)
     ok = bool((rv == plen).all().item())
     for a in range(0, out.shape[0], step):
@@ -317,7 +316,6 @@ def run_c4(args, info, dev):
     for _ in range(max(args.warmup, 1)):
         codec.decompress_pages(comp, clen, plen, out=out, rv=rv, max_comp_len=mx)
     torch.cuda.synchronize()
-    comp_bytes = int(clen.to(torch.int64).sum().item())
     events = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(args.steps)]
     runner.barrier(info)
     torch.cuda.synchronize()
@@ -332,6 +330,7 @@ def run_c4(args, info, dev):
     if not pages_equal(out, pages, rv, plen):   # the last timed step's output, after the timed region
         raise SystemExit("C4: round trip failed")
     del pages
+    comp_bytes = int(clen.to(torch.int64).sum().item())
     d_ms = sum(e[0].elapsed_time(e[1]) for e in events) / args.steps
     total = runner.sum_over_ranks(info, float(n))
     algo = n * plen + comp_bytes
@@ -400,8 +399,10 @@ def main():
     max_comp = int(clen.max().item())
     for _ in range(max(args.warmup - 1, 0)):
         step(max_comp=max_comp)
+    # no other kernel between the warm-up and the timed steps: the first LZ4 decode after a foreign
+    # kernel on the stream (a torch reduction, fill or compare) ran 29.3 instead of 23.8 ms on every
+    # box tried (profiles/r06_steps*.jsonl); the byte count and the check come after the timed region
     torch.cuda.synchronize()
-    comp_bytes = int(clen.to(torch.int64).sum().item())
 
     events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
     runner.barrier(info)
@@ -415,6 +416,7 @@ def main():
     elapsed = runner.max_over_ranks(info, t1 - t0)
     if not (bool((clen > 0).all().item()) and pages_equal(out, pages, rv, plen)):
         raise SystemExit("round trip failed on the benchmark pages")
+    comp_bytes = int(clen.to(torch.int64).sum().item())
 
     c_ms = sum(e[0].elapsed_time(e[1]) for e in events) / args.steps
     d_ms = sum(e[1].elapsed_time(e[2]) for e in events) / args.steps
@@ -452,6 +454,8 @@ def main():
         "compress_gib_s": round(page_bytes / (c_ms * 1e-3) / GIB, 3),
         "decompress_gib_s": round(page_bytes / (d_ms * 1e-3) / GIB, 3),
         "kernel_ms": {"lz4_encode": round(c_ms, 4), "lz4_decode": round(d_ms, 4)},
+        "kernel_ms_steps": {"lz4_encode": [round(e[0].elapsed_time(e[1]), 3) for e in events],
+                            "lz4_decode": [round(e[1].elapsed_time(e[2]), 3) for e in events]},
         "roofline_by_kernel": {k: round(algo_bytes / (v * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) for k, v in kernels.items()},
         "ratio": round(page_bytes / comp_bytes, 4),
     }
