@@ -193,3 +193,46 @@ def test_failed_host_batch_leaves_nothing_for_the_next_call(oracle_mod):
         assert np.array_equal(out2, pages[:m])
     finally:
         lib.tyche_set_device(_lib.ALL_DEVICES)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("direct", [1, 0])
+def test_host_decompress_chunks(oracle_mod, knobs, direct):
+    """The host path's chunked LZ4 decompress, the kernels writing pages straight into the pinned
+    arena (HOST_DIRECT_OUT=1, the default) and staged through HBM and a D2H copy (0): a ragged
+    multi-chunk batch -- 8 and 16 KiB pages, every pagegen distribution, every 7th stream
+    corrupted, every 11th destination short -- gives the restated LZ4_decompress_safe's result for
+    every page and its bytes for every page that decodes."""
+    knobs(HOST_DIRECT_OUT=direct, HOST_CHUNK_MB=8)
+    lib = _lib.load()
+    assert lib.tyche_set_device(0) == 0
+    try:
+        O = oracle_mod
+        rng = np.random.default_rng(606 + direct)
+        n = 6000
+        plens = np.where(np.arange(n) % 3 == 0, 8192, 16384)
+        pages = [O.pagegen(1, int(plens[i]), seed=5 + i, first=i, dist=i % 6)[0] for i in range(n)]
+        streams, caps = [], []
+        for i in range(n):
+            c = bytearray(O.lz4_compress(pages[i].tobytes()))
+            if i % 7 == 3:
+                c[int(rng.integers(0, len(c)))] ^= 1 << int(rng.integers(0, 8))
+            streams.append(bytes(c))
+            caps.append(int(plens[i]) if i % 11 != 5 else int(rng.integers(100, int(plens[i]))))
+        bufs = [np.frombuffer(s, dtype=np.uint8).copy() for s in streams]
+        outs = [np.zeros(c, dtype=np.uint8) for c in caps]
+        vp = ctypes.c_void_p * n
+        src = vp(*[b.ctypes.data for b in bufs])
+        slen = (ctypes.c_uint32 * n)(*[len(s) for s in streams])
+        dst = vp(*[o.ctypes.data for o in outs])
+        dcap = (ctypes.c_uint32 * n)(*caps)
+        res = np.zeros(n, dtype=np.int32)
+        rc = lib.tyche_decompress_host(1, n, src, slen, dst, dcap, res.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))
+        assert rc == 0, _lib.last_error()
+        for i in range(n):
+            r, want = O.lz4_decompress(streams[i], caps[i])
+            assert res[i] == r, (i, res[i], r)
+            if r > 0:
+                assert outs[i][:r].tobytes() == want[:r], i
+    finally:
+        lib.tyche_set_device(_lib.ALL_DEVICES)
