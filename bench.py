@@ -240,6 +240,17 @@ def e2e_host(pages_dev: torch.Tensor, n: int) -> dict:
     res["link_bound_decompress_gib_s"] = round(min(d2h, h2d * ratio), 3)
     res["frac_of_link_bound"] = {"compress": round(res["compress_gib_s"] / res["link_bound_compress_gib_s"], 3),
                                  "decompress": round(res["decompress_gib_s"] / res["link_bound_decompress_gib_s"], 3)}
+    # the same with the smaller direction's bytes moving at the probe's bidirectional rate (both
+    # directions at once) and the rest of the larger direction alone at its own rate
+    bi = link["bidir_each_gib_s"]
+
+    def both_ways(big, small, rate_big):   # GiB/s of uncompressed pages for `big` and `small` bytes
+        t = small / bi + (big - small) / rate_big
+        return nbytes / GIB / t
+    comp_b = nbytes / ratio
+    res["link_bound_bidir_gib_s"] = {"compress": round(both_ways(nbytes / GIB, comp_b / GIB, h2d), 3),
+                                     "decompress": round(both_ways(nbytes / GIB, comp_b / GIB, d2h), 3)}
+    res["frac_of_bidir_bound"] = {k: round(res[f"{k}_gib_s"] / v, 3) for k, v in res["link_bound_bidir_gib_s"].items()}
     return res
 
 
