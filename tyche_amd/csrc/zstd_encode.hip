@@ -171,7 +171,8 @@ constexpr uint32_t kTabBytes = 3u * kCtWords * 4u;   // 1152
 constexpr uint32_t kPblkWords = 4;   // parse blocks: page start, page end, first sequence, sequences
 constexpr uint32_t kAreaHead = 16u + kMaxBlk * kBlkWords * 4u + kMaxBlk * kPblkWords * 4u;
 // area: [0] emitted blocks, [1] parse blocks | block records | parse blocks | tables |
-//       sequence codes (16 B, pass B) | the parse's sequences (8 B, pass A2)
+//       sequence records (8 B, pass B; the region keeps 16 B per sequence, the split parse's
+//       scratch) | the parse's sequences (8 B, pass A2)
 __host__ __device__ inline uint32_t enc_rec_cap(uint32_t in_cap) { return in_cap / 4u + 64u; }
 __host__ __device__ inline size_t enc_area_bytes(uint32_t in_cap) {
     return ((size_t)kAreaHead + (size_t)kMaxBlk * kTabBytes + (size_t)enc_rec_cap(in_cap) * 24u + 255u) & ~(size_t)255u;
@@ -207,6 +208,33 @@ __device__ __forceinline__ SeqCode seq_code_at(const Enc &e, uint32_t i) {
     const uint2 r = e.seq[i];
     const uint32_t ll = r.x & 0xFFFFu, off = r.x >> 16, rc = r.y >> 16;
     return seq_code(ll, r.y & 0xFFFFu, rc ? rc : off + 3u);
+}
+
+// Pass A2's record of a sequence for pass B, 8 bytes (round 6; 16-byte records of codes and
+// extra-bit values before, 2x the HBM bytes between the passes): the literal length, the match
+// length - 3 and the offset code (pages < 64 KiB: 16, 16 and 17 bits) with the LL and ML codes,
+//   x = ll | llc << 16 | mlc << 22 | (ofcode >> 16) << 28,  y = (ml - 3) | (ofcode & 0xFFFF) << 16;
+// pass B derives the extra-bit counts and values as seq_code does (ZSTD_seqToCodes,
+// zstd_compress.c:535-556).
+__device__ __forceinline__ uint2 seq_record_at(const Enc &e, uint32_t i) {
+    const uint2 r = e.seq[i];
+    const uint32_t ll = r.x & 0xFFFFu, off = r.x >> 16, rc = r.y >> 16, ml = r.y & 0xFFFFu;
+    const uint32_t ofcode = rc ? rc : off + 3u;
+    const SeqCode c = seq_code(ll, ml, ofcode);
+    return make_uint2(ll | (c.llc << 16) | (c.mlc << 22) | ((ofcode >> 16) << 28), (ml - 3u) | (ofcode << 16));
+}
+__device__ __forceinline__ SeqCode seq_record_codes(uint2 r) {
+    SeqCode c;
+    const uint32_t ll = r.x & 0xFFFFu, m = r.y & 0xFFFFu, ofcode = (r.y >> 16) | ((r.x >> 28) << 16);
+    c.llc = (r.x >> 16) & 63u;
+    c.mlc = (r.x >> 22) & 63u;
+    c.llb = ll < 16u ? 0u : ll < 64u ? 1u + (ll >= 24u) + (ll >= 32u) + (ll >= 48u) : hb(ll);
+    c.mlb = m < 32u ? 0u : m < 128u ? 1u + (m >= 40u) + (m >= 48u) + (m >= 64u) + (m >= 96u) : hb(m);
+    c.ofc = hb(ofcode);
+    c.llv = ll & ((1u << c.llb) - 1u);
+    c.mlv = m & ((1u << c.mlb) - 1u);
+    c.ofv = ofcode & ((1u << c.ofc) - 1u);
+    return c;
 }
 
 // Offset_Value of every sequence of the block against the repeat history
@@ -589,15 +617,11 @@ __device__ __forceinline__ bool emit_block(Enc &e, uint32_t bend, bool last, uin
         SPROF_MARK(4);
         SPROF_ADD(9, n);
         if (e.area) {
-            // pass A: the codes and tables go to the area, the bitstream's bound stays open
-            uint4 *R = area_rec(e.area) + e.nrec;
+            // pass A: the sequences' records and the tables go to the area, the bitstream's bound stays open
+            uint2 *R = (uint2 *)area_rec(e.area) + e.nrec;
             for (uint32_t g = 0; g < n; g += kWave) {
                 const uint32_t i = g + lane;
-                if (i < n) {
-                    const SeqCode c = seq_code_at(e, i);
-                    R[i] = make_uint4(c.llc | (c.mlc << 8) | (c.ofc << 16), c.llv | (c.llb << 24), c.mlv | (c.mlb << 24),
-                                      c.ofv);
-                }
+                if (i < n) R[i] = seq_record_at(e, i);
             }
             uint32_t *T = area_tab(e.area, e.nblk);
             const huf::SmallCT *ts[3] = {&tll, &tof, &tml};
@@ -1314,7 +1338,7 @@ static_assert(kFseSlot.words % 4u == 0, "slot of 16-byte pieces");
 constexpr uint32_t kFsePf = TYCHE_ZSTD_FSE_PF;   // sequence records in flight per lane (pass B)
 // ZSTD_compressSequences' bitstream (zstd_compress.c:695-735) for n >= 1
 // sequences; the same steps as emit_block's wave-uniform loop.  Returns its size.
-__device__ uint32_t fse_lane(uint8_t *out, const uint4 *R, uint32_t n, const uint32_t *T) {
+__device__ uint32_t fse_lane(uint8_t *out, const uint2 *R, uint32_t n, const uint32_t *T) {
     const uint32_t *tll = T + kFseSlot.sll, *tof = T + kFseSlot.sof, *tml = T + kFseSlot.sml;
     const uint8_t *xll = (const uint8_t *)(T + kFseSlot.xll), *xof = (const uint8_t *)(T + kFseSlot.xof),
                   *xml = (const uint8_t *)(T + kFseSlot.xml);
@@ -1329,19 +1353,20 @@ __device__ uint32_t fse_lane(uint8_t *out, const uint4 *R, uint32_t n, const uin
     // the records are loaded kFsePf steps ahead (a ring of registers, slot u of each pass of
     // kFsePf steps): at one wave per two SIMDs (the LDS slots) a load one step ahead left
     // every step waiting on HBM
-    uint4 q[kFsePf];
+    uint2 q[kFsePf];
 #pragma unroll
-    for (uint32_t u = 0; u < kFsePf; u++) q[u] = u < n ? R[n - 1u - u] : make_uint4(0, 0, 0, 0);
+    for (uint32_t u = 0; u < kFsePf; u++) q[u] = u < n ? R[n - 1u - u] : make_uint2(0, 0);
     for (uint32_t base = n; base > 0; base = base > kFsePf ? base - kFsePf : 0u) {
 #pragma unroll
         for (uint32_t u = 0; u < kFsePf; u++) {
             const bool live = base > u;
             const uint32_t i = base - 1u - u;   // wraps when !live: every use below is gated
-            const uint4 r = q[u];
+            const uint2 r = q[u];
             if (live && i >= kFsePf) q[u] = R[i - kFsePf];
             if (!live) continue;
-            const uint32_t llc = r.x & 0xFFu, mlc = (r.x >> 8) & 0xFFu, ofc = r.x >> 16;
-            const uint32_t llb = r.y >> 24, mlb = r.z >> 24;
+            const SeqCode c = seq_record_codes(r);
+            const uint32_t llc = c.llc, mlc = c.mlc, ofc = c.ofc;
+            const uint32_t llb = c.llb, mlb = c.mlb;
             if (i == n - 1u) {
                 sml = lct_init2(tml, xml, mlc);
                 sof = lct_init2(tof, xof, ofc);
@@ -1352,9 +1377,9 @@ __device__ uint32_t fse_lane(uint8_t *out, const uint4 *R, uint32_t n, const uin
                 lct_encode(b, sll, tll, xll, llc);
                 if (ofc + mlb + llb >= 64u - 7u - (9u + 9u + 8u)) lb_flush(b, s);
             }
-            lb_add(b, r.y & 0xFFFFFFu, llb);
-            lb_add(b, r.z & 0xFFFFFFu, mlb);
-            lb_add(b, r.w, ofc);
+            lb_add(b, c.llv, llb);
+            lb_add(b, c.mlv, mlb);
+            lb_add(b, c.ofv, ofc);
             lb_flush(b, s);
         }
     }
@@ -1398,7 +1423,7 @@ __global__ __launch_bounds__(64) void zstd_fse_kernel(tyche_batch_t b, size_t fi
         } else {
             for (uint32_t w = 0; w < 3u * kCtWords / 4u; w++) ((u32x4 *)lt)[w] = ((const u32x4 *)g)[w];
         }
-        B[3] = fse_lane(dst + B[0] + 3u + B[2], area_rec(area) + B[5], B[4], lt);
+        B[3] = fse_lane(dst + B[0] + 3u + B[2], (const uint2 *)area_rec(area) + B[5], B[4], lt);
     }
 }
 
