@@ -553,7 +553,63 @@ __device__ bool dtable_states(uint32_t *cells, uint16_t *next, uint32_t table_lo
 // ------------------------------------------------------------ Huffman (HUF_readStats + HUF_readDTableX2)
 // Reads the table description at in[ip, ip+n).  Returns header bytes or < 0;
 // fills W.huf and sets tlog.
-__device__ int32_t huf_read_table(const Work &W, int32_t ip, int32_t n, uint32_t &tlog, uint32_t lane) {
+// HUF_readDTableX2's fill (huf_decompress.c): symbol s of weight w takes (1 << w) >> 1 entries after
+// the earlier symbols of that weight, entry = s | nbBits << 8 (nbBits = tlog + 1 - w); rank[k] is the
+// number of symbols of weight k (the last, implied weight included).  The whole wave; hpair only for
+// tlog 12 (see below).
+__device__ void huf_fill(const uint8_t *w, uint32_t nsym, uint32_t tlog, const uint32_t (&rank)[13], uint16_t *huf,
+                         uint8_t *hpair, uint32_t lane) {
+    // rank starts (HUF_readDTableX2 "Prepare ranks")
+    uint32_t start[13];
+    {
+        uint32_t nx = 0;
+#pragma unroll
+        for (uint32_t k = 1; k < 13; k++) {
+            start[k] = nx;
+            if (k < tlog + 1u) nx += rank[k] << (k - 1);
+        }
+    }
+    for (uint32_t s0 = 0; s0 < nsym; s0 += kWave) {
+        const uint32_t s = s0 + lane;
+        const uint32_t wv = s < nsym ? w[s] : 0u;
+        uint32_t at = 0;
+#pragma unroll
+        for (uint32_t k = 1; k < 13; k++) {
+            const uint64_t m = __ballot(s < nsym && wv == k);
+            if (wv == k) at = start[k] + (__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0)) << (k - 1));
+            start[k] += (uint32_t)__builtin_popcountll(m) << (k - 1);
+        }
+        // tableLog 12: the table is indexed by 11 bits.  Symbols of weight >= 2
+        // start at even 12-bit positions and cover an even number of them, so
+        // they halve exactly; the weight-1 symbols (12-bit codes, an even number
+        // of them, first in the table) go to hpair and their 11-bit entries say
+        // "12 bits, see hpair".
+        const bool t12 = tlog == 12u;
+        uint32_t len = s < nsym && wv ? (1u << wv) >> 1 : 0u;
+        const uint16_t e = (uint16_t)(s | ((tlog + 1u - wv) << 8));
+        if (t12) {
+            if (len == 1u) {
+                hpair[at] = (uint8_t)s;
+                huf[at >> 1] = (uint16_t)(12u << 8);
+                len = 0;
+            }
+            at >>= 1;
+            len >>= 1;
+        }
+        if (len <= 16) {
+            for (uint32_t i = 0; i < len; i++) huf[at + i] = e;
+        }
+        uint64_t big = __ballot(len > 16);
+        while (big) {
+            const uint32_t l = (uint32_t)__builtin_ctzll(big);
+            big &= big - 1;
+            const uint32_t bat = rdlane(at, l), blen = rdlane(len, l), be = rdlane((uint32_t)e, l);
+            for (uint32_t i = lane; i < blen; i += kWave) huf[bat + i] = (uint16_t)be;
+        }
+    }
+}
+
+__device__ int32_t huf_read_table(const Work &W, int32_t ip, int32_t n, uint32_t &tlog, uint32_t &nsym_out, uint32_t lane) {
     const uint8_t *in = W.in;
     if (n < 1) return kErr;
     int32_t isize = (int32_t)u8u(in, ip);
@@ -664,55 +720,8 @@ __device__ int32_t huf_read_table(const Work &W, int32_t ip, int32_t n, uint32_t
     if (rank[1] < 2 || (rank[1] & 1u)) return kErr;
     __builtin_amdgcn_wave_barrier();
     const uint32_t nsym = osize + 1u;
-    // rank starts (HUF_readDTableX2 "Prepare ranks")
-    uint32_t start[13];
-    {
-        uint32_t nx = 0;
-#pragma unroll
-        for (uint32_t k = 1; k < 13; k++) {
-            start[k] = nx;
-            if (k < tlog + 1u) nx += rank[k] << (k - 1);
-        }
-    }
-    // fill: symbol s of weight w takes (1 << w) >> 1 entries after the earlier symbols of that weight
-    for (uint32_t s0 = 0; s0 < nsym; s0 += kWave) {
-        const uint32_t s = s0 + lane;
-        const uint32_t wv = s < nsym ? W.w[s] : 0u;
-        uint32_t at = 0;
-#pragma unroll
-        for (uint32_t k = 1; k < 13; k++) {
-            const uint64_t m = __ballot(s < nsym && wv == k);
-            if (wv == k) at = start[k] + (__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0)) << (k - 1));
-            start[k] += (uint32_t)__builtin_popcountll(m) << (k - 1);
-        }
-        // tableLog 12: the table is indexed by 11 bits.  Symbols of weight >= 2
-        // start at even 12-bit positions and cover an even number of them, so
-        // they halve exactly; the weight-1 symbols (12-bit codes, an even number
-        // of them, first in the table) go to hpair and their 11-bit entries say
-        // "12 bits, see hpair".
-        const bool t12 = tlog == 12u;
-        uint32_t len = s < nsym && wv ? (1u << wv) >> 1 : 0u;
-        const uint16_t e = (uint16_t)(s | ((tlog + 1u - wv) << 8));
-        if (t12) {
-            if (len == 1u) {
-                W.hpair[at] = (uint8_t)s;
-                W.huf[at >> 1] = (uint16_t)(12u << 8);
-                len = 0;
-            }
-            at >>= 1;
-            len >>= 1;
-        }
-        if (len <= 16) {
-            for (uint32_t i = 0; i < len; i++) W.huf[at + i] = e;
-        }
-        uint64_t big = __ballot(len > 16);
-        while (big) {
-            const uint32_t l = (uint32_t)__builtin_ctzll(big);
-            big &= big - 1;
-            const uint32_t bat = rdlane(at, l), blen = rdlane(len, l), be = rdlane((uint32_t)e, l);
-            for (uint32_t i = lane; i < blen; i += kWave) W.huf[bat + i] = (uint16_t)be;
-        }
-    }
+    nsym_out = nsym;
+    huf_fill(W.w, nsym, tlog, rank, W.huf, W.hpair, lane);
     __builtin_amdgcn_wave_barrier();
     return isize + 1;
 }
@@ -954,6 +963,7 @@ struct SeqTables {
     // the table in W.huf was not published), tables published, literal jobs written
     int32_t huf_pub;
     uint32_t nhuf, nlj;
+    uint32_t huf_nsym;   // symbols (weights) of the Huffman table in force
 };
 
 // ZSTD_buildSeqTable (zstd_decompress.c:693-724).  Returns bytes read or < 0.
@@ -1155,41 +1165,44 @@ __device__ int32_t decode_block(const Work &W, SeqTables &T, const Ent &E, uint3
                 J[2] = (uint32_t)lsize;
                 J[3] = lat;
                 J[4] = (uint32_t)T.huf_pub;
-                J[5] = T.huf_log | ((single ? 1u : 0u) << 8);
+                J[5] = T.huf_log | ((single ? 1u : 0u) << 8) | (T.huf_nsym << 16);
             }
             T.nlj++;
             return true;
         };
-        auto publish = [&](uint32_t tl) {   // after a new table: publish it if it fits a slot
+        // after a new table: publish it if it fits a slot -- its symbols' weights (round 6: at most 256
+        // bytes instead of the 2^tl-entry decoding table, which zstd_lit_kernel rebuilds in LDS)
+        auto publish = [&](uint32_t tl, uint32_t nsym) {
             T.huf_pub = -1;
+            T.huf_nsym = nsym;
             if (!(kSplit && E.defer_lit) || tl > 11u || T.nhuf >= kMaxHuf) return;
-            uint16_t *g = E.hufs + T.nhuf * kHufCells;
-            for (uint32_t i = lane; i < (1u << tl); i += kWave) g[i] = W.huf[i];
+            uint8_t *g = (uint8_t *)(E.hufs + T.nhuf * kHufCells);
+            for (uint32_t i = lane; i < nsym; i += kWave) g[i] = W.w[i];
             T.huf_pub = (int32_t)(T.nhuf * kHufCells);
             T.nhuf++;
         };
         if (ltype == 3u) {
             ok = defer(cs, csize) || huf_decode<kSplit>(W, cs, csize, single, (uint32_t)lsize, T.huf_log, dst, lane);
         } else if (single) {
-            uint32_t tl;
-            const int32_t hs = huf_read_table(W, cs, csize, tl, lane);
+            uint32_t tl, nsym = 0;
+            const int32_t hs = huf_read_table(W, cs, csize, tl, nsym, lane);
             SPROF_MARK(7);
             ok = hs >= 0 && hs < csize;
             if (ok) {
                 T.huf_log = tl;
-                publish(tl);
+                publish(tl, nsym);
                 ok = defer(cs + hs, csize - hs) || huf_decode<kSplit>(W, cs + hs, csize - hs, true, (uint32_t)lsize, tl, dst, lane);
             }
         } else {
             ok = lsize != 0 && csize < lsize && csize > 1;
             if (ok) {
-                uint32_t tl;
-                const int32_t hs = huf_read_table(W, cs, csize, tl, lane);
+                uint32_t tl, nsym = 0;
+                const int32_t hs = huf_read_table(W, cs, csize, tl, nsym, lane);
                 SPROF_MARK(7);
                 ok = hs >= 0 && hs < csize;
                 if (ok) {
                     T.huf_log = tl;
-                    publish(tl);
+                    publish(tl, nsym);
                     ok = defer(cs + hs, csize - hs) ||
                          huf_decode<kSplit>(W, cs + hs, csize - hs, false, (uint32_t)lsize, tl, dst, lane);
                 }
@@ -2271,7 +2284,8 @@ __global__ __launch_bounds__(64) void zstd_seqexec_kernel(tyche_batch_t b, size_
 // Pass 1 decoded a section's 1 or 4 Huffman streams in lanes 0-3 of its wave, ~480 cycles per
 // symbol (the whole wave's instruction stream for 4 lanes: 60 % of pass 1, tools/zstd_phases.py).
 // Here lane 4g + s decodes stream s of page g of the workgroup, kGroups pages per wave: the
-// page's published table is copied to its group's LDS slot (kHufCells x 16 bit) and each lane
+// page's decoding table is rebuilt from its published weights in its group's LDS slot (kHufCells
+// x 16 bit) and each lane
 // walks its stream from global memory (huf_decode's reader, checks and end test), writing
 // whole aligned 8-byte words of the literal buffer.  A failed stream fails the page.
 template <uint32_t kGroups>
@@ -2280,6 +2294,7 @@ __global__ __launch_bounds__(64) void zstd_lit_kernel(tyche_batch_t b, size_t fi
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t lane = threadIdx.x, g = lane >> 2, s = lane & 3u;
     uint16_t *tab = (uint16_t *)smem + min(g, kGroups - 1u) * kHufCells;
+    uint8_t *wbuf = smem + kGroups * kHufCells * 2u;   // a table's weights (<= 256 bytes)
     const size_t j = (size_t)blockIdx.x * kGroups + g;
     const bool act = g < kGroups && j < count && st[j] >= 0;
     Ent E;
@@ -2297,7 +2312,7 @@ __global__ __launch_bounds__(64) void zstd_lit_kernel(tyche_batch_t b, size_t fi
     bool ok = true;
     for (uint32_t q = 0; q < maxj; q++) {
         const bool has = act && q < njobs;
-        uint32_t cs = 0, n = 0, lsize = 0, lat = 0, toff = 0, tlog = 0;
+        uint32_t cs = 0, n = 0, lsize = 0, lat = 0, toff = 0, tlog = 0, nsym = 0;
         bool single = false;
         if (has) {
             const uint32_t *J = E.litjobs + 4u + q * kLitJobWords;
@@ -2308,13 +2323,30 @@ __global__ __launch_bounds__(64) void zstd_lit_kernel(tyche_batch_t b, size_t fi
             toff = J[4];
             tlog = J[5] & 255u;
             single = ((J[5] >> 8) & 1u) != 0u;
-            // the group's four lanes copy the table, a quarter each (16-byte pieces; a slot holds
-            // kHufCells entries, so a tiny table copies one whole piece)
-            const uint32_t pieces = max(1u, (2u << tlog) / 16u), per = (pieces + 3u) / 4u;
-            const u32x4 *gt = (const u32x4 *)(E.hufs + toff);
-            for (uint32_t k = s * per; k < min(pieces, (s + 1u) * per); k++) ((u32x4 *)tab)[k] = gt[k];
+            nsym = J[5] >> 16;
         }
-        __builtin_amdgcn_wave_barrier();
+        // each group's decoding table from its published weights, the whole wave per group (the
+        // weights through the wave's LDS scratch, then HUF_readDTableX2's fill, huf_fill): 256
+        // bytes read per table instead of the 2^tlog-entry table
+        const uint64_t gmask = __ballot(has && s == 0u);
+        for (uint64_t gm = gmask; gm; gm &= gm - 1) {
+            const uint32_t l = (uint32_t)__builtin_ctzll(gm), gg = l >> 2;
+            const uint32_t gn = rdlane(nsym, l), glog = rdlane(tlog, l), gtoff = rdlane(toff, l);
+            const uint32_t lo = rdlane((uint32_t)(uintptr_t)E.hufs, l), hi = rdlane((uint32_t)((uintptr_t)E.hufs >> 32), l);
+            const uint8_t *gw = (const uint8_t *)((const uint16_t *)(uintptr_t)(((uint64_t)hi << 32) | lo) + gtoff);
+            for (uint32_t i = lane; i < gn; i += kWave) wbuf[i] = gw[i];
+            __builtin_amdgcn_wave_barrier();
+            uint32_t rank[13];
+#pragma unroll
+            for (uint32_t k = 0; k < 13; k++) rank[k] = 0;
+            for (uint32_t s0 = 0; s0 < gn; s0 += kWave) {
+                const uint32_t wv = s0 + lane < gn ? wbuf[s0 + lane] : 0u;
+#pragma unroll
+                for (uint32_t k = 1; k < 12; k++) rank[k] += (uint32_t)__builtin_popcountll(__ballot(s0 + lane < gn && wv == k));
+            }
+            huf_fill(wbuf, gn, glog, rank, (uint16_t *)smem + gg * kHufCells, nullptr, lane);
+            __builtin_amdgcn_wave_barrier();
+        }
         if (has && ok) {
             int32_t sstart = 0, slen = 0;
             uint32_t o0 = 0, cnt = 0;
@@ -2561,7 +2593,7 @@ hipError_t launch_zstd_decode(const tyche_batch_t &b, uint32_t in_cap, uint32_t 
             int32_t *stp = st;
             void *args[] = {(void *)&b, &f, &nn, &in_cap, &out_cap, &wsp, &pb, &stp};
             (void)hipLaunchKernel(kl, dim3((unsigned)((n + kgroups - 1) / kgroups)), dim3(64), args,
-                                  (size_t)kgroups * kHufCells * 2u, s);
+                                  (size_t)kgroups * kHufCells * 2u + 256u, s);
         }
         if (!seqexec)
             hipLaunchKernelGGL(zstd_seq_kernel, dim3((unsigned)((n + kWave - 1) / kWave)), dim3(kWave), kSeqLds, s, b,
