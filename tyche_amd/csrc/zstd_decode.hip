@@ -209,6 +209,14 @@ struct Work {
     int16_t *norm;       // 256 normalized counts
     uint16_t *next;      // 256 symbolNext counters
     uint8_t *w;          // 256 Huffman weights
+    // Pass 1 (zstd_entropy_kernel, round 6) stages the frame lazily: only the byte ranges its parse
+    // reads (stage_range), so the literal streams and sequence bitstreams it hands to
+    // zstd_lit_kernel and zstd_seqexec_kernel cross HBM once.  gsrc == nullptr: the whole frame was
+    // staged up front (the other kernels).
+    const uint8_t *gsrc;   // the frame in global memory
+    uint32_t ghead;        // gsrc & 15 (in = 16-byte-aligned stage + ghead)
+    int32_t gL;            // frame bytes
+    mutable int32_t wlo, whi;   // [wlo, whi): the staged window the parse is in
 };
 
 // 8 bytes at any LDS byte address from three aligned dwords: an unaligned LDS
@@ -222,6 +230,31 @@ __device__ __forceinline__ uint64_t ld64(const uint8_t *p) {
     return (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, s) | ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, s) << 32);
 }
 __device__ __forceinline__ uint32_t highbit(uint32_t v) { return 31u - (uint32_t)__builtin_clz(v); }
+
+// Makes frame bytes [a, e) readable in W.in (lazy staging, Work::gsrc; the whole wave).  The parse
+// reads forward only: a range starting inside the current window extends it, one starting past
+// it opens a new window (the bytes skipped -- deferred sections -- are never read in pass 1).
+// Bytes at and past L read as the kStreamPad zeros, as with the whole frame staged.
+__device__ __forceinline__ void stage_range(const Work &W, int32_t a, int32_t e, uint32_t lane) {
+    if (!W.gsrc) return;
+    a = max(a, 0);
+    e = min(e, W.gL);
+    if (e <= a || (a >= W.wlo && e <= W.whi)) return;
+    const bool extend = a >= W.wlo && a <= W.whi;
+    const int32_t from = extend ? W.whi : a;
+    const uint32_t v0 = (W.ghead + (uint32_t)from) >> 4, v1 = (W.ghead + (uint32_t)e + 15u) >> 4;
+    const u32x4 *g = (const u32x4 *)((uintptr_t)W.gsrc - W.ghead);
+    u32x4 *l = (u32x4 *)(const_cast<uint8_t *>(W.in) - W.ghead);
+    for (uint32_t v = v0 + lane; v < v1; v += kWave) l[v] = gload_nt(g + v);
+    __builtin_amdgcn_wave_barrier();
+    const int32_t top = (int32_t)(v1 * 16u - W.ghead);   // staged through here (the last vector whole)
+    if (top > W.gL) {   // that vector carried bytes past L over the zero pad: restore it
+        if (lane < kStreamPad / 4) lds_st32(const_cast<uint8_t *>(W.in) + W.gL + lane * 4, 0u);
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (!extend) W.wlo = a;
+    W.whi = min(top, W.gL);
+}
 
 // Wave-uniform reads of the staged frame: the value goes through
 // v_readfirstlane so everything computed from it stays in SGPRs.
@@ -970,6 +1003,9 @@ struct SeqTables {
 __device__ int32_t seq_table(const Work &W, uint32_t *cells, uint32_t &log, uint32_t type, uint32_t max,
                              uint32_t max_log, int32_t ip, int32_t n, const DTab &def, uint32_t def_log,
                              bool flag_repeat, uint32_t lane) {
+    // an RLE byte, or a normalized-count header: its reader stops after at most ~80 bytes (53
+    // symbols of <= 10 bits and the repeat flags, FSE_readNCount)
+    if (type == 1 || type == 2) stage_range(W, ip, ip + min(n, 256), lane);
     if (type == 1) {   // set_rle
         if (n < 1) return kErr;
         const uint32_t sym = u8u(W.in, ip);
@@ -1127,6 +1163,7 @@ __device__ int32_t decode_block(const Work &W, SeqTables &T, const Ent &E, uint3
     if (n >= (int32_t)kBlockMax) return kErr;
     // ---- literals section (ZSTD_decodeLiteralsBlock)
     if (n < 3) return kErr;
+    stage_range(W, ip, ip + 5, lane);   // the section header (<= 5 bytes)
     const uint32_t b0 = u8u(in, ip);
     const uint32_t ltype = b0 & 3u, lhl = (b0 >> 2) & 3u;
     const uint8_t *lit;
@@ -1181,32 +1218,35 @@ __device__ int32_t decode_block(const Work &W, SeqTables &T, const Ent &E, uint3
             T.huf_pub = (int32_t)(T.nhuf * kHufCells);
             T.nhuf++;
         };
+        // streams decoded here are staged first; deferred ones never are (lazy staging).  One
+        // decode site for the three cases: the stream's range and table log
+        int32_t hat = cs, hlen = csize;
+        uint32_t htl = T.huf_log;
+        bool here = false;
         if (ltype == 3u) {
-            ok = defer(cs, csize) || huf_decode<kSplit>(W, cs, csize, single, (uint32_t)lsize, T.huf_log, dst, lane);
-        } else if (single) {
-            uint32_t tl, nsym = 0;
-            const int32_t hs = huf_read_table(W, cs, csize, tl, nsym, lane);
-            SPROF_MARK(7);
-            ok = hs >= 0 && hs < csize;
-            if (ok) {
-                T.huf_log = tl;
-                publish(tl, nsym);
-                ok = defer(cs + hs, csize - hs) || huf_decode<kSplit>(W, cs + hs, csize - hs, true, (uint32_t)lsize, tl, dst, lane);
-            }
+            ok = true;
+            here = !defer(cs, csize);
         } else {
-            ok = lsize != 0 && csize < lsize && csize > 1;
+            ok = single || (lsize != 0 && csize < lsize && csize > 1);
             if (ok) {
                 uint32_t tl, nsym = 0;
+                stage_range(W, cs, cs + min(csize, 144), lane);   // the table description: <= 1 + 128 bytes
                 const int32_t hs = huf_read_table(W, cs, csize, tl, nsym, lane);
                 SPROF_MARK(7);
                 ok = hs >= 0 && hs < csize;
                 if (ok) {
                     T.huf_log = tl;
                     publish(tl, nsym);
-                    ok = defer(cs + hs, csize - hs) ||
-                         huf_decode<kSplit>(W, cs + hs, csize - hs, false, (uint32_t)lsize, tl, dst, lane);
+                    hat = cs + hs;
+                    hlen = csize - hs;
+                    htl = tl;
+                    here = !defer(hat, hlen);
                 }
             }
+        }
+        if (ok && here) {
+            stage_range(W, hat, hat + hlen, lane);
+            ok = huf_decode<kSplit>(W, hat, hlen, single, (uint32_t)lsize, htl, dst, lane);
         }
         if (!ok) return kErr;
         T.lit_entropy = true;
@@ -1221,6 +1261,7 @@ __device__ int32_t decode_block(const Work &W, SeqTables &T, const Ent &E, uint3
         else { lh = 1; lsize = (int32_t)(b0 >> 3); }
         if (ltype == 0u) {   // raw
             if (lh + lsize > n) return kErr;
+            stage_range(W, ip + lh, ip + lh + lsize, lane);
             lit = in + ip + lh;
             lit_in_window = false;
             lcons = lh + lsize;
@@ -1242,6 +1283,7 @@ __device__ int32_t decode_block(const Work &W, SeqTables &T, const Ent &E, uint3
                 if (lat + (uint32_t)lsize > E.lcap) return kErr;
                 dst = E.lit + lat;
             }
+            stage_range(W, ip + lh, ip + lh + 1, lane);
             const uint8_t v = in[ip + lh];
             for (int32_t i = (int32_t)lane; i < lsize; i += (int32_t)kWave) dst[i] = v;
             lit = dst;
@@ -1256,6 +1298,7 @@ __device__ int32_t decode_block(const Work &W, SeqTables &T, const Ent &E, uint3
     int32_t sp = ip + lcons;
     const int32_t send = ip + n;
     if (send - sp < 1) return kErr;
+    stage_range(W, sp, sp + 4, lane);   // nbSeq (<= 3 bytes) and the modes byte
     int32_t nbseq = (int32_t)u8u(in, sp++);
     int32_t op0 = op, lp = 0;
     uint32_t cmd_at = 0, nseq_all = 0;
@@ -1319,6 +1362,7 @@ __device__ int32_t decode_block(const Work &W, SeqTables &T, const Ent &E, uint3
         }
         // ---- sequence loop (ZSTD_decompressSequences)
         T.fse_entropy = true;
+        stage_range(W, sp, send, lane);
         BitD b;
         if (!bitd_init_u(b, in, sp, send - sp)) return kErr;
         uint32_t sll = bitd_read(b, T.ll_log);
@@ -1430,6 +1474,7 @@ template <bool kSplit>
 __device__ int32_t decode_frame(const Work &W, const Ent &E, int32_t L, int32_t cap, uint32_t lane, bool jobs = false) {
     const uint8_t *in = W.in;
     if (L < 9) return kErr;
+    stage_range(W, 0, 18, lane);   // the frame header (<= 18 bytes)
     const uint32_t magic = u32u(in, 0);
     const uint32_t fhd = u8u(in, 4);
     const uint32_t did = fhd & 3u, single = (fhd >> 5) & 1u, fcs_id = fhd >> 6;
@@ -1483,6 +1528,7 @@ __device__ int32_t decode_frame(const Work &W, const Ent &E, int32_t L, int32_t 
     uint32_t ecur = 0, litc = 0;
     for (;;) {
         if (remaining < 3) return kErr;
+        stage_range(W, ip, ip + 3, lane);
         const uint32_t bh = u8u(in, ip) | (u8u(in, ip + 1) << 8) | (u8u(in, ip + 2) << 16);
         const uint32_t last = bh & 1u, btype = (bh >> 1) & 3u, csize0 = bh >> 3;
         if (btype == 3u) return kErr;
@@ -1499,6 +1545,7 @@ __device__ int32_t decode_frame(const Work &W, const Ent &E, int32_t L, int32_t 
                 const uint32_t at = lit_place(litc, (uint32_t)op, (uint32_t)csize);
                 if (at + (uint32_t)csize > E.lcap) return kErr;
                 if (ecur >= E.ecap) return E.over;
+                stage_range(W, ip, ip + csize, lane);
                 lds_to_lit(E.lit + at, in, ip, csize, lane);
                 put_cmd(E, ecur++, kCmdRaw | (at << 2), (uint32_t)csize, 0u, lane);
                 litc = at + (uint32_t)csize;
@@ -1508,6 +1555,7 @@ __device__ int32_t decode_frame(const Work &W, const Ent &E, int32_t L, int32_t 
             dec = csize;
         } else {
             if ((int64_t)csize0 > (int64_t)(cap - op)) return kErrDst;
+            stage_range(W, ip, ip + 1, lane);
             const uint8_t v = in[ip];
             if constexpr (kSplit) {
                 if (ecur >= E.ecap) return E.over;
@@ -1527,6 +1575,7 @@ __device__ int32_t decode_frame(const Work &W, const Ent &E, int32_t L, int32_t 
     uint32_t sum = 0;
     if (checksum) {
         if (remaining < 4) return kErr;
+        stage_range(W, ip, ip + 4, lane);
         sum = lds_ld32(in + ip);
         if constexpr (!kSplit)
             if (sum != xxh64_lds(W.win, (uint32_t)op, lane)) return kErr;
@@ -1574,6 +1623,10 @@ __global__ __launch_bounds__(64) void zstd_decode_kernel(tyche_batch_t b, size_t
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t lane = threadIdx.x;
     Work W;
+    W.gsrc = nullptr;
+    W.ghead = 0;
+    W.gL = 0;
+    W.wlo = W.whi = 0;
     W.win = smem;
     W.huf = (uint16_t *)(smem + lay.off_huf);
     W.hpair = smem + lay.off_hp;
@@ -2412,10 +2465,14 @@ __global__ __launch_bounds__(64) void zstd_lit_kernel(tyche_batch_t b, size_t fi
 __global__ __launch_bounds__(64) void zstd_entropy_kernel(tyche_batch_t b, size_t first, size_t count, uint32_t in_cap,
                                                           uint32_t out_cap, Layout lay, uint8_t *ws, size_t ws_page,
                                                           int32_t *st, unsigned *ctr, bool use_jobs, bool fused,
-                                                          bool defer_lit) {
+                                                          bool defer_lit, bool lazy_stage) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t lane = threadIdx.x;
     Work W;
+    W.gsrc = nullptr;
+    W.ghead = 0;
+    W.gL = 0;
+    W.wlo = W.whi = 0;
     W.win = nullptr;
     W.huf = (uint16_t *)(smem + lay.off_huf);
     W.hpair = smem + lay.off_hp;
@@ -2434,18 +2491,28 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(tyche_batch_t b, size_
             rv = kResultTooLarge;
         } else {
             WAVE_SYNC();
-            const uint32_t head = stage_in(p.src, p.src_len, stage, lane, kWave);
+            // (lazy staging, Work::gsrc: nothing staged yet but the zero pad)
+            const uint32_t head = (uint32_t)((uintptr_t)p.src & 15u);
             uint8_t *in = stage + head;
-            WAVE_SYNC();
             if (lane < kStreamPad / 4) lds_st32(in + p.src_len + lane * 4, 0u);
             WAVE_SYNC();
             W.in = in;
+            W.gsrc = lazy_stage ? p.src : nullptr;
+            W.ghead = head;
+            W.gL = (int32_t)p.src_len;
+            if (!lazy_stage) {
+                (void)stage_in(p.src, p.src_len, stage, lane, kWave);
+                WAVE_SYNC();
+                if (lane < kStreamPad / 4) lds_st32(in + p.src_len + lane * 4, 0u);
+                WAVE_SYNC();
+            }
             Ent E = ent_of(ws + j * ws_page, in_cap, out_cap, fused);
             E.defer_lit = fused && defer_lit;
             SPROF_DECL
             // jobs first; a page whose jobs do not fit is redone with the chains inline (fused
             // layout: by the one-wave kernel after pass 2)
             for (bool jobs = use_jobs || fused;; jobs = false) {
+                W.wlo = W.whi = 0;   // (a redo parses from the frame's start again)
                 rv = decode_frame<true>(W, E, (int32_t)p.src_len, (int32_t)p.dst_cap, lane, jobs);
                 if (rv == kRetryInline && fused) rv = kRetryFused;
                 if (!(rv == kRetryInline && jobs)) break;
@@ -2541,6 +2608,8 @@ hipError_t launch_zstd_decode(const tyche_batch_t &b, uint32_t in_cap, uint32_t 
     const bool slots6 = knob("ZSTD_SEQ_SLOTS", 7) == 6;
     // literal streams lane-per-stream (zstd_lit_kernel) between pass 1 and zstd_seqexec_kernel
     const long lit_groups = knob("ZSTD_LIT_LANES", 8);   // pages per wave: 8 / 16; 0 = streams in pass 1
+    // TYCHE_ZSTD_LAZY_STAGE 0: pass 1 stages every frame whole (A/B; default 1: only the ranges it reads)
+    const bool lazy_stage = knob("ZSTD_LAZY_STAGE", 1) != 0;
     const bool lit_lanes = seqexec && lit_groups > 0;
     const void *kl = lit_groups == 16 ? (const void *)zstd_lit_kernel<16> : (const void *)zstd_lit_kernel<8>;
     const uint32_t kgroups = lit_groups == 16 ? 16u : 8u;
@@ -2584,7 +2653,7 @@ hipError_t launch_zstd_decode(const tyche_batch_t &b, uint32_t in_cap, uint32_t 
             WorkCounter ctr(s, g1 < n);
             if (!ctr.get()) return hipErrorOutOfMemory;
             hipLaunchKernelGGL(zstd_entropy_kernel, dim3((unsigned)g1), dim3(kWave), l1.total, s, b, first, n, in_cap,
-                               out_cap, l1, ent, page_bytes, st, ctr.get(), use_jobs, seqexec, lit_lanes);
+                               out_cap, l1, ent, page_bytes, st, ctr.get(), use_jobs, seqexec, lit_lanes, lazy_stage);
         }
         if (lit_lanes) {
             (void)prepare_launch(kl);
