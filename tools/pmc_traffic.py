@@ -1,16 +1,17 @@
 """Turns the two rocprofv3 PMC passes of tools/run_codec.py into HBM bytes per page.
 
-    python tools/pmc_traffic.py profiles/r01_pmc_fetch_size.csv profiles/r01_pmc_write_size.csv \
-        --pages 262144 --page-len 16384 -o profiles/r01_traffic.json
+    python tools/pmc_traffic.py <reads.csv> <WRITE_SIZE.csv> --pages 1048576 --page-len 16384 -o out.json
 
-Correction: FETCH_SIZE and WRITE_SIZE are in KiB.  On gfx950 FETCH_SIZE reports
-half the bytes of a wide coalesced 16-B/lane streaming read (MI355X_MICROARCH.md,
-HBM section): the kernels that stage whole pages into LDS read that way, so
-their read bytes are 2 * FETCH_SIZE.  The lane-per-page LZ4 decoder reads
-scattered 16-byte pieces, one lane per page; for that pattern the calibration
-probe (tools/probes/fetch_calib.hip, profiles/r02_fetch_calib.json) shows
-FETCH_SIZE = 64 B per fabric read request = the bytes actually fetched, so its
-read bytes are 1 * FETCH_SIZE.  Each kernel's figure is
+Reads: the `rdreq` pass of tools/gpu_traffic.sh (TCC_EA0_RDREQ_DRAM_32B_sum: the L2's
+memory-side read requests in 32-byte units, a 128-byte request counted as 4), read bytes =
+32 * that count.  Round 6's calibration (tools/probes/fetch_calib.hip,
+profiles/r06_fetch_calib.json) shows every gfx950 read request is a 128-byte line --
+coalesced 16/8/1-byte streams and scattered 16-byte loads alike (TCC_EA0_RDREQ_sum * 4 =
+TCC_EA0_RDREQ_DRAM_32B_sum, TCC_BUBBLE_sum ~0) -- and that FETCH_SIZE counts each at 64
+bytes: with a FETCH_SIZE pass instead, read bytes = 2 * FETCH_SIZE for every kernel.
+(Rounds 2-5 took the lane LZ4 decoder's FETCH_SIZE at face value -- r02_fetch_calib.json
+read a 16-byte random load's one request as 64 bytes -- and so reported half its reads.)
+WRITE_SIZE is in KiB and taken as is.  Each kernel's figure is
 its bytes per codec call divided by the pages of a call.  A call is one
 dispatch, except where --calls says how many calls the kernel's dispatches
 make up (the LZ4 decoder runs two size-class launches per call:
@@ -39,26 +40,25 @@ KERNELS = {"lz4_encode": ("lz4_encode_",), "lz4_decode": ("lz4_decode_",),
            "zlib_encode": ("zlib_deflate_kernel",), "zlib_decode": ("zlib_inflate_kernel",)}
 
 
-# read-byte factor per FETCH_SIZE byte, by kernel symbol (see the module docstring)
-SCATTERED = ("lz4_decode_ring_kernel", "lz4_decode_ringlb_kernel", "lz4_decode_lane_kernel", "lz4_decode_quad_kernel",
-             "lz4_decode_lc_kernel",
-             "zstd_seq_kernel",
-             "zstd_fse_kernel", "zstd_exec_lane_kernel", "zstd_seqexec_kernel", "zstd_lit_kernel")
+RDREQ = "TCC_EA0_RDREQ_DRAM_32B_sum"
 
 
 def per_dispatch(path, counter):
-    """kernel -> list of per-dispatch values; FETCH_SIZE already scaled to read bytes (KiB)."""
+    """kernel -> list of per-dispatch values in KiB: read bytes for `reads` (RDREQ * 32 B, or
+    2 * FETCH_SIZE), WRITE_SIZE as is."""
     acc = defaultdict(float)
     names = {}
-    for r in csv.DictReader(open(path)):
+    rows = list(csv.DictReader(open(path)))
+    if counter == "reads":
+        counter = RDREQ if any(r["Counter_Name"] == RDREQ for r in rows) else "FETCH_SIZE"
+    for r in rows:
         if r["Counter_Name"] != counter:
             continue
         acc[r["Dispatch_Id"]] += float(r["Counter_Value"])
         names[r["Dispatch_Id"]] = r["Kernel_Name"]
     out = defaultdict(list)
     for d, v in acc.items():
-        if counter == "FETCH_SIZE":
-            v *= 1.0 if any(sym in names[d] for sym in SCATTERED) else 2.0
+        v *= 32.0 / 1024.0 if counter == RDREQ else 2.0 if counter == "FETCH_SIZE" else 1.0
         for k, syms in KERNELS.items():
             if any(sym in names[d] for sym in syms):
                 out[k].append(v)
@@ -76,7 +76,7 @@ def _head():
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("fetch")
+    ap.add_argument("fetch", help="the rdreq (or FETCH_SIZE) pass")
     ap.add_argument("write")
     ap.add_argument("--pages", type=int, required=True)
     ap.add_argument("--page-len", type=int, default=16384)
@@ -84,12 +84,12 @@ def main():
     ap.add_argument("--calls", action="append", default=[], help="kernel=N: its dispatches make up N codec calls")
     a = ap.parse_args()
     calls = {kv.split("=")[0]: int(kv.split("=")[1]) for kv in a.calls}
-    f = per_dispatch(a.fetch, "FETCH_SIZE")
+    f = per_dispatch(a.fetch, "reads")
     w = per_dispatch(a.write, "WRITE_SIZE")
     res = {"pages_per_call": a.pages, "page_len": a.page_len, "calls": calls,
-           "formula": "(c*FETCH_SIZE + WRITE_SIZE) * 1024 / pages; c = 2 for the page-staging kernels (gfx950 "
-                      "half count of coalesced streaming reads), 1 for the scattered lane LZ4 decoder (calibrated, "
-                      "tools/probes/fetch_calib.hip)",
+           "formula": "(read bytes + WRITE_SIZE * 1024) / pages; read bytes = 32 * TCC_EA0_RDREQ_DRAM_32B_sum "
+                      "(or 2 * 1024 * FETCH_SIZE: gfx950 read requests are 128-byte lines counted at 64 B, every "
+                      "access pattern, profiles/r06_fetch_calib.json)",
            "bytes_per_page": {}, "read_bytes_per_page": {}, "write_bytes_per_page": {},
            # the kernel code these counters describe: bench.py reports `traffic` only while this
            # digest equals the digest of the sources it runs (a stale summary must not look current)
