@@ -145,6 +145,7 @@ struct Enc {
     uint32_t nblk, nrec; // blocks and sequence records written to the area
     uint32_t rec_cap;
     uint32_t logcap;     // 7: LL / OF / ML table logs FSE_optimalTableLog's, capped at 7 / 6 / 7; 6: fixed 6 / 5 / 6
+    const uint32_t *psum;   // split encode: the parse block's literal bytes, span and extra bits (nullptr: summed here)
     __device__ uint32_t nrec_cap() const { return rec_cap; }
 };
 
@@ -168,7 +169,10 @@ constexpr uint32_t kStateBits = 7u + 6u + 7u;   // bits one sequence's three sta
 // table log, then the 128 stateTable bytes (values < 256)
 constexpr uint32_t kCtWords = 64u + 32u;
 constexpr uint32_t kTabBytes = 3u * kCtWords * 4u;   // 1152
-constexpr uint32_t kPblkWords = 4;   // parse blocks: page start, page end, first sequence, sequences
+// parse blocks: page start, page end, first sequence, sequences, then the block's literal bytes,
+// sequence span (page bytes) and extra bits at raw offsets, which pass A2 would otherwise read the
+// sequence list again for (emit_block's sizes; round 6), one word spare
+constexpr uint32_t kPblkWords = 8;
 constexpr uint32_t kAreaHead = 16u + kMaxBlk * kBlkWords * 4u + kMaxBlk * kPblkWords * 4u;
 // area: [0] emitted blocks, [1] parse blocks | block records | parse blocks | tables |
 //       sequence records (8 B, pass B; the region keeps 16 B per sequence, the split parse's
@@ -215,14 +219,7 @@ __device__ __forceinline__ SeqCode seq_code_at(const Enc &e, uint32_t i) {
 // length - 3 and the offset code (pages < 64 KiB: 16, 16 and 17 bits) with the LL and ML codes,
 //   x = ll | llc << 16 | mlc << 22 | (ofcode >> 16) << 28,  y = (ml - 3) | (ofcode & 0xFFFF) << 16;
 // pass B derives the extra-bit counts and values as seq_code does (ZSTD_seqToCodes,
-// zstd_compress.c:535-556).
-__device__ __forceinline__ uint2 seq_record_at(const Enc &e, uint32_t i) {
-    const uint2 r = e.seq[i];
-    const uint32_t ll = r.x & 0xFFFFu, off = r.x >> 16, rc = r.y >> 16, ml = r.y & 0xFFFFu;
-    const uint32_t ofcode = rc ? rc : off + 3u;
-    const SeqCode c = seq_code(ll, ml, ofcode);
-    return make_uint2(ll | (c.llc << 16) | (c.mlc << 22) | ((ofcode >> 16) << 28), (ml - 3u) | (ofcode << 16));
-}
+// zstd_compress.c:535-556).  Written by resolve_repeats.
 __device__ __forceinline__ SeqCode seq_record_codes(uint2 r) {
     SeqCode c;
     const uint32_t ll = r.x & 0xFFFFu, m = r.y & 0xFFFFu, ofcode = (r.y >> 16) | ((r.x >> 28) << 16);
@@ -250,8 +247,13 @@ __device__ __forceinline__ SeqCode seq_record_codes(uint2 r) {
 //                 off[q] != r1 before q; swaps and E keep r2).
 // Returns the history after the block through h0..h2 (committed only if the
 // block is emitted compressed: raw blocks leave the decoder's history alone).
+// The same pass counts the LL / ML / OF codes into e.htab (0 / 64 / 128, zeroed by the
+// caller) and hands each sequence on: split encode (e.area), its 8-byte record to R for
+// pass B; one-kernel encode, its repeat code into e.seq[i].y for the bitstream below
+// (round 6: one pass over the block's sequences instead of three -- the repeat codes
+// written back, the histogram and the records each read the list again)
 __device__ __forceinline__ void resolve_repeats(const Enc &e, uint32_t n, uint32_t lane, uint32_t &h0, uint32_t &h1,
-                                                uint32_t &h2) {
+                                                uint32_t &h2, uint2 *R) {
     uint32_t c0 = e.r0, c1 = e.r1, c2 = e.r2;
     const uint64_t below = (1ull << lane) - 1ull;
     for (uint32_t g = 0; g < n; g += kWave) {
@@ -273,7 +275,18 @@ __device__ __forceinline__ void resolve_repeats(const Enc &e, uint32_t n, uint32
         uint32_t rc;
         if (ll) rc = off == r0b ? 1u : off == r1b ? 2u : off == r2b ? 3u : 0u;
         else rc = off == r1b ? 1u : off == r2b ? 2u : 0u;
-        if (i < n) e.seq[i].y = (r.y & 0xFFFFu) | (rc << 16);
+#ifdef TYCHE_NO_RESOLVE
+        rc = 0;   // timing ablation: raw offsets only
+#endif
+        if (i < n) {
+            const uint32_t ml = r.y & 0xFFFFu, ofcode = rc ? rc : off + 3u;
+            const SeqCode c = seq_code(ll, ml, ofcode);
+            atomicAdd(&e.htab[c.llc], 1u);
+            atomicAdd(&e.htab[64u + c.mlc], 1u);
+            atomicAdd(&e.htab[128u + c.ofc], 1u);
+            if (R) R[i] = make_uint2(ll | (c.llc << 16) | (c.mlc << 22) | ((ofcode >> 16) << 28), (ml - 3u) | (ofcode << 16));
+            else e.seq[i].y = ml | (rc << 16);
+        }
         // the history after the group's last sequence
         const uint32_t last = min(n - g, kWave) - 1u;
         const uint32_t o_l = rdlane(off, last), r0_l = rdlane(r0b, last), r1_l = rdlane(r1b, last),
@@ -488,9 +501,14 @@ __device__ uint32_t huf_literals(Enc &e, uint32_t n, uint32_t trail, uint32_t li
 __device__ __forceinline__ bool emit_block(Enc &e, uint32_t bend, bool last, uint32_t lane) {
     SPROF_DECL
     const uint32_t n = e.nseq, blen = bend - e.bstart;
-    // ---- per-sequence sizes (lane-parallel over 64-sequence groups)
+    // ---- per-sequence sizes (lane-parallel over 64-sequence groups; the split parse sums them)
     uint32_t lit_sum = 0, span = 0, xbits = 0;
-    for (uint32_t g = 0; g < n; g += kWave) {
+    if (e.psum) {
+        lit_sum = __builtin_amdgcn_readfirstlane(e.psum[0]);
+        span = __builtin_amdgcn_readfirstlane(e.psum[1]);
+        xbits = __builtin_amdgcn_readfirstlane(e.psum[2]);
+    }
+    for (uint32_t g = 0; !e.psum && g < n; g += kWave) {
         const uint32_t i = g + lane;
         uint32_t ll = 0, ml = 0, xb = 0;
         if (i < n) {
@@ -553,23 +571,11 @@ __device__ __forceinline__ bool emit_block(Enc &e, uint32_t bend, bool last, uin
     o += nsh;
     uint32_t h0 = e.r0, h1 = e.r1, h2 = e.r2;
     if (n) {
-#ifndef TYCHE_NO_RESOLVE
-        resolve_repeats(e, n, lane, h0, h1, h2);
-#else
-        for (uint32_t i = lane; i < n; i += kWave) e.seq[i].y &= 0xFFFFu;   // timing ablation: raw offsets only
-#endif
-        __builtin_amdgcn_wave_barrier();
-        // ---- code histograms (htab is free once the literals are out): LL at 0, ML at 64, OF at 128
+        // ---- repeat codes, code histograms (htab is free once the literals are out: LL at 0, ML at
+        // 64, OF at 128) and, split encode, the sequences' records for pass B
         for (uint32_t k = lane; k < 192u; k += kWave) e.htab[k] = 0;
         __builtin_amdgcn_wave_barrier();
-        for (uint32_t g = 0; g < n; g += kWave) {
-            if (g + lane < n) {
-                const SeqCode c = seq_code_at(e, g + lane);
-                atomicAdd(&e.htab[c.llc], 1u);
-                atomicAdd(&e.htab[64u + c.mlc], 1u);
-                atomicAdd(&e.htab[128u + c.ofc], 1u);
-            }
-        }
+        resolve_repeats(e, n, lane, h0, h1, h2, e.area ? (uint2 *)area_rec(e.area) + e.nrec : nullptr);
         __builtin_amdgcn_wave_barrier();
         // ---- tables: per-block distributions from 64 sequences on (MIN_SEQ_FOR_DYNAMIC_FSE)
         // at FSE_optimalTableLog's accuracy capped at LL 7 / OF 6 / ML 7 (the reference caps at
@@ -617,12 +623,8 @@ __device__ __forceinline__ bool emit_block(Enc &e, uint32_t bend, bool last, uin
         SPROF_MARK(4);
         SPROF_ADD(9, n);
         if (e.area) {
-            // pass A: the sequences' records and the tables go to the area, the bitstream's bound stays open
-            uint2 *R = (uint2 *)area_rec(e.area) + e.nrec;
-            for (uint32_t g = 0; g < n; g += kWave) {
-                const uint32_t i = g + lane;
-                if (i < n) R[i] = seq_record_at(e, i);
-            }
+            // pass A: the tables go to the area (the records went with resolve_repeats), the
+            // bitstream's bound stays open
             uint32_t *T = area_tab(e.area, e.nblk);
             const huf::SmallCT *ts[3] = {&tll, &tof, &tml};
 #pragma unroll
@@ -749,6 +751,7 @@ __device__ __forceinline__ int32_t encode_page(const uint8_t *in, uint32_t L, ui
     e.nrec = 0;
     e.rec_cap = 0;
     e.logcap = logcap;
+    e.psum = nullptr;
     auto sink = [&](const uint2 *r, uint32_t n, uint32_t anchor) -> bool {
         uint32_t ls, ll, ml, off;
         lzp::decode_record(r, n, anchor, lane, ls, ll, ml, off, TYCHE_SINK_BACK ? in : nullptr);
@@ -793,21 +796,33 @@ __device__ __forceinline__ int32_t parse_to_area_with(uint32_t L, uint8_t *area,
                                                       Parse &&parse, const uint8_t *sink_in) {
     uint2 *S = area_seq(area, rec_cap);
     uint32_t nseq = 0, bseq = 0, bstart = 0, cursor = 0, npb = 0;
+    uint32_t a_lit = 0, a_span = 0, a_xb = 0;   // this lane's share of the block's sums
     auto put_pblk = [&](uint32_t bend) {
+        const uint32_t lit = huf::wave_sum(a_lit), span = huf::wave_sum(a_span), xb = huf::wave_sum(a_xb);
         if (lane == 0) {
             uint32_t *P = area_pblk(area, npb);
             P[0] = bstart;
             P[1] = bend;
             P[2] = bseq;
             P[3] = nseq - bseq;
+            P[4] = lit;
+            P[5] = span;
+            P[6] = xb;
         }
+        a_lit = a_span = a_xb = 0;
         npb++;
     };
     auto sink = [&](const uint2 *r, uint32_t n, uint32_t anchor) -> bool {
         uint32_t ls, ll, ml, off;
         lzp::decode_record(r, n, anchor, lane, ls, ll, ml, off, sink_in);   // (sink_in: lz_parse.h back_at)
         if (nseq + n > rec_cap) return false;
-        if (lane < n) S[nseq + lane] = make_uint2(ll | (off << 16), ml);
+        if (lane < n) {
+            S[nseq + lane] = make_uint2(ll | (off << 16), ml);
+            const SeqCode c = seq_code(ll, ml, off + 3u);   // emit_block's bound: no repeat offsets
+            a_lit += ll;
+            a_span += ll + ml;
+            a_xb += c.llb + c.mlb + c.ofc;
+        }
         nseq += n;
         const uint2 lastr = r[n - 1];
         cursor = (lastr.x & 0xFFFFu) + (lastr.y & 0xFFFFu);
@@ -878,6 +893,7 @@ __device__ __forceinline__ int32_t emit_page(const uint8_t *src, uint32_t L, uin
         const uint32_t bend = __builtin_amdgcn_readfirstlane(P[1]);
         e.seq = S + __builtin_amdgcn_readfirstlane(P[2]);
         e.nseq = __builtin_amdgcn_readfirstlane(P[3]);
+        e.psum = P + 4;
         if (!emit_block(e, bend, k + 1u == npb, lane)) return 0;
     }
     if (lane == 0) ((uint32_t *)area)[0] = e.nblk;
@@ -1199,12 +1215,18 @@ __global__ __launch_bounds__(kNW * 64) void zstd_parse_split_kernel(tyche_batch_
                 uint32_t npb = 0, pos = 0;
                 for (uint32_t bs = 0; bs < total || npb == 0; bs += kZBlk) {
                     const uint32_t cnt = min(kZBlk, total - bs);
-                    uint32_t span = 0;
+                    uint32_t span = 0, lit = 0, xb = 0;
                     for (uint32_t j = lane; j < cnt; j += kWave) {
                         const uint2 q = S[bs + j];
-                        span += (q.x & 0xFFFFu) + q.y;
+                        const uint32_t ll = q.x & 0xFFFFu;
+                        const SeqCode c = seq_code(ll, q.y, (q.x >> 16) + 3u);   // emit_block's bound
+                        span += ll + q.y;
+                        lit += ll;
+                        xb += c.llb + c.mlb + c.ofc;
                     }
                     span = huf::wave_sum(span);
+                    lit = huf::wave_sum(lit);
+                    xb = huf::wave_sum(xb);
                     const bool last = bs + kZBlk >= total;
                     if (lane == 0) {
                         uint32_t *P = area_pblk(area, npb);
@@ -1212,6 +1234,9 @@ __global__ __launch_bounds__(kNW * 64) void zstd_parse_split_kernel(tyche_batch_
                         P[1] = last ? L : pos + span;
                         P[2] = bs;
                         P[3] = cnt;
+                        P[4] = lit;
+                        P[5] = span;
+                        P[6] = xb;
                     }
                     pos += span;
                     npb++;
