@@ -146,6 +146,7 @@ struct Enc {
     uint32_t rec_cap;
     uint32_t logcap;     // 7: LL / OF / ML table logs FSE_optimalTableLog's, capped at 7 / 6 / 7; 6: fixed 6 / 5 / 6
     const uint32_t *psum;   // split encode: the parse block's literal bytes, span and extra bits (nullptr: summed here)
+    const uint8_t *lit;     // split encode: the block's literals, in order, from pass A1 (nullptr: gathered from in)
     __device__ uint32_t nrec_cap() const { return rec_cap; }
 };
 
@@ -175,8 +176,11 @@ constexpr uint32_t kTabBytes = 3u * kCtWords * 4u;   // 1152
 constexpr uint32_t kPblkWords = 8;
 constexpr uint32_t kAreaHead = 16u + kMaxBlk * kBlkWords * 4u + kMaxBlk * kPblkWords * 4u;
 // area: [0] emitted blocks, [1] parse blocks | block records | parse blocks | tables |
-//       sequence records (8 B, pass B; the region keeps 16 B per sequence, the split parse's
-//       scratch) | the parse's sequences (8 B, pass A2)
+//       scratch (16 B per sequence: the split parse's per-part sequence slices, then the
+//       page's literals in order) | the parse's sequences (8 B; pass A2 overwrites each with
+//       its record for pass B as it reads it).  Round 6: pass A1 copies the literals out of
+//       the page it holds in LDS, so that pass A2 reads them once and contiguously instead of
+//       gathering them from the page in HBM.
 __host__ __device__ inline uint32_t enc_rec_cap(uint32_t in_cap) { return in_cap / 4u + 64u; }
 __host__ __device__ inline size_t enc_area_bytes(uint32_t in_cap) {
     return ((size_t)kAreaHead + (size_t)kMaxBlk * kTabBytes + (size_t)enc_rec_cap(in_cap) * 24u + 255u) & ~(size_t)255u;
@@ -190,6 +194,48 @@ __device__ __forceinline__ uint32_t *area_tab(uint8_t *a, uint32_t k) {
 }
 __device__ __forceinline__ uint4 *area_rec(uint8_t *a) { return (uint4 *)(a + kAreaHead + (size_t)kMaxBlk * kTabBytes); }
 __device__ __forceinline__ uint2 *area_seq(uint8_t *a, uint32_t rec_cap) { return (uint2 *)(area_rec(a) + rec_cap); }
+__device__ __forceinline__ uint8_t *area_lit(uint8_t *a) { return (uint8_t *)area_rec(a); }   // (16 rec_cap > in_cap)
+
+// Copies the literal runs [ls, ls + ll) of the wave's lanes, in lane order, from the page in
+// LDS to dst[0, sum of ll), 64 bytes a step; returns the sum of ll.  Byte j's run is the last
+// one starting at or before j.  With `map` (64 dwords of LDS): the runs starting in the step
+// mark their position there with their source delta (page position - literal position), and a
+// prefix max over the map gives each byte its run -- one LDS round trip a step; without it, a
+// binary search over the lanes' exclusive prefix (six dependent lane permutes a step; it cost
+// the split parse 9 % of its time, round 6).  Lanes with ll = 0 are never a byte's run.
+__device__ __forceinline__ uint32_t copy_runs(const uint8_t *in, uint32_t ls, uint32_t ll, uint8_t *dst, uint32_t lane,
+                                              uint32_t *map) {
+    const uint32_t inc = (uint32_t)wave_incl_sum((int32_t)ll), excl = inc - ll;
+    const uint32_t total = rdlane(inc, kWave - 1);
+    if (map) {
+        uint32_t carry = 0;   // the delta of the run the previous step ended in
+        for (uint32_t j0 = 0; j0 < total; j0 += kWave) {
+            map[lane] = 0;
+            __builtin_amdgcn_wave_barrier();
+            if (ll && excl >= j0 && excl < j0 + kWave) map[excl - j0] = ((excl - j0 + 1u) << 16) | (ls - excl);
+            __builtin_amdgcn_wave_barrier();
+            const uint32_t k = (uint32_t)wave_incl_max((int32_t)map[lane]);
+            const uint32_t d = k ? (k & 0xFFFFu) : carry;
+            const uint32_t j = j0 + lane;
+            if (j < total) dst[j] = in[j + d];
+            carry = rdlane(d, kWave - 1);
+            __builtin_amdgcn_wave_barrier();
+        }
+        return total;
+    }
+    for (uint32_t j0 = 0; j0 < total; j0 += kWave) {
+        const uint32_t j = j0 + lane;
+        uint32_t o = 0;
+#pragma unroll
+        for (uint32_t step = kWave / 2; step; step >>= 1) {
+            const uint32_t c = o + step;
+            if ((uint32_t)__shfl((int)excl, (int)c) <= j) o = c;
+        }
+        const uint32_t src = (uint32_t)__shfl((int)ls, (int)o) + j - (uint32_t)__shfl((int)excl, (int)o);
+        if (j < total) dst[j] = in[src];
+    }
+    return total;
+}
 // a block record (lane 0)
 __device__ __forceinline__ void put_blk(Enc &e, uint32_t g_start, uint32_t g_len, uint32_t pre, uint32_t fse, uint32_t n,
                                         uint32_t rec, uint32_t flags, uint32_t lane) {
@@ -215,7 +261,8 @@ __device__ __forceinline__ SeqCode seq_code_at(const Enc &e, uint32_t i) {
 }
 
 // Pass A2's record of a sequence for pass B, 8 bytes (round 6; 16-byte records of codes and
-// extra-bit values before, 2x the HBM bytes between the passes): the literal length, the match
+// extra-bit values before, 2x the HBM bytes between the passes; in place of the sequence since
+// round 6): the literal length, the match
 // length - 3 and the offset code (pages < 64 KiB: 16, 16 and 17 bits) with the LL and ML codes,
 //   x = ll | llc << 16 | mlc << 22 | (ofcode >> 16) << 28,  y = (ml - 3) | (ofcode & 0xFFFF) << 16;
 // pass B derives the extra-bit counts and values as seq_code does (ZSTD_seqToCodes,
@@ -360,10 +407,14 @@ __device__ uint32_t huf_literals(Enc &e, uint32_t n, uint32_t trail, uint32_t li
     __builtin_amdgcn_wave_barrier();
     uint8_t *dst = e.dst;
     uint32_t *hist = e.htab;
-    for_each_literal(e, n, trail, lane, [&](uint32_t j, uint32_t v) {
-        dst[scr + j] = (uint8_t)v;
-        atomicAdd(&hist[v], 1u);
-    });
+    if (e.lit) {   // split encode: the literals are in the area already (no scratch copy)
+        for (uint32_t j = lane; j < lit_total; j += kWave) atomicAdd(&hist[e.lit[j]], 1u);
+    } else {
+        for_each_literal(e, n, trail, lane, [&](uint32_t j, uint32_t v) {
+            dst[scr + j] = (uint8_t)v;
+            atomicAdd(&hist[v], 1u);
+        });
+    }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");   // scratch stores visible, L1 invalidated
     __builtin_amdgcn_wave_barrier();
     uint32_t c[4], l[4], code[4];
@@ -437,6 +488,7 @@ __device__ uint32_t huf_literals(Enc &e, uint32_t n, uint32_t trail, uint32_t li
     // ---- streams: symbols last to first, bits LSB first (HUF_compress1X_usingCTable), end mark
     uint32_t sp = wpos + whdr + (single ? 0u : 6u);
     const uint32_t seg = (lit_total + 3u) / 4u;
+    const uint8_t *lits = e.lit ? e.lit : e.dst + scr;
     for (uint32_t st = 0; st < nst; st++) {
         const uint32_t a = single ? 0u : st * seg;
         const uint32_t bnd = single ? lit_total : (st == 3u ? lit_total : min(lit_total, (st + 1u) * seg));
@@ -447,7 +499,7 @@ __device__ uint32_t huf_literals(Enc &e, uint32_t n, uint32_t trail, uint32_t li
         for (uint32_t k0 = 0; a + k0 < bnd; k0 += kWave) {
             const bool act = a + k0 + lane < bnd;
             uint32_t ent = 0;
-            if (act) ent = e.htab[e.dst[scr + bnd - 1u - (k0 + lane)]];
+            if (act) ent = e.htab[lits[bnd - 1u - (k0 + lane)]];
             const uint32_t len = ent >> 16, cv = ent & 0xFFFFu;
             const int32_t bi = wave_incl_sum((int32_t)len);
             const uint32_t b = nbits + (uint32_t)bi - len;
@@ -555,7 +607,11 @@ __device__ __forceinline__ bool emit_block(Enc &e, uint32_t bend, bool last, uin
         if (lane < fl) e.dst[o + lane] = (uint8_t)(h >> (8u * lane));
         uint8_t *dst = e.dst;
         const uint32_t lo0 = o + fl;
-        for_each_literal(e, n, trail, lane, [&](uint32_t j, uint32_t v) { dst[lo0 + j] = (uint8_t)v; });
+        if (e.lit) {
+            for (uint32_t j = lane; j < lit_total; j += kWave) dst[lo0 + j] = e.lit[j];
+        } else {
+            for_each_literal(e, n, trail, lane, [&](uint32_t j, uint32_t v) { dst[lo0 + j] = (uint8_t)v; });
+        }
         lsec = fl + lit_total;
     }
     o += lsec;
@@ -575,7 +631,7 @@ __device__ __forceinline__ bool emit_block(Enc &e, uint32_t bend, bool last, uin
         // 64, OF at 128) and, split encode, the sequences' records for pass B
         for (uint32_t k = lane; k < 192u; k += kWave) e.htab[k] = 0;
         __builtin_amdgcn_wave_barrier();
-        resolve_repeats(e, n, lane, h0, h1, h2, e.area ? (uint2 *)area_rec(e.area) + e.nrec : nullptr);
+        resolve_repeats(e, n, lane, h0, h1, h2, e.area ? e.seq : nullptr);   // (split: records in place)
         __builtin_amdgcn_wave_barrier();
         // ---- tables: per-block distributions from 64 sequences on (MIN_SEQ_FOR_DYNAMIC_FSE)
         // at FSE_optimalTableLog's accuracy capped at LL 7 / OF 6 / ML 7 (the reference caps at
@@ -752,6 +808,7 @@ __device__ __forceinline__ int32_t encode_page(const uint8_t *in, uint32_t L, ui
     e.rec_cap = 0;
     e.logcap = logcap;
     e.psum = nullptr;
+    e.lit = nullptr;
     auto sink = [&](const uint2 *r, uint32_t n, uint32_t anchor) -> bool {
         uint32_t ls, ll, ml, off;
         lzp::decode_record(r, n, anchor, lane, ls, ll, ml, off, TYCHE_SINK_BACK ? in : nullptr);
@@ -790,13 +847,17 @@ static_assert(kZBlk >= kWave && (65536u / 4u + kZBlk - 1u) / kZBlk + 1u <= kMaxB
 // Pass A1: the parse of one page (LDS, 64 zero bytes after) into the area: the
 // sequences, and blocks cut where encode_page's sink cuts them.  Returns 1, or
 // 0 when a bound is exceeded (the page is then stored uncompressed by the caller).
-// parse(sink) runs the parse over the page and returns its last anchor.
+// parse(sink) runs the parse over the page and returns its last anchor.  The literals go
+// to the area's literal region as the sequences come (copy_runs from the page `in`).
 template <typename Parse>
-__device__ __forceinline__ int32_t parse_to_area_with(uint32_t L, uint8_t *area, uint32_t rec_cap, uint32_t lane,
-                                                      Parse &&parse, const uint8_t *sink_in) {
+__device__ __forceinline__ int32_t parse_to_area_with(const uint8_t *in, uint32_t L, uint8_t *area, uint32_t rec_cap,
+                                                      uint32_t lane, Parse &&parse, const uint8_t *sink_in,
+                                                      uint32_t *map) {
     uint2 *S = area_seq(area, rec_cap);
+    uint8_t *lits = area_lit(area);
     uint32_t nseq = 0, bseq = 0, bstart = 0, cursor = 0, npb = 0;
     uint32_t a_lit = 0, a_span = 0, a_xb = 0;   // this lane's share of the block's sums
+    uint32_t lpos = 0, blit = 0;                // literals copied; the block's first
     auto put_pblk = [&](uint32_t bend) {
         const uint32_t lit = huf::wave_sum(a_lit), span = huf::wave_sum(a_span), xb = huf::wave_sum(a_xb);
         if (lane == 0) {
@@ -808,8 +869,10 @@ __device__ __forceinline__ int32_t parse_to_area_with(uint32_t L, uint8_t *area,
             P[4] = lit;
             P[5] = span;
             P[6] = xb;
+            P[7] = blit;
         }
         a_lit = a_span = a_xb = 0;
+        blit = lpos;
         npb++;
     };
     auto sink = [&](const uint2 *r, uint32_t n, uint32_t anchor) -> bool {
@@ -823,6 +886,7 @@ __device__ __forceinline__ int32_t parse_to_area_with(uint32_t L, uint8_t *area,
             a_span += ll + ml;
             a_xb += c.llb + c.mlb + c.ofc;
         }
+        lpos += copy_runs(in, ls, ll, lits + lpos, lane, map);
         nseq += n;
         const uint2 lastr = r[n - 1];
         cursor = (lastr.x & 0xFFFFu) + (lastr.y & 0xFFFFu);
@@ -837,16 +901,18 @@ __device__ __forceinline__ int32_t parse_to_area_with(uint32_t L, uint8_t *area,
     };
     const uint32_t anchor = parse(sink);
     if (anchor == 0xFFFFFFFFu) return 0;
+    for (uint32_t j = lane; anchor + j < L; j += kWave) lits[lpos + j] = in[anchor + j];   // the last literals
     put_pblk(L);
     if (lane == 0) ((uint32_t *)area)[1] = npb;
     return 1;
 }
 template <int kW>
 __device__ __forceinline__ int32_t parse_to_area(const uint8_t *in, uint32_t L, uint16_t *table, uint2 *rec,
-                                                 uint8_t *area, uint32_t rec_cap, uint32_t lane) {
+                                                 uint8_t *area, uint32_t rec_cap, uint32_t lane, uint32_t *map) {
     return parse_to_area_with(
-        L, area, rec_cap, lane, [&](auto &sink) { return lzp::parse_page<true, false, kW>(in, L, table, rec, lane, sink); },
-        TYCHE_SINK_BACK ? in : nullptr);
+        in, L, area, rec_cap, lane,
+        [&](auto &sink) { return lzp::parse_page<true, false, kW>(in, L, table, rec, lane, sink); },
+        TYCHE_SINK_BACK ? in : nullptr, map);
 }
 
 // Pass A2: frame header and every block of the page from the area (the page
@@ -891,9 +957,11 @@ __device__ __forceinline__ int32_t emit_page(const uint8_t *src, uint32_t L, uin
         const uint32_t *P = area_pblk(area, k);
         e.bstart = __builtin_amdgcn_readfirstlane(P[0]);
         const uint32_t bend = __builtin_amdgcn_readfirstlane(P[1]);
-        e.seq = S + __builtin_amdgcn_readfirstlane(P[2]);
+        e.nrec = __builtin_amdgcn_readfirstlane(P[2]);   // the block's records replace its sequences
+        e.seq = S + e.nrec;
         e.nseq = __builtin_amdgcn_readfirstlane(P[3]);
         e.psum = P + 4;
+        e.lit = area_lit(area) + __builtin_amdgcn_readfirstlane(P[7]);
         if (!emit_block(e, bend, k + 1u == npb, lane)) return 0;
     }
     if (lane == 0) ((uint32_t *)area)[0] = e.nblk;
@@ -915,7 +983,8 @@ __global__ __launch_bounds__(64) void zstd_encode_kernel(tyche_batch_t b, size_t
     uint2 *seq = rec + kWave;                                          // kSeqCap block sequences
     uint32_t *htab = (uint32_t *)(seq + kSeqCap);                      // literal histogram / Huffman codes
     uint8_t *wts = (uint8_t *)(htab + kHtab);                          // Huffman weights
-    uint8_t *stage = kParse ? (uint8_t *)seq : wts + 256;               // A1: no block buffers
+    uint32_t *lmap = (uint32_t *)seq;                                   // A1: no block buffers, a copy map
+    uint8_t *stage = kParse ? (uint8_t *)seq + kWave * 4 : wts + 256;   // (A1: lds1 has room for it)
     const size_t stride = gridDim.x;
 
     size_t page = blockIdx.x;   // chunk-local
@@ -950,7 +1019,7 @@ __global__ __launch_bounds__(64) void zstd_encode_kernel(tyche_batch_t b, size_t
             WAVE_SYNC();
             in[p.src_len + lane] = 0;
             WAVE_SYNC();
-            if (kParse) rv = parse_to_area<kW>(in, p.src_len, table, rec, ws + page * ws_page, enc_rec_cap(in_cap), lane);
+            if (kParse) rv = parse_to_area<kW>(in, p.src_len, table, rec, ws + page * ws_page, enc_rec_cap(in_cap), lane, lmap);
             else rv = encode_page(in, p.src_len, table, map, rec, seq, htab, wts, p.dst, p.dst_cap, logcap, lane);
         }
         if (lane == 0) {
@@ -1018,9 +1087,9 @@ __global__ __launch_bounds__(128) void zstd_parse_pipe_kernel(tyche_batch_t b, s
         int32_t rv = kResultTooLarge;
         if (L <= in_cap) {   // uniform over the workgroup: both waves run the parse's barriers
             if (wave == 1) {
-                rv = parse_to_area_with(L, ws + page * ws_page, rec_cap, lane, [&](auto &sink) {
+                rv = parse_to_area_with(in, L, ws + page * ws_page, rec_cap, lane, [&](auto &sink) {
                     return lzp::parse_page_piped(in, L, table, rec, slots, &hdr->flag, 1u, lane, sink);
-                }, nullptr);   // (the piped parse's records carry their extension)
+                }, nullptr, nullptr);   // (the piped parse's records carry their extension)
             } else {
                 auto none = [](const uint2 *, uint32_t, uint32_t) -> bool { return true; };
                 (void)lzp::parse_page_piped(in, L, table, rec, slots, &hdr->flag, 0u, lane, none);
@@ -1071,6 +1140,7 @@ struct ZSplitHdr {
     uint32_t n[kNW];        // sequences of part w
     uint32_t cursor[kNW];   // end of part w's last match (its start if none)
     uint32_t ok[kNW];       // part w's sequences fit its slice
+    uint32_t lit[kNW];      // part w's literal bytes (before its first run's extension)
 };
 template <uint32_t kNW>
 constexpr size_t zsplit_hdr_bytes() { return (sizeof(ZSplitHdr<kNW>) + 63) & ~(size_t)63; }
@@ -1161,18 +1231,21 @@ __global__ __launch_bounds__(kNW * 64) void zstd_parse_split_kernel(tyche_batch_
                 auto drop = [&](const uint2 *, uint32_t, uint32_t) -> bool { return true; };
                 (void)lzp::parse_page<true, false, kZWays>(in, b0 + kLastLiterals, table, rec, lane, drop, wstart, rep);
             }
-            uint32_t nseq = 0;
+            uint32_t nseq = 0, a_lit = 0;
             auto sink = [&](const uint2 *r, uint32_t n, uint32_t anchor) -> bool {
                 uint32_t ls, ll, ml, off;
                 lzp::decode_record(r, n, anchor, lane, ls, ll, ml, off, TYCHE_SINK_BACK ? in : nullptr);
                 if (nseq + n > slice) return false;
                 if (lane < n) W[nseq + lane] = make_uint2(ll | (off << 16), ml);
+                a_lit += ll;   // (0 on lanes >= n)
                 nseq += n;
                 __builtin_amdgcn_wave_barrier();
                 return true;
             };
             const uint32_t cur = lzp::parse_page<true, false, kZWays>(in, Lp, table, rec, lane, sink, b0, rep);
+            a_lit = huf::wave_sum(a_lit);
             if (lane == 0) {
+                hdr->lit[wave] = a_lit;
                 hdr->ok[wave] = cur != 0xFFFFFFFFu ? 1u : 0u;
                 hdr->n[wave] = nseq;
                 hdr->cursor[wave] = nseq ? cur : b0;
@@ -1185,15 +1258,21 @@ __global__ __launch_bounds__(kNW * 64) void zstd_parse_split_kernel(tyche_batch_
         }
         __syncthreads();   // every part parsed
         bool ok = fits;
-        uint32_t off_w = 0, prev_end = 0, total = 0;
+        // lit_w / lit_all: the page's literal bytes before this part / in all parts, each part's
+        // first run extended back to the end of the last part before it with a sequence (pe)
+        uint32_t off_w = 0, prev_end = 0, total = 0, lit_w = 0, lit_all = 0, pe = 0;
         for (uint32_t w = 0; w < kNW; w++) {
             const uint32_t nw = rfl(hdr->n[w]);
             ok = ok && rfl(hdr->ok[w]);
+            const uint32_t lw = rfl(hdr->lit[w]) + (w > 0 && nw ? bnd(w) - pe : 0u);
             if (w < wave) {
                 off_w += nw;
+                lit_w += lw;
                 if (nw) prev_end = rfl(hdr->cursor[w]);
             }
             total += nw;
+            lit_all += lw;
+            if (nw) pe = rfl(hdr->cursor[w]);
         }
         uint2 *S = area_seq(area, rec_cap);
         if (ok) {   // the slices into place; the part's first literal run starts at the previous part's end
@@ -1204,7 +1283,25 @@ __global__ __launch_bounds__(kNW * 64) void zstd_parse_split_kernel(tyche_batch_
                 S[off_w + j] = q;
             }
         }
-        __syncthreads();
+        __syncthreads();   // the slices are free: the literal region takes their place
+        if (ok) {   // the part's literals, from the staged page to the literal region, in page order
+            const uint32_t nw = rfl(hdr->n[wave]);
+            uint8_t *lits = area_lit(area);
+            const uint2 *Sw = S + off_w;
+            uint32_t pos = prev_end, lo = lit_w;   // page position and literal offset of the next run
+            uint2 qn = lane < nw ? Sw[lane] : make_uint2(0u, 0u);   // the list a group ahead of the copy
+            for (uint32_t j0 = 0; j0 < nw; j0 += kWave) {
+                const uint32_t j = j0 + lane;
+                const uint2 q = qn;
+                qn = j + kWave < nw ? Sw[j + kWave] : make_uint2(0u, 0u);
+                const uint32_t ll = q.x & 0xFFFFu, sz = ll + q.y;
+                const uint32_t inc = (uint32_t)wave_incl_sum((int32_t)sz);
+                lo += copy_runs(in, pos + inc - sz, ll, lits + lo, lane, (uint32_t *)rec);   // (rec: free after the parse)
+                pos += rdlane(inc, kWave - 1);
+            }
+            if (wave == kNW - 1)   // the literals after the page's last match
+                for (uint32_t j = lane; pe + j < L; j += kWave) lits[lit_all + j] = in[pe + j];
+        }
         if (wave == 0) {
             if (!fits) {
                 if (lane == 0) st[page] = kResultTooLarge;
@@ -1212,7 +1309,7 @@ __global__ __launch_bounds__(kNW * 64) void zstd_parse_split_kernel(tyche_batch_
                 if (lane == 0) st[page] = 0;
             } else {
                 // parse blocks of kZBlk sequences over the whole list: page spans from the sequences' sizes
-                uint32_t npb = 0, pos = 0;
+                uint32_t npb = 0, pos = 0, lpos = 0;
                 for (uint32_t bs = 0; bs < total || npb == 0; bs += kZBlk) {
                     const uint32_t cnt = min(kZBlk, total - bs);
                     uint32_t span = 0, lit = 0, xb = 0;
@@ -1237,8 +1334,10 @@ __global__ __launch_bounds__(kNW * 64) void zstd_parse_split_kernel(tyche_batch_
                         P[4] = lit;
                         P[5] = span;
                         P[6] = xb;
+                        P[7] = lpos;
                     }
                     pos += span;
+                    lpos += lit;
                     npb++;
                     if (last) break;
                 }
@@ -1423,7 +1522,7 @@ __device__ uint32_t fse_lane(uint8_t *out, const uint2 *R, uint32_t n, const uin
 
 // Each lane copies its block's three tables into its own LDS slot (kFseSlot).
 __global__ __launch_bounds__(64) void zstd_fse_kernel(tyche_batch_t b, size_t first, size_t count, uint8_t *ws,
-                                                      size_t ws_page, const int32_t *st) {
+                                                      size_t ws_page, const int32_t *st, uint32_t rec_cap) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const size_t j = (size_t)blockIdx.x * kWave + threadIdx.x;
     if (j >= count || st[j] <= 0) return;
@@ -1448,7 +1547,7 @@ __global__ __launch_bounds__(64) void zstd_fse_kernel(tyche_batch_t b, size_t fi
         } else {
             for (uint32_t w = 0; w < 3u * kCtWords / 4u; w++) ((u32x4 *)lt)[w] = ((const u32x4 *)g)[w];
         }
-        B[3] = fse_lane(dst + B[0] + 3u + B[2], (const uint2 *)area_rec(area) + B[5], B[4], lt);
+        B[3] = fse_lane(dst + B[0] + 3u + B[2], (const uint2 *)area_seq(area, rec_cap) + B[5], B[4], lt);
     }
 }
 
@@ -1512,7 +1611,7 @@ hipError_t launch_zstd_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream
     if (in_cap > 65535u) return hipErrorInvalidValue;    // 16-bit positions in the parse and sequence records
     const size_t page_lds = (in_cap + 16u + kPad + 15u) & ~15u;
     const size_t lds = kTableSlots * sizeof(uint16_t) + kWave + kWave * 8 + kSeqCap * 8 + kHtab * 4 + 256 + page_lds;
-    const size_t lds1 = kTableSlots * sizeof(uint16_t) + kWave + kWave * 8 + page_lds;   // pass A1
+    const size_t lds1 = kTableSlots * sizeof(uint16_t) + kWave + kWave * 8 + kWave * 4 + page_lds;   // pass A1 (+ copy map)
     const long mn = knob("ZSTD_SPLIT_MIN", 4096);   // small batches: one launch (latency)
     const size_t split_min = mn > 0 ? (size_t)mn : 4096;
     const bool split = knob("ZSTD_ENC_SPLIT", 1) != 0 && b.count >= split_min;
@@ -1628,7 +1727,8 @@ hipError_t launch_zstd_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream
                                page_bytes, st, ctr.get(), logcap);
         }
         hipLaunchKernelGGL(zstd_fse_kernel, dim3((unsigned)((n + kWave - 1) / kWave)), dim3(kWave),
-                           kWave * kFseSlot.words * 4u, s, b, first, n, ws, page_bytes, (const int32_t *)st);
+                           kWave * kFseSlot.words * 4u, s, b, first, n, ws, page_bytes, (const int32_t *)st,
+                           enc_rec_cap(in_cap));
         {
             const size_t g = std::min<size_t>(n, ncu * 8u);
             WorkCounter ctr(s, g < n);
