@@ -123,6 +123,11 @@ __device__ __forceinline__ SeqCode seq_code(uint32_t ll, uint32_t ml, uint32_t o
 }
 
 // ------------------------------------------------------------ block emission
+// The sequence map of a page's sequence region (split encode; seq_slot below)
+struct SeqMap {
+    uint32_t c1, c2, c3, slice;
+};
+
 // Sequences of the current block live in LDS: seq[i] = (ll | off << 16, ml | rc << 16),
 // rc = the repeat code chosen at emission (0: the offset is sent as off + 3).
 struct Enc {
@@ -147,6 +152,9 @@ struct Enc {
     uint32_t logcap;     // 7: LL / OF / ML table logs FSE_optimalTableLog's, capped at 7 / 6 / 7; 6: fixed 6 / 5 / 6
     const uint32_t *psum;   // split encode: the parse block's literal bytes, span and extra bits (nullptr: summed here)
     const uint8_t *lit;     // split encode: the block's literals, in order, from pass A1 (nullptr: gathered from in)
+    uint2 *sreg;            // split encode: the sequence region, sequence `sfirst + i` of the block at
+    SeqMap smap;            //   sreg[seq_slot(smap, sfirst + i)] (e.seq is not used)
+    uint32_t sfirst;
     __device__ uint32_t nrec_cap() const { return rec_cap; }
 };
 
@@ -175,12 +183,14 @@ constexpr uint32_t kTabBytes = 3u * kCtWords * 4u;   // 1152
 // sequence list again for (emit_block's sizes; round 6), one word spare
 constexpr uint32_t kPblkWords = 8;
 constexpr uint32_t kAreaHead = 16u + kMaxBlk * kBlkWords * 4u + kMaxBlk * kPblkWords * 4u;
-// area: [0] emitted blocks, [1] parse blocks | block records | parse blocks | tables |
-//       scratch (16 B per sequence: the split parse's per-part sequence slices, then the
-//       page's literals in order) | the parse's sequences (8 B; pass A2 overwrites each with
-//       its record for pass B as it reads it).  Round 6: pass A1 copies the literals out of
-//       the page it holds in LDS, so that pass A2 reads them once and contiguously instead of
-//       gathering them from the page in HBM.
+// area: [0] emitted blocks, [1] parse blocks, [2..3] the sequence map | block records | parse
+//       blocks | tables | the parse's sequences (16 B per sequence of room: the split parse's
+//       per-part slices, where they stay -- the map below; pass A2 overwrites each with its
+//       record for pass B as it reads it) | the page's literals in page order (8 B per
+//       sequence of room).  Round 6: pass A1 copies the literals out of the page it holds in
+//       LDS, so that pass A2 reads them once and contiguously instead of gathering them from
+//       the page in HBM, and leaves its parts' sequences where it wrote them instead of
+//       joining them into one list (one write and one read of every sequence less).
 __host__ __device__ inline uint32_t enc_rec_cap(uint32_t in_cap) { return in_cap / 4u + 64u; }
 __host__ __device__ inline size_t enc_area_bytes(uint32_t in_cap) {
     return ((size_t)kAreaHead + (size_t)kMaxBlk * kTabBytes + (size_t)enc_rec_cap(in_cap) * 24u + 255u) & ~(size_t)255u;
@@ -194,7 +204,25 @@ __device__ __forceinline__ uint32_t *area_tab(uint8_t *a, uint32_t k) {
 }
 __device__ __forceinline__ uint4 *area_rec(uint8_t *a) { return (uint4 *)(a + kAreaHead + (size_t)kMaxBlk * kTabBytes); }
 __device__ __forceinline__ uint2 *area_seq(uint8_t *a, uint32_t rec_cap) { return (uint2 *)(area_rec(a) + rec_cap); }
-__device__ __forceinline__ uint8_t *area_lit(uint8_t *a) { return (uint8_t *)area_rec(a); }   // (16 rec_cap > in_cap)
+__device__ __forceinline__ uint8_t *area_lit(uint8_t *a, uint32_t rec_cap) { return (uint8_t *)area_seq(a, rec_cap); }   // (8 rec_cap > in_cap)
+// Sequence i of a page (in page order) lives in part k's slice of the sequence region: parts
+// 0..3 start at 0, slice, 2 slice, 3 slice and hold [0, c1), [c1, c2), [c2, c3), [c3, ...)
+// (one-wave parse: one part, c1 = c2 = c3 = 0xFFFF).  Kept in area words 2..3 as 16-bit fields.
+__device__ __forceinline__ SeqMap seq_map(const uint8_t *a, bool uniform) {   // uniform: one page per wave
+    uint32_t w2 = ((const uint32_t *)a)[2], w3 = ((const uint32_t *)a)[3];
+    if (uniform) {
+        w2 = __builtin_amdgcn_readfirstlane(w2);
+        w3 = __builtin_amdgcn_readfirstlane(w3);
+    }
+    return SeqMap{w2 & 0xFFFFu, w2 >> 16, w3 & 0xFFFFu, w3 >> 16};
+}
+__device__ __forceinline__ void put_seq_map(uint8_t *a, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t slice) {
+    ((uint32_t *)a)[2] = c1 | (c2 << 16);
+    ((uint32_t *)a)[3] = c3 | (slice << 16);
+}
+__device__ __forceinline__ uint32_t seq_slot(const SeqMap &m, uint32_t i) {
+    return i >= m.c3 ? i - m.c3 + 3u * m.slice : i >= m.c2 ? i - m.c2 + 2u * m.slice : i >= m.c1 ? i - m.c1 + m.slice : i;
+}
 
 // Copies the literal runs [ls, ls + ll) of the wave's lanes, in lane order, from the page in
 // LDS to dst[0, sum of ll), 64 bytes a step; returns the sum of ll.  Byte j's run is the last
@@ -295,8 +323,9 @@ __device__ __forceinline__ SeqCode seq_record_codes(uint2 r) {
 // Returns the history after the block through h0..h2 (committed only if the
 // block is emitted compressed: raw blocks leave the decoder's history alone).
 // The same pass counts the LL / ML / OF codes into e.htab (0 / 64 / 128, zeroed by the
-// caller) and hands each sequence on: split encode (e.area), its 8-byte record to R for
-// pass B; one-kernel encode, its repeat code into e.seq[i].y for the bitstream below
+// caller) and hands each sequence on: split encode (R = e.sreg), its 8-byte record for pass B
+// in the sequence's own slot; one-kernel encode, its repeat code into e.seq[i].y for the
+// bitstream below
 // (round 6: one pass over the block's sequences instead of three -- the repeat codes
 // written back, the histogram and the records each read the list again)
 __device__ __forceinline__ void resolve_repeats(const Enc &e, uint32_t n, uint32_t lane, uint32_t &h0, uint32_t &h1,
@@ -305,7 +334,8 @@ __device__ __forceinline__ void resolve_repeats(const Enc &e, uint32_t n, uint32
     const uint64_t below = (1ull << lane) - 1ull;
     for (uint32_t g = 0; g < n; g += kWave) {
         const uint32_t i = g + lane;
-        const uint2 r = i < n ? e.seq[i] : make_uint2(0u, 0u);
+        uint2 *sp = R ? e.sreg + seq_slot(e.smap, e.sfirst + min(i, n - 1u)) : e.seq + i;
+        const uint2 r = i < n ? *sp : make_uint2(0u, 0u);
         const uint32_t ll = r.x & 0xFFFFu, off = r.x >> 16;
         const uint32_t up = (uint32_t)__shfl((int)off, (int)(lane ? lane - 1u : 0u));
         const uint32_t r0b = lane ? up : c0;
@@ -331,8 +361,8 @@ __device__ __forceinline__ void resolve_repeats(const Enc &e, uint32_t n, uint32
             atomicAdd(&e.htab[c.llc], 1u);
             atomicAdd(&e.htab[64u + c.mlc], 1u);
             atomicAdd(&e.htab[128u + c.ofc], 1u);
-            if (R) R[i] = make_uint2(ll | (c.llc << 16) | (c.mlc << 22) | ((ofcode >> 16) << 28), (ml - 3u) | (ofcode << 16));
-            else e.seq[i].y = ml | (rc << 16);
+            if (R) *sp = make_uint2(ll | (c.llc << 16) | (c.mlc << 22) | ((ofcode >> 16) << 28), (ml - 3u) | (ofcode << 16));
+            else sp->y = ml | (rc << 16);
         }
         // the history after the group's last sequence
         const uint32_t last = min(n - g, kWave) - 1u;
@@ -631,7 +661,7 @@ __device__ __forceinline__ bool emit_block(Enc &e, uint32_t bend, bool last, uin
         // 64, OF at 128) and, split encode, the sequences' records for pass B
         for (uint32_t k = lane; k < 192u; k += kWave) e.htab[k] = 0;
         __builtin_amdgcn_wave_barrier();
-        resolve_repeats(e, n, lane, h0, h1, h2, e.area ? e.seq : nullptr);   // (split: records in place)
+        resolve_repeats(e, n, lane, h0, h1, h2, e.area ? e.sreg : nullptr);   // (split: records in place)
         __builtin_amdgcn_wave_barrier();
         // ---- tables: per-block distributions from 64 sequences on (MIN_SEQ_FOR_DYNAMIC_FSE)
         // at FSE_optimalTableLog's accuracy capped at LL 7 / OF 6 / ML 7 (the reference caps at
@@ -853,8 +883,8 @@ template <typename Parse>
 __device__ __forceinline__ int32_t parse_to_area_with(const uint8_t *in, uint32_t L, uint8_t *area, uint32_t rec_cap,
                                                       uint32_t lane, Parse &&parse, const uint8_t *sink_in,
                                                       uint32_t *map) {
-    uint2 *S = area_seq(area, rec_cap);
-    uint8_t *lits = area_lit(area);
+    uint2 *S = (uint2 *)area_rec(area);   // one part: the sequence map below is the identity
+    uint8_t *lits = area_lit(area, rec_cap);
     uint32_t nseq = 0, bseq = 0, bstart = 0, cursor = 0, npb = 0;
     uint32_t a_lit = 0, a_span = 0, a_xb = 0;   // this lane's share of the block's sums
     uint32_t lpos = 0, blit = 0;                // literals copied; the block's first
@@ -903,7 +933,10 @@ __device__ __forceinline__ int32_t parse_to_area_with(const uint8_t *in, uint32_
     if (anchor == 0xFFFFFFFFu) return 0;
     for (uint32_t j = lane; anchor + j < L; j += kWave) lits[lpos + j] = in[anchor + j];   // the last literals
     put_pblk(L);
-    if (lane == 0) ((uint32_t *)area)[1] = npb;
+    if (lane == 0) {
+        ((uint32_t *)area)[1] = npb;
+        put_seq_map(area, 0xFFFFu, 0xFFFFu, 0xFFFFu, 0u);
+    }
     return 1;
 }
 template <int kW>
@@ -952,16 +985,18 @@ __device__ __forceinline__ int32_t emit_page(const uint8_t *src, uint32_t L, uin
     e.logcap = logcap;
     e.cursor = 0;
     const uint32_t npb = __builtin_amdgcn_readfirstlane(((const uint32_t *)area)[1]);
-    uint2 *S = area_seq(area, rec_cap);
+    e.sreg = (uint2 *)area_rec(area);
+    e.smap = seq_map(area, true);
+    e.seq = nullptr;
     for (uint32_t k = 0; k < npb; k++) {
         const uint32_t *P = area_pblk(area, k);
         e.bstart = __builtin_amdgcn_readfirstlane(P[0]);
         const uint32_t bend = __builtin_amdgcn_readfirstlane(P[1]);
         e.nrec = __builtin_amdgcn_readfirstlane(P[2]);   // the block's records replace its sequences
-        e.seq = S + e.nrec;
+        e.sfirst = e.nrec;
         e.nseq = __builtin_amdgcn_readfirstlane(P[3]);
         e.psum = P + 4;
-        e.lit = area_lit(area) + __builtin_amdgcn_readfirstlane(P[7]);
+        e.lit = area_lit(area, rec_cap) + __builtin_amdgcn_readfirstlane(P[7]);
         if (!emit_block(e, bend, k + 1u == npb, lane)) return 0;
     }
     if (lane == 0) ((uint32_t *)area)[0] = e.nblk;
@@ -1260,13 +1295,12 @@ __global__ __launch_bounds__(kNW * 64) void zstd_parse_split_kernel(tyche_batch_
         bool ok = fits;
         // lit_w / lit_all: the page's literal bytes before this part / in all parts, each part's
         // first run extended back to the end of the last part before it with a sequence (pe)
-        uint32_t off_w = 0, prev_end = 0, total = 0, lit_w = 0, lit_all = 0, pe = 0;
+        uint32_t prev_end = 0, total = 0, lit_w = 0, lit_all = 0, pe = 0;
         for (uint32_t w = 0; w < kNW; w++) {
             const uint32_t nw = rfl(hdr->n[w]);
             ok = ok && rfl(hdr->ok[w]);
             const uint32_t lw = rfl(hdr->lit[w]) + (w > 0 && nw ? bnd(w) - pe : 0u);
             if (w < wave) {
-                off_w += nw;
                 lit_w += lw;
                 if (nw) prev_end = rfl(hdr->cursor[w]);
             }
@@ -1274,26 +1308,23 @@ __global__ __launch_bounds__(kNW * 64) void zstd_parse_split_kernel(tyche_batch_
             lit_all += lw;
             if (nw) pe = rfl(hdr->cursor[w]);
         }
-        uint2 *S = area_seq(area, rec_cap);
-        if (ok) {   // the slices into place; the part's first literal run starts at the previous part's end
+        if (ok) {
+            // the part's first literal run starts at the end of the last part before it with a
+            // sequence: its first sequence is extended back in place (ll, the low 16 bits: cannot
+            // carry out, < 2^16)
             const uint32_t nw = rfl(hdr->n[wave]);
-            for (uint32_t j = lane; j < nw; j += kWave) {
-                uint2 q = W[j];
-                if (j == 0 && wave > 0) q.x += b0 - prev_end;   // ll (low 16 bits): cannot carry out (< 2^16)
-                S[off_w + j] = q;
+            uint2 qn = lane < nw ? W[lane] : make_uint2(0u, 0u);   // the slice a group ahead of the copy below
+            if (lane == 0 && wave > 0 && nw) {
+                qn.x += b0 - prev_end;
+                W[0] = qn;   // (the store waits for the load it depends on)
             }
-        }
-        __syncthreads();   // the slices are free: the literal region takes their place
-        if (ok) {   // the part's literals, from the staged page to the literal region, in page order
-            const uint32_t nw = rfl(hdr->n[wave]);
-            uint8_t *lits = area_lit(area);
-            const uint2 *Sw = S + off_w;
+            // and the part's literals, from the staged page to the literal region, in page order
+            uint8_t *lits = area_lit(area, rec_cap);
             uint32_t pos = prev_end, lo = lit_w;   // page position and literal offset of the next run
-            uint2 qn = lane < nw ? Sw[lane] : make_uint2(0u, 0u);   // the list a group ahead of the copy
             for (uint32_t j0 = 0; j0 < nw; j0 += kWave) {
                 const uint32_t j = j0 + lane;
                 const uint2 q = qn;
-                qn = j + kWave < nw ? Sw[j + kWave] : make_uint2(0u, 0u);
+                qn = j + kWave < nw ? W[j + kWave] : make_uint2(0u, 0u);
                 const uint32_t ll = q.x & 0xFFFFu, sz = ll + q.y;
                 const uint32_t inc = (uint32_t)wave_incl_sum((int32_t)sz);
                 lo += copy_runs(in, pos + inc - sz, ll, lits + lo, lane, (uint32_t *)rec);   // (rec: free after the parse)
@@ -1302,19 +1333,30 @@ __global__ __launch_bounds__(kNW * 64) void zstd_parse_split_kernel(tyche_batch_
             if (wave == kNW - 1)   // the literals after the page's last match
                 for (uint32_t j = lane; pe + j < L; j += kWave) lits[lit_all + j] = in[pe + j];
         }
+        __syncthreads();   // every part's first sequence extended
         if (wave == 0) {
             if (!fits) {
                 if (lane == 0) st[page] = kResultTooLarge;
             } else if (!ok || (total + kZBlk - 1) / kZBlk + 1 > kMaxBlk) {
                 if (lane == 0) st[page] = 0;
             } else {
-                // parse blocks of kZBlk sequences over the whole list: page spans from the sequences' sizes
+                // parse blocks of kZBlk sequences over the whole list (the parts' slices, in page
+                // order: the sequence map): page spans from the sequences' sizes
+                SeqMap m;
+                m.slice = slice;
+                m.c1 = rfl(hdr->n[0]);
+                m.c2 = kNW > 1 ? m.c1 + rfl(hdr->n[min(1u, kNW - 1u)]) : 0xFFFFu;
+                m.c3 = kNW > 2 ? m.c2 + rfl(hdr->n[min(2u, kNW - 1u)]) : 0xFFFFu;
+                if (kNW < 4) m.c3 = 0xFFFFu;
+                if (kNW < 3) m.c2 = 0xFFFFu;
+                if (kNW < 2) m.c1 = 0xFFFFu;
+                const uint2 *Wall = (const uint2 *)area_rec(area);
                 uint32_t npb = 0, pos = 0, lpos = 0;
                 for (uint32_t bs = 0; bs < total || npb == 0; bs += kZBlk) {
                     const uint32_t cnt = min(kZBlk, total - bs);
                     uint32_t span = 0, lit = 0, xb = 0;
                     for (uint32_t j = lane; j < cnt; j += kWave) {
-                        const uint2 q = S[bs + j];
+                        const uint2 q = Wall[seq_slot(m, bs + j)];
                         const uint32_t ll = q.x & 0xFFFFu;
                         const SeqCode c = seq_code(ll, q.y, (q.x >> 16) + 3u);   // emit_block's bound
                         span += ll + q.y;
@@ -1343,6 +1385,7 @@ __global__ __launch_bounds__(kNW * 64) void zstd_parse_split_kernel(tyche_batch_
                 }
                 if (lane == 0) {
                     ((uint32_t *)area)[1] = npb;
+                    put_seq_map(area, m.c1, m.c2, m.c3, m.slice);
                     st[page] = 1;
                 }
             }
@@ -1462,7 +1505,8 @@ static_assert(kFseSlot.words % 4u == 0, "slot of 16-byte pieces");
 constexpr uint32_t kFsePf = TYCHE_ZSTD_FSE_PF;   // sequence records in flight per lane (pass B)
 // ZSTD_compressSequences' bitstream (zstd_compress.c:695-735) for n >= 1
 // sequences; the same steps as emit_block's wave-uniform loop.  Returns its size.
-__device__ uint32_t fse_lane(uint8_t *out, const uint2 *R, uint32_t n, const uint32_t *T) {
+__device__ uint32_t fse_lane(uint8_t *out, const uint2 *Rg, const SeqMap m, uint32_t first, uint32_t n, const uint32_t *T) {
+    auto R = [&](uint32_t i) { return Rg[seq_slot(m, first + i)]; };   // record i of the block
     const uint32_t *tll = T + kFseSlot.sll, *tof = T + kFseSlot.sof, *tml = T + kFseSlot.sml;
     const uint8_t *xll = (const uint8_t *)(T + kFseSlot.xll), *xof = (const uint8_t *)(T + kFseSlot.xof),
                   *xml = (const uint8_t *)(T + kFseSlot.xml);
@@ -1479,14 +1523,14 @@ __device__ uint32_t fse_lane(uint8_t *out, const uint2 *R, uint32_t n, const uin
     // every step waiting on HBM
     uint2 q[kFsePf];
 #pragma unroll
-    for (uint32_t u = 0; u < kFsePf; u++) q[u] = u < n ? R[n - 1u - u] : make_uint2(0, 0);
+    for (uint32_t u = 0; u < kFsePf; u++) q[u] = u < n ? R(n - 1u - u) : make_uint2(0, 0);
     for (uint32_t base = n; base > 0; base = base > kFsePf ? base - kFsePf : 0u) {
 #pragma unroll
         for (uint32_t u = 0; u < kFsePf; u++) {
             const bool live = base > u;
             const uint32_t i = base - 1u - u;   // wraps when !live: every use below is gated
             const uint2 r = q[u];
-            if (live && i >= kFsePf) q[u] = R[i - kFsePf];
+            if (live && i >= kFsePf) q[u] = R(i - kFsePf);
             if (!live) continue;
             const SeqCode c = seq_record_codes(r);
             const uint32_t llc = c.llc, mlc = c.mlc, ofc = c.ofc;
@@ -1522,7 +1566,7 @@ __device__ uint32_t fse_lane(uint8_t *out, const uint2 *R, uint32_t n, const uin
 
 // Each lane copies its block's three tables into its own LDS slot (kFseSlot).
 __global__ __launch_bounds__(64) void zstd_fse_kernel(tyche_batch_t b, size_t first, size_t count, uint8_t *ws,
-                                                      size_t ws_page, const int32_t *st, uint32_t rec_cap) {
+                                                      size_t ws_page, const int32_t *st) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const size_t j = (size_t)blockIdx.x * kWave + threadIdx.x;
     if (j >= count || st[j] <= 0) return;
@@ -1547,7 +1591,7 @@ __global__ __launch_bounds__(64) void zstd_fse_kernel(tyche_batch_t b, size_t fi
         } else {
             for (uint32_t w = 0; w < 3u * kCtWords / 4u; w++) ((u32x4 *)lt)[w] = ((const u32x4 *)g)[w];
         }
-        B[3] = fse_lane(dst + B[0] + 3u + B[2], (const uint2 *)area_seq(area, rec_cap) + B[5], B[4], lt);
+        B[3] = fse_lane(dst + B[0] + 3u + B[2], (const uint2 *)area_rec(area), seq_map(area, false), B[5], B[4], lt);
     }
 }
 
@@ -1618,11 +1662,14 @@ hipError_t launch_zstd_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream
     // sequence-table accuracy: FSE_optimalTableLog capped at LL/ML 7, OF 6 (6: fixed 6 / 5 / 6, round 2's)
     const uint32_t logcap = knob("ZSTD_FSE_LOG", 7) <= 6 ? 6u : 7u;
     const size_t page_bytes = enc_area_bytes(in_cap);
-    size_t budget = (size_t)8 << 30;
+    // scratch: at most 16 GiB or a quarter of the free memory, as the decoder's (round 6: 8 GiB or an
+    // eighth before -- 28 instead of 14 chunks per 1M x 32 KiB pages, encode 553.7 vs 542.6 ms, the
+    // FSE pass and every chunk's tail paid per launch; profiles/r06_zstd_ab/c3_pass_ms_litcopy.json)
+    size_t budget = (size_t)16 << 30;
     size_t free_b = 0, total_b = 0;
     if (b.count * page_bytes > ((size_t)1 << 30) && hipMemGetInfo(&free_b, &total_b) == hipSuccess && ((free_b += scratch_idle_bytes()), true) &&
-        free_b / 8 < budget)
-        budget = free_b / 8;
+        free_b / 4 < budget)
+        budget = free_b / 4;
     const long mb = knob("ZSTD_SCRATCH_MB", 0);
     if (mb > 0) budget = (size_t)mb << 20;
     const size_t chunk = split ? std::max<size_t>(1, std::min<size_t>(b.count, budget / page_bytes)) : b.count;
@@ -1727,8 +1774,7 @@ hipError_t launch_zstd_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream
                                page_bytes, st, ctr.get(), logcap);
         }
         hipLaunchKernelGGL(zstd_fse_kernel, dim3((unsigned)((n + kWave - 1) / kWave)), dim3(kWave),
-                           kWave * kFseSlot.words * 4u, s, b, first, n, ws, page_bytes, (const int32_t *)st,
-                           enc_rec_cap(in_cap));
+                           kWave * kFseSlot.words * 4u, s, b, first, n, ws, page_bytes, (const int32_t *)st);
         {
             const size_t g = std::min<size_t>(n, ncu * 8u);
             WorkCounter ctr(s, g < n);
