@@ -1176,6 +1176,9 @@ struct ZSplitHdr {
     uint32_t cursor[kNW];   // end of part w's last match (its start if none)
     uint32_t ok[kNW];       // part w's sequences fit its slice
     uint32_t lit[kNW];      // part w's literal bytes (before its first run's extension)
+    uint32_t span[kNW];     // part w's page bytes (likewise)
+    uint32_t xb[kNW];       // part w's extra bits at raw offsets (emit_block's bound; likewise)
+    uint32_t ll0[kNW];      // part w's first literal length (likewise)
 };
 template <uint32_t kNW>
 constexpr size_t zsplit_hdr_bytes() { return (sizeof(ZSplitHdr<kNW>) + 63) & ~(size_t)63; }
@@ -1266,21 +1269,32 @@ __global__ __launch_bounds__(kNW * 64) void zstd_parse_split_kernel(tyche_batch_
                 auto drop = [&](const uint2 *, uint32_t, uint32_t) -> bool { return true; };
                 (void)lzp::parse_page<true, false, kZWays>(in, b0 + kLastLiterals, table, rec, lane, drop, wstart, rep);
             }
-            uint32_t nseq = 0, a_lit = 0;
+            uint32_t nseq = 0, a_lit = 0, a_span = 0, a_xb = 0, ll0 = 0;
             auto sink = [&](const uint2 *r, uint32_t n, uint32_t anchor) -> bool {
                 uint32_t ls, ll, ml, off;
                 lzp::decode_record(r, n, anchor, lane, ls, ll, ml, off, TYCHE_SINK_BACK ? in : nullptr);
                 if (nseq + n > slice) return false;
-                if (lane < n) W[nseq + lane] = make_uint2(ll | (off << 16), ml);
-                a_lit += ll;   // (0 on lanes >= n)
+                if (lane < n) {
+                    W[nseq + lane] = make_uint2(ll | (off << 16), ml);
+                    const SeqCode c = seq_code(ll, ml, off + 3u);   // emit_block's bound: no repeat offsets
+                    a_lit += ll;
+                    a_span += ll + ml;
+                    a_xb += c.llb + c.mlb + c.ofc;
+                }
+                if (nseq == 0) ll0 = rdlane(ll, 0);
                 nseq += n;
                 __builtin_amdgcn_wave_barrier();
                 return true;
             };
             const uint32_t cur = lzp::parse_page<true, false, kZWays>(in, Lp, table, rec, lane, sink, b0, rep);
             a_lit = huf::wave_sum(a_lit);
+            a_span = huf::wave_sum(a_span);
+            a_xb = huf::wave_sum(a_xb);
             if (lane == 0) {
                 hdr->lit[wave] = a_lit;
+                hdr->span[wave] = a_span;
+                hdr->xb[wave] = a_xb;
+                hdr->ll0[wave] = ll0;
                 hdr->ok[wave] = cur != 0xFFFFFFFFu ? 1u : 0u;
                 hdr->n[wave] = nseq;
                 hdr->cursor[wave] = nseq ? cur : b0;
@@ -1351,11 +1365,24 @@ __global__ __launch_bounds__(kNW * 64) void zstd_parse_split_kernel(tyche_batch_
                 if (kNW < 3) m.c2 = 0xFFFFu;
                 if (kNW < 2) m.c1 = 0xFFFFu;
                 const uint2 *Wall = (const uint2 *)area_rec(area);
+                // one block (almost every page up to 32 KiB): its sums are the parts' from the parse,
+                // each part's first run extended back as in its first sequence (round 6: the list
+                // is not read again)
+                uint32_t one_lit = 0, one_span = 0, one_xb = 0, pe1 = 0;
+                for (uint32_t w = 0; w < kNW; w++) {
+                    const uint32_t nw = rfl(hdr->n[w]);
+                    if (!nw) continue;
+                    const uint32_t adj = w > 0 ? bnd(w) - pe1 : 0u, a = rfl(hdr->ll0[w]);
+                    one_lit += rfl(hdr->lit[w]) + adj;
+                    one_span += rfl(hdr->span[w]) + adj;
+                    one_xb += rfl(hdr->xb[w]) + seq_code(a + adj, 3u, 4u).llb - seq_code(a, 3u, 4u).llb;
+                    pe1 = rfl(hdr->cursor[w]);
+                }
                 uint32_t npb = 0, pos = 0, lpos = 0;
                 for (uint32_t bs = 0; bs < total || npb == 0; bs += kZBlk) {
                     const uint32_t cnt = min(kZBlk, total - bs);
                     uint32_t span = 0, lit = 0, xb = 0;
-                    for (uint32_t j = lane; j < cnt; j += kWave) {
+                    for (uint32_t j = lane; total > kZBlk && j < cnt; j += kWave) {
                         const uint2 q = Wall[seq_slot(m, bs + j)];
                         const uint32_t ll = q.x & 0xFFFFu;
                         const SeqCode c = seq_code(ll, q.y, (q.x >> 16) + 3u);   // emit_block's bound
@@ -1363,9 +1390,9 @@ __global__ __launch_bounds__(kNW * 64) void zstd_parse_split_kernel(tyche_batch_
                         lit += ll;
                         xb += c.llb + c.mlb + c.ofc;
                     }
-                    span = huf::wave_sum(span);
-                    lit = huf::wave_sum(lit);
-                    xb = huf::wave_sum(xb);
+                    span = total > kZBlk ? huf::wave_sum(span) : one_span;
+                    lit = total > kZBlk ? huf::wave_sum(lit) : one_lit;
+                    xb = total > kZBlk ? huf::wave_sum(xb) : one_xb;
                     const bool last = bs + kZBlk >= total;
                     if (lane == 0) {
                         uint32_t *P = area_pblk(area, npb);
