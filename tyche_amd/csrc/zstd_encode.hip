@@ -127,6 +127,10 @@ __device__ __forceinline__ SeqCode seq_code(uint32_t ll, uint32_t ml, uint32_t o
 struct SeqMap {
     uint32_t c1, c2, c3, slice;
 };
+// The literal map of a page's literal region (split encode; lit_pos below)
+struct LitMap {
+    uint32_t w[5];
+};
 
 // Sequences of the current block live in LDS: seq[i] = (ll | off << 16, ml | rc << 16),
 // rc = the repeat code chosen at emission (0: the offset is sent as off + 3).
@@ -151,7 +155,9 @@ struct Enc {
     uint32_t rec_cap;
     uint32_t logcap;     // 7: LL / OF / ML table logs FSE_optimalTableLog's, capped at 7 / 6 / 7; 6: fixed 6 / 5 / 6
     const uint32_t *psum;   // split encode: the parse block's literal bytes, span and extra bits (nullptr: summed here)
-    const uint8_t *lit;     // split encode: the block's literals, in order, from pass A1 (nullptr: gathered from in)
+    const uint8_t *lit;     // split encode: the literal region from pass A1 (nullptr: literals gathered from in);
+    LitMap lmap;            //   literal j of the block at lit[lit_pos(lmap, lofs + j)]
+    uint32_t lofs;
     uint2 *sreg;            // split encode: the sequence region, sequence `sfirst + i` of the block at
     SeqMap smap;            //   sreg[seq_slot(smap, sfirst + i)] (e.seq is not used)
     uint32_t sfirst;
@@ -182,7 +188,8 @@ constexpr uint32_t kTabBytes = 3u * kCtWords * 4u;   // 1152
 // sequence span (page bytes) and extra bits at raw offsets, which pass A2 would otherwise read the
 // sequence list again for (emit_block's sizes; round 6), one word spare
 constexpr uint32_t kPblkWords = 8;
-constexpr uint32_t kAreaHead = 16u + kMaxBlk * kBlkWords * 4u + kMaxBlk * kPblkWords * 4u;
+constexpr uint32_t kAreaHdr = 48u;   // [0] emitted blocks, [1] parse blocks, [2..3] sequence map, [4..8] literal map
+constexpr uint32_t kAreaHead = kAreaHdr + kMaxBlk * kBlkWords * 4u + kMaxBlk * kPblkWords * 4u;
 // area: [0] emitted blocks, [1] parse blocks, [2..3] the sequence map | block records | parse
 //       blocks | tables | the parse's sequences (16 B per sequence of room: the split parse's
 //       per-part slices, where they stay -- the map below; pass A2 overwrites each with its
@@ -195,9 +202,9 @@ __host__ __device__ inline uint32_t enc_rec_cap(uint32_t in_cap) { return in_cap
 __host__ __device__ inline size_t enc_area_bytes(uint32_t in_cap) {
     return ((size_t)kAreaHead + (size_t)kMaxBlk * kTabBytes + (size_t)enc_rec_cap(in_cap) * 24u + 255u) & ~(size_t)255u;
 }
-__device__ __forceinline__ uint32_t *area_blk(uint8_t *a, uint32_t k) { return (uint32_t *)(a + 16u) + k * kBlkWords; }
+__device__ __forceinline__ uint32_t *area_blk(uint8_t *a, uint32_t k) { return (uint32_t *)(a + kAreaHdr) + k * kBlkWords; }
 __device__ __forceinline__ uint32_t *area_pblk(uint8_t *a, uint32_t k) {
-    return (uint32_t *)(a + 16u + kMaxBlk * kBlkWords * 4u) + k * kPblkWords;
+    return (uint32_t *)(a + kAreaHdr + kMaxBlk * kBlkWords * 4u) + k * kPblkWords;
 }
 __device__ __forceinline__ uint32_t *area_tab(uint8_t *a, uint32_t k) {
     return (uint32_t *)(a + kAreaHead + (size_t)k * kTabBytes);
@@ -219,6 +226,23 @@ __device__ __forceinline__ SeqMap seq_map(const uint8_t *a, bool uniform) {   //
 __device__ __forceinline__ void put_seq_map(uint8_t *a, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t slice) {
     ((uint32_t *)a)[2] = c1 | (c2 << 16);
     ((uint32_t *)a)[3] = c3 | (slice << 16);
+}
+// The page's literals (in page order: literal j of the page) lie in the literal region in up to
+// five runs (split parse: each part's own literals where its part starts, behind the bytes its
+// first run was extended back over, then the literals after the last match): run k starts at
+// literal c_k and region byte s_k; area words 4..8 hold c_k | s_k << 16 (c_k = 0xFFFF: unused).
+__device__ __forceinline__ LitMap lit_map(const uint8_t *a) {
+    LitMap m;
+#pragma unroll
+    for (int k = 0; k < 5; k++) m.w[k] = __builtin_amdgcn_readfirstlane(((const uint32_t *)a)[4 + k]);
+    return m;
+}
+__device__ __forceinline__ uint32_t lit_pos(const LitMap &m, uint32_t j) {
+    uint32_t p = j;
+#pragma unroll
+    for (int k = 0; k < 5; k++)
+        if (j >= (m.w[k] & 0xFFFFu)) p = j - (m.w[k] & 0xFFFFu) + (m.w[k] >> 16);
+    return p;
 }
 __device__ __forceinline__ uint32_t seq_slot(const SeqMap &m, uint32_t i) {
     return i >= m.c3 ? i - m.c3 + 3u * m.slice : i >= m.c2 ? i - m.c2 + 2u * m.slice : i >= m.c1 ? i - m.c1 + m.slice : i;
@@ -438,7 +462,7 @@ __device__ uint32_t huf_literals(Enc &e, uint32_t n, uint32_t trail, uint32_t li
     uint8_t *dst = e.dst;
     uint32_t *hist = e.htab;
     if (e.lit) {   // split encode: the literals are in the area already (no scratch copy)
-        for (uint32_t j = lane; j < lit_total; j += kWave) atomicAdd(&hist[e.lit[j]], 1u);
+        for (uint32_t j = lane; j < lit_total; j += kWave) atomicAdd(&hist[e.lit[lit_pos(e.lmap, e.lofs + j)]], 1u);
     } else {
         for_each_literal(e, n, trail, lane, [&](uint32_t j, uint32_t v) {
             dst[scr + j] = (uint8_t)v;
@@ -518,7 +542,7 @@ __device__ uint32_t huf_literals(Enc &e, uint32_t n, uint32_t trail, uint32_t li
     // ---- streams: symbols last to first, bits LSB first (HUF_compress1X_usingCTable), end mark
     uint32_t sp = wpos + whdr + (single ? 0u : 6u);
     const uint32_t seg = (lit_total + 3u) / 4u;
-    const uint8_t *lits = e.lit ? e.lit : e.dst + scr;
+    auto lit_at = [&](uint32_t j) -> uint32_t { return e.lit ? e.lit[lit_pos(e.lmap, e.lofs + j)] : e.dst[scr + j]; };
     for (uint32_t st = 0; st < nst; st++) {
         const uint32_t a = single ? 0u : st * seg;
         const uint32_t bnd = single ? lit_total : (st == 3u ? lit_total : min(lit_total, (st + 1u) * seg));
@@ -529,7 +553,7 @@ __device__ uint32_t huf_literals(Enc &e, uint32_t n, uint32_t trail, uint32_t li
         for (uint32_t k0 = 0; a + k0 < bnd; k0 += kWave) {
             const bool act = a + k0 + lane < bnd;
             uint32_t ent = 0;
-            if (act) ent = e.htab[lits[bnd - 1u - (k0 + lane)]];
+            if (act) ent = e.htab[lit_at(bnd - 1u - (k0 + lane))];
             const uint32_t len = ent >> 16, cv = ent & 0xFFFFu;
             const int32_t bi = wave_incl_sum((int32_t)len);
             const uint32_t b = nbits + (uint32_t)bi - len;
@@ -638,7 +662,7 @@ __device__ __forceinline__ bool emit_block(Enc &e, uint32_t bend, bool last, uin
         uint8_t *dst = e.dst;
         const uint32_t lo0 = o + fl;
         if (e.lit) {
-            for (uint32_t j = lane; j < lit_total; j += kWave) dst[lo0 + j] = e.lit[j];
+            for (uint32_t j = lane; j < lit_total; j += kWave) dst[lo0 + j] = e.lit[lit_pos(e.lmap, e.lofs + j)];
         } else {
             for_each_literal(e, n, trail, lane, [&](uint32_t j, uint32_t v) { dst[lo0 + j] = (uint8_t)v; });
         }
@@ -936,6 +960,8 @@ __device__ __forceinline__ int32_t parse_to_area_with(const uint8_t *in, uint32_
     if (lane == 0) {
         ((uint32_t *)area)[1] = npb;
         put_seq_map(area, 0xFFFFu, 0xFFFFu, 0xFFFFu, 0u);
+        ((uint32_t *)area)[4] = 0u;   // one literal run from region byte 0
+        for (int k = 1; k < 5; k++) ((uint32_t *)area)[4 + k] = 0xFFFFu;
     }
     return 1;
 }
@@ -988,6 +1014,8 @@ __device__ __forceinline__ int32_t emit_page(const uint8_t *src, uint32_t L, uin
     e.sreg = (uint2 *)area_rec(area);
     e.smap = seq_map(area, true);
     e.seq = nullptr;
+    e.lit = area_lit(area, rec_cap);
+    e.lmap = lit_map(area);
     for (uint32_t k = 0; k < npb; k++) {
         const uint32_t *P = area_pblk(area, k);
         e.bstart = __builtin_amdgcn_readfirstlane(P[0]);
@@ -996,7 +1024,7 @@ __device__ __forceinline__ int32_t emit_page(const uint8_t *src, uint32_t L, uin
         e.sfirst = e.nrec;
         e.nseq = __builtin_amdgcn_readfirstlane(P[3]);
         e.psum = P + 4;
-        e.lit = area_lit(area, rec_cap) + __builtin_amdgcn_readfirstlane(P[7]);
+        e.lofs = __builtin_amdgcn_readfirstlane(P[7]);
         if (!emit_block(e, bend, k + 1u == npb, lane)) return 0;
     }
     if (lane == 0) ((uint32_t *)area)[0] = e.nblk;
@@ -1182,7 +1210,7 @@ struct ZSplitHdr {
 };
 template <uint32_t kNW>
 constexpr size_t zsplit_hdr_bytes() { return (sizeof(ZSplitHdr<kNW>) + 63) & ~(size_t)63; }
-constexpr size_t kZWaveRegion = kTableSlots * sizeof(uint16_t) + kWave * 8;   // table, 64 records
+constexpr size_t kZWaveRegion = kTableSlots * sizeof(uint16_t) + kWave * 8 + kWave * 4;   // table, 64 records, copy map
 template <uint32_t kNW>
 constexpr size_t zsplit_stage_off() { return zsplit_hdr_bytes<kNW>() + kNW * kZWaveRegion; }
 
@@ -1199,6 +1227,7 @@ __global__ __launch_bounds__(kNW * 64) void zstd_parse_split_kernel(tyche_batch_
     uint8_t *region = smem + zsplit_hdr_bytes<kNW>() + wave * kZWaveRegion;
     uint16_t *table = (uint16_t *)region;
     uint2 *rec = (uint2 *)(region + kTableSlots * sizeof(uint16_t));
+    uint32_t *cmap = (uint32_t *)(rec + kWave);   // copy_runs' map
     uint8_t *stage = smem + zsplit_stage_off<kNW>();
     const uint32_t rec_cap = enc_rec_cap(in_cap);
     const uint32_t slice = (2u * rec_cap) / kNW;   // the code region holds 2 rec_cap sequences of 8 bytes
@@ -1269,11 +1298,13 @@ __global__ __launch_bounds__(kNW * 64) void zstd_parse_split_kernel(tyche_batch_
                 auto drop = [&](const uint2 *, uint32_t, uint32_t) -> bool { return true; };
                 (void)lzp::parse_page<true, false, kZWays>(in, b0 + kLastLiterals, table, rec, lane, drop, wstart, rep);
             }
-            uint32_t nseq = 0, a_lit = 0, a_span = 0, a_xb = 0, ll0 = 0;
+            uint32_t nseq = 0, a_lit = 0, a_span = 0, a_xb = 0, ll0 = 0, lown = 0;
+            uint8_t *lits = area_lit(area, rec_cap) + b0;   // the part's own literals, in order (round 6)
             auto sink = [&](const uint2 *r, uint32_t n, uint32_t anchor) -> bool {
                 uint32_t ls, ll, ml, off;
                 lzp::decode_record(r, n, anchor, lane, ls, ll, ml, off, TYCHE_SINK_BACK ? in : nullptr);
                 if (nseq + n > slice) return false;
+                lown += copy_runs(in, ls, ll, lits + lown, lane, cmap);
                 if (lane < n) {
                     W[nseq + lane] = make_uint2(ll | (off << 16), ml);
                     const SeqCode c = seq_code(ll, ml, off + 3u);   // emit_block's bound: no repeat offsets
@@ -1307,45 +1338,31 @@ __global__ __launch_bounds__(kNW * 64) void zstd_parse_split_kernel(tyche_batch_
         }
         __syncthreads();   // every part parsed
         bool ok = fits;
-        // lit_w / lit_all: the page's literal bytes before this part / in all parts, each part's
-        // first run extended back to the end of the last part before it with a sequence (pe)
-        uint32_t prev_end = 0, total = 0, lit_w = 0, lit_all = 0, pe = 0;
+        // prev_end / pe: the end of the last part with a sequence before this one / of all
+        uint32_t prev_end = 0, total = 0, pe = 0;
         for (uint32_t w = 0; w < kNW; w++) {
             const uint32_t nw = rfl(hdr->n[w]);
             ok = ok && rfl(hdr->ok[w]);
-            const uint32_t lw = rfl(hdr->lit[w]) + (w > 0 && nw ? bnd(w) - pe : 0u);
-            if (w < wave) {
-                lit_w += lw;
-                if (nw) prev_end = rfl(hdr->cursor[w]);
-            }
+            if (w < wave && nw) prev_end = rfl(hdr->cursor[w]);
             total += nw;
-            lit_all += lw;
             if (nw) pe = rfl(hdr->cursor[w]);
         }
         if (ok) {
             // the part's first literal run starts at the end of the last part before it with a
             // sequence: its first sequence is extended back in place (ll, the low 16 bits: cannot
-            // carry out, < 2^16)
+            // carry out, < 2^16), and the bytes it now covers join the literal region at their
+            // page positions, right below the part's own literals (copied by the sink)
             const uint32_t nw = rfl(hdr->n[wave]);
-            uint2 qn = lane < nw ? W[lane] : make_uint2(0u, 0u);   // the slice a group ahead of the copy below
             if (lane == 0 && wave > 0 && nw) {
-                qn.x += b0 - prev_end;
-                W[0] = qn;   // (the store waits for the load it depends on)
+                uint2 q = W[0];
+                q.x += b0 - prev_end;
+                W[0] = q;   // (the store waits for the load it depends on)
             }
-            // and the part's literals, from the staged page to the literal region, in page order
             uint8_t *lits = area_lit(area, rec_cap);
-            uint32_t pos = prev_end, lo = lit_w;   // page position and literal offset of the next run
-            for (uint32_t j0 = 0; j0 < nw; j0 += kWave) {
-                const uint32_t j = j0 + lane;
-                const uint2 q = qn;
-                qn = j + kWave < nw ? W[j + kWave] : make_uint2(0u, 0u);
-                const uint32_t ll = q.x & 0xFFFFu, sz = ll + q.y;
-                const uint32_t inc = (uint32_t)wave_incl_sum((int32_t)sz);
-                lo += copy_runs(in, pos + inc - sz, ll, lits + lo, lane, (uint32_t *)rec);   // (rec: free after the parse)
-                pos += rdlane(inc, kWave - 1);
-            }
-            if (wave == kNW - 1)   // the literals after the page's last match
-                for (uint32_t j = lane; pe + j < L; j += kWave) lits[lit_all + j] = in[pe + j];
+            if (wave > 0 && nw)
+                for (uint32_t j = lane; prev_end + j < b0; j += kWave) lits[prev_end + j] = in[prev_end + j];
+            if (wave == kNW - 1)   // the literals after the page's last match, at their page positions
+                for (uint32_t j = lane; pe + j < L; j += kWave) lits[pe + j] = in[pe + j];
         }
         __syncthreads();   // every part's first sequence extended
         if (wave == 0) {
@@ -1413,6 +1430,18 @@ __global__ __launch_bounds__(kNW * 64) void zstd_parse_split_kernel(tyche_batch_
                 if (lane == 0) {
                     ((uint32_t *)area)[1] = npb;
                     put_seq_map(area, m.c1, m.c2, m.c3, m.slice);
+                    // the literal map: each part with a sequence from the end of the last one before
+                    // it (its extended first run, then its own literals), then the last literals
+                    uint32_t lc = 0, pe2 = 0, ns = 0;
+                    for (uint32_t w = 0; w < kNW; w++) {
+                        const uint32_t nw = hdr->n[w];
+                        if (!nw) continue;
+                        ((uint32_t *)area)[4 + ns++] = lc | (pe2 << 16);
+                        lc += bnd(w) - pe2 + hdr->lit[w];
+                        pe2 = hdr->cursor[w];
+                    }
+                    ((uint32_t *)area)[4 + ns++] = lc | (pe2 << 16);
+                    for (; ns < 5u; ns++) ((uint32_t *)area)[4 + ns] = 0xFFFFu;
                     st[page] = 1;
                 }
             }
@@ -1634,7 +1663,7 @@ __global__ __launch_bounds__(64) void zstd_pack_kernel(tyche_batch_t b, size_t f
             uint8_t *dst = batch_page(b, first + j).dst;
             uint32_t q = 0;
             for (uint32_t k = 0; k < nblk; k++) {
-                const uint32_t *B = (const uint32_t *)(area + 16u) + k * kBlkWords;
+                const uint32_t *B = (const uint32_t *)(area + kAreaHdr) + k * kBlkWords;
                 const uint32_t g = __builtin_amdgcn_readfirstlane(B[0]), glen = __builtin_amdgcn_readfirstlane(B[1]);
                 const uint32_t pre = __builtin_amdgcn_readfirstlane(B[2]), fse = __builtin_amdgcn_readfirstlane(B[3]);
                 const uint32_t fl = __builtin_amdgcn_readfirstlane(B[7]);
