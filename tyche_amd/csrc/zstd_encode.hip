@@ -1651,44 +1651,76 @@ __global__ __launch_bounds__(64) void zstd_fse_kernel(tyche_batch_t b, size_t fi
     }
 }
 
-// ---- pass C: close the gaps, patch the compressed blocks' headers
-__global__ __launch_bounds__(64) void zstd_pack_kernel(tyche_batch_t b, size_t first, size_t count, uint8_t *ws,
-                                                       size_t ws_page, const int32_t *st, unsigned *ctr) {
-    const uint32_t lane = threadIdx.x;
-    for (size_t j = blockIdx.x; j < count; j = ctr ? claim_page(ctr, lane) : j + gridDim.x) {
-        int32_t rv = st[j];
-        if (rv > 0) {
-            const uint8_t *area = ws + j * ws_page;
-            const uint32_t nblk = __builtin_amdgcn_readfirstlane(((const uint32_t *)area)[0]);
-            uint8_t *dst = batch_page(b, first + j).dst;
-            uint32_t q = 0;
-            for (uint32_t k = 0; k < nblk; k++) {
-                const uint32_t *B = (const uint32_t *)(area + kAreaHdr) + k * kBlkWords;
-                const uint32_t g = __builtin_amdgcn_readfirstlane(B[0]), glen = __builtin_amdgcn_readfirstlane(B[1]);
-                const uint32_t pre = __builtin_amdgcn_readfirstlane(B[2]), fse = __builtin_amdgcn_readfirstlane(B[3]);
-                const uint32_t fl = __builtin_amdgcn_readfirstlane(B[7]);
-                if (k == 0) q = g;   // the frame header stays
-                const bool comp = (fl & 2u) != 0;
-                const uint32_t clen = comp ? 3u + pre + fse : glen;
-                const uint32_t bh = (fl & 1u) | (2u << 1) | ((pre + fse) << 3);
-                if (g == q) {
-                    if (comp && lane < 3) dst[q + lane] = (uint8_t)(bh >> (8u * lane));
-                } else {
-                    // left move in 64-byte steps: a step's reads precede its writes
-                    for (uint32_t c0 = 0; c0 < clen; c0 += kWave) {
-                        const uint32_t i = c0 + lane;
-                        uint8_t v = i < clen ? dst[g + i] : 0;
-                        if (comp && i < 3u) v = (uint8_t)(bh >> (8u * i));
-                        __builtin_amdgcn_wave_barrier();
-                        if (i < clen) dst[q + i] = v;
-                        __builtin_amdgcn_wave_barrier();
-                    }
-                }
-                q += clen;
+// ---- pass C: close the gaps, patch the compressed blocks' headers.  One page per lane
+// (round 6; a wave per page before, 12 ms per 1M pages of mostly three-byte header patches):
+// a page whose blocks all sit where the frame needs them (every 32 KiB page: one block) is
+// patched by its lane; a page with a gap to close is left to the whole wave, one such page
+// at a time, after the lane pass.
+__device__ __forceinline__ int32_t pack_page_wave(uint8_t *dst, const uint8_t *area, uint32_t lane) {
+    const uint32_t nblk = __builtin_amdgcn_readfirstlane(((const uint32_t *)area)[0]);
+    uint32_t q = 0;
+    for (uint32_t k = 0; k < nblk; k++) {
+        const uint32_t *B = (const uint32_t *)(area + kAreaHdr) + k * kBlkWords;
+        const uint32_t g = __builtin_amdgcn_readfirstlane(B[0]), glen = __builtin_amdgcn_readfirstlane(B[1]);
+        const uint32_t pre = __builtin_amdgcn_readfirstlane(B[2]), fse = __builtin_amdgcn_readfirstlane(B[3]);
+        const uint32_t fl = __builtin_amdgcn_readfirstlane(B[7]);
+        if (k == 0) q = g;   // the frame header stays
+        const bool comp = (fl & 2u) != 0;
+        const uint32_t clen = comp ? 3u + pre + fse : glen;
+        const uint32_t bh = (fl & 1u) | (2u << 1) | ((pre + fse) << 3);
+        if (g == q) {
+            if (comp && lane < 3) dst[q + lane] = (uint8_t)(bh >> (8u * lane));
+        } else {
+            // left move in 64-byte steps: a step's reads precede its writes
+            for (uint32_t c0 = 0; c0 < clen; c0 += kWave) {
+                const uint32_t i = c0 + lane;
+                uint8_t v = i < clen ? dst[g + i] : 0;
+                if (comp && i < 3u) v = (uint8_t)(bh >> (8u * i));
+                __builtin_amdgcn_wave_barrier();
+                if (i < clen) dst[q + i] = v;
+                __builtin_amdgcn_wave_barrier();
             }
-            rv = (int32_t)q;
         }
-        if (lane == 0) b.results[first + j] = rv;
+        q += clen;
+    }
+    return (int32_t)q;
+}
+__global__ __launch_bounds__(64) void zstd_pack_kernel(tyche_batch_t b, size_t first, size_t count, uint8_t *ws,
+                                                       size_t ws_page, const int32_t *st) {
+    const uint32_t lane = threadIdx.x;
+    const size_t j = (size_t)blockIdx.x * kWave + lane;
+    int32_t rv = j < count ? st[j] : 0;
+    bool wave_page = false;
+    if (j < count && rv > 0) {
+        const uint8_t *area = ws + j * ws_page;
+        uint8_t *dst = batch_page(b, first + j).dst;
+        const uint32_t nblk = ((const uint32_t *)area)[0];
+        uint32_t q = 0;
+        for (uint32_t k = 0; k < nblk; k++) {
+            const uint32_t *B = (const uint32_t *)(area + kAreaHdr) + k * kBlkWords;
+            const uint32_t g = B[0], glen = B[1], pre = B[2], fse = B[3], fl = B[7];
+            if (k == 0) q = g;
+            if (g != q) {   // a gap to close: the wave's
+                wave_page = true;
+                break;
+            }
+            const bool comp = (fl & 2u) != 0;
+            if (comp) {
+                const uint32_t bh = (fl & 1u) | (2u << 1) | ((pre + fse) << 3);
+                dst[q] = (uint8_t)bh;
+                dst[q + 1] = (uint8_t)(bh >> 8);
+                dst[q + 2] = (uint8_t)(bh >> 16);
+            }
+            q += comp ? 3u + pre + fse : glen;
+        }
+        rv = (int32_t)q;
+    }
+    if (j < count && !wave_page) b.results[first + j] = rv;
+    for (uint64_t m = __ballot(wave_page); m; m &= m - 1ull) {
+        const uint32_t k = (uint32_t)__builtin_ctzll(m);
+        const size_t jj = (size_t)blockIdx.x * kWave + k;
+        const int32_t r = pack_page_wave(batch_page(b, first + jj).dst, ws + jj * ws_page, lane);
+        if (lane == 0) b.results[first + jj] = r;
     }
 }
 
@@ -1831,13 +1863,8 @@ hipError_t launch_zstd_encode(const tyche_batch_t &b, uint32_t in_cap, hipStream
         }
         hipLaunchKernelGGL(zstd_fse_kernel, dim3((unsigned)((n + kWave - 1) / kWave)), dim3(kWave),
                            kWave * kFseSlot.words * 4u, s, b, first, n, ws, page_bytes, (const int32_t *)st);
-        {
-            const size_t g = std::min<size_t>(n, ncu * 8u);
-            WorkCounter ctr(s, g < n);
-            if (!ctr.get()) return hipErrorOutOfMemory;
-            hipLaunchKernelGGL(zstd_pack_kernel, dim3((unsigned)g), dim3(kWave), 0, s, b, first, n, ws, page_bytes,
-                               (const int32_t *)st, ctr.get());
-        }
+        hipLaunchKernelGGL(zstd_pack_kernel, dim3((unsigned)((n + kWave - 1) / kWave)), dim3(kWave), 0, s, b, first, n, ws,
+                           page_bytes, (const int32_t *)st);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
